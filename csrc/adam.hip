@@ -1,0 +1,216 @@
+// K6 — fused Adam for MI355X: deterministic slab reduction + Adam + bf16 weight packing.
+//
+// The reference's only optimizer is inside libxgboost (Newton boosting,
+// Main.java:137-138); the north star's Adam comes from the declared-but-unused
+// DL4J updater (pom.xml:62-66).  One flat fp32 master buffer
+// (params, m, v); each thread owns one parameter:
+//   g  = grad_scale * sum_{slab} slabs[slab][p]     (fixed order -> bitwise reproducible)
+//   m  = b1 m + (1-b1) g ;  v = b2 v + (1-b2) g^2
+//   p -= lr * (m / bc1) / (sqrt(v / bc2) + eps)      (torch.optim.Adam semantics)
+// and, for the fused small MLP, writes the bf16 value of p into the LDS-ready
+// weight images consumed by mlp_fused.hip (so the train kernel's prologue is a
+// straight 48 KB copy).  Modes let DP insert an RCCL all-reduce between the slab
+// reduction and the update.
+#include "common.h"
+
+namespace {
+
+constexpr int IN = 64, HID = 128, OUT = 64;
+constexpr int P_W2 = IN * HID, P_B2 = P_W2 + HID * OUT, P_TOTAL = P_B2 + OUT;
+constexpr int IMG_W1T = 0, IMG_W2P = 16384, IMG_W2Q = 32768, IMG_B2 = 49152;
+
+// true for padding slots that must stay exactly zero (W1 row 63, W2 cols 62/63, b2[62/63])
+EM_DEVICE bool mlp_pad_slot(int p) {
+  if (p < P_W2) return (p >> 7) == 63;
+  if (p < P_B2) return ((p - P_W2) & 63) >= 62;
+  return (p - P_B2) >= 62;
+}
+
+EM_DEVICE void mlp_pack_one(int p, float val, uint8_t* img) {
+  const uint16_t b = f2bf_bits(val);
+  if (p < P_W2) {  // W1[f][c] -> W1T image row c, feature f
+    const int f = p >> 7, c = p & 127;
+    const uint32_t off = IMG_W1T + c * 128 + ((((f >> 3) ^ ((c >> 1) & 7))) << 4) + (f & 7) * 2;
+    *reinterpret_cast<uint16_t*>(img + off) = b;
+  } else if (p < P_B2) {  // W2[c][o]
+    const int q = p - P_W2, c = q >> 6, o = q & 63;
+    {  // W2P: row o, hid c = 32t + perm(s,h,j)
+      const int t = c >> 5, cc = c & 31, s = cc >> 4, a = (cc >> 3) & 1, hh = (cc >> 2) & 1, bb = cc & 3;
+      const int j = 4 * a + bb, k16 = (2 * t + s) * 2 + hh;
+      const uint32_t off = IMG_W2P + o * 256 + ((k16 ^ (o & 15)) << 4) + j * 2;
+      *reinterpret_cast<uint16_t*>(img + off) = b;
+    }
+    {  // W2Q: row c, out o = 32u + perm(s,h,j)
+      const int u = o >> 5, oo = o & 31, s = oo >> 4, a = (oo >> 3) & 1, hh = (oo >> 2) & 1, bb = oo & 3;
+      const int j = 4 * a + bb, k8 = (2 * u + s) * 2 + hh;
+      const uint32_t off = IMG_W2Q + c * 128 + ((k8 ^ ((c >> 1) & 7)) << 4) + j * 2;
+      *reinterpret_cast<uint16_t*>(img + off) = b;
+    }
+  } else {
+    *reinterpret_cast<float*>(img + IMG_B2 + (p - P_B2) * 4) = val;
+  }
+}
+
+// 4 threads per parameter (slab-split), 64 parameters per 256-thread block.
+// Bias-correction step counter kept on the device: every block reads `step` first; the last block
+// to finish (ticket) publishes step+1.  So one launch = one Adam step, with no host round-trip,
+// and the whole train step can be replayed from a hipGraph.
+EM_DEVICE int adam_begin(int* state) { return __hip_atomic_load(&state[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1; }
+EM_DEVICE void adam_end(int* state, int t) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int tk = __hip_atomic_fetch_add(&state[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == (int)gridDim.x - 1) {
+      __hip_atomic_store(&state[0], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&state[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, float grad_scale, float* __restrict__ params,
+                 float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io, const float* __restrict__ hp,
+                 int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img, const float* __restrict__ loss_slabs,
+                 float* __restrict__ loss_out, float loss_scale) {
+  const int tstep = (mode != 1) ? adam_begin(state) : 0;
+  // hp = {lr, beta1, beta2, eps, weight_decay}; state = {step, ticket} (device ints, graph-replay safe)
+  __shared__ float part[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + tx;
+  float g = 0.f;
+  if (mode != 2) {
+    float acc0 = 0.f, acc1 = 0.f;
+    if (p < P) {
+      int sl = ty;
+      for (; sl + 4 < nslab; sl += 8) {
+        acc0 += slabs[(size_t)sl * P + p];
+        acc1 += slabs[(size_t)(sl + 4) * P + p];
+      }
+      if (sl < nslab) acc0 += slabs[(size_t)sl * P + p];
+    }
+    part[ty][tx] = acc0 + acc1;
+    __syncthreads();
+    g = ((part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx])) * grad_scale;
+  } else if (p < P) {
+    g = grad_io[p];
+  }
+  if (blockIdx.x == 0 && loss_slabs && loss_out && threadIdx.x < 64) {
+    float l = 0.f;
+    for (int i = threadIdx.x; i < nslab; i += 64) l += loss_slabs[i];
+    l = wave_sum(l);
+    if (threadIdx.x == 0) loss_out[0] = l * loss_scale;
+  }
+  if (mode == 1) {
+    if (ty == 0 && p < P) grad_io[p] = g;
+    return;
+  }
+  if (ty == 0 && p < P) {
+    const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+    const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
+    if (mlp_img && mlp_pad_slot(p)) {
+      params[p] = 0.f;
+      m[p] = 0.f;
+      v[p] = 0.f;
+      mlp_pack_one(p, 0.f, mlp_img);
+    } else {
+      float w = params[p];
+      g += wd * w;
+      const float mm = b1 * m[p] + (1.f - b1) * g;
+      const float vv = b2 * v[p] + (1.f - b2) * g * g;
+      m[p] = mm;
+      v[p] = vv;
+      w -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
+      params[p] = w;
+      if (mlp_img) mlp_pack_one(p, w, mlp_img);
+    }
+  }
+  adam_end(state, tstep);
+}
+
+__global__ void mlp_pack_kernel(const float* __restrict__ params, uint8_t* __restrict__ img) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P_TOTAL) return;
+  mlp_pack_one(p, mlp_pad_slot(p) ? 0.f : params[p], img);
+}
+
+// plain multi-tensor-style Adam over a flat buffer (generic path: K6 for any model)
+__global__ void __launch_bounds__(256)
+adam_flat_kernel(float* __restrict__ params, const float* __restrict__ grad, float* __restrict__ m,
+                 float* __restrict__ v, int64_t n, const float* __restrict__ hp, int* __restrict__ state,
+                 float grad_scale, __bf16* __restrict__ shadow) {
+  const int tstep = adam_begin(state);
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+  const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
+  for (int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += (int64_t)gridDim.x * blockDim.x * 4) {
+    if (i4 + 4 <= n) {
+      f32x4 w = *reinterpret_cast<const f32x4*>(params + i4);
+      f32x4 g = *reinterpret_cast<const f32x4*>(grad + i4);
+      f32x4 mm = *reinterpret_cast<const f32x4*>(m + i4);
+      f32x4 vv = *reinterpret_cast<const f32x4*>(v + i4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gg = g[k] * grad_scale + wd * w[k];
+        mm[k] = b1 * mm[k] + (1.f - b1) * gg;
+        vv[k] = b2 * vv[k] + (1.f - b2) * gg * gg;
+        w[k] -= lr * (mm[k] / bc1) / (sqrtf(vv[k] / bc2) + eps);
+      }
+      *reinterpret_cast<f32x4*>(params + i4) = w;
+      *reinterpret_cast<f32x4*>(m + i4) = mm;
+      *reinterpret_cast<f32x4*>(v + i4) = vv;
+      if (shadow) {
+        bf16x4 sb;
+        sb[0] = (__bf16)w[0]; sb[1] = (__bf16)w[1]; sb[2] = (__bf16)w[2]; sb[3] = (__bf16)w[3];
+        *reinterpret_cast<bf16x4*>(shadow + i4) = sb;
+      }
+    } else {
+      for (int64_t i = i4; i < n; ++i) {
+        float w = params[i];
+        const float gg = grad[i] * grad_scale + wd * w;
+        const float mm = b1 * m[i] + (1.f - b1) * gg;
+        const float vv = b2 * v[i] + (1.f - b2) * gg * gg;
+        m[i] = mm;
+        v[i] = vv;
+        w -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
+        params[i] = w;
+        if (shadow) shadow[i] = (__bf16)w;
+      }
+    }
+  }
+  adam_end(state, tstep);
+}
+
+}  // namespace
+
+EM_API int em_adam_slab(const float* slabs, int nslab, int P, float grad_scale, float* params, float* m, float* v,
+                        float* grad_io, const float* hp, int* state, int mode, void* mlp_img, const float* loss_slabs,
+                        float* loss_out, float loss_scale, hipStream_t stream) {
+  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0)) || (mode != 0 && !grad_io)) return EM_ERR_ARG;
+  if (mode != 1 && (!params || !m || !v || !hp || !state)) return EM_ERR_ARG;
+  if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
+  const int nb = (P + 63) / 64;
+  hipLaunchKernelGGL(adam_slab_kernel, dim3(nb), dim3(256), 0, stream, slabs, nslab, P, grad_scale, params, m, v,
+                     grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_mlp_fused_pack(const float* params, void* img, hipStream_t stream) {
+  if (!params || !img) return EM_ERR_ARG;
+  hipLaunchKernelGGL(mlp_pack_kernel, dim3((P_TOTAL + 255) / 256), dim3(256), 0, stream, params, (uint8_t*)img);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_adam_flat(float* params, const float* grad, float* m, float* v, int64_t n, const float* hp, int* state,
+                        float grad_scale, void* shadow_bf16, hipStream_t stream) {
+  if (!params || !grad || !m || !v || !hp || !state || n < 0) return EM_ERR_ARG;
+  if (n == 0) return 0;
+  int64_t nb = (n / 4 + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)nb), dim3(256), 0, stream, params, grad, m, v, n, hp, state,
+                     grad_scale, (__bf16*)shadow_bf16);
+  EM_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,237 @@
+"""MLP models for 62-in / 62-out draw prediction.
+
+The north star re-implements the DL4J ``MultiLayerNetwork`` path that the reference
+declares (``pom.xml:62-66``, "Neural Networks" in ``README.md:6``) but never builds.
+Two execution paths share one parameter convention (DL4J layer order, per layer
+``W [nIn, nOut]`` then ``b [nOut]``):
+
+* :class:`DrawMLP` — a ``torch.nn.Module`` for arbitrary layer sizes / lag windows.
+  On the GPU its dense layers run on our MFMA GEMM kernels
+  (:mod:`euromillioner_amd.ops.linear`); on the CPU it is plain PyTorch (the
+  world_size=1 plumbing config of BASELINE.json).
+* :class:`FusedSmallMLP` — the flagship 62->128->62 trainer: one fused HIP launch for
+  forward+loss+backward (``csrc/mlp_fused.hip``) plus one fused Adam launch
+  (``csrc/adam.hip``), optional RCCL data parallelism in between.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import losses as L
+
+
+def dl4j_xavier_(w: torch.Tensor, fan_in: int, fan_out: int, gen: torch.Generator | None = None) -> torch.Tensor:
+    """DL4J ``WeightInit.XAVIER``: N(0, 2 / (nIn + nOut))."""
+    with torch.no_grad():
+        w.normal_(0.0, math.sqrt(2.0 / (fan_in + fan_out)), generator=gen)
+    return w
+
+
+class DrawMLP(nn.Module):
+    def __init__(self, sizes=(62, 128, 62), activation: str = "relu", loss: str = "softmax", seed: int = 0,
+                 use_hip: bool | None = None, dtype: torch.dtype = torch.float32):
+        super().__init__()
+        if len(sizes) < 2:
+            raise ValueError("need at least input and output sizes")
+        if activation not in ("relu", "sigmoid", "tanh", "identity"):
+            raise ValueError(f"unknown activation {activation}")
+        self.sizes = tuple(int(s) for s in sizes)
+        self.activation = activation
+        self.loss_name = loss
+        self.use_hip = use_hip
+        self.compute_dtype = dtype
+        self.layers = nn.ModuleList(nn.Linear(a, b) for a, b in zip(self.sizes[:-1], self.sizes[1:]))
+        g = torch.Generator().manual_seed(seed)
+        for lin in self.layers:
+            dl4j_xavier_(lin.weight, lin.in_features, lin.out_features, g)
+            nn.init.zeros_(lin.bias)
+
+    def _act(self, x):
+        if self.activation == "relu":
+            return torch.relu(x)
+        if self.activation == "sigmoid":
+            return torch.sigmoid(x)
+        if self.activation == "tanh":
+            return torch.tanh(x)
+        return x
+
+    def _hip_ok(self, x: torch.Tensor) -> bool:
+        if not x.is_cuda:
+            return False
+        return self.use_hip is not False
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._hip_ok(x):
+            from ..ops import linear as LIN
+
+            act = {"relu": "relu", "sigmoid": "sigmoid", "identity": "none", "tanh": "tanh"}[self.activation]
+            h = x
+            for i, lin in enumerate(self.layers):
+                last = i == len(self.layers) - 1
+                h = LIN.linear(h, lin.weight, lin.bias, activation="none" if last else act,
+                               compute_dtype=self.compute_dtype)
+            return h
+        h = x.to(self.compute_dtype) if self.compute_dtype != torch.float32 else x
+        for i, lin in enumerate(self.layers):
+            w, b = lin.weight, lin.bias
+            if self.compute_dtype != torch.float32:
+                w, b = w.to(self.compute_dtype), b.to(self.compute_dtype)
+            h = torch.nn.functional.linear(h, w, b)
+            if i < len(self.layers) - 1:
+                h = self._act(h)
+        return h.float()
+
+    def loss(self, logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        return L.LOSSES[self.loss_name](logits, target)
+
+    def n_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+
+class FusedSmallMLP:
+    """Flagship trainer: 62->128->62 ReLU MLP, bf16 MFMA compute, fp32 master weights + Adam."""
+
+    def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
+                 state_dict: dict | None = None, process_group=None):
+        from ..ops import fused_mlp as FM
+        from ..ops import _native as N
+
+        if loss not in FM.LOSS_KINDS:
+            raise ValueError(f"loss must be one of {list(FM.LOSS_KINDS)}")
+        self.FM = FM
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("FusedSmallMLP runs on the GPU (use DrawMLP for CPU)")
+        N.lib()  # fail loudly if the HIP library is missing
+        self.loss_name = loss
+        self.group = process_group
+        dev = self.device
+        P = FM.P_TOTAL
+        if state_dict is None:
+            ref = DrawMLP((62, 128, 62), seed=seed)
+            state_dict = {"l1.weight": ref.layers[0].weight.data, "l1.bias": ref.layers[0].bias.data,
+                          "l2.weight": ref.layers[1].weight.data, "l2.bias": ref.layers[1].bias.data}
+        self.params = FM.flatten(state_dict, device=dev)
+        self.m = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
+        self.state = torch.zeros(2, dtype=torch.int32, device=dev)  # {adam step, ticket}
+        self.img = torch.zeros(FM.IMG_BYTES, dtype=torch.uint8, device=dev)
+        self.nslab_max = N.cu_count(dev)
+        self.slabs = torch.zeros(self.nslab_max, P, dtype=torch.float32, device=dev)
+        self.loss_slabs = torch.zeros(self.nslab_max, dtype=torch.float32, device=dev)
+        self.grad_io = torch.zeros(P + 1, dtype=torch.float32, device=dev)  # [grads..., loss]
+        self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
+        FM.pack(self.params, self.img)
+        self._checked = False
+
+    # ------------------------------------------------------------------ training
+    @property
+    def world(self) -> int:
+        if self.group is None:
+            return 1
+        import torch.distributed as dist
+
+        return dist.get_world_size(self.group)
+
+    def step(self, draws: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None,
+             global_batch: int | None = None) -> torch.Tensor:
+        """One optimizer step over B local samples; returns the (global) mean loss as a device tensor."""
+        FM = self.FM
+        nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
+                                  offset=offset, sidx=sidx, check=not self._checked)
+        self._checked = True
+        gb = global_batch if global_batch is not None else B * self.world
+        scale = 1.0 / max(gb, 1)
+        if self.loss_name == "bce":
+            scale /= 62.0
+        lscale = 1.0 / max(gb, 1) / (62.0 if self.loss_name == "bce" else 1.0)
+        if self.group is None:
+            FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=0,
+                         img=self.img, loss_slabs=self.loss_slabs, loss_out=self.loss_out, loss_scale=lscale)
+            return self.loss_out
+        import torch.distributed as dist
+
+        loss_view = self.grad_io[FM.P_TOTAL:]
+        FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=1,
+                     grad_io=self.grad_io, loss_slabs=self.loss_slabs, loss_out=loss_view, loss_scale=lscale)
+        dist.all_reduce(self.grad_io, op=dist.ReduceOp.SUM, group=self.group)
+        FM.adam_slab(None, 0, 1.0, self.params, self.m, self.v, self.hp, self.state, mode=2, grad_io=self.grad_io,
+                     img=self.img)
+        return loss_view
+
+    def grads(self, draws: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None):
+        """(mean loss, flat gradient) without updating — for tests / gradient checks."""
+        FM = self.FM
+        nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
+                                  offset=offset, sidx=sidx)
+        scale = 1.0 / B / (62.0 if self.loss_name == "bce" else 1.0)
+        FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=1,
+                     grad_io=self.grad_io, loss_slabs=self.loss_slabs, loss_out=self.grad_io[FM.P_TOTAL:],
+                     loss_scale=scale)
+        g = self.grad_io[:FM.P_TOTAL].clone()
+        return self.grad_io[FM.P_TOTAL].item(), g
+
+    # ------------------------------------------------------------------ inference / eval
+    def logits(self, draws: torch.Tensor, B: int, offset: int = 0, sidx=None) -> torch.Tensor:
+        return self.FM.forward_logits(draws, B, self.img, offset=offset, sidx=sidx)
+
+    def evaluate(self, draws: torch.Tensor, B: int, offset: int = 0, sidx=None, chunk: int = 1 << 22) -> dict:
+        FM = self.FM
+        tot = np.zeros(8, dtype=np.float64)
+        done = 0
+        while done < B:
+            b = min(chunk, B - done)
+            lg = self.logits(draws, b, offset=offset + done if sidx is None else 0,
+                             sidx=None if sidx is None else sidx[done:done + b])
+            part = FM.draw_metrics(lg, draws, b, loss=self.loss_name, offset=offset + done if sidx is None else 0,
+                                   sidx=None if sidx is None else sidx[done:done + b])
+            tot += part.double().sum(0).cpu().numpy()
+            done += b
+        if self.group is not None:
+            import torch.distributed as dist
+
+            t = torch.tensor(tot, dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, group=self.group)
+            tot = t.cpu().numpy()
+        cnt = max(tot[7], 1.0)
+        out = {k: float(tot[i] / cnt) for i, k in enumerate(FM.METRIC_NAMES[:-1])}
+        out["count"] = int(tot[7])
+        return out
+
+    # ------------------------------------------------------------------ state
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        return {k: v.detach().clone().cpu() for k, v in self.FM.unflatten(self.params).items()}
+
+    def optimizer_state(self) -> dict:
+        FM = self.FM
+        return {"m": {k: v.clone().cpu() for k, v in FM.unflatten(self.m).items()},
+                "v": {k: v.clone().cpu() for k, v in FM.unflatten(self.v).items()},
+                "step": int(self.state[0].item()),
+                "hp": self.hp.cpu().tolist()}
+
+    def load_optimizer_state(self, st: dict) -> None:
+        FM = self.FM
+        self.m.copy_(FM.flatten(st["m"], device=self.device))
+        self.v.copy_(FM.flatten(st["v"], device=self.device))
+        self.state[0] = int(st.get("step", 0))
+        self.state[1] = 0
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.copy_(self.FM.flatten(sd, device=self.device))
+        self.FM.pack(self.params, self.img)
+
+    def broadcast_parameters(self, src: int = 0) -> None:
+        """C2: initial parameter sync (identical init on every rank)."""
+        if self.group is None:
+            return
+        import torch.distributed as dist
+
+        dist.broadcast(self.params, src=dist.get_global_rank(self.group, src) if hasattr(dist, "get_global_rank")
+                       else src, group=self.group)
+        self.FM.pack(self.params, self.img)

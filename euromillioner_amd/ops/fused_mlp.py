@@ -1,0 +1,165 @@
+"""Python face of the fused small-MLP kernels (``csrc/mlp_fused.hip``, ``csrc/adam.hip``,
+``csrc/metrics.hip``).
+
+Flat fp32 parameter layout (``P = 16448`` floats; the pads stay exactly 0):
+
+=========  ===============  =================================================
+offset     shape            meaning
+=========  ===============  =================================================
+0          W1 [64][128]     rows 0..61 = Linear(62,128).weight^T, row 62 = b1
+8192       W2 [128][64]     cols 0..61 = Linear(128,62).weight^T
+16384      b2 [64]          0..61 = Linear(128,62).bias
+=========  ===============  =================================================
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+IN, HID, OUT = 64, 128, 64
+P_W1, P_W2, P_B2 = 0, IN * HID, IN * HID + HID * OUT
+P_TOTAL = P_B2 + OUT
+IMG_BYTES = 49408
+LOSS_KINDS = {"softmax": 0, "bce": 1}
+
+
+def unflatten(flat: torch.Tensor) -> dict[str, torch.Tensor]:
+    """Logical (PyTorch nn.Linear-shaped) views of the flat buffer."""
+    W1 = flat[P_W1:P_W2].view(IN, HID)
+    W2 = flat[P_W2:P_B2].view(HID, OUT)
+    b2 = flat[P_B2:P_TOTAL]
+    return {
+        "l1.weight": W1[:62].t(),  # [128, 62]
+        "l1.bias": W1[62],  # [128]
+        "l2.weight": W2[:, :62].t(),  # [62, 128]
+        "l2.bias": b2[:62],  # [62]
+    }
+
+
+def flatten(sd: dict[str, torch.Tensor], device=None) -> torch.Tensor:
+    flat = torch.zeros(P_TOTAL, dtype=torch.float32, device=device)
+    W1 = flat[P_W1:P_W2].view(IN, HID)
+    W2 = flat[P_W2:P_B2].view(HID, OUT)
+    W1[:62] = sd["l1.weight"].t().to(flat)
+    W1[62] = sd["l1.bias"].to(flat)
+    W2[:, :62] = sd["l2.weight"].t().to(flat)
+    flat[P_B2:P_B2 + 62] = sd["l2.bias"].to(flat)
+    return flat
+
+
+def pad_mask(device=None) -> torch.Tensor:
+    """1 for real parameters, 0 for the padding slots."""
+    m = torch.zeros(P_TOTAL, dtype=torch.float32, device=device)
+    m[P_W1:P_W2].view(IN, HID)[:63] = 1
+    m[P_W2:P_B2].view(HID, OUT)[:, :62] = 1
+    m[P_B2:P_B2 + 62] = 1
+    return m
+
+
+def pack(params: torch.Tensor, img: torch.Tensor) -> None:
+    N.check_cuda(params, "params", torch.float32)
+    N.check_cuda(img, "img", torch.uint8)
+    if params.numel() != P_TOTAL or img.numel() < IMG_BYTES:
+        raise ValueError("bad params/img size")
+    N.call("em_mlp_fused_pack", params.data_ptr(), img.data_ptr(), N.stream_handle(params.device))
+
+
+def _check_draws(draws: torch.Tensor, sidx: torch.Tensor | None, B: int, offset: int, need_next: bool = True):
+    N.check_cuda(draws, "draws", torch.uint8)
+    if draws.dim() != 2 or draws.shape[1] != 8:
+        raise ValueError("draws must be [N, 8] uint8")
+    n = draws.shape[0]
+    if sidx is not None:
+        N.check_cuda(sidx, "sample_idx", torch.int32)
+        if sidx.numel() < B:
+            raise ValueError("sample_idx shorter than B")
+        if B > 0:
+            lo, hi = int(sidx[:B].min()), int(sidx[:B].max())
+            if lo < 0 or hi + (1 if need_next else 0) >= n:
+                raise ValueError("sample_idx out of range")
+    elif B > 0 and (offset < 0 or offset + B - 1 + (1 if need_next else 0) >= n):
+        raise ValueError(f"samples [{offset}, {offset + B}) + next draw exceed {n} draws")
+
+
+def train_partials(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.Tensor, loss_slabs: torch.Tensor,
+                   loss: str = "softmax", offset: int = 0, sidx: torch.Tensor | None = None,
+                   check: bool = True) -> int:
+    """Launch K7: per-workgroup gradient slabs for B samples.  Returns the grid size used."""
+    if check:
+        _check_draws(draws, sidx, B, offset)
+        N.check_cuda(img, "img", torch.uint8)
+        N.check_cuda(slabs, "slabs", torch.float32)
+        N.check_cuda(loss_slabs, "loss_slabs", torch.float32)
+        if slabs.dim() != 2 or slabs.shape[1] != P_TOTAL or loss_slabs.numel() < slabs.shape[0]:
+            raise ValueError("slabs must be [nslab, P]")
+    groups = (B + 127) // 128
+    nslab = max(1, min(slabs.shape[0], groups))
+    N.call("em_mlp_fused_train", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
+           img.data_ptr(), slabs.data_ptr(), loss_slabs.data_ptr(), nslab, LOSS_KINDS[loss],
+           N.stream_handle(draws.device))
+    return nslab
+
+
+def forward_logits(draws: torch.Tensor, B: int, img: torch.Tensor, out: torch.Tensor | None = None, offset: int = 0,
+                   sidx: torch.Tensor | None = None) -> torch.Tensor:
+    _check_draws(draws, sidx, B, offset, need_next=False)
+    if out is None:
+        out = torch.empty(B, OUT, dtype=torch.float32, device=draws.device)
+    N.check_cuda(out, "out", torch.float32)
+    if out.shape[0] < B or out.shape[1] != OUT:
+        raise ValueError("out must be [B, 64]")
+    nb = max(1, min(N.cu_count(draws.device) * 2, (B + 127) // 128))
+    N.call("em_mlp_fused_forward", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
+           img.data_ptr(), out.data_ptr(), nb, N.stream_handle(draws.device))
+    return out
+
+
+def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params: torch.Tensor, m: torch.Tensor,
+              v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor, mode: int = 0, grad_io: torch.Tensor | None = None,
+              img: torch.Tensor | None = None, loss_slabs: torch.Tensor | None = None,
+              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0) -> None:
+    P = params.numel()
+    N.call("em_adam_slab", slabs.data_ptr() if slabs is not None else None, int(nslab), int(P), float(grad_scale),
+           params.data_ptr(), m.data_ptr(), v.data_ptr(), grad_io.data_ptr() if grad_io is not None else None,
+           hp.data_ptr(), state.data_ptr(), int(mode), img.data_ptr() if img is not None else None,
+           loss_slabs.data_ptr() if loss_slabs is not None else None,
+           loss_out.data_ptr() if loss_out is not None else None, float(loss_scale), N.stream_handle(params.device))
+
+
+def adam_flat(params: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor,
+              state: torch.Tensor, grad_scale: float = 1.0, shadow: torch.Tensor | None = None) -> None:
+    for t, nm in ((params, "params"), (grad, "grad"), (m, "m"), (v, "v")):
+        N.check_cuda(t, nm, torch.float32)
+    if shadow is not None:
+        N.check_cuda(shadow, "shadow", torch.bfloat16)
+    N.call("em_adam_flat", params.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), params.numel(),
+           hp.data_ptr(), state.data_ptr(), float(grad_scale), shadow.data_ptr() if shadow is not None else None,
+           N.stream_handle(params.device))
+
+
+METRIC_NAMES = ("loss", "acc", "acc_thr", "hits_main", "hits_star", "exact", "trivial_acc", "count")
+
+
+def draw_metrics(logits: torch.Tensor, draws: torch.Tensor, B: int, loss: str = "softmax", offset: int = 0,
+                 sidx: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-block partial sums [nblocks, 8] (see METRIC_NAMES); sum on the host in fp64."""
+    _check_draws(draws, sidx, B, offset)
+    N.check_cuda(logits, "logits", torch.float32)
+    nb = (B + 255) // 256
+    part = torch.zeros(max(nb, 1), 8, dtype=torch.float32, device=logits.device)
+    N.call("em_draw_metrics", logits.data_ptr(), logits.stride(0), draws.data_ptr(),
+           sidx.data_ptr() if sidx is not None else None, B, offset, LOSS_KINDS[loss], part.data_ptr(),
+           N.stream_handle(logits.device))
+    return part
+
+
+def onehot(draws: torch.Tensor, B: int, offset: int = 0, which: int = 0, bias: bool = False,
+           sidx: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """K14: multi-hot bf16 [B, 64] of draws[idx + which] (which=1 -> targets)."""
+    _check_draws(draws, sidx, B, offset, need_next=(which == 1))
+    if out is None:
+        out = torch.empty(B, 64, dtype=torch.bfloat16, device=draws.device)
+    N.call("em_onehot_encode", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset, which,
+           1 if bias else 0, out.data_ptr(), N.stream_handle(draws.device))
+    return out

@@ -1,0 +1,134 @@
+"""GPU numerics for the fused small-MLP kernels vs a plain PyTorch fp32 reference."""
+import numpy as np
+import pytest
+import torch
+
+from euromillioner_amd.data.draws import DrawSet, multi_hot
+from euromillioner_amd.models import losses as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_grads(sd, ds_numbers, offset, B, loss, bf16=True):
+    X = torch.from_numpy(multi_hot(ds_numbers[offset:offset + B])).cuda()
+    Y = torch.from_numpy(multi_hot(ds_numbers[offset + 1:offset + 1 + B])).cuda()
+    rnd = (lambda t: t.bfloat16().float()) if bf16 else (lambda t: t)
+    W1 = rnd(sd["l1.weight"].cuda()).requires_grad_()
+    b1 = rnd(sd["l1.bias"].cuda()).requires_grad_()
+    W2 = rnd(sd["l2.weight"].cuda()).requires_grad_()
+    b2 = sd["l2.bias"].cuda().clone().requires_grad_()
+    h = torch.relu(X @ W1.t() + b1)
+    z = rnd(h) @ W2.t() + b2
+    l = L.LOSSES[loss](z, Y)
+    l.backward()
+    return l.item(), {"l1.weight": W1.grad, "l1.bias": b1.grad, "l2.weight": W2.grad, "l2.bias": b2.grad}, z.detach()
+
+
+@pytest.fixture(scope="module")
+def data():
+    ds = DrawSet.synthetic(n=6000, seed=11, planted=0.6, calendar=False)
+    return ds, torch.from_numpy(ds.numbers).cuda()
+
+
+@pytest.mark.parametrize("loss", ["softmax", "bce"])
+@pytest.mark.parametrize("B,offset", [(4096, 0), (1000, 7), (37, 100)])
+def test_fused_grads_match_reference(data, loss, B, offset):
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    ds, draws = data
+    m = FusedSmallMLP(loss=loss, seed=5)
+    lk, gk = m.grads(draws, B, offset=offset)
+    lr_, gr, _ = _ref_grads(m.state_dict(), ds.numbers, offset, B, loss)
+    gflat = FM.flatten(gr, device="cuda")
+    assert abs(lk - lr_) <= 2e-3 * max(1.0, abs(lr_)), (lk, lr_)
+    err = (gk - gflat).norm() / gflat.norm()
+    assert err < 2e-2, float(err)
+    # padding slots carry exactly zero gradient
+    assert float((gk * (1 - FM.pad_mask("cuda"))).abs().max()) == 0.0
+
+
+def test_fused_forward_and_metrics(data):
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    ds, draws = data
+    m = FusedSmallMLP(loss="softmax", seed=2)
+    B, off = 3001, 3
+    lg = m.logits(draws, B, offset=off)
+    _, _, zref = _ref_grads(m.state_dict(), ds.numbers, off, B, "softmax")
+    assert torch.allclose(lg[:, :62], zref, atol=2e-2, rtol=2e-2)
+    part = FM.draw_metrics(lg, draws, B, offset=off)
+    tot = part.double().sum(0).cpu().numpy()
+    Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).cuda()
+    ref = L.draw_metrics_torch(lg, Y)
+    assert tot[7] == B
+    for i, k in enumerate(FM.METRIC_NAMES[:-1]):
+        assert abs(tot[i] / B - ref[k]) < 2e-3, (k, tot[i] / B, ref[k])
+
+
+def test_fused_adam_matches_torch(data):
+    """K6 (mode 2: from a given gradient) == torch.optim.Adam, several steps."""
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    m = FusedSmallMLP(loss="softmax", seed=1, lr=3e-3)
+    p_ref = m.params.clone().requires_grad_()
+    opt = torch.optim.Adam([p_ref], lr=3e-3, betas=(0.9, 0.999), eps=1e-8)
+    mask = FM.pad_mask("cuda")
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(5):
+        g = torch.randn(FM.P_TOTAL, device="cuda", generator=gen) * mask
+        m.grad_io[:FM.P_TOTAL] = g
+        FM.adam_slab(None, 0, 1.0, m.params, m.m, m.v, m.hp, m.state, mode=2, grad_io=m.grad_io, img=m.img)
+        p_ref.grad = g.clone()
+        opt.step()
+    torch.cuda.synchronize()
+    assert int(m.state[0]) == 5 and int(m.state[1]) == 0
+    assert torch.allclose(m.params, p_ref.detach(), atol=1e-6, rtol=1e-5)
+
+
+def test_fused_training_learns_planted_structure():
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds = DrawSet.synthetic(n=400_000, seed=3, planted=0.9, calendar=False)
+    draws = torch.from_numpy(ds.numbers).cuda()
+    ns = ds.n_samples
+    margin = int(0.7 * ns)
+    m = FusedSmallMLP(loss="softmax", seed=0, lr=1e-2)
+    B = 65536
+    for it in range(60):
+        off = (it * B) % (margin - B)
+        m.step(draws, B, offset=off)
+    ev = m.evaluate(draws, ns - margin, offset=margin)
+    assert ev["acc"] > 0.93, ev
+    assert ev["acc"] > ev["trivial_acc"]
+
+
+def test_fused_deterministic(data):
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds, draws = data
+    outs = []
+    for _ in range(2):
+        m = FusedSmallMLP(loss="softmax", seed=9)
+        for it in range(3):
+            m.step(draws, 4000, offset=it * 100)
+        outs.append(m.params.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_fused_sample_index_path(data):
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds, draws = data
+    m = FusedSmallMLP(loss="softmax", seed=4)
+    idx = torch.arange(50, 2050, dtype=torch.int32, device="cuda")
+    l1, g1 = m.grads(draws, 2000, sidx=idx)
+    l2, g2 = m.grads(draws, 2000, offset=50)
+    assert abs(l1 - l2) < 1e-6
+    assert torch.allclose(g1, g2, atol=1e-7)
+    perm = torch.randperm(2000, device="cuda").to(torch.int32) + 50
+    l3, g3 = m.grads(draws, 2000, sidx=perm)
+    assert abs(l3 - l2) < 1e-4
+    assert torch.allclose(g3, g2, atol=1e-5, rtol=1e-3)
