@@ -28,6 +28,55 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+class _TorchBaseline:
+    """Same model/loss/optimizer in plain PyTorch (bf16 autocast GEMMs via hipBLASLt) — comparison only."""
+
+    def __init__(self, dev, a, draws, B, group):
+        from euromillioner_amd.models.mlp import DrawMLP
+        from euromillioner_amd.ops import fused_mlp as FM
+
+        self.FM, self.draws, self.B, self.group, self.loss_name = FM, draws, B, group, a.loss
+        self.net = DrawMLP((62, 128, 62), loss=a.loss, seed=a.seed, use_hip=False).to(dev)
+        self.opt = torch.optim.Adam(self.net.parameters(), lr=a.lr)
+        self.x = torch.empty(B, 64, dtype=torch.bfloat16, device=dev)
+        self.y = torch.empty(B, 64, dtype=torch.bfloat16, device=dev)
+        self.loss_out = torch.zeros(1, device=dev)
+        self.grad_io = torch.zeros(1, device=dev)
+
+    def step(self, off):
+        FM = self.FM
+        FM.onehot(self.draws, self.B, offset=off, which=0, out=self.x)
+        FM.onehot(self.draws, self.B, offset=off, which=1, out=self.y)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            z = self.net(self.x[:, :62])
+        loss = self.net.loss(z.float(), self.y[:, :62])
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.group is not None:
+            import torch.distributed as dist
+
+            for p in self.net.parameters():
+                dist.all_reduce(p.grad, group=self.group)
+                p.grad /= dist.get_world_size(self.group)
+        self.opt.step()
+        self.loss_out = loss.detach().reshape(1)
+        return self.loss_out
+
+    def broadcast_parameters(self):
+        pass
+
+    def evaluate(self, draws, n, offset):
+        from euromillioner_amd.data.draws import multi_hot  # noqa: F401
+        from euromillioner_amd.models.losses import draw_metrics_torch
+
+        b = min(n, 1 << 21)
+        x = self.FM.onehot(draws, b, offset=offset, which=0)
+        y = self.FM.onehot(draws, b, offset=offset, which=1)
+        with torch.no_grad():
+            z = self.net(x[:, :62].float())
+        return draw_metrics_torch(z, y.float(), self.loss_name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -41,6 +90,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="replay the step from a hipGraph (1 GPU)")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
+                    help="fused = our HIP kernels (headline); torch = plain PyTorch/hipBLASLt eager (comparison)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -62,19 +113,27 @@ def main():
 
     n_draws = a.draws_per_gpu
     nums, _ = generate_draws(n_draws, seed=a.seed + 1000 * rank, planted=a.planted, native=True)
-    draws = torch.from_numpy(nums).to(dev)
+    from euromillioner_amd.ops.fused_mlp import rows_to_masks
+
+    draws = rows_to_masks(torch.from_numpy(nums).to(dev))  # device feature masks (8 B / draw)
     n_samples = n_draws - 1
     margin = int(0.7 * n_samples)
     B = a.batch
     if margin < B:
         raise SystemExit("dataset too small for the batch")
 
-    model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group)
-    model.broadcast_parameters()
     n_off = max(1, (margin - B) // B)
+    if a.impl == "fused":
+        model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group)
+        model.broadcast_parameters()
 
-    def step(i):
-        return model.step(draws, B, offset=(i % n_off) * B)
+        def step(i):
+            return model.step(draws, B, offset=(i % n_off) * B)
+    else:
+        model = _TorchBaseline(dev, a, draws, B, group)
+
+        def step(i):
+            return model.step((i % n_off) * B)
 
     use_graph = bool(a.graph) and world == 1
     graph = None

@@ -11,6 +11,7 @@
 //   hits_main/star  |top-5 ∩ target main|, |top-2 ∩ target stars|
 //   exact           the whole 62-vector predicted exactly
 //   trivial         element-wise accuracy of the all-zero prediction (0.887 floor)
+// Samples are read as 64-bit feature masks (see em_rows_to_masks).
 // Partial sums per 256-sample block -> [nblocks][8] (summed on the host side in fp64).
 #include "common.h"
 
@@ -61,7 +62,7 @@ EM_DEVICE uint64_t topk_mask(const float* z, int lo, int hi) {
 }
 
 __global__ void __launch_bounds__(256)
-draw_metrics_kernel(const float* __restrict__ logits, int ld, const uint8_t* __restrict__ draws,
+draw_metrics_kernel(const float* __restrict__ logits, int ld, const uint64_t* __restrict__ masks,
                     const int32_t* __restrict__ sidx, int64_t B, int64_t offset, int loss_kind,
                     float* __restrict__ partials) {
   __shared__ float red[4][8];
@@ -69,7 +70,7 @@ draw_metrics_kernel(const float* __restrict__ logits, int ld, const uint8_t* __r
   float st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (s < B) {
     const int64_t idx = sidx ? (int64_t)sidx[s] : offset + s;
-    const uint64_t tm = draw_mask8(draws + (idx + 1) * 8);
+    const uint64_t tm = masks[idx + 1] & (MAIN_BITS | STAR_BITS);
     float z[64];
     const f32x4* zr = reinterpret_cast<const f32x4*>(logits + s * ld);
 #pragma unroll
@@ -126,8 +127,14 @@ draw_metrics_kernel(const float* __restrict__ logits, int ld, const uint8_t* __r
   }
 }
 
-// K14: draw rows -> multi-hot bf16 [B][64] (optional constant-1 bias feature at 62)
-__global__ void onehot_kernel(const uint8_t* __restrict__ draws, const int32_t* __restrict__ sidx, int64_t B,
+// draw rows [n][8] -> 64-bit feature masks (the on-device sample format of every draw kernel)
+__global__ void rows_to_masks_kernel(const uint8_t* __restrict__ rows, int64_t n, uint64_t* __restrict__ masks) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) masks[i] = draw_mask8(rows + i * 8);
+}
+
+// K14: feature masks -> multi-hot bf16 [B][64] (optional constant-1 bias feature at 62)
+__global__ void onehot_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int64_t B,
                               int64_t offset, int which, int with_bias, __bf16* __restrict__ out) {
   // one thread per (sample, 8-feature chunk): 16-byte stores
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -135,14 +142,14 @@ __global__ void onehot_kernel(const uint8_t* __restrict__ draws, const int32_t* 
   const int64_t s = e >> 3;
   const int c = (int)(e & 7);
   const int64_t idx = (sidx ? (int64_t)sidx[s] : offset + s) + which;
-  uint64_t m = draw_mask8(draws + idx * 8);
+  uint64_t m = masks[idx] & (MAIN_BITS | STAR_BITS);
   if (with_bias) m |= 1ull << 62;
   *reinterpret_cast<bf16x8*>(out + s * 64 + c * 8) = bits_to_bf16x8((uint32_t)(m >> (8 * c)) & 0xFFu);
 }
 
 }  // namespace
 
-EM_API int em_draw_metrics(const float* logits, int ld, const uint8_t* draws, const int32_t* sidx, int64_t B,
+EM_API int em_draw_metrics(const float* logits, int ld, const uint64_t* draws, const int32_t* sidx, int64_t B,
                            int64_t offset, int loss_kind, float* partials, hipStream_t stream) {
   if (!logits || !draws || !partials || ld < 64 || (ld & 3) || B < 0) return EM_ERR_ARG;
   if (B == 0) return 0;
@@ -153,7 +160,15 @@ EM_API int em_draw_metrics(const float* logits, int ld, const uint8_t* draws, co
   return 0;
 }
 
-EM_API int em_onehot_encode(const uint8_t* draws, const int32_t* sidx, int64_t B, int64_t offset, int which,
+EM_API int em_rows_to_masks(const uint8_t* rows, int64_t n, uint64_t* masks, hipStream_t stream) {
+  if (!rows || !masks || n < 0) return EM_ERR_ARG;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rows_to_masks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, rows, n, masks);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_onehot_encode(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset, int which,
                             int with_bias, void* out, hipStream_t stream) {
   if (!draws || !out || B < 0) return EM_ERR_ARG;
   if (B == 0) return 0;

@@ -1,4 +1,5 @@
 // K7 — fused persistent small-MLP training step for MI355X (gfx950).
+// EM_BUILD_FLAGS: -mllvm -amdgpu-mfma-vgpr-form=1
 //
 // Model (BASELINE.json config 2): multi-hot 62-wide draw
 // vector -> Linear(62,128) -> ReLU -> Linear(128,62) -> grouped softmax-CE
@@ -39,20 +40,18 @@ constexpr uint64_t MAIN_BITS = (1ull << 50) - 1;
 constexpr uint64_t STAR_BITS = ((1ull << 12) - 1) << 50;
 constexpr uint64_t BIAS_BIT = 1ull << 62;
 
-EM_DEVICE uint64_t draw_mask(uint2 row) {
-  uint64_t m = 0;
-  const uint32_t w0 = row.x, w1 = row.y;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    uint32_t n = (k < 4) ? ((w0 >> (8 * k)) & 0xFF) : (w1 & 0xFF);
-    m |= (n >= 1 && n <= 50) ? (1ull << (n - 1)) : 0ull;
-  }
-#pragma unroll
-  for (int k = 1; k < 3; ++k) {
-    uint32_t s = (w1 >> (8 * k)) & 0xFF;
-    m |= (s >= 1 && s <= 12) ? (1ull << (49 + s)) : 0ull;
-  }
-  return m;
+// Samples are read as precomputed 64-bit feature masks (bit n-1: main number n, bit 49+s: star s;
+// em_rows_to_masks builds them once per dataset), so the hot loop spends no VALU on decoding rows.
+
+// 256-entry LDS table: byte b -> 8 bf16 {0,1} (element j = bit j); an X fragment is one ds_read_b128
+constexpr int LUT_BYTES = 4096;
+EM_DEVICE void fill_lut(char* lut, int tid) {
+  if (tid < 256) *reinterpret_cast<bf16x8*>(lut + tid * 16) = bits_to_bf16x8((uint32_t)tid);
+}
+EM_DEVICE bf16x8 lut_frag(const char* lut, uint64_t m, int q, int h) {
+  const uint32_t w = q < 2 ? (uint32_t)m : (uint32_t)(m >> 32);
+  const uint32_t byte = (w >> (16 * (q & 1) + 8 * h)) & 0xFFu;
+  return *reinterpret_cast<const bf16x8*>(lut + byte * 16);
 }
 
 // byte offsets into the LDS weight images (see em_adam_pack for the writer)
@@ -71,7 +70,7 @@ template <int LOSS>  // 0 = grouped softmax CE (main 50 / stars 12), 1 = sigmoid
 EM_DEVICE void loss_and_grad(const f32x16 (&z)[2], int h, uint64_t tmask, bool valid, float (&dz)[2][16],
                              float& loss_acc) {
   // per-slot class: 0 main, 1 star, 2 pad ; target bit per slot
-  const uint32_t tm[2] = {(uint32_t)tmask >> (4 * h), (uint32_t)(tmask >> 32) >> (4 * h)};
+  const uint32_t tm[2] = {(uint32_t)tmask >> (4 * h), (uint32_t)(tmask >> 32) >> (4 * h)};  // slot bits
   auto cls = [&](int u, int i) -> int {
     const int o = 32 * u + oo0(i) + 4 * h;
     return o < 50 ? 0 : (o < 62 ? 1 : 2);
@@ -142,49 +141,119 @@ EM_DEVICE void loss_and_grad(const f32x16 (&z)[2], int h, uint64_t tmask, bool v
   }
 }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// NOTE (ROCm 7.2 clang): `__builtin_bit_cast(s16x2, v[k])` on an element of an ext_vector inside an
+// unrolled loop is miscompiled (every k reads element 0).  These memcpy-based casts compile to the
+// expected one v_pk_* per dword; tests/test_fused_mlp_gpu.py checks logits and gradients end to end.
+EM_DEVICE s16x2 as_s16x2(uint32_t x) {
+  s16x2 r;
+  __builtin_memcpy(&r, &x, 4);
+  return r;
+}
+EM_DEVICE uint32_t as_u32(s16x2 x) {
+  uint32_t r;
+  __builtin_memcpy(&r, &x, 4);
+  return r;
+}
+
+// relu on packed bf16 pairs: for sign-magnitude bf16, max(x, 0) as int16 == relu (one v_pk_max_i16 per 2 values)
 EM_DEVICE bf16x8 relu_pack(const f32x16& a, int q) {
-  return pack8(fmaxf(a[8 * q + 0], 0.f), fmaxf(a[8 * q + 1], 0.f), fmaxf(a[8 * q + 2], 0.f), fmaxf(a[8 * q + 3], 0.f),
-               fmaxf(a[8 * q + 4], 0.f), fmaxf(a[8 * q + 5], 0.f), fmaxf(a[8 * q + 6], 0.f), fmaxf(a[8 * q + 7], 0.f));
+  const bf16x8 p = pack8(a[8 * q + 0], a[8 * q + 1], a[8 * q + 2], a[8 * q + 3], a[8 * q + 4], a[8 * q + 5],
+                         a[8 * q + 6], a[8 * q + 7]);
+  u32x4 d = __builtin_bit_cast(u32x4, p);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = d[k];
+    d[k] = as_u32(__builtin_elementwise_max(as_s16x2(x), (s16x2){0, 0}));
+  }
+  return __builtin_bit_cast(bf16x8, d);
+}
+
+// dZ1 = dH * (Z1 > 0) on packed bf16: the relu'd H fragment is 0 exactly where Z1 <= 0
+EM_DEVICE bf16x8 mask_by(const bf16x8 hfrag, const f32x16& a, int q) {
+  const bf16x8 p = pack8(a[8 * q + 0], a[8 * q + 1], a[8 * q + 2], a[8 * q + 3], a[8 * q + 4], a[8 * q + 5],
+                         a[8 * q + 6], a[8 * q + 7]);
+  u32x4 d = __builtin_bit_cast(u32x4, p);
+  const u32x4 hh = __builtin_bit_cast(u32x4, hfrag);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = hh[k];
+    const s16x2 m = ((s16x2){0, 0} - as_s16x2(x)) >> (s16x2){15, 15};
+    d[k] &= as_u32(m);
+  }
+  return __builtin_bit_cast(bf16x8, d);
+}
+
+// wave-private [32 samples][128 hid] bf16 image, 256-B rows, chunk ^= row&15
+EM_DEVICE uint32_t himg_off(uint32_t base, int row, int col) {
+  return base + row * 256 + ((((col >> 3) ^ (row & 15))) << 4) + (col & 7) * 2;
+}
+
+// A "samples as K" fragment (rows = lane column, k = samples in accumulator-perm order) from a
+// [32 samples][C cols] image via ds_read_b64_tr_b16 (two 4-row blocks per fragment).
+template <int HIMG>
+EM_DEVICE bf16x8 tr_frag(const char* smem, uint32_t base, int colbase, int q, int h, int q4, int p4, int g1) {
+  const int col = colbase + 16 * g1 + 4 * p4;
+  const int r0 = 16 * q + 4 * h + q4;
+  if (HIMG) return cat_tr(lds_tr16(smem, himg_off(base, r0, col)), lds_tr16(smem, himg_off(base, r0 + 8, col)));
+  return cat_tr(lds_tr16(smem, img_off(base, r0, col)), lds_tr16(smem, img_off(base, r0 + 8, col)));
 }
 
 // LDS layout of the train kernel (bytes):
-//   [0, IMG_BYTES)                 weight images + b2 (copied from wimg)
-//   per wave w at IMG_BYTES + w*WREG:  X image 4 KB | D2 image 4 KB | FRAG 8 KB
-// Wave pairs (0,1) and (2,3) split the weight-gradient products: the even wave
-// accumulates dW2 (A = H fragments) and the odd wave dW1ᵀ (A = dZ1 fragments)
-// for BOTH tiles of the pair; each hands the other the fragments it does not
-// keep through FRAG.  128 accumulator registers per wave instead of 256.
+//   [0, IMG_BYTES)                      weight images + b2 (copied from wimg)
+//   [IMG_BYTES, +LUT_BYTES)             byte -> bf16x8 table for X fragments
+//   per wave w at WBASE + w*WREG:       X image 4 KB | D2 image 4 KB | H image 8 KB
+// Every wave is independent inside the loop (no barrier): it keeps the FULL dW2 and dW1ᵀ
+// accumulators (2 x 8 tiles x 16 = 256 AGPRs, pinned with inline-asm MFMAs) while all
+// transient MFMAs are VGPR-form builtins.  The images are wave-private transposes:
+//   X  [32 samples][64 feat]  -> B operand of dW1ᵀ = dZ1ᵀ·X   (tr reads)
+//   D2 [32 samples][64 out]   -> B operand of dW2  = Hᵀ·dZ2   (tr reads)
+//   H  [32 samples][128 hid]  -> A operand of dW2 and the relu mask of dZ1 (tr reads),
+//                                instead of recomputing Z1 = X·W1 in the other orientation.
 constexpr int WREG = 16384;
-constexpr int TRAIN_LDS = IMG_BYTES + 4 * WREG + 4 * 64 * 4 + 64;
+constexpr int WBASE = IMG_BYTES + LUT_BYTES;
+constexpr int RED_BYTES = 2 * 65536;                       // epilogue: two 64 KB fp32 dW images
+constexpr int LOOP_LDS = WBASE + 4 * WREG;
+constexpr int TRAIN_LDS = (LOOP_LDS > RED_BYTES ? LOOP_LDS : RED_BYTES) + 4 * 64 * 4 + 64;
+
+// dW accumulation MFMA with the accumulator pinned in AGPRs ("+a").  Every other MFMA is a
+// VGPR-form builtin (file built with -mllvm -amdgpu-mfma-vgpr-form=1), so no AGPR<->VGPR copies
+// are needed for results the VALU consumes.  The leading s_nop 1 covers a VALU write of an A/B
+// operand right before the asm (hipcc does not pad hazards into inline asm).
+EM_DEVICE void mfma_acc_agpr(f32x16& d, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+}
 
 template <int LOSS>
 __global__ void __launch_bounds__(256, 1)
-mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restrict__ sidx, int64_t B,
-                       int64_t offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+mlp_fused_train_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                       int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                        float* __restrict__ loss_slabs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const bool even = (wave & 1) == 0;
 
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
     u32x4* dst = reinterpret_cast<u32x4*>(smem);
     for (int i = tid; i < IMG_BYTES / 16; i += 256) dst[i] = src[i];
   }
+  const char* lut = smem + IMG_BYTES;
+  fill_lut(smem + IMG_BYTES, tid);
   __syncthreads();
 
-  const uint32_t XB = IMG_BYTES + wave * WREG, DB = XB + 4096, FB = XB + 8192;
-  const uint32_t pXB = IMG_BYTES + (wave ^ 1) * WREG, pDB = pXB + 4096, pFB = pXB + 8192;
-  // the B-operand image this wave's dW product reads: D2 (even, dW2) or X (odd, dW1ᵀ)
-  const uint32_t myB = even ? DB : XB, parB = even ? pDB : pXB;
+  const uint32_t XB = WBASE + wave * WREG, DB = XB + 4096, HB = XB + 8192;
 
-  f32x16 dacc[4][2];
+  f32x16 dW2[4][2], dW1T[4][2];  // AGPR-resident for the whole launch
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) dacc[t][u] = f32x16{};
+    for (int u = 0; u < 2; ++u) {
+      dW2[t][u] = f32x16{};
+      dW1T[t][u] = f32x16{};
+    }
   float db2[2][16];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -192,43 +261,55 @@ mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restr
     for (int i = 0; i < 16; ++i) db2[u][i] = 0.f;
   float loss_acc = 0.f;
 
-  const int64_t ngroups = (B + 127) / 128;
+  const int ntiles = (B + 31) / 32;
+  const int nwaves = gridDim.x * 4;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
 
-  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int64_t s = grp * 128 + wave * 32 + r;
-    const bool valid = s < B;
-    uint64_t imask = 0, tmask = 0;
-    if (valid) {
-      const int64_t idx = sidx ? (int64_t)sidx[s] : (offset + s);
-      const uint2 rin = *reinterpret_cast<const uint2*>(draws + idx * 8);
-      const uint2 rtg = *reinterpret_cast<const uint2*>(draws + (idx + 1) * 8);
-      imask = draw_mask(rin) | BIAS_BIT;
-      tmask = draw_mask(rtg);
+  // software prefetch of the next tile's feature masks (input draw, target draw)
+  auto fetch = [&](int tile, uint64_t& mi, uint64_t& mt) {
+    const int s = tile * 32 + r;
+    mi = 0;
+    mt = 0;
+    if (tile < ntiles && s < B) {
+      const int idx = sidx ? sidx[s] : (offset + s);
+      mi = masks[idx];
+      mt = masks[idx + 1];
     }
+  };
+  const int first = blockIdx.x * 4 + wave;
+  uint64_t nin, ntg;
+  fetch(first, nin, ntg);
+
+  for (int tile = first; tile < ntiles; tile += nwaves) {
+    const int s = tile * 32 + r;
+    const bool valid = s < B;
+    const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
+    const uint64_t tmask = valid ? ntg : 0ull;
+    fetch(tile + nwaves, nin, ntg);
+
     bf16x8 xf[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xf[q] = bits_to_bf16x8((uint32_t)(imask >> (16 * q + 8 * h)) & 0xFFu);
+    for (int q = 0; q < 4; ++q) xf[q] = lut_frag(lut, imask, q, h);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<bf16x8*>(smem + XB + r * 128 + ((((2 * q + h) ^ (r & 7))) << 4)) = xf[q];
 
-    // ---- F1 (Z1ᵀ = W1ᵀ·Xᵀ) and R1 (Z1 = X·W1) per hidden tile: shared LDS fragments ----
-    bf16x8 hT[4][2], hR[4][2];
+    // ---- F1: Z1ᵀ = W1ᵀ·Xᵀ -> relu -> Hᵀ fragments (B of F2) + H image (samples x hid) ----
+    bf16x8 hT[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      bf16x8 w[4];
+      f32x16 a1 = f32x16{};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = lds_frag(smem, w1t_off(32 * t + r, 2 * q + h));
-      f32x16 a1 = f32x16{}, aR = f32x16{};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a1 = mfma32(w[q], xf[q], a1);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) aR = mfma32(xf[q], w[q], aR);
+      for (int q = 0; q < 4; ++q) a1 = mfma32(lds_frag(smem, w1t_off(32 * t + r, 2 * q + h)), xf[q], a1);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         hT[t][q] = relu_pack(a1, q);
-        hR[t][q] = relu_pack(aR, q);
+        // element j <-> hid 32t + 16q + 8(j>>2) + 4h + (j&3): two 8-byte pieces per fragment
+        const u32x4 d = __builtin_bit_cast(u32x4, hT[t][q]);
+        *reinterpret_cast<u32x2*>(smem + HB + r * 256 + ((((4 * t + 2 * q) ^ (r & 15))) << 4) + h * 8) =
+            u32x2{d[0], d[1]};
+        *reinterpret_cast<u32x2*>(smem + HB + r * 256 + ((((4 * t + 2 * q + 1) ^ (r & 15))) << 4) + h * 8) =
+            u32x2{d[2], d[3]};
       }
     }
 
@@ -266,14 +347,15 @@ mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restr
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const bf16x8 f = dzf[u][g >> 1];
-        bf16x4 v;
-        v[0] = f[4 * (g & 1) + 0]; v[1] = f[4 * (g & 1) + 1]; v[2] = f[4 * (g & 1) + 2]; v[3] = f[4 * (g & 1) + 3];
-        *reinterpret_cast<bf16x4*>(smem + DB + r * 128 + ((((4 * u + g) ^ (r & 7))) << 4) + h * 8) = v;
+        const u32x4 f = __builtin_bit_cast(u32x4, dzf[u][g >> 1]);
+        *reinterpret_cast<u32x2*>(smem + DB + r * 128 + ((((4 * u + g) ^ (r & 7))) << 4) + h * 8) =
+            u32x2{f[2 * (g & 1)], f[2 * (g & 1) + 1]};
       }
 
-    // ---- B1: dH = dZ2·W2ᵀ, dZ1 = dH * (Z1 > 0) ----
-    bf16x8 keep[4][2];
+    wave_lds_sync();  // X / H / D2 images complete (written by all lanes of this wave)
+
+    // ---- B1: dH = dZ2·W2ᵀ ; dZ1 = dH * (Z1 > 0) with H fragments from the H image ----
+    bf16x8 hR[4][2], dz1[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x16 aD = f32x16{};
@@ -284,36 +366,28 @@ mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restr
           aD = mfma32(dzf[u][q], lds_frag(smem, w2q_off(32 * t + r, (2 * u + q) * 2 + h)), aD);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        bf16x8 d;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = (__bf16)((float)hR[t][q][j] > 0.f ? aD[8 * q + j] : 0.f);
-        // even keeps H (dW2), hands dZ1 to the odd partner; odd keeps dZ1 (dW1ᵀ), hands H
-        const bf16x8 give = even ? d : hR[t][q];
-        keep[t][q] = even ? hR[t][q] : d;
-        *reinterpret_cast<bf16x8*>(smem + FB + ((t * 2 + q) * 64 + lane) * 16) = give;
+        hR[t][q] = tr_frag<1>(smem, HB, 32 * t, q, h, q4, p4, g1);
+        dz1[t][q] = mask_by(hR[t][q], aD, q);
       }
     }
 
-    __syncthreads();  // partner's X / D2 / FRAG images are complete
-
-    // ---- dW (K = 32 samples per tile, own tile + partner tile) ----
+    // ---- dW2 += Hᵀ·dZ2, dW1ᵀ += dZ1ᵀ·X   (K = the tile's 32 samples) ----
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int col = 32 * u + 16 * g1 + 4 * p4;
-        const int r0 = 16 * q + 4 * h + q4;
-        const bf16x8 bo = cat_tr(lds_tr16(smem, img_off(myB, r0, col)), lds_tr16(smem, img_off(myB, r0 + 8, col)));
-        const bf16x8 bp = cat_tr(lds_tr16(smem, img_off(parB, r0, col)), lds_tr16(smem, img_off(parB, r0 + 8, col)));
+        const bf16x8 bd = tr_frag<0>(smem, DB, 32 * u, q, h, q4, p4, g1);
+        const bf16x8 bx = tr_frag<0>(smem, XB, 32 * u, q, h, q4, p4, g1);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          dacc[t][u] = mfma32(keep[t][q], bo, dacc[t][u]);
-          dacc[t][u] = mfma32(lds_frag(smem, pFB + ((t * 2 + q) * 64 + lane) * 16), bp, dacc[t][u]);
+          mfma_acc_agpr(dW2[t][u], hR[t][q], bd);
+          mfma_acc_agpr(dW1T[t][u], dz1[t][q], bx);
         }
       }
 
-    __syncthreads();  // images are overwritten next round
+    wave_lds_sync();  // images are overwritten by the next tile
   }
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // MFMA (asm, AGPR D) -> v_accvgpr_read hazard
 
   // ================= epilogue: per-workgroup reduction =================
 #pragma unroll
@@ -326,10 +400,11 @@ mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restr
       db2[u][i] = v;
     }
   const float lsum = wave_sum(loss_acc);
-  float* RED = reinterpret_cast<float*>(smem);  // 2 x 32 KB (waves 0 and 1 publish)
-  float* DB2S = reinterpret_cast<float*>(smem + IMG_BYTES + 4 * WREG);
+  __syncthreads();  // all waves are done with the loop's LDS
+  float* RED0 = reinterpret_cast<float*>(smem);
+  float* RED1 = reinterpret_cast<float*>(smem + 65536);
+  float* DB2S = reinterpret_cast<float*>(smem + (TRAIN_LDS - 4 * 64 * 4 - 64));
   float* LOSSS = DB2S + 4 * 64;
-  // (the loop ended with a barrier: LDS images are free)
   if (r == 0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -337,37 +412,38 @@ mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restr
       for (int i = 0; i < 16; ++i) DB2S[wave * 64 + 32 * u + oo0(i) + 4 * h] = db2[u][i];
   }
   if (lane == 0) LOSSS[wave] = lsum;
-  if (wave < 2) {
-    float* R = RED + wave * 8192;
+  // tile T: 0..7 -> dW2[T>>1][T&1], 8..15 -> dW1ᵀ[(T-8)>>1][(T-8)&1]; layout [T][g][lane][4]
+  auto region_io = [&](float* R, bool add) {
 #pragma unroll
-    for (int T = 0; T < 8; ++T)
+    for (int T = 0; T < 16; ++T) {
+      const f32x16& acc = (T < 8) ? dW2[T >> 1][T & 1] : dW1T[(T - 8) >> 1][(T - 8) & 1];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x16& acc = dacc[T >> 1][T & 1];
-        *reinterpret_cast<f32x4*>(R + ((T * 4 + g) * 64 + lane) * 4) =
-            f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+        f32x4* p = reinterpret_cast<f32x4*>(R + ((T * 4 + g) * 64 + lane) * 4);
+        f32x4 v = {acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+        if (add) v += *p;
+        *p = v;
       }
-  }
+    }
+  };
+  if (wave == 0) region_io(RED0, false);
+  if (wave == 1) region_io(RED1, false);
   __syncthreads();
+  if (wave == 2) region_io(RED0, true);
+  if (wave == 3) region_io(RED1, true);
+  __syncthreads();
+
   float* slab = slabs + (size_t)blockIdx.x * P_TOTAL;
-  if (wave >= 2) {
-    const float* R = RED + (wave - 2) * 8192;
+  for (int e = tid; e < 16 * 4 * 64; e += 256) {
+    const int T = e >> 8, g = (e >> 6) & 3, l = e & 63, hh = l >> 5, rr = l & 31;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED0 + e * 4) + *reinterpret_cast<const f32x4*>(RED1 + e * 4);
+    const int c0 = 32 * ((T & 7) >> 1) + 8 * g + 4 * hh;  // hidden rows c0..c0+3
+    const int col = 32 * (T & 1) + rr;
+    if (T < 8) {  // dW2[c][o]
 #pragma unroll
-    for (int T = 0; T < 8; ++T) {
-      const int t = T >> 1, u = T & 1;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x16& acc = dacc[t][u];
-        const f32x4 v = *reinterpret_cast<const f32x4*>(R + ((T * 4 + g) * 64 + lane) * 4) +
-                        f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
-        const int c0 = 32 * t + 8 * g + 4 * h;  // hidden rows c0..c0+3
-        if (wave == 2) {  // dW2[c][o], o = 32u + r
-#pragma unroll
-          for (int k = 0; k < 4; ++k) slab[P_W2 + (c0 + k) * OUT + 32 * u + r] = v[k];
-        } else {  // dW1ᵀ tile -> W1[f][c], f = 32u + r
-          *reinterpret_cast<f32x4*>(slab + P_W1 + (32 * u + r) * HID + c0) = v;
-        }
-      }
+      for (int k = 0; k < 4; ++k) slab[P_W2 + (c0 + k) * OUT + col] = v[k];
+    } else {  // dW1ᵀ tile -> W1[f][c]
+      *reinterpret_cast<f32x4*>(slab + P_W1 + col * HID + c0) = v;
     }
   }
   if (tid < 64) slab[P_B2 + tid] = DB2S[tid] + DB2S[64 + tid] + DB2S[128 + tid] + DB2S[192 + tid];
@@ -376,8 +452,8 @@ mlp_fused_train_kernel(const uint8_t* __restrict__ draws, const int32_t* __restr
 
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
 __global__ void __launch_bounds__(256)
-mlp_fused_forward_kernel(const uint8_t* __restrict__ draws, const int32_t* __restrict__ sidx, int64_t B,
-                         int64_t offset, const uint8_t* __restrict__ wimg, float* __restrict__ logits) {
+mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                         int offset, const uint8_t* __restrict__ wimg, float* __restrict__ logits) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -386,20 +462,18 @@ mlp_fused_forward_kernel(const uint8_t* __restrict__ draws, const int32_t* __res
     u32x4* dst = reinterpret_cast<u32x4*>(smem);
     for (int i = tid; i < IMG_BYTES / 16; i += 256) dst[i] = src[i];
   }
+  const char* lut = smem + IMG_BYTES;
+  fill_lut(smem + IMG_BYTES, tid);
   __syncthreads();
-  const int64_t ntiles = (B + 31) / 32;
+  const int ntiles = (B + 31) / 32;
   const int nwaves = gridDim.x * 4;
-  for (int64_t tile = blockIdx.x * 4 + wave; tile < ntiles; tile += nwaves) {
-    const int64_t s = tile * 32 + r;
+  for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += nwaves) {
+    const int s = tile * 32 + r;
     const bool valid = s < B;
-    uint64_t imask = 0;
-    if (valid) {
-      const int64_t idx = sidx ? (int64_t)sidx[s] : (offset + s);
-      imask = draw_mask(*reinterpret_cast<const uint2*>(draws + idx * 8)) | BIAS_BIT;
-    }
+    const uint64_t imask = valid ? (masks[sidx ? sidx[s] : (offset + s)] | BIAS_BIT) : 0ull;
     bf16x8 xf[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xf[q] = bits_to_bf16x8((uint32_t)(imask >> (16 * q + 8 * h)) & 0xFFu);
+    for (int q = 0; q < 4; ++q) xf[q] = lut_frag(lut, imask, q, h);
     f32x16 a1[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -432,7 +506,7 @@ mlp_fused_forward_kernel(const uint8_t* __restrict__ draws, const int32_t* __res
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 v = {z[4 * g + 0], z[4 * g + 1], z[4 * g + 2], z[4 * g + 3]};
-          *reinterpret_cast<f32x4*>(logits + s * OUT + 32 * u + 8 * g + 4 * h) = v;
+          *reinterpret_cast<f32x4*>(logits + (int64_t)s * OUT + 32 * u + 8 * g + 4 * h) = v;
         }
       }
     }
@@ -445,11 +519,12 @@ EM_API int em_mlp_fused_param_count() { return P_TOTAL; }
 EM_API int em_mlp_fused_image_bytes() { return IMG_BYTES; }
 EM_API int em_mlp_fused_lds_bytes() { return TRAIN_LDS; }
 
-// draws: [ndraws, 8] uint8; sample s = (draws[i], draws[i+1]) with i = sidx ? sidx[s] : offset+s
-EM_API int em_mlp_fused_train(const uint8_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
+// masks: [ndraws] uint64 feature masks; sample s = (masks[i], masks[i+1]) with i = sidx ? sidx[s] : offset+s
+EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
                               const void* wimg, float* slabs, float* loss_slabs, int nslab, int loss_kind,
                               hipStream_t stream) {
-  if (!draws || !wimg || !slabs || !loss_slabs || nslab <= 0 || B < 0) return EM_ERR_ARG;
+  if (!draws || !wimg || !slabs || !loss_slabs || nslab <= 0 || B < 0 || B + offset + 1 > (int64_t)INT32_MAX)
+    return EM_ERR_ARG;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -459,19 +534,20 @@ EM_API int em_mlp_fused_train(const uint8_t* draws, const int32_t* sidx, int64_t
     attr_set = true;
   }
   if (loss_kind == 0)
-    hipLaunchKernelGGL(mlp_fused_train_kernel<0>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, B, offset,
+    hipLaunchKernelGGL(mlp_fused_train_kernel<0>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, (int)B, (int)offset,
                        (const uint8_t*)wimg, slabs, loss_slabs);
   else
-    hipLaunchKernelGGL(mlp_fused_train_kernel<1>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, B, offset,
+    hipLaunchKernelGGL(mlp_fused_train_kernel<1>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, (int)B, (int)offset,
                        (const uint8_t*)wimg, slabs, loss_slabs);
   EM_CHECK_LAUNCH();
   return 0;
 }
 
-EM_API int em_mlp_fused_forward(const uint8_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
+EM_API int em_mlp_fused_forward(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
                                 const void* wimg, float* logits, int nblocks, hipStream_t stream) {
-  if (!draws || !wimg || !logits || nblocks <= 0) return EM_ERR_ARG;
-  hipLaunchKernelGGL(mlp_fused_forward_kernel, dim3(nblocks), dim3(256), IMG_BYTES, stream, draws, sidx, B, offset,
+  if (!draws || !wimg || !logits || nblocks <= 0 || B + offset > (int64_t)INT32_MAX) return EM_ERR_ARG;
+  hipLaunchKernelGGL(mlp_fused_forward_kernel, dim3(nblocks), dim3(256), IMG_BYTES + LUT_BYTES, stream, draws, sidx,
+                     (int)B, (int)offset,
                      (const uint8_t*)wimg, logits);
   EM_CHECK_LAUNCH();
   return 0;

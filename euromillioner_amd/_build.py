@@ -79,8 +79,20 @@ def _needs_build(src: str, obj: str, headers) -> bool:
     return any(os.path.getmtime(h) > t for h in headers)
 
 
+def _file_flags(src: str) -> list[str]:
+    """Per-file flags from a ``// EM_BUILD_FLAGS: ...`` line in the first 40 lines."""
+    out: list[str] = []
+    with open(src, encoding="utf-8", errors="replace") as f:
+        for i, line in enumerate(f):
+            if i > 40:
+                break
+            if "EM_BUILD_FLAGS:" in line:
+                out += line.split("EM_BUILD_FLAGS:", 1)[1].split()
+    return out
+
+
 def _compile(src: str, obj: str, extra=()):
-    cmd = [_hipcc()] + COMMON_FLAGS + list(extra) + ["-I", CSRC]
+    cmd = [_hipcc()] + COMMON_FLAGS + _file_flags(src) + list(extra) + ["-I", CSRC]
     if src.endswith(".hip"):
         cmd += ["-x", "hip"]
     cmd += ["-c", src, "-o", obj]
@@ -161,7 +173,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, e
 def resource_usage(src_name: str) -> str:
     """Compile one source with ``-Rpass-analysis=kernel-resource-usage`` (VGPR/AGPR/LDS report)."""
     src = os.path.join(CSRC, src_name)
-    cmd = [_hipcc()] + COMMON_FLAGS + ["-I", CSRC, "-x", "hip", "-Rpass-analysis=kernel-resource-usage",
+    cmd = [_hipcc()] + COMMON_FLAGS + _file_flags(src) + ["-I", CSRC, "-x", "hip", "-Rpass-analysis=kernel-resource-usage",
                                        "--cuda-device-only", "-c", src, "-o", "/dev/null"]
     p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     return p.stdout

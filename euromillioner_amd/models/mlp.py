@@ -139,9 +139,21 @@ class FusedSmallMLP:
 
         return dist.get_world_size(self.group)
 
+    @staticmethod
+    def prepare(draws) -> torch.Tensor:
+        """Draw rows (numpy [N,8] or GPU uint8 [N,8]) -> device feature masks consumed by every method."""
+        from ..ops import fused_mlp as FM
+
+        if isinstance(draws, torch.Tensor):
+            if draws.dtype == torch.int64 and draws.dim() == 1:
+                return draws
+            return FM.rows_to_masks(draws.cuda() if not draws.is_cuda else draws)
+        return FM.masks_from_numpy(draws, "cuda")
+
     def step(self, draws: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None,
              global_batch: int | None = None) -> torch.Tensor:
-        """One optimizer step over B local samples; returns the (global) mean loss as a device tensor."""
+        """One optimizer step over B local samples (``draws`` = feature masks from :meth:`prepare`);
+        returns the (global) mean loss as a device tensor."""
         FM = self.FM
         nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
                                   offset=offset, sidx=sidx, check=not self._checked)

@@ -45,6 +45,7 @@ _SIGS = {
                             _c_void_p]),
     "em_draw_metrics": (_i32, [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p]),
     "em_onehot_encode": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p]),
+    "em_rows_to_masks": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p]),
 }
 
 

@@ -65,11 +65,33 @@ def pack(params: torch.Tensor, img: torch.Tensor) -> None:
     N.call("em_mlp_fused_pack", params.data_ptr(), img.data_ptr(), N.stream_handle(params.device))
 
 
+def rows_to_masks(rows: torch.Tensor) -> torch.Tensor:
+    """[N, 8] uint8 draw rows (GPU) -> [N] int64 (bit pattern = uint64 feature mask).
+
+    Every draw kernel reads samples in this format: bit n-1 = main number n,
+    bit 49+s = star s (the bias feature 62 is added in-kernel)."""
+    N.check_cuda(rows, "rows", torch.uint8)
+    if rows.dim() != 2 or rows.shape[1] != 8:
+        raise ValueError("rows must be [N, 8] uint8")
+    out = torch.empty(rows.shape[0], dtype=torch.int64, device=rows.device)
+    N.call("em_rows_to_masks", rows.data_ptr(), rows.shape[0], out.data_ptr(), N.stream_handle(rows.device))
+    return out
+
+
+def masks_from_numpy(numbers, device) -> torch.Tensor:
+    """Host path: numpy [N, 8] rows -> device int64 masks (via data.draws.mask_bits)."""
+    from ..data.draws import mask_bits
+
+    return torch.from_numpy(mask_bits(numbers).view("int64")).to(device)
+
+
 def _check_draws(draws: torch.Tensor, sidx: torch.Tensor | None, B: int, offset: int, need_next: bool = True):
-    N.check_cuda(draws, "draws", torch.uint8)
-    if draws.dim() != 2 or draws.shape[1] != 8:
-        raise ValueError("draws must be [N, 8] uint8")
+    N.check_cuda(draws, "masks", torch.int64)
+    if draws.dim() != 1:
+        raise ValueError("masks must be a 1-D int64 tensor of feature masks (see rows_to_masks)")
     n = draws.shape[0]
+    if n >= 2**31 - 1:
+        raise ValueError("at most 2^31-2 draws per device")
     if sidx is not None:
         N.check_cuda(sidx, "sample_idx", torch.int32)
         if sidx.numel() < B:

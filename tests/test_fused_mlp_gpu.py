@@ -26,8 +26,10 @@ def _ref_grads(sd, ds_numbers, offset, B, loss, bf16=True):
 
 @pytest.fixture(scope="module")
 def data():
+    from euromillioner_amd.ops.fused_mlp import rows_to_masks
+
     ds = DrawSet.synthetic(n=6000, seed=11, planted=0.6, calendar=False)
-    return ds, torch.from_numpy(ds.numbers).cuda()
+    return ds, rows_to_masks(torch.from_numpy(ds.numbers).cuda())
 
 
 @pytest.mark.parametrize("loss", ["softmax", "bce"])
@@ -92,7 +94,7 @@ def test_fused_training_learns_planted_structure():
     from euromillioner_amd.models.mlp import FusedSmallMLP
 
     ds = DrawSet.synthetic(n=400_000, seed=3, planted=0.9, calendar=False)
-    draws = torch.from_numpy(ds.numbers).cuda()
+    draws = FusedSmallMLP.prepare(ds.numbers)
     ns = ds.n_samples
     margin = int(0.7 * ns)
     m = FusedSmallMLP(loss="softmax", seed=0, lr=1e-2)
@@ -103,6 +105,23 @@ def test_fused_training_learns_planted_structure():
     ev = m.evaluate(draws, ns - margin, offset=margin)
     assert ev["acc"] > 0.93, ev
     assert ev["acc"] > ev["trivial_acc"]
+
+
+def test_rows_to_masks_matches_host(data):
+    from euromillioner_amd.data.draws import mask_bits
+
+    ds, masks = data
+    host = torch.from_numpy(mask_bits(ds.numbers).view("int64"))
+    assert torch.equal(masks.cpu(), host)
+
+
+def test_onehot_kernel(data):
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    ds, masks = data
+    oh = FM.onehot(masks, 500, offset=10, which=1, bias=True).float().cpu()
+    ref = multi_hot(ds.numbers[11:511], width=64, bias=True)
+    assert torch.equal(oh, torch.from_numpy(ref))
 
 
 def test_fused_deterministic(data):
