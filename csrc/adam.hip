@@ -68,30 +68,39 @@ EM_DEVICE void adam_end(int* state, int t) {
   }
 }
 
-__global__ void __launch_bounds__(256)
-adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, float grad_scale, float* __restrict__ params,
+// 16 threads per parameter (slab-split, all loads issued up front), 64 parameters per 1024-thread block.
+// The slab reduction is latency-bound (16 MB spread over 256 slabs): every thread keeps its 16
+// loads in flight at once.
+constexpr int AS_P = 64, AS_G = 16;
+__global__ void __launch_bounds__(AS_P * AS_G)
+adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, float grad_scale, float* __restrict__ params,
                  float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io, const float* __restrict__ hp,
                  int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img, const float* __restrict__ loss_slabs,
                  float* __restrict__ loss_out, float loss_scale) {
   const int tstep = (mode != 1) ? adam_begin(state) : 0;
   // hp = {lr, beta1, beta2, eps, weight_decay}; state = {step, ticket} (device ints, graph-replay safe)
-  __shared__ float part[4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int p = blockIdx.x * 64 + tx;
+  __shared__ float part[AS_G][AS_P];
+  const int tx = threadIdx.x % AS_P, ty = threadIdx.x / AS_P;
+  const int p = blockIdx.x * AS_P + tx;
   float g = 0.f;
   if (mode != 2) {
-    float acc0 = 0.f, acc1 = 0.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (p < P) {
       int sl = ty;
-      for (; sl + 4 < nslab; sl += 8) {
-        acc0 += slabs[(size_t)sl * P + p];
-        acc1 += slabs[(size_t)(sl + 4) * P + p];
+      for (; sl + 3 * AS_G < nslab; sl += 4 * AS_G) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += slabs[(size_t)(sl + k * AS_G) * stride + p];
       }
-      if (sl < nslab) acc0 += slabs[(size_t)sl * P + p];
+      for (; sl < nslab; sl += AS_G) acc[0] += slabs[(size_t)sl * stride + p];
     }
-    part[ty][tx] = acc0 + acc1;
+    part[ty][tx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     __syncthreads();
-    g = ((part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx])) * grad_scale;
+    if (ty == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < AS_G; ++k) t += part[k][tx];
+      g = t * grad_scale;
+    }
   } else if (p < P) {
     g = grad_io[p];
   }
@@ -182,14 +191,14 @@ adam_flat_kernel(float* __restrict__ params, const float* __restrict__ grad, flo
 
 }  // namespace
 
-EM_API int em_adam_slab(const float* slabs, int nslab, int P, float grad_scale, float* params, float* m, float* v,
+EM_API int em_adam_slab(const float* slabs, int nslab, int P, int stride, float grad_scale, float* params, float* m, float* v,
                         float* grad_io, const float* hp, int* state, int mode, void* mlp_img, const float* loss_slabs,
                         float* loss_out, float loss_scale, hipStream_t stream) {
-  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0)) || (mode != 0 && !grad_io)) return EM_ERR_ARG;
+  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0 || stride < P)) || (mode != 0 && !grad_io)) return EM_ERR_ARG;
   if (mode != 1 && (!params || !m || !v || !hp || !state)) return EM_ERR_ARG;
   if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
-  const int nb = (P + 63) / 64;
-  hipLaunchKernelGGL(adam_slab_kernel, dim3(nb), dim3(256), 0, stream, slabs, nslab, P, grad_scale, params, m, v,
+  const int nb = (P + AS_P - 1) / AS_P;
+  hipLaunchKernelGGL(adam_slab_kernel, dim3(nb), dim3(AS_P * AS_G), 0, stream, slabs, nslab, P, stride, grad_scale, params, m, v,
                      grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale);
   EM_CHECK_LAUNCH();
   return 0;

@@ -91,6 +91,12 @@ EM_DEVICE float wave_sum(float v) {
   return v;
 }
 
+EM_DEVICE double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 EM_DEVICE float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));

@@ -34,6 +34,9 @@ namespace {
 
 constexpr int IN = 64, HID = 128, OUT = 64;
 constexpr int P_W1 = 0, P_W2 = IN * HID, P_B2 = P_W2 + HID * OUT, P_TOTAL = P_B2 + OUT;  // 16448
+// gradient slabs are SLAB_STRIDE floats apart (P_TOTAL rounded to an odd multiple of 256 B so the
+// cross-slab reduction in em_adam_slab does not hit the same HBM channel for every slab)
+constexpr int SLAB_STRIDE = 16640;
 constexpr int IMG_W1T = 0, IMG_W2P = 16384, IMG_W2Q = 32768, IMG_B2 = 49152, IMG_BYTES = 49408;
 
 constexpr uint64_t MAIN_BITS = (1ull << 50) - 1;
@@ -433,7 +436,7 @@ mlp_fused_train_kernel(const uint64_t* __restrict__ masks, const int32_t* __rest
   if (wave == 3) region_io(RED1, true);
   __syncthreads();
 
-  float* slab = slabs + (size_t)blockIdx.x * P_TOTAL;
+  float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
   for (int e = tid; e < 16 * 4 * 64; e += 256) {
     const int T = e >> 8, g = (e >> 6) & 3, l = e & 63, hh = l >> 5, rr = l & 31;
     const f32x4 v = *reinterpret_cast<const f32x4*>(RED0 + e * 4) + *reinterpret_cast<const f32x4*>(RED1 + e * 4);
@@ -516,6 +519,7 @@ mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __re
 }  // namespace
 
 EM_API int em_mlp_fused_param_count() { return P_TOTAL; }
+EM_API int em_mlp_fused_slab_stride() { return SLAB_STRIDE; }
 EM_API int em_mlp_fused_image_bytes() { return IMG_BYTES; }
 EM_API int em_mlp_fused_lds_bytes() { return TRAIN_LDS; }
 

@@ -1,0 +1,232 @@
+"""Typed configuration.  Every default is the reference's hard-coded constant.
+
+The reference has no config system: ``Main.main`` ignores ``args`` (``Main.java:35``)
+and hard-codes every value.  Those literals become defaults here:
+
+==========================  ==================================  ==========================
+field                       value                               reference
+==========================  ==================================  ==========================
+data.from_date/to_date      1900-01-01 .. 2020-06-14            Main.java:37 (URL query)
+data.html_table_class       "table table-bordered ..."          Main.java:62
+data.train_pct              70                                  Main.java:83
+data.date_format            "E, MMM d, yyyy"                    Main.java:92
+data.label_column           0                                   Main.java:110-111
+gbdt.*                      gbtree, eta 1.0, max_depth 3,       Main.java:113-126
+                            cpu_predictor, reg:logistic,
+                            subsample 1, nthread 6, gamma 1.0,
+                            eval_metric logloss
+gbdt.nround                 500                                 Main.java:136
+log.level                   INFO                                log4j.properties:2
+==========================  ==================================  ==========================
+
+Precedence (lowest -> highest): dataclass defaults < YAML/JSON file < ``EUROM_*``
+environment variables (``EUROM_GBDT__ETA=0.3``) < explicit CLI flags.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from typing import Any
+
+REFERENCE_URL = ("http://portalseven.com/lottery/euromillions_winning_numbers.jsp"
+                 "?fromDate=1900-01-01&toDate=2020-06-14&viewType=3")  # Main.java:37 (never fetched here)
+REFERENCE_TABLE_CLASS = "table table-bordered table-condensed table-striped text-center table-hover"  # Main.java:62
+
+
+@dataclasses.dataclass
+class DataConfig:
+    source: str = "synthetic"  # synthetic | csv | html | reference-csv
+    path: str | None = None
+    from_date: str = "1900-01-01"
+    to_date: str = "2020-06-14"
+    html_table_class: str = REFERENCE_TABLE_CLASS
+    train_pct: float = 70.0
+    date_format: str = "E, MMM d, yyyy"
+    label_column: int = 0
+    n_draws: int | None = None  # synthetic: None = the reference's calendar range (~1.33k draws)
+    seed: int = 0
+    planted: float = 0.0  # synthetic Markov structure strength (0 = iid draws)
+    lags: int = 1
+    workdir: str | None = None
+
+
+@dataclasses.dataclass
+class GBDTConfig:
+    booster: str = "gbtree"
+    eta: float = 1.0
+    max_depth: int = 3
+    predictor: str = "cpu_predictor"  # accepted for parity; prediction runs on the GPU kernel when available
+    objective: str = "reg:logistic"
+    subsample: float = 1.0
+    silent: int = 1  # deprecated XGBoost key kept for parity (defect D-j)
+    nthread: int = 6
+    gamma: float = 1.0
+    eval_metric: str = "logloss"
+    nround: int = 500
+    reg_lambda: float = 1.0  # XGBoost default
+    min_child_weight: float = 1.0  # XGBoost default
+    base_score: float = 0.5  # XGBoost default
+    max_bin: int = 256
+    target: str = "reference"  # reference (label_column of the raw features) | next-draw
+    device: str = "auto"  # auto | cuda | cpu
+
+
+@dataclasses.dataclass
+class RFConfig:
+    n_trees: int = 100
+    max_depth: int = 8
+    min_samples_leaf: int = 1
+    feature_subset: str = "sqrt"  # sqrt | all | log2 | <float fraction>
+    bootstrap: bool = True
+    seed: int = 0
+    device: str = "auto"
+
+
+@dataclasses.dataclass
+class MLPConfig:
+    model: str = "mlp"  # mlp (62-128-62 fused) | mlp-wide (62-8192-8192-62) | custom
+    hidden: tuple = (128,)
+    activation: str = "relu"
+    loss: str = "softmax"  # softmax (grouped 50/12 CE) | bce
+    lr: float = 3e-3
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    batch: int = 1 << 20
+    steps: int = 200
+    epochs: int | None = None
+    dtype: str = "bf16"
+    seed: int = 0
+    eval_every: int = 50
+    shuffle: bool = True
+
+
+@dataclasses.dataclass
+class DistConfig:
+    dp: int = 1
+    backend: str = "auto"  # auto -> nccl (RCCL) on GPU, gloo on CPU
+    bucket_mb: float = 25.0
+    timeout_s: float = 300.0
+    fault_at_step: int | None = None  # test-only fault injection
+    fault_rank: int | None = None
+
+
+@dataclasses.dataclass
+class CkptConfig:
+    path: str | None = None
+    resume: str | None = None
+    every: int = 0
+
+
+@dataclasses.dataclass
+class LogConfig:
+    level: str = "INFO"
+    json_metrics: bool = True
+
+
+@dataclasses.dataclass
+class RunConfig:
+    data: DataConfig = dataclasses.field(default_factory=DataConfig)
+    gbdt: GBDTConfig = dataclasses.field(default_factory=GBDTConfig)
+    rf: RFConfig = dataclasses.field(default_factory=RFConfig)
+    mlp: MLPConfig = dataclasses.field(default_factory=MLPConfig)
+    dist: DistConfig = dataclasses.field(default_factory=DistConfig)
+    ckpt: CkptConfig = dataclasses.field(default_factory=CkptConfig)
+    log: LogConfig = dataclasses.field(default_factory=LogConfig)
+    model: str = "gbdt"  # gbdt | rf | mlp | mlp-wide
+    device: str = "auto"
+    reference_compat: bool = False  # reproduce D-f (second booster trained on validation) + checkPredicts
+
+    # ------------------------------------------------------------------ helpers
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+    def gbdt_params(self) -> dict:
+        """The reference's XGBoost parameter map (Main.java:113-126)."""
+        g = self.gbdt
+        return {"booster": g.booster, "eta": g.eta, "max_depth": g.max_depth, "predictor": g.predictor,
+                "objective": g.objective, "subsample": g.subsample, "silent": g.silent, "nthread": g.nthread,
+                "gamma": g.gamma, "eval_metric": g.eval_metric}
+
+
+def _coerce(cur: Any, val: Any, typ: Any = None):
+    if isinstance(val, str):
+        if isinstance(cur, bool) or typ in (bool, "bool"):
+            return val.strip().lower() in ("1", "true", "yes", "on")
+        if isinstance(cur, int) and not isinstance(cur, bool):
+            return int(val)
+        if isinstance(cur, float):
+            return float(val)
+        if isinstance(cur, tuple):
+            parts = [p for p in val.replace("x", ",").split(",") if p.strip()]
+            return tuple(type(cur[0])(p) if cur else float(p) for p in parts)
+        if cur is None:
+            low = val.strip().lower()
+            if low in ("none", "null", ""):
+                return None
+            for conv in (int, float):
+                try:
+                    return conv(val)
+                except ValueError:
+                    pass
+        return val
+    if isinstance(cur, tuple) and isinstance(val, list):
+        return tuple(val)
+    return val
+
+
+def set_path(cfg: RunConfig, dotted: str, value: Any) -> None:
+    obj: Any = cfg
+    parts = dotted.split(".")
+    for p in parts[:-1]:
+        obj = getattr(obj, p)
+    leaf = parts[-1]
+    if not hasattr(obj, leaf):
+        raise KeyError(f"unknown config key {dotted}")
+    setattr(obj, leaf, _coerce(getattr(obj, leaf), value))
+
+
+def apply_mapping(cfg: RunConfig, mapping: dict, prefix: str = "") -> None:
+    for k, v in mapping.items():
+        key = f"{prefix}{k}"
+        if isinstance(v, dict):
+            apply_mapping(cfg, v, key + ".")
+        else:
+            set_path(cfg, key, v)
+
+
+def load_file(cfg: RunConfig, path: str) -> None:
+    with open(path, encoding="utf-8") as f:
+        text = f.read()
+    if path.endswith((".yaml", ".yml")):
+        import yaml
+
+        data = yaml.safe_load(text) or {}
+    else:
+        data = json.loads(text)
+    apply_mapping(cfg, data)
+
+
+def apply_env(cfg: RunConfig, environ=None) -> None:
+    """EUROM_<SECTION>__<FIELD>=value  (e.g. EUROM_GBDT__ETA=0.3, EUROM_MODEL=rf)."""
+    env = os.environ if environ is None else environ
+    for k, v in env.items():
+        if not k.startswith("EUROM_") or k in ("EUROM_AUTOBUILD", "EUROM_FORCE_BUILD", "EUROM_OFFLOAD_ARCH"):
+            continue
+        dotted = k[len("EUROM_"):].lower().replace("__", ".")
+        try:
+            set_path(cfg, dotted, v)
+        except (KeyError, AttributeError):
+            continue
+
+
+def build_config(file: str | None = None, overrides: dict | None = None, environ=None) -> RunConfig:
+    cfg = RunConfig()
+    if file:
+        load_file(cfg, file)
+    apply_env(cfg, environ)
+    for k, v in (overrides or {}).items():
+        if v is not None:
+            set_path(cfg, k, v)
+    return cfg

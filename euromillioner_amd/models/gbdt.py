@@ -1,0 +1,454 @@
+"""Gradient-boosted trees with XGBoost ``gbtree`` semantics (the reference's learner).
+
+Reference: ``Main.java:113-141`` trains ``XGBoost.train(..., nround=500)`` with
+``booster=gbtree, eta=1.0, max_depth=3, objective=reg:logistic, subsample=1,
+gamma=1.0, eval_metric=logloss`` (``lambda=1``, ``min_child_weight=1``,
+``base_score=0.5`` are XGBoost defaults) and predicts with ``cpu_predictor``.
+Upstream XGBoost runs this in C++ (libxgboost via JNI); here:
+
+* ``backend="hip"`` — a device-resident engine (``csrc/gbdt.hip``): per round a
+  gradient kernel, per level a deterministic histogram kernel (K8), a split-scan
+  kernel (K9), a partition kernel (K10), then prune/leaf/margin-update (K12) and a
+  fused metric reduction (K13); prediction is the tree-ensemble kernel (K11).  The
+  C++ driver runs all rounds without host round-trips.
+* ``backend="numpy"`` — the oracle used by the tests and on CPU-only machines.
+
+Split finding is histogram-based over per-feature cut points.  When a feature has
+at most ``max_bin`` distinct values (true for every reference feature: dow 7,
+month 12, day 31, year 17, numbers <= 50, stars <= 12) the cut points are the
+midpoints between consecutive distinct values, so the candidate splits — and hence
+the trees — are exactly those of XGBoost's exact-greedy updater
+(``tests/test_gbdt.py::test_hist_equals_exact``).
+
+Semantics implemented (XGBoost 1.x ``ColMaker`` + ``TreePruner``):
+* loss_chg = G_L^2/(H_L+l) + G_R^2/(H_R+l) - G^2/(H+l); a node splits only if
+  loss_chg > 1e-6 and both children have hessian sum >= min_child_weight;
+  ties keep the lower feature index (then the lower cut);
+* bottom-up pruning: a split whose children are both leaves is removed while
+  loss_chg < gamma (``min_split_loss``);
+* leaf value = -G/(H+l) * eta; margins start at logit(base_score);
+* reg:logistic/binary:logistic: g = p - y, h = max(p(1-p), 1e-16), labels must be
+  in [0, 1] (XGBoost raises otherwise); reg:squarederror: g = m - y, h = 1.
+
+Multiple targets (``Y [n, T]``) train T independent boosters in lock-step (the
+default "next-draw" task: one booster per number/star, 62 in all).
+"""
+from __future__ import annotations
+
+import json
+import math
+
+import numpy as np
+
+KRT_EPS = 1e-6
+OBJECTIVES = ("reg:logistic", "binary:logistic", "reg:squarederror")
+
+
+# ----------------------------------------------------------------------------- binning
+def make_cuts(X: np.ndarray, max_bin: int = 256) -> list[np.ndarray]:
+    """Per-feature split values.  bin(x) = number of cuts < x ... i.e. searchsorted(cuts, x, 'left')
+    with rows going LEFT of cut c when x < cuts[c]."""
+    cuts = []
+    for f in range(X.shape[1]):
+        col = X[:, f]
+        col = col[~np.isnan(col)]
+        u = np.unique(col)
+        if len(u) <= 1:
+            cuts.append(np.zeros(0, dtype=np.float64))
+            continue
+        if len(u) <= max_bin:
+            c = (u[:-1].astype(np.float64) + u[1:].astype(np.float64)) * 0.5
+        else:
+            qs = np.quantile(col.astype(np.float64), np.linspace(0, 1, max_bin + 1)[1:-1])
+            c = np.unique(qs)
+        cuts.append(c)
+    return cuts
+
+
+def apply_bins(X: np.ndarray, cuts: list[np.ndarray]) -> np.ndarray:
+    """bin index per value: number of cuts strictly below x (x < cut -> left of it)."""
+    n, F = X.shape
+    nb = max((len(c) for c in cuts), default=0) + 1
+    dtype = np.uint8 if nb <= 256 else np.uint16
+    out = np.zeros((n, F), dtype=dtype)
+    for f in range(F):
+        if len(cuts[f]):
+            out[:, f] = np.searchsorted(cuts[f], X[:, f], side="right")
+    return out
+
+
+# ----------------------------------------------------------------------------- trees
+class TreeArrays:
+    """Heap-numbered trees: node i has children 2i+1 / 2i+2.  status 0 unused, 1 split, 2 leaf."""
+
+    def __init__(self, n_trees: int, max_depth: int):
+        nn = 2 ** (max_depth + 1) - 1
+        self.max_depth = max_depth
+        self.feat = np.full((n_trees, nn), -1, dtype=np.int32)
+        self.sbin = np.zeros((n_trees, nn), dtype=np.int32)  # go left iff bin <= sbin
+        self.split_value = np.zeros((n_trees, nn), dtype=np.float64)  # go left iff x < split_value
+        self.status = np.zeros((n_trees, nn), dtype=np.int8)
+        self.leaf = np.zeros((n_trees, nn), dtype=np.float64)
+        self.gain = np.zeros((n_trees, nn), dtype=np.float64)
+        self.cover = np.zeros((n_trees, nn), dtype=np.float64)
+
+    @property
+    def n_trees(self):
+        return self.feat.shape[0]
+
+    def set_split_values(self, cuts):
+        for t in range(self.n_trees):
+            for i in np.nonzero(self.status[t] == 1)[0]:
+                self.split_value[t, i] = cuts[self.feat[t, i]][self.sbin[t, i]]
+
+
+def predict_margin_values(trees: TreeArrays, X: np.ndarray, tree_task: np.ndarray, n_tasks: int,
+                          base_margin: float) -> np.ndarray:
+    """Raw-value traversal (cpu_predictor equivalent): margin[n, T]."""
+    n = X.shape[0]
+    out = np.full((n, n_tasks), base_margin, dtype=np.float64)
+    rows = np.arange(n)
+    for k in range(trees.n_trees):
+        node = np.zeros(n, dtype=np.int64)
+        for _ in range(trees.max_depth + 1):
+            st = trees.status[k, node]
+            sp = st == 1
+            if not sp.any():
+                break
+            f = trees.feat[k, node[sp]]
+            go_right = ~(X[rows[sp], f] < trees.split_value[k, node[sp]])
+            node[sp] = 2 * node[sp] + 1 + go_right
+        out[:, tree_task[k]] += trees.leaf[k, node]
+    return out
+
+
+# ----------------------------------------------------------------------------- objectives
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def base_margin_for(objective: str, base_score: float) -> float:
+    if objective in ("reg:logistic", "binary:logistic"):
+        return float(math.log(base_score / (1.0 - base_score)))
+    return float(base_score)
+
+
+def transform(objective: str, margin: np.ndarray) -> np.ndarray:
+    return _sigmoid(margin) if objective in ("reg:logistic", "binary:logistic") else margin
+
+
+def check_labels(objective: str, y: np.ndarray) -> None:
+    if objective in ("reg:logistic", "binary:logistic"):
+        if np.any((y < 0) | (y > 1)) or np.any(np.isnan(y)):
+            # XGBoost: LogisticRegression::CheckLabel -> XGBoostError
+            raise ValueError("label must be in [0,1] for logistic regression")
+
+
+def gradients(objective: str, margin: np.ndarray, y: np.ndarray):
+    if objective in ("reg:logistic", "binary:logistic"):
+        p = _sigmoid(margin)
+        return p - y, np.maximum(p * (p.dtype.type(1) - p), p.dtype.type(1e-16))
+    if objective == "reg:squarederror":
+        return margin - y, np.ones_like(margin)
+    raise ValueError(f"unsupported objective {objective}")
+
+
+# ----------------------------------------------------------------------------- numpy oracle
+def _best_split_hist(hg, hh, G, H, lam, mcw):
+    """hg/hh: [F, B] node histograms.  Returns (gain, f, bin, GL, HL) or None."""
+    cg = np.cumsum(hg, axis=1)[:, :-1]  # left = bins <= b
+    ch = np.cumsum(hh, axis=1)[:, :-1]
+    if cg.size == 0:
+        return None
+    gr, hr = G - cg, H - ch
+    ok = (ch >= mcw) & (hr >= mcw)
+    root = G * G / (H + lam)
+    gain = np.where(ok, cg * cg / (ch + lam) + gr * gr / (hr + lam) - root, -np.inf)
+    # first max in (feature, bin) order == lower feature index wins ties
+    flat = int(np.argmax(gain))
+    f, b = divmod(flat, gain.shape[1])
+    g = float(gain[f, b])
+    if not np.isfinite(g) or g <= KRT_EPS:
+        return None
+    return g, f, b, float(cg[f, b]), float(ch[f, b])
+
+
+def grow_tree_numpy(bins, nbins, g, h, max_depth, lam, mcw, gamma, eta, trees: TreeArrays, k: int):
+    n, F = bins.shape
+    node = np.zeros(n, dtype=np.int64)
+    G = np.zeros(2 ** (max_depth + 1) - 1)
+    H = np.zeros_like(G)
+    G[0], H[0] = g.astype(np.float64).sum(), h.astype(np.float64).sum()
+    trees.status[k, 0] = 2
+    for depth in range(max_depth):
+        for i in range(2 ** depth - 1, 2 ** (depth + 1) - 1):
+            if trees.status[k, i] != 2:
+                continue
+            sel = node == i
+            if not sel.any():
+                continue
+            hg = np.zeros((F, nbins))
+            hh = np.zeros((F, nbins))
+            bs = bins[sel]
+            gs, hs = g[sel].astype(np.float64), h[sel].astype(np.float64)
+            for f in range(F):
+                hg[f] = np.bincount(bs[:, f], weights=gs, minlength=nbins)
+                hh[f] = np.bincount(bs[:, f], weights=hs, minlength=nbins)
+            best = _best_split_hist(hg, hh, G[i], H[i], lam, mcw)
+            if best is None:
+                continue
+            gain, f, b, GL, HL = best
+            trees.status[k, i] = 1
+            trees.feat[k, i], trees.sbin[k, i], trees.gain[k, i] = f, b, gain
+            l, r = 2 * i + 1, 2 * i + 2
+            G[l], H[l], G[r], H[r] = GL, HL, G[i] - GL, H[i] - HL
+            trees.status[k, l] = trees.status[k, r] = 2
+            right = sel & (bins[:, f] > b)
+            node[sel] = l
+            node[right] = r
+    _prune_and_leaves(trees, k, G, H, lam, gamma, eta, max_depth)
+    trees.cover[k] = H
+    return node
+
+
+def _prune_and_leaves(trees: TreeArrays, k, G, H, lam, gamma, eta, max_depth):
+    for i in range(2 ** max_depth - 2, -1, -1):  # bottom-up over internal slots
+        if trees.status[k, i] == 1:
+            l, r = 2 * i + 1, 2 * i + 2
+            if trees.status[k, l] == 2 and trees.status[k, r] == 2 and trees.gain[k, i] < gamma:
+                trees.status[k, i] = 2
+                trees.status[k, l] = trees.status[k, r] = 0
+                trees.feat[k, i] = -1
+    for i in range(len(G)):
+        if trees.status[k, i] == 2:
+            trees.leaf[k, i] = np.float32(-G[i] / (H[i] + lam) * eta)  # leaf values are float (XGBoost)
+
+
+def _leaf_of(trees: TreeArrays, k, node):
+    node = node.copy()
+    for _ in range(trees.max_depth + 1):
+        bad = trees.status[k, node] != 2
+        if not bad.any():
+            break
+        node[bad] = (node[bad] - 1) // 2
+    return node
+
+
+class GBDT:
+    """XGBoost-semantics booster(s).  Y may be [n] or [n, T] (T boosters in lock-step)."""
+
+    def __init__(self, eta=1.0, max_depth=3, objective="reg:logistic", subsample=1.0, gamma=1.0,
+                 reg_lambda=1.0, min_child_weight=1.0, base_score=0.5, nround=500, max_bin=256,
+                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1):
+        if objective not in OBJECTIVES:
+            raise ValueError(f"objective must be one of {OBJECTIVES}")
+        self.eta, self.max_depth, self.objective = float(eta), int(max_depth), objective
+        self.subsample, self.gamma, self.lam = float(subsample), float(gamma), float(reg_lambda)
+        self.mcw, self.base_score, self.nround = float(min_child_weight), float(base_score), int(nround)
+        self.max_bin, self.eval_metric, self.seed = int(max_bin), eval_metric, int(seed)
+        self.backend = backend
+        self.log, self.log_every = log, log_every
+        self.trees: TreeArrays | None = None
+        self.cuts = None
+        self.n_tasks = 1
+        self.history: list[dict] = []
+
+    @classmethod
+    def from_params(cls, params: dict, nround: int = 500, **kw):
+        """Build from the reference's parameter map (Main.java:113-126)."""
+        p = dict(params)
+        if p.get("booster", "gbtree") != "gbtree":
+            raise ValueError("only booster=gbtree is supported")
+        return cls(eta=float(p.get("eta", 0.3)), max_depth=int(p.get("max_depth", 6)),
+                   objective=p.get("objective", "reg:squarederror"), subsample=float(p.get("subsample", 1)),
+                   gamma=float(p.get("gamma", 0.0)), reg_lambda=float(p.get("lambda", 1.0)),
+                   min_child_weight=float(p.get("min_child_weight", 1.0)),
+                   base_score=float(p.get("base_score", 0.5)), eval_metric=p.get("eval_metric", "logloss"),
+                   nround=nround, **kw)
+
+    @property
+    def base_margin(self) -> float:
+        return base_margin_for(self.objective, self.base_score)
+
+    def _resolve_backend(self):
+        if self.backend != "auto":
+            return self.backend
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                from ..ops import _native
+
+                _native.lib()
+                return "hip"
+        except Exception:  # noqa: BLE001
+            pass
+        return "numpy"
+
+    def fit(self, X: np.ndarray, Y: np.ndarray, evals: dict | None = None):
+        X = np.asarray(X, dtype=np.float64)
+        Y = np.asarray(Y, dtype=np.float64)
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        check_labels(self.objective, Y)
+        self.n_tasks = Y.shape[1]
+        self.cuts = make_cuts(X, self.max_bin)
+        bins = apply_bins(X, self.cuts)
+        nbins = max((len(c) for c in self.cuts), default=0) + 1
+        evals = evals or {}
+        backend = self._resolve_backend()
+        self.backend_used = backend
+        if backend == "hip":
+            from . import gbdt_hip
+
+            self.trees, self.history = gbdt_hip.fit(self, X, bins, nbins, Y, evals)
+        else:
+            self.trees, self.history = self._fit_numpy(X, bins, nbins, Y, evals)
+        self.trees.set_split_values(self.cuts)
+        return self
+
+    def _fit_numpy(self, X, bins, nbins, Y, evals):
+        n, T = Y.shape
+        R = self.nround
+        trees = TreeArrays(T * R, self.max_depth)
+        # float32 margins / gradients, float64 histogram sums: XGBoost's GradientPair / GradStats
+        margin = np.full((n, T), self.base_margin, dtype=np.float32)
+        ev_margin = {k: np.full((len(v[0]), T), self.base_margin, dtype=np.float32) for k, v in evals.items()}
+        Y32 = Y.astype(np.float32)
+        ev_bins = {k: apply_bins(np.asarray(v[0], np.float64), self.cuts) for k, v in evals.items()}
+        rng = np.random.default_rng(self.seed)
+        hist = []
+        for rnd in range(R):
+            for t in range(T):
+                k = rnd * T + t
+                g, h = gradients(self.objective, margin[:, t], Y32[:, t])
+                if self.subsample < 1.0:
+                    keep = rng.random(n) < self.subsample
+                    g, h = g * keep, h * keep
+                node = grow_tree_numpy(bins, nbins, g, h, self.max_depth, self.lam, self.mcw, self.gamma,
+                                       self.eta, trees, k)
+                margin[:, t] += trees.leaf[k, _leaf_of(trees, k, node)].astype(np.float32)
+                for name, eb in ev_bins.items():
+                    en = _route_bins(trees, k, eb)
+                    ev_margin[name][:, t] += trees.leaf[k, en].astype(np.float32)
+            rec = {"round": rnd}
+            for name, (ex, ey) in evals.items():
+                rec[name] = self._metric(np.asarray(ey, np.float64).reshape(len(ex), -1), ev_margin[name])
+            hist.append(rec)
+            self._log_round(rec)
+        return trees, hist
+
+    def _metric(self, y, margin):
+        from .. import metrics as M
+
+        p = transform(self.objective, margin)
+        return M.EVAL_METRICS[self.eval_metric](y, p)
+
+    def _log_round(self, rec):
+        if self.log is None or (rec["round"] % self.log_every and rec["round"] != self.nround - 1):
+            return
+        parts = [f"[{rec['round']}]"] + [f"{k}-{self.eval_metric}:{v:.6f}" for k, v in rec.items() if k != "round"]
+        self.log.info("\t".join(parts))
+
+    # ------------------------------------------------------------------ inference
+    def predict_margin(self, X: np.ndarray, backend: str | None = None) -> np.ndarray:
+        X = np.asarray(X, dtype=np.float64)
+        be = backend or getattr(self, "backend_used", "numpy")
+        if be == "hip":
+            from . import gbdt_hip
+
+            return gbdt_hip.predict_margin(self, X)
+        task = np.arange(self.trees.n_trees) % self.n_tasks
+        return predict_margin_values(self.trees, X, task, self.n_tasks, self.base_margin)
+
+    def predict(self, X: np.ndarray, backend: str | None = None) -> np.ndarray:
+        """Like Booster.predict: float32 [n, T] (reg:logistic -> probabilities)."""
+        return transform(self.objective, self.predict_margin(X, backend)).astype(np.float32)
+
+    # ------------------------------------------------------------------ persistence
+    def to_json(self) -> dict:
+        """XGBoost-JSON-like dump (learner/gradient_booster/model/trees)."""
+        tr = self.trees
+        trees = []
+        for k in range(tr.n_trees):
+            nodes = []
+            for i in np.nonzero(tr.status[k])[0]:
+                nd = {"nodeid": int(i), "cover": float(tr.cover[k, i])}
+                if tr.status[k, i] == 1:
+                    nd.update(split=f"f{int(tr.feat[k, i])}", split_condition=float(tr.split_value[k, i]),
+                              yes=int(2 * i + 1), no=int(2 * i + 2), gain=float(tr.gain[k, i]))
+                else:
+                    nd["leaf"] = float(tr.leaf[k, i])
+                nodes.append(nd)
+            trees.append({"id": k, "task": int(k % self.n_tasks), "nodes": nodes})
+        return {"learner": {"objective": self.objective, "base_score": self.base_score,
+                            "num_target": self.n_tasks,
+                            "params": {"eta": self.eta, "max_depth": self.max_depth, "gamma": self.gamma,
+                                       "lambda": self.lam, "min_child_weight": self.mcw,
+                                       "subsample": self.subsample, "nround": self.nround},
+                            "gradient_booster": {"name": "gbtree", "model": {"trees": trees}}}}
+
+    def save(self, path: str) -> None:
+        with open(path, "w", encoding="utf-8") as f:
+            json.dump(self.to_json(), f)
+
+    @classmethod
+    def load(cls, path: str) -> "GBDT":
+        with open(path, encoding="utf-8") as f:
+            d = json.load(f)["learner"]
+        p = d["params"]
+        m = cls(eta=p["eta"], max_depth=p["max_depth"], objective=d["objective"], gamma=p["gamma"],
+                reg_lambda=p["lambda"], min_child_weight=p["min_child_weight"], base_score=d["base_score"],
+                nround=p["nround"], subsample=p.get("subsample", 1.0), backend="numpy")
+        m.n_tasks = d["num_target"]
+        trees = d["gradient_booster"]["model"]["trees"]
+        tr = TreeArrays(len(trees), m.max_depth)
+        for k, t in enumerate(trees):
+            for nd in t["nodes"]:
+                i = nd["nodeid"]
+                tr.cover[k, i] = nd.get("cover", 0.0)
+                if "leaf" in nd:
+                    tr.status[k, i], tr.leaf[k, i] = 2, nd["leaf"]
+                else:
+                    tr.status[k, i] = 1
+                    tr.feat[k, i] = int(nd["split"][1:])
+                    tr.split_value[k, i] = nd["split_condition"]
+                    tr.gain[k, i] = nd.get("gain", 0.0)
+        m.trees = tr
+        m.backend_used = "numpy"
+        return m
+
+
+def _route_bins(trees: TreeArrays, k: int, bins: np.ndarray) -> np.ndarray:
+    n = bins.shape[0]
+    node = np.zeros(n, dtype=np.int64)
+    rows = np.arange(n)
+    for _ in range(trees.max_depth + 1):
+        sp = trees.status[k, node] == 1
+        if not sp.any():
+            break
+        f = trees.feat[k, node[sp]]
+        node[sp] = 2 * node[sp] + 1 + (bins[rows[sp], f] > trees.sbin[k, node[sp]])
+    return node
+
+
+# ----------------------------------------------------------------------------- exact greedy (verification)
+def exact_greedy_split(x: np.ndarray, g: np.ndarray, h: np.ndarray, lam: float, mcw: float):
+    """XGBoost ColMaker enumeration on one feature: best (gain, threshold) over distinct values."""
+    order = np.argsort(x, kind="stable")
+    xs, gs, hs = x[order], g[order], h[order]
+    G, H = gs.sum(), hs.sum()
+    best = (-np.inf, None)
+    GL = HL = 0.0
+    for i in range(len(xs) - 1):
+        GL += gs[i]
+        HL += hs[i]
+        if xs[i + 1] == xs[i]:
+            continue
+        GR, HR = G - GL, H - HL
+        if HL < mcw or HR < mcw:
+            continue
+        gain = GL * GL / (HL + lam) + GR * GR / (HR + lam) - G * G / (H + lam)
+        if gain > best[0]:
+            best = (gain, (xs[i] + xs[i + 1]) * 0.5)
+    return best

@@ -1,0 +1,123 @@
+"""Device side of :mod:`euromillioner_amd.models.gbdt`: buffers + calls into ``csrc/gbdt.hip``."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ..ops import _native as N
+from .gbdt import TreeArrays, apply_bins
+
+_v, _i, _i64, _f, _u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint32
+
+
+class _Eval(ctypes.Structure):
+    _fields_ = [("bins", _v), ("Y", _v), ("margin", _v), ("n", _i)]
+
+
+N.register_signatures({
+    "em_gbdt_fit": (_i, [_v, _v, _i, _i, _i, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f, _f,
+                         _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
+    "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
+    "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
+})
+
+OBJ = {"reg:logistic": 0, "binary:logistic": 0, "reg:squarederror": 1}
+MET = {"logloss": 0, "rmse": 1, "error": 2}
+
+
+def _dev():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25):
+    dev = _dev()
+    n, F = bins.shape
+    T = Y.shape[1]
+    R, D = model.nround, model.max_depth
+    NN = 2 ** (D + 1) - 1
+    if nbins > 256:
+        raise ValueError("GPU GBDT supports at most 256 bins per feature")
+    d_bins = torch.from_numpy(np.ascontiguousarray(bins, dtype=np.uint8)).to(dev)
+    d_Y = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float32)).to(dev)
+    margin = torch.empty(T * n, dtype=torch.float32, device=dev)
+    stream = N.stream_handle(dev)
+    N.call("em_gbdt_init_margin", margin.data_ptr(), T * n, float(model.base_margin), stream)
+    ev_names = list(evals.keys())
+    ev_keep = []
+    ev_structs = (_Eval * max(1, len(ev_names)))()
+    for i, name in enumerate(ev_names):
+        ex, ey = evals[name]
+        eb = apply_bins(np.asarray(ex, np.float64), model.cuts)
+        db = torch.from_numpy(np.ascontiguousarray(eb, dtype=np.uint8)).to(dev)
+        dy = torch.from_numpy(np.ascontiguousarray(np.asarray(ey, np.float32).reshape(len(ex), -1))).to(dev)
+        em = torch.empty(T * len(ex), dtype=torch.float32, device=dev)
+        N.call("em_gbdt_init_margin", em.data_ptr(), em.numel(), float(model.base_margin), stream)
+        ev_keep += [db, dy, em]
+        ev_structs[i] = _Eval(db.data_ptr(), dy.data_ptr(), em.data_ptr(), len(ex))
+    g = torch.empty(T * n, dtype=torch.float32, device=dev)
+    h = torch.empty_like(g)
+    node = torch.empty(T * n, dtype=torch.int16, device=dev)
+    nchunks = (n + 1023) // 1024
+    pdoubles = nchunks * T * (2 ** (D - 1)) * F * nbins * 2
+    partial = torch.empty(max(pdoubles, 1), dtype=torch.float64, device=dev)
+    Gs = torch.zeros(T * NN, dtype=torch.float64, device=dev)
+    Hs = torch.zeros_like(Gs)
+    mpart = torch.zeros(4096, dtype=torch.float64, device=dev)
+    status = torch.zeros(R * T * NN, dtype=torch.int8, device=dev)
+    feat = torch.zeros(R * T * NN, dtype=torch.int16, device=dev)
+    sbin = torch.zeros(R * T * NN, dtype=torch.uint8, device=dev)
+    leaf = torch.zeros(R * T * NN, dtype=torch.float32, device=dev)
+    gain = torch.zeros_like(leaf)
+    cover = torch.zeros_like(leaf)
+    hist = torch.zeros(R * (1 + len(ev_names)), dtype=torch.float32, device=dev)
+    history = []
+    r0 = 0
+    while r0 < R:
+        r1 = min(R, r0 + rounds_per_call)
+        N.call("em_gbdt_fit", d_bins.data_ptr(), d_Y.data_ptr(), n, F, nbins, T, margin.data_ptr(), ev_structs,
+               len(ev_names), r0, r1, D, OBJ[model.objective], MET[model.eval_metric], model.eta, model.lam,
+               model.gamma, model.mcw, model.subsample, model.seed & 0xFFFFFFFF, g.data_ptr(), h.data_ptr(),
+               node.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
+               status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), gain.data_ptr(),
+               cover.data_ptr(), hist.data_ptr(), stream)
+        hh = hist.view(R, 1 + len(ev_names))[r0:r1].cpu().numpy()
+        for i, rnd in enumerate(range(r0, r1)):
+            rec = {"round": rnd}
+            # XGBoost4J watch order: evals only (train appears if the caller passed it as a watch)
+            for j, name in enumerate(ev_names):
+                rec[name] = float(hh[i, 1 + j])
+            history.append(rec)
+            model._log_round(rec)
+        r0 = r1
+    trees = TreeArrays(R * T, D)
+    trees.status[:] = status.view(R * T, NN).cpu().numpy()
+    trees.feat[:] = feat.view(R * T, NN).cpu().numpy().astype(np.int32)
+    trees.sbin[:] = sbin.view(R * T, NN).cpu().numpy().astype(np.int32)
+    trees.leaf[:] = leaf.view(R * T, NN).cpu().numpy().astype(np.float64)
+    trees.gain[:] = gain.view(R * T, NN).cpu().numpy().astype(np.float64)
+    trees.cover[:] = cover.view(R * T, NN).cpu().numpy().astype(np.float64)
+    model._device_trees = (status, feat, sbin, leaf)
+    return trees, history
+
+
+def predict_margin(model, X):
+    dev = _dev()
+    tr = model.trees
+    bins = apply_bins(X, model.cuts)
+    n, F = bins.shape
+    T = model.n_tasks
+    NN = 2 ** (tr.max_depth + 1) - 1
+    dt = getattr(model, "_device_trees", None)
+    if dt is None:
+        dt = (torch.from_numpy(tr.status.reshape(-1)).to(dev), torch.from_numpy(tr.feat.astype(np.int16).reshape(-1)).to(dev),
+              torch.from_numpy(tr.sbin.astype(np.uint8).reshape(-1)).to(dev),
+              torch.from_numpy(tr.leaf.astype(np.float32).reshape(-1)).to(dev))
+        model._device_trees = dt
+    status, feat, sbin, leaf = dt
+    d_bins = torch.from_numpy(np.ascontiguousarray(bins, dtype=np.uint8)).to(dev)
+    margin = torch.full((T * n,), float(model.base_margin), dtype=torch.float32, device=dev)
+    N.call("em_gbdt_predict", d_bins.data_ptr(), margin.data_ptr(), T, n, F, tr.max_depth, 0, tr.n_trees,
+           status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), N.stream_handle(dev))
+    return margin.view(T, n).t().cpu().numpy().astype(np.float64)

@@ -123,7 +123,7 @@ class FusedSmallMLP:
         self.state = torch.zeros(2, dtype=torch.int32, device=dev)  # {adam step, ticket}
         self.img = torch.zeros(FM.IMG_BYTES, dtype=torch.uint8, device=dev)
         self.nslab_max = N.cu_count(dev)
-        self.slabs = torch.zeros(self.nslab_max, P, dtype=torch.float32, device=dev)
+        self.slabs = torch.zeros(self.nslab_max, FM.SLAB_STRIDE, dtype=torch.float32, device=dev)
         self.loss_slabs = torch.zeros(self.nslab_max, dtype=torch.float32, device=dev)
         self.grad_io = torch.zeros(P + 1, dtype=torch.float32, device=dev)  # [grads..., loss]
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)

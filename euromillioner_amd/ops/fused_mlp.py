@@ -21,6 +21,7 @@ IN, HID, OUT = 64, 128, 64
 P_W1, P_W2, P_B2 = 0, IN * HID, IN * HID + HID * OUT
 P_TOTAL = P_B2 + OUT
 IMG_BYTES = 49408
+SLAB_STRIDE = 16640  # floats between per-workgroup gradient slabs (csrc/mlp_fused.hip)
 LOSS_KINDS = {"softmax": 0, "bce": 1}
 
 
@@ -113,8 +114,8 @@ def train_partials(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.
         N.check_cuda(img, "img", torch.uint8)
         N.check_cuda(slabs, "slabs", torch.float32)
         N.check_cuda(loss_slabs, "loss_slabs", torch.float32)
-        if slabs.dim() != 2 or slabs.shape[1] != P_TOTAL or loss_slabs.numel() < slabs.shape[0]:
-            raise ValueError("slabs must be [nslab, P]")
+        if slabs.dim() != 2 or slabs.shape[1] != SLAB_STRIDE or loss_slabs.numel() < slabs.shape[0]:
+            raise ValueError("slabs must be [nslab, SLAB_STRIDE]")
     groups = (B + 127) // 128
     nslab = max(1, min(slabs.shape[0], groups))
     N.call("em_mlp_fused_train", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
@@ -142,7 +143,9 @@ def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params:
               img: torch.Tensor | None = None, loss_slabs: torch.Tensor | None = None,
               loss_out: torch.Tensor | None = None, loss_scale: float = 1.0) -> None:
     P = params.numel()
-    N.call("em_adam_slab", slabs.data_ptr() if slabs is not None else None, int(nslab), int(P), float(grad_scale),
+    stride = slabs.shape[1] if slabs is not None else P
+    N.call("em_adam_slab", slabs.data_ptr() if slabs is not None else None, int(nslab), int(P), int(stride),
+           float(grad_scale),
            params.data_ptr(), m.data_ptr(), v.data_ptr(), grad_io.data_ptr() if grad_io is not None else None,
            hp.data_ptr(), state.data_ptr(), int(mode), img.data_ptr() if img is not None else None,
            loss_slabs.data_ptr() if loss_slabs is not None else None,

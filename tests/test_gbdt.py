@@ -1,0 +1,128 @@
+"""GBDT with XGBoost semantics: formulas, pruning, exact-vs-hist equivalence, persistence."""
+import numpy as np
+import pytest
+
+from euromillioner_amd.data.draws import DrawSet, featurize_raw, multi_hot
+from euromillioner_amd.models import gbdt as G
+
+
+def _ref_data(n=None):
+    ds = DrawSet.synthetic(seed=1)
+    raw = featurize_raw(ds).astype(float)
+    return raw[:, 1:], (raw[:, 0] >= 5).astype(float)
+
+
+def test_single_split_hand_computed():
+    # 4 rows, one feature; logistic from margin 0: p = .5, g = p - y, h = .25
+    X = np.array([[0.0], [0.0], [1.0], [1.0]])
+    y = np.array([0.0, 0.0, 1.0, 1.0])
+    m = G.GBDT(nround=1, max_depth=1, gamma=0.0, eta=1.0, min_child_weight=0.1, backend="numpy").fit(X, y)
+    tr = m.trees
+    # G_L = 1.0 (0.5+0.5), H_L = 0.5 ; G_R = -1.0, H_R = 0.5 ; G = 0, H = 1
+    gain = 1.0 / 1.5 + 1.0 / 1.5 - 0.0
+    assert tr.status[0, 0] == 1 and abs(tr.gain[0, 0] - gain) < 1e-6
+    assert abs(tr.leaf[0, 1] - (-1.0 / 1.5)) < 1e-6 and abs(tr.leaf[0, 2] - (1.0 / 1.5)) < 1e-6
+    assert tr.split_value[0, 0] == 0.5
+
+
+def test_gamma_prunes_weak_split():
+    X = np.array([[0.0], [0.0], [1.0], [1.0]])
+    y = np.array([0.0, 0.0, 1.0, 1.0])
+    m = G.GBDT(nround=1, max_depth=1, gamma=2.0, min_child_weight=0.1, backend="numpy").fit(X, y)  # gain 1.33 < gamma
+    assert m.trees.status[0, 0] == 2 and (m.trees.status[0, 1:] == 0).all()
+
+
+def test_min_child_weight_blocks_split():
+    X = np.array([[0.0], [1.0], [1.0], [1.0]])
+    y = np.array([1.0, 0.0, 0.0, 0.0])
+    m = G.GBDT(nround=1, max_depth=1, gamma=0.0, min_child_weight=0.5, backend="numpy").fit(X, y)
+    assert m.trees.status[0, 0] == 2  # left child hessian 0.25 < 0.5
+
+
+def test_logistic_rejects_out_of_range_labels():
+    X, _ = _ref_data()
+    dow = featurize_raw(DrawSet.synthetic(seed=1))[:, 0].astype(float)
+    with pytest.raises(ValueError, match=r"label must be in \[0,1\]"):
+        G.GBDT(nround=1, backend="numpy").fit(X, dow)  # the reference's label_column=0 (defect D-d)
+
+
+def test_hist_equals_exact_first_split():
+    X, y = _ref_data()
+    g = np.full(len(y), 0.5) - y
+    h = np.full(len(y), 0.25)
+    cuts = G.make_cuts(X, 256)
+    bins = G.apply_bins(X, cuts)
+    nb = max(len(c) for c in cuts) + 1
+    hg = np.zeros((X.shape[1], nb))
+    hh = np.zeros_like(hg)
+    for f in range(X.shape[1]):
+        hg[f] = np.bincount(bins[:, f], weights=g, minlength=nb)
+        hh[f] = np.bincount(bins[:, f], weights=h, minlength=nb)
+    gain, f, b, _, _ = G._best_split_hist(hg, hh, g.sum(), h.sum(), 1.0, 1.0)
+    ex = [G.exact_greedy_split(X[:, k], g, h, 1.0, 1.0) for k in range(X.shape[1])]
+    best_f = int(np.argmax([e[0] for e in ex]))
+    assert best_f == f
+    assert abs(ex[f][0] - gain) < 1e-9 and ex[f][1] == cuts[f][b]
+
+
+def test_reference_config_trains_and_predicts():
+    X, y = _ref_data()
+    n = int(0.7 * len(y))
+    m = G.GBDT.from_params({"booster": "gbtree", "eta": 1.0, "max_depth": 3, "objective": "reg:logistic",
+                            "subsample": 1, "gamma": 1.0, "eval_metric": "logloss"}, nround=30, backend="numpy")
+    m.fit(X[:n], y[:n], evals={"train": (X[:n], y[:n]), "test": (X[n:], y[n:])})
+    assert len(m.history) == 30
+    assert m.history[-1]["train"] < m.history[0]["train"]
+    p = m.predict(X[:n])
+    assert p.dtype == np.float32 and p.shape == (n, 1)
+    # cpu_predictor traversal on raw values == margins accumulated during training
+    assert np.allclose(G.transform(m.objective, m.predict_margin(X[:n])), p, atol=1e-6)
+
+
+def test_multi_task_next_draw():
+    ds = DrawSet.synthetic(n=3000, seed=4, planted=0.9, calendar=False)
+    X = multi_hot(ds.numbers[:-1])
+    Y = multi_hot(ds.numbers[1:])
+    m = G.GBDT(nround=10, max_depth=3, gamma=1.0, eta=0.5, backend="numpy").fit(X[:2000], Y[:2000])
+    P = m.predict(X[2000:])
+    assert P.shape == (len(X) - 2000, 62)
+    from euromillioner_amd import metrics as M
+
+    met = M.draw_metrics(np.log(P / (1 - P)), Y[2000:])
+    assert met["acc"] > 0.93
+
+
+def test_json_roundtrip(tmp_path):
+    X, y = _ref_data()
+    m = G.GBDT(nround=5, backend="numpy").fit(X, y)
+    p = tmp_path / "m.json"
+    m.save(str(p))
+    m2 = G.GBDT.load(str(p))
+    assert np.array_equal(m.predict(X), m2.predict(X))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obj", ["reg:logistic", "reg:squarederror"])
+def test_hip_engine_matches_oracle(obj):
+    X, y = _ref_data()
+    n = int(0.7 * len(y))
+    kw = dict(nround=40, max_depth=3, gamma=1.0, eta=1.0 if obj == "reg:logistic" else 0.3, objective=obj,
+              eval_metric="logloss" if obj == "reg:logistic" else "rmse")
+    a = G.GBDT(backend="numpy", **kw).fit(X[:n], y[:n], evals={"test": (X[n:], y[n:])})
+    b = G.GBDT(backend="hip", **kw).fit(X[:n], y[:n], evals={"test": (X[n:], y[n:])})
+    assert np.array_equal(a.trees.status, b.trees.status)
+    assert np.array_equal(a.trees.feat, b.trees.feat)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)
+    assert np.allclose(a.predict(X[n:]), b.predict(X[n:], backend="hip"), atol=1e-5)
+    assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-4
+
+
+@pytest.mark.gpu
+def test_hip_engine_multitask():
+    ds = DrawSet.synthetic(n=20000, seed=4, planted=0.9, calendar=False)
+    X = multi_hot(ds.numbers[:-1])
+    Y = multi_hot(ds.numbers[1:])
+    a = G.GBDT(nround=8, eta=0.5, backend="numpy").fit(X[:15000], Y[:15000])
+    b = G.GBDT(nround=8, eta=0.5, backend="hip").fit(X[:15000], Y[:15000])
+    assert np.array_equal(a.trees.feat, b.trees.feat)
+    assert np.allclose(a.predict(X[15000:]), b.predict(X[15000:], backend="hip"), atol=1e-5)
