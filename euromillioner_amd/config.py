@@ -68,7 +68,7 @@ class GBDTConfig:
     min_child_weight: float = 1.0  # XGBoost default
     base_score: float = 0.5  # XGBoost default
     max_bin: int = 256
-    target: str = "reference"  # reference (label_column of the raw features) | next-draw
+    target: str = "next-draw"  # next-draw (62 boosters) | reference (label_column of the raw features; D-d)
     device: str = "auto"  # auto | cuda | cpu
 
 

@@ -259,12 +259,14 @@ class GBDT:
         p = dict(params)
         if p.get("booster", "gbtree") != "gbtree":
             raise ValueError("only booster=gbtree is supported")
-        return cls(eta=float(p.get("eta", 0.3)), max_depth=int(p.get("max_depth", 6)),
-                   objective=p.get("objective", "reg:squarederror"), subsample=float(p.get("subsample", 1)),
-                   gamma=float(p.get("gamma", 0.0)), reg_lambda=float(p.get("lambda", 1.0)),
-                   min_child_weight=float(p.get("min_child_weight", 1.0)),
-                   base_score=float(p.get("base_score", 0.5)), eval_metric=p.get("eval_metric", "logloss"),
-                   nround=nround, **kw)
+        args = dict(eta=float(p.get("eta", 0.3)), max_depth=int(p.get("max_depth", 6)),
+                    objective=p.get("objective", "reg:squarederror"), subsample=float(p.get("subsample", 1)),
+                    gamma=float(p.get("gamma", 0.0)), reg_lambda=float(p.get("lambda", 1.0)),
+                    min_child_weight=float(p.get("min_child_weight", 1.0)),
+                    base_score=float(p.get("base_score", 0.5)), eval_metric=p.get("eval_metric", "logloss"),
+                    nround=nround)
+        args.update(kw)
+        return cls(**args)
 
     @property
     def base_margin(self) -> float:
@@ -308,29 +310,94 @@ class GBDT:
         return self
 
     def _fit_numpy(self, X, bins, nbins, Y, evals):
+        """Oracle, vectorised over tasks and nodes: per level one GEMM of the one-hot bin matrix
+        [n, sum(bins)] with (g, h) scattered by (task, node)."""
         n, T = Y.shape
-        R = self.nround
-        trees = TreeArrays(T * R, self.max_depth)
+        R, D = self.nround, self.max_depth
+        NN = 2 ** (D + 1) - 1
+        F = bins.shape[1]
+        trees = TreeArrays(R * T, D)
         # float32 margins / gradients, float64 histogram sums: XGBoost's GradientPair / GradStats
         margin = np.full((n, T), self.base_margin, dtype=np.float32)
         ev_margin = {k: np.full((len(v[0]), T), self.base_margin, dtype=np.float32) for k, v in evals.items()}
-        Y32 = Y.astype(np.float32)
         ev_bins = {k: apply_bins(np.asarray(v[0], np.float64), self.cuts) for k, v in evals.items()}
+        Y32 = Y.astype(np.float32)
+        nbf = np.array([len(c) + 1 for c in self.cuts])
+        off = np.concatenate([[0], np.cumsum(nbf)])
+        onehot = np.zeros((n, off[-1]), dtype=np.float64)
+        for f in range(F):
+            onehot[np.arange(n), off[f] + bins[:, f]] = 1.0
+        row_feat = np.repeat(np.arange(F), nbf)
+        rowseg_start = off[row_feat]
+        valid_row = (np.arange(off[-1]) - rowseg_start) < (nbf[row_feat] - 1)  # not the last bin of a feature
         rng = np.random.default_rng(self.seed)
         hist = []
+        tix = np.arange(T)
         for rnd in range(R):
+            g, h = gradients(self.objective, margin, Y32)
+            if self.subsample < 1.0:
+                keep = (rng.random((n, T)) < self.subsample).astype(np.float32)
+                g, h = g * keep, h * keep
+            g64, h64 = g.astype(np.float64), h.astype(np.float64)
+            node = np.zeros((n, T), dtype=np.int64)
+            st = np.zeros((T, NN), np.int8)
+            st[:, 0] = 2
+            feat = np.full((T, NN), -1, np.int32)
+            sbin = np.zeros((T, NN), np.int32)
+            gain = np.zeros((T, NN))
+            Gs = np.zeros((T, NN))
+            Hs = np.zeros((T, NN))
+            Gs[:, 0], Hs[:, 0] = g64.sum(0), h64.sum(0)
+            for depth in range(D):
+                first, nl = 2 ** depth - 1, 2 ** depth
+                rel = node - first  # [n, T]
+                act = (rel >= 0) & (rel < nl)
+                col = np.where(act, tix[None, :] * nl + rel, 0)
+                Zg = np.zeros((n, T * nl))
+                Zh = np.zeros((n, T * nl))
+                rows = np.nonzero(act)
+                Zg[rows[0], col[rows]] = g64[rows]
+                Zh[rows[0], col[rows]] = h64[rows]
+                HG = onehot.T @ Zg  # [sum bins, T*nl]
+                HH = onehot.T @ Zh
+                # segmented prefix sums: left sums for "bin <= b" of feature f, all columns at once
+                CG, CH = np.cumsum(HG, axis=0), np.cumsum(HH, axis=0)
+                baseg = np.where(rowseg_start[:, None] > 0, CG[np.maximum(rowseg_start - 1, 0)], 0.0)
+                baseh = np.where(rowseg_start[:, None] > 0, CH[np.maximum(rowseg_start - 1, 0)], 0.0)
+                GL, HL = CG - baseg, CH - baseh
+                cols_t = np.repeat(tix, nl)
+                cols_i = np.tile(np.arange(nl), T) + first
+                Gn, Hn = Gs[cols_t, cols_i], Hs[cols_t, cols_i]
+                GR, HR = Gn[None, :] - GL, Hn[None, :] - HL
+                ok = valid_row[:, None] & (HL >= self.mcw) & (HR >= self.mcw) & (st[cols_t, cols_i] == 2)[None, :]
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    gn = GL * GL / (HL + self.lam) + GR * GR / (HR + self.lam) - (Gn * Gn / (Hn + self.lam))[None, :]
+                gn = np.where(ok, gn, -np.inf)
+                br = np.argmax(gn, axis=0)  # first max: lower feature, then lower bin
+                bv = gn[br, np.arange(gn.shape[1])]
+                for c in np.nonzero(np.isfinite(bv) & (bv > KRT_EPS))[0]:
+                    t, i, rrow = cols_t[c], cols_i[c], br[c]
+                    f = row_feat[rrow]
+                    st[t, i], feat[t, i], sbin[t, i], gain[t, i] = 1, f, rrow - off[f], bv[c]
+                    l, r = 2 * i + 1, 2 * i + 2
+                    st[t, l] = st[t, r] = 2
+                    Gs[t, l], Hs[t, l] = GL[rrow, c], HL[rrow, c]
+                    Gs[t, r], Hs[t, r] = Gs[t, i] - GL[rrow, c], Hs[t, i] - HL[rrow, c]
+                # partition
+                nd = node
+                k = (st[tix[None, :], nd] == 1) & act
+                fsel = feat[tix[None, :], nd]
+                bsel = bins[np.arange(n)[:, None], np.maximum(fsel, 0)]
+                child = 2 * nd + 1 + (bsel > sbin[tix[None, :], nd])
+                node = np.where(k, child, nd)
             for t in range(T):
-                k = rnd * T + t
-                g, h = gradients(self.objective, margin[:, t], Y32[:, t])
-                if self.subsample < 1.0:
-                    keep = rng.random(n) < self.subsample
-                    g, h = g * keep, h * keep
-                node = grow_tree_numpy(bins, nbins, g, h, self.max_depth, self.lam, self.mcw, self.gamma,
-                                       self.eta, trees, k)
-                margin[:, t] += trees.leaf[k, _leaf_of(trees, k, node)].astype(np.float32)
+                kk = rnd * T + t
+                trees.status[kk], trees.feat[kk], trees.sbin[kk], trees.gain[kk] = st[t], feat[t], sbin[t], gain[t]
+                _prune_and_leaves(trees, kk, Gs[t], Hs[t], self.lam, self.gamma, self.eta, D)
+                trees.cover[kk] = np.where(trees.status[kk] > 0, Hs[t], 0.0)
+                margin[:, t] += trees.leaf[kk, _leaf_of(trees, kk, node[:, t])].astype(np.float32)
                 for name, eb in ev_bins.items():
-                    en = _route_bins(trees, k, eb)
-                    ev_margin[name][:, t] += trees.leaf[k, en].astype(np.float32)
+                    ev_margin[name][:, t] += trees.leaf[kk, _route_bins(trees, kk, eb)].astype(np.float32)
             rec = {"round": rnd}
             for name, (ex, ey) in evals.items():
                 rec[name] = self._metric(np.asarray(ey, np.float64).reshape(len(ex), -1), ev_margin[name])

@@ -1,0 +1,156 @@
+"""End-to-end pipelines (T8).
+
+:func:`run_reference_pipeline` is the MI355X-native counterpart of ``Main.main``
+(``Main.java:35-148``): acquire draws -> featurize -> positional 70/30 split ->
+XGBoost-semantics GBDT (500 rounds, the reference's parameter map) with a train/test
+watch list -> predict -> print ``checkPredicts`` -> plus a metrics JSON line.
+
+Differences from the reference, all documented in SURVEY.md §7.5:
+* acquisition: no network — synthetic draws on the reference's calendar, a CSV, or an
+  offline copy of the HTML page (``--html``);
+* CSVs are proper newline-terminated files written to ``--workdir`` (D-b/D-c/D-h);
+* default target is the next draw (62 boosters), because the reference's label
+  (column 0 = day_of_week, 1..7) is invalid for ``reg:logistic`` (D-d); ``--target
+  reference`` reproduces it (and fails the same way XGBoost does unless the objective
+  is changed, e.g. ``--objective reg:squarederror``);
+* ``--reference-compat`` reproduces D-f (a second booster trained on the validation
+  split) so ``check_predicts`` compares the same two arrays as the reference;
+* errors are reported accurately with a non-zero exit code (D-g).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import os
+import tempfile
+import time
+
+import numpy as np
+
+from . import log as L
+from . import metrics as M
+from .config import RunConfig
+from .data.draws import DrawSet, featurize_raw, multi_hot, positional_split
+
+
+def load_draws(cfg: RunConfig) -> DrawSet:
+    d = cfg.data
+    if d.source == "synthetic":
+        ds = DrawSet.synthetic(n=d.n_draws, seed=d.seed, planted=d.planted)
+    elif d.source == "csv":
+        from .data.csv_io import read_draws_csv
+
+        ds = read_draws_csv(_need(d.path))
+    elif d.source == "reference-csv":
+        from .data.csv_io import read_reference_csv, reference_records_to_drawset
+
+        paths = [p for p in _need(d.path).split(",") if p]
+        ds = reference_records_to_drawset(np.concatenate([read_reference_csv(p) for p in paths]))
+    elif d.source == "html":
+        from .data.html_table import parse_results_table
+
+        with open(_need(d.path), encoding="utf-8") as f:
+            ds = parse_results_table(f.read(), d.html_table_class)
+    else:
+        raise ValueError(f"unknown data source {d.source!r}")
+    if ds.dates is not None and len(ds):
+        lo = np.datetime64(d.from_date, "D")
+        hi = np.datetime64(d.to_date, "D")
+        keep = (ds.dates >= lo) & (ds.dates <= hi)
+        if not keep.all() and d.source != "synthetic":
+            ds = DrawSet(ds.numbers[keep], ds.dates[keep], ds.meta)
+    ds.validate()
+    return ds
+
+
+def _need(path):
+    if not path:
+        raise ValueError("this data source needs --data-path")
+    if not os.path.exists(path.split(",")[0]):
+        raise FileNotFoundError(path)
+    return path
+
+
+def gbdt_dataset(ds: DrawSet, cfg: RunConfig):
+    """(X, Y, feature names) for the configured GBDT target."""
+    if cfg.gbdt.target == "reference":
+        raw = featurize_raw(ds).astype(np.float64)
+        lc = cfg.data.label_column
+        y = raw[:, lc]
+        X = np.delete(raw, lc, axis=1)
+        return X, y[:, None], "reference"
+    # next-draw: multi-hot of draw t (+ its date fields) -> multi-hot of draw t+1, 62 boosters
+    X = multi_hot(ds.numbers[:-1]).astype(np.float64)
+    if ds.dates is not None:
+        raw = featurize_raw(ds)[:-1, :4].astype(np.float64)
+        X = np.concatenate([X, raw], axis=1)
+    Y = multi_hot(ds.numbers[1:]).astype(np.float64)
+    return X, Y, "next-draw"
+
+
+def run_reference_pipeline(cfg: RunConfig, out=None) -> dict:
+    log = L.get("Main")
+    t0 = time.time()
+    ds = load_draws(cfg)
+    log.info(f"loaded {len(ds)} draws from {cfg.data.source} "
+             f"({ds.meta.get('planted', 0.0) if cfg.data.source == 'synthetic' else 'n/a'} planted)")
+    workdir = cfg.data.workdir or tempfile.mkdtemp(prefix="emn_")
+    os.makedirs(workdir, exist_ok=True)
+    X, Y, target = gbdt_dataset(ds, cfg)
+    n = len(X)
+    margin = positional_split(n, cfg.data.train_pct)
+    Xtr, Ytr, Xva, Yva = X[:margin], Y[:margin], X[margin:], Y[margin:]
+    # materialise the split like Main.java:69-108 (fixed format), for inspection / reuse
+    from .data.csv_io import write_draws_csv
+
+    write_draws_csv(os.path.join(workdir, "emn.csv"), ds.slice(0, margin + (1 if target == "next-draw" else 0)))
+    write_draws_csv(os.path.join(workdir, "emn_validation.csv"), ds.slice(margin, len(ds)))
+
+    from .models.gbdt import GBDT
+
+    g = cfg.gbdt
+    mk = dict(nround=g.nround, reg_lambda=g.reg_lambda, min_child_weight=g.min_child_weight,
+              base_score=g.base_score, max_bin=g.max_bin, backend=_gbdt_backend(cfg), log=log,
+              log_every=max(1, g.nround // 20))
+    watches = {"train": (Xtr, Ytr), "test": (Xva, Yva)}
+    booster = GBDT.from_params(cfg.gbdt_params(), **mk).fit(Xtr, Ytr, evals=watches)
+    p_train = booster.predict(Xtr)
+    if cfg.reference_compat:
+        booster_test = GBDT.from_params(cfg.gbdt_params(), **mk).fit(Xva, Yva, evals=watches)  # D-f
+        p_val = booster_test.predict(Xva)
+    else:
+        p_val = booster.predict(Xva)
+    compat = M.check_predicts(p_train, p_val)
+    (out.write if out else print)(str(compat).lower() + ("\n" if out else ""))  # Main.java:143 prints the boolean
+    res = {"pipeline": "reference", "target": target, "n_draws": len(ds), "n_train": int(margin),
+           "n_val": int(n - margin), "backend": booster.backend_used, "check_predicts": compat,
+           "train_" + g.eval_metric: booster.history[-1].get("train") if booster.history else None,
+           "val_" + g.eval_metric: booster.history[-1].get("test") if booster.history else None,
+           "seconds": round(time.time() - t0, 3), "workdir": workdir}
+    if target == "next-draw" and len(Xva):
+        margins = booster.predict_margin(Xva)
+        res["val"] = M.draw_metrics(margins, Yva, loss="bce")
+        res["chance"] = M.chance_levels()
+    if cfg.ckpt.path:
+        booster.save(cfg.ckpt.path)
+        res["checkpoint"] = cfg.ckpt.path
+    return res
+
+
+def _gbdt_backend(cfg: RunConfig) -> str:
+    dev = cfg.gbdt.device if cfg.gbdt.device != "auto" else cfg.device
+    if dev == "cpu":
+        return "numpy"
+    if dev == "cuda":
+        return "hip"
+    return "auto"
+
+
+def date_str(d) -> str:
+    return str(np.datetime64(d, "D")) if d is not None else ""
+
+
+def next_draw_date(last: np.datetime64) -> np.datetime64:
+    d = last.astype(_dt.date) + _dt.timedelta(days=1)
+    while not (d.weekday() == 4 or (d.weekday() == 1 and d >= _dt.date(2011, 5, 10))):
+        d += _dt.timedelta(days=1)
+    return np.datetime64(d, "D")

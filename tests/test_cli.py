@@ -1,0 +1,77 @@
+"""CLI integration: the default pipeline (== Main.main), subcommands, exit codes."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(args, env=None, timeout=600):
+    e = dict(os.environ)
+    e.update(env or {})
+    e["PYTHONPATH"] = ROOT
+    p = subprocess.run([sys.executable, "-m", "euromillioner_amd"] + args, capture_output=True, text=True,
+                       timeout=timeout, env=e, cwd=ROOT)
+    return p.returncode, p.stdout, p.stderr
+
+
+def last_json(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+def test_default_pipeline_small(tmp_path):
+    rc, out, err = run(["--nround", "10", "--workdir", str(tmp_path), "--device", "cpu"])
+    assert rc == 0, err + out
+    lines = out.splitlines()
+    assert "false" in lines  # Main.java:143 prints checkPredicts(train, validation) -> lengths differ
+    res = last_json(out)
+    assert res["n_draws"] == 1328 and res["n_train"] == int(0.7 * 1327) and res["target"] == "next-draw"
+    assert os.path.exists(tmp_path / "emn.csv") and os.path.exists(tmp_path / "emn_validation.csv")
+    assert "train-logloss" in out  # per-round watch-list logging (XGBoost4J format)
+
+
+def test_reference_target_fails_like_xgboost():
+    rc, out, err = run(["--target", "reference", "--nround", "2", "--device", "cpu"])
+    assert rc == 3
+    assert "label must be in [0,1]" in out + err
+
+
+def test_reference_compat_squared_error():
+    rc, out, err = run(["--target", "reference", "--objective", "reg:squarederror", "--eval-metric", "rmse",
+                        "--nround", "5", "--reference-compat", "--device", "cpu"])
+    assert rc == 0, err + out
+    assert last_json(out)["check_predicts"] is False
+
+
+def test_gen_and_csv_source(tmp_path):
+    f = tmp_path / "d.csv"
+    rc, out, _ = run(["gen", "--n", "500", "--planted", "0.9", "--out", str(f)])
+    assert rc == 0 and json.loads(out)["draws"] == 500
+    rc, out, err = run(["run", "--data-source", "csv", "--data-path", str(f), "--nround", "20", "--eta", "0.5",
+                        "--device", "cpu"])
+    assert rc == 0, err
+    res = last_json(out)
+    assert res["n_draws"] == 500 and res["val"]["acc"] > 0.9
+
+
+def test_html_source():
+    fix = os.path.join(ROOT, "tests", "fixtures", "results_table.html")
+    rc, out, err = run(["--data-source", "html", "--data-path", fix, "--nround", "3", "--device", "cpu"])
+    assert rc == 0, err
+    assert last_json(out)["n_draws"] == 12
+
+
+def test_missing_file_exit_code():
+    rc, out, err = run(["--data-source", "csv", "--data-path", "/nonexistent.csv"])
+    assert rc == 3
+
+
+def test_bad_flag_value():
+    rc, _, _ = run(["--nround", "abc"])
+    assert rc == 2
+
+
+def test_info():
+    rc, out, _ = run(["info"])
+    assert rc == 0 and "native" in json.loads(out)
