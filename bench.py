@@ -92,7 +92,15 @@ def main():
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="fused = our HIP kernels (headline); torch = plain PyTorch/hipBLASLt eager (comparison)")
+    ap.add_argument("--model", default="mlp", choices=["mlp", "mlp-wide"],
+                    help="mlp = 62->128->62 (headline, fused kernel); mlp-wide = 62->8192->8192->62 (GEMM path)")
+    ap.add_argument("--hidden", default=None, help="GEMM-path hidden sizes, e.g. 8192,8192")
     a = ap.parse_args()
+    if a.model == "mlp-wide":
+        if a.batch == 1 << 20:
+            a.batch = 1 << 16
+        if a.draws_per_gpu == (1 << 24) + 1:
+            a.draws_per_gpu = (1 << 20) * 3 + 1
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -123,7 +131,18 @@ def main():
         raise SystemExit("dataset too small for the batch")
 
     n_off = max(1, (margin - B) // B)
-    if a.impl == "fused":
+    sizes = (62, 128, 62)
+    if a.model == "mlp-wide":
+        from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+
+        hidden = tuple(int(h) for h in (a.hidden or "8192,8192").split(","))
+        sizes = (62,) + hidden + (62,)
+        model = GemmMLPTrainer(sizes, dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group)
+        model.broadcast_parameters()
+
+        def step(i):
+            return model.step(draws, B, offset=(i % n_off) * B)
+    elif a.impl == "fused":
         model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group)
         model.broadcast_parameters()
 
@@ -137,8 +156,9 @@ def main():
 
     use_graph = bool(a.graph) and world == 1
     graph = None
+    loss_t = None
     for i in range(a.warmup):
-        step(i)
+        loss_t = step(i)
     torch.cuda.synchronize()
     if use_graph:
         # offsets baked into graph nodes: capture n_off variants lazily would be heavy; capture a
@@ -151,7 +171,7 @@ def main():
             for gi in range(G):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):
-                    step(gi)
+                    loss_t = step(gi)
                 graphs.append(g)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -180,13 +200,19 @@ def main():
         t = torch.tensor([ms], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
-    loss = float(model.loss_out.item() if group is None else model.grad_io[-1].item())
+    loss = float(loss_t.reshape(-1)[0].item()) if loss_t is not None else float("nan")
 
     ev = {}
     if not a.no_eval:
         ev = model.evaluate(draws, n_samples - margin, offset=margin)
 
     value = B * world / (ms / 1000.0)
+    desc = "mlp " + "->".join(str(x) for x in sizes) + " relu, " + (
+        "grouped softmax-CE" if a.loss == "softmax" else "sigmoid-BCE")
+    extra = {}
+    if a.model == "mlp-wide":
+        tf = model.flops_per_sample() * B / (ms / 1000.0) / 1e12
+        extra = {"tflops_per_gpu": tf, "flops_per_sample": model.flops_per_sample()}
     if rank == 0:
         out = {
             "metric": "samples/sec training 3-layer MLP (62-in/62-out)",
@@ -201,12 +227,12 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (seeded Euromillions draws, planted Markov p=%.2f; random-init weights)" % a.planted,
-            "config": {"model": "mlp 62->128->62 relu, grouped softmax-CE" if a.loss == "softmax" else
-                       "mlp 62->128->62 relu, sigmoid-BCE",
+            "config": {"model": desc,
                        "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": B, "optimizer": "adam", "hipgraph": use_graph},
             "train_loss_last": loss,
             "val": ev,
+            **extra,
         }
         print(json.dumps(out))
     if world > 1:

@@ -147,6 +147,52 @@ __global__ void onehot_kernel(const uint64_t* __restrict__ masks, const int32_t*
   *reinterpret_cast<bf16x8*>(out + s * 64 + c * 8) = bits_to_bf16x8((uint32_t)(m >> (8 * c)) & 0xFFu);
 }
 
+// K10: loss + dL/dlogits for the GEMM-path MLPs.  One wavefront per sample, lane j = output j
+// (62 live lanes; 62/63 are padding and get dz = 0).  dz is written bf16 (the next GEMM's
+// operand) already scaled by grad_scale (1/global_batch); per-block loss sums -> partials.
+__global__ void loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __restrict__ masks,
+                                 const int32_t* __restrict__ sidx, int64_t B, int64_t offset, int loss_kind,
+                                 float grad_scale, __bf16* __restrict__ dz, int ldz, float* __restrict__ partials) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ float red[4];
+  const int64_t s = (int64_t)blockIdx.x * 4 + w;
+  float loss = 0.f;
+  if (s < B) {
+    const int64_t idx = sidx ? (int64_t)sidx[s] : offset + s;
+    const uint64_t tm = masks[idx + 1] & (MAIN_BITS | STAR_BITS);
+    const bool live = lane < 62;
+    const float z = live ? logits[s * ld + lane] : 0.f;
+    const float y = live ? (float)((tm >> lane) & 1ull) : 0.f;
+    float g = 0.f;
+    if (loss_kind == 0) {
+      const bool main = lane < 50;
+      const float mx_m = wave_max(main ? z : -INFINITY);
+      const float mx_s = wave_max(live && !main ? z : -INFINITY);
+      const float mx = main ? mx_m : mx_s;
+      const float e = live ? __expf(z - mx) : 0.f;
+      const float se_m = wave_sum(main ? e : 0.f), se_s = wave_sum(live && !main ? e : 0.f);
+      const float se = main ? se_m : se_s;
+      // target counts as wave sums: a lane-selected pair of 64-bit popcounts here produced wrong
+      // counts for some waves on gfx950 (ROCm 7.2; ISA looked right, results were nondeterministic)
+      const float sy_m = wave_sum(main ? y : 0.f), sy_s = wave_sum(live && !main ? y : 0.f);
+      const float sy = main ? sy_m : sy_s;
+      const float inv = 1.f / fmaxf(sy, 1.f);
+      const float p = e / se;
+      g = live ? (p * sy - y) * inv : 0.f;
+      loss = wave_sum(live ? -y * (z - mx - __logf(se)) * inv : 0.f);
+    } else {
+      const float sg = 1.f / (1.f + __expf(-z));
+      g = live ? (sg - y) * (1.f / 62.f) : 0.f;
+      const float l = fmaxf(z, 0.f) - z * y + __logf(1.f + __expf(-fabsf(z)));
+      loss = wave_sum(live ? l : 0.f) * (1.f / 62.f);
+    }
+    dz[s * ldz + lane] = (__bf16)(g * grad_scale);
+  }
+  if (lane == 0) red[w] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 }  // namespace
 
 EM_API int em_draw_metrics(const float* logits, int ld, const uint64_t* draws, const int32_t* sidx, int64_t B,
@@ -175,6 +221,18 @@ EM_API int em_onehot_encode(const uint64_t* draws, const int32_t* sidx, int64_t 
   const int64_t n = B * 8;
   hipLaunchKernelGGL(onehot_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, draws, sidx, B, offset,
                      which, with_bias, (__bf16*)out);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_loss_grad(const float* logits, int ld, const uint64_t* masks, const int32_t* sidx, int64_t B,
+                        int64_t offset, int loss_kind, float grad_scale, void* dz, int ldz, float* partials,
+                        hipStream_t stream) {
+  if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
+    return EM_ERR_ARG;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(loss_grad_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks, sidx,
+                     B, offset, loss_kind, grad_scale, (__bf16*)dz, ldz, partials);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,253 @@
+"""GEMM-path MLP trainer: any ``62 -> h1 -> ... -> 62`` stack on the K1-K3 MFMA GEMM.
+
+Used for the BASELINE "Wide MLP (62->8192->8192->62) bf16 DP=8" config and for custom
+layer sizes; the 62->128->62 flagship uses the single-launch fused kernel instead
+(:class:`~euromillioner_amd.models.mlp.FusedSmallMLP`).  The reference's DL4J
+``MultiLayerNetwork.fit`` (declared ``pom.xml:62-66``, never called) is the behaviour
+being re-implemented: dense layers, ReLU, softmax/BCE output, Adam.
+
+Per step (all on the current HIP stream, no host sync):
+
+1. K14 multi-hot encode of the batch straight from the 64-bit draw masks -> bf16 [B, 64];
+2. forward GEMMs with fused bias+act (bf16 activations), fp32 logits;
+3. K10 fused loss + dL/dlogits (bf16, pre-scaled by 1 / global batch);
+4. backward, last layer first: wgrad (fp32, written in place into the flat gradient
+   buffer) + bias colsum, then dgrad with act' fused; as soon as a layer's gradients
+   exist their all-reduce is launched (``async_op``: RCCL's stream overlaps the
+   remaining backward GEMMs; chunks of ``bucket_mb``);
+5. one fused Adam over the flat fp32 master weights that also refreshes the bf16
+   shadow the GEMMs read (no per-step weight casts).
+
+Flat layout per layer (padded: input and output 62 -> 64, hidden to multiples of 8; the
+pads stay exactly zero): ``W [N_pad, K_pad]`` (nn.Linear orientation) then ``b [N_pad]``;
+one extra slot at the end carries the step loss through the same all-reduce.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import fused_mlp as FM
+from ..ops import linear as LIN
+from ..ops import _native as N
+from .mlp import DrawMLP, FusedSmallMLP
+
+
+def _pad(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+class GemmMLPTrainer:
+    def __init__(self, sizes=(62, 8192, 8192, 62), device="cuda", activation: str = "relu", loss: str = "softmax",
+                 lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
+                 state_dict: dict | None = None, process_group=None, bucket_mb: float = 25.0):
+        if sizes[0] != 62 or sizes[-1] != 62:
+            raise ValueError("draw MLPs are 62-in / 62-out")
+        if activation not in ("relu", "tanh", "sigmoid"):
+            raise ValueError("activation must be relu|tanh|sigmoid")
+        if activation == "sigmoid" and any(h % 8 for h in sizes[1:-1]):
+            raise ValueError("sigmoid needs hidden sizes that are multiples of 8 (sigmoid(0) != 0 on pads)")
+        if loss not in FM.LOSS_KINDS:
+            raise ValueError(f"loss must be one of {list(FM.LOSS_KINDS)}")
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("GemmMLPTrainer runs on the GPU (use DrawMLP on the CPU)")
+        N.lib()
+        self.sizes = tuple(int(s) for s in sizes)
+        self.padded = (64,) + tuple(_pad(h) for h in self.sizes[1:-1]) + (64,)
+        self.activation, self.loss_name, self.group = activation, loss, process_group
+        self.bucket_elems = max(1 << 16, int(bucket_mb * (1 << 20) // 4))
+        self.offsets = []
+        off = 0
+        for kp, np_ in zip(self.padded[:-1], self.padded[1:]):
+            self.offsets.append((off, off + np_ * kp, off + np_ * kp + np_))
+            off += np_ * kp + np_
+        self.P = off
+        dev = self.device
+        self.params = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(self.P + 1, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        self.shadow = torch.zeros(self.P, dtype=torch.bfloat16, device=dev)
+        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
+        self.state = torch.zeros(2, dtype=torch.int32, device=dev)
+        if state_dict is None:
+            state_dict = DrawMLP(self.sizes, activation=activation, seed=seed).state_dict()
+        self.load_state_dict(state_dict)
+        self._ws_cache: dict[int, dict] = {}
+        self._checked = False
+
+    # ------------------------------------------------------------------ layout
+    def _views(self, flat: torch.Tensor, i: int):
+        a, b, c = self.offsets[i]
+        np_, kp = self.padded[i + 1], self.padded[i]
+        return flat[a:b].view(np_, kp), flat[b:c]
+
+    @property
+    def world(self) -> int:
+        if self.group is None:
+            return 1
+        import torch.distributed as dist
+
+        return dist.get_world_size(self.group)
+
+    def flops_per_sample(self) -> float:
+        """Executed MFMA FLOPs per sample (forward + wgrad + dgrad of layers >= 1), padded shapes."""
+        f = 0.0
+        for i, (kp, np_) in enumerate(zip(self.padded[:-1], self.padded[1:])):
+            f += 2 * kp * np_ * (3 if i > 0 else 2)
+        return f
+
+    def _ws(self, B: int) -> dict:
+        ws = self._ws_cache.get(B)
+        if ws is None:
+            dev = self.device
+            ws = {"x": torch.empty(B, 64, dtype=torch.bfloat16, device=dev),
+                  "act": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in self.padded[1:-1]],
+                  "dz": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in self.padded[1:]],
+                  "logits": torch.empty(B, 64, dtype=torch.float32, device=dev),
+                  "part": torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=dev)}
+            self._ws_cache = {B: ws}  # keep one batch size resident
+        return ws
+
+    # ------------------------------------------------------------------ compute
+    @staticmethod
+    def prepare(draws) -> torch.Tensor:
+        return FusedSmallMLP.prepare(draws)
+
+    def _forward(self, masks, B, offset, sidx, ws):
+        x = FM.onehot(masks, B, offset=offset, which=0, bias=False, sidx=sidx, out=ws["x"])
+        h, inputs = x, []
+        L = len(self.offsets)
+        for i in range(L):
+            w, b = self._views(self.shadow, i)
+            _, bf = self._views(self.params, i)
+            inputs.append(h)
+            last = i == L - 1
+            out = ws["logits"] if last else ws["act"][i]
+            h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out)
+        return h, inputs
+
+    def _check(self, masks, B, offset, sidx):
+        if not self._checked:
+            FM._check_draws(masks, sidx, B, offset)
+            self._checked = True
+
+    def step(self, masks: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None,
+             global_batch: int | None = None) -> torch.Tensor:
+        """One optimizer step on B local samples; returns the global mean loss (device tensor)."""
+        self._check(masks, B, offset, sidx)
+        ws = self._ws(B)
+        gb = global_batch if global_batch is not None else B * self.world
+        logits, inputs = self._forward(masks, B, offset, sidx, ws)
+        dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
+                                 grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
+        torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
+        self.grads[self.P:].mul_(1.0 / gb)
+        handles = []
+        dist = None
+        if self.group is not None:
+            import torch.distributed as dist
+        L = len(self.offsets)
+        for i in reversed(range(L)):
+            gw, gbias = self._views(self.grads, i)
+            LIN.linear_wgrad(dz, inputs[i], out=gw)
+            LIN.colsum(dz, out=gbias)
+            if dist is not None:
+                a = self.offsets[i][0]
+                c = self.offsets[i][2] if i < L - 1 else self.P + 1  # the last layer also carries the loss slot
+                for s in range(a, c, self.bucket_elems):
+                    handles.append(dist.all_reduce(self.grads[s:min(c, s + self.bucket_elems)],
+                                                   op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            if i > 0:
+                w, _ = self._views(self.shadow, i)
+                dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
+        for h in handles:
+            h.wait()
+        FM.adam_flat(self.params, self.grads[:self.P], self.m, self.v, self.hp, self.state, 1.0, shadow=self.shadow)
+        return self.grads[self.P:]
+
+    def grads_only(self, masks, B, offset=0, sidx=None):
+        """(loss, {name: grad}) for tests: same kernels, no all-reduce, no update."""
+        ws = self._ws(B)
+        logits, inputs = self._forward(masks, B, offset, sidx, ws)
+        dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx, grad_scale=1.0 / B,
+                                 dz=ws["dz"][-1], partials=ws["part"])
+        out = {}
+        for i in reversed(range(len(self.offsets))):
+            gw, gbias = self._views(self.grads, i)
+            LIN.linear_wgrad(dz, inputs[i], out=gw)
+            LIN.colsum(dz, out=gbias)
+            k, n = self.sizes[i], self.sizes[i + 1]
+            out[f"layers.{i}.weight"] = gw[:n, :k].clone()
+            out[f"layers.{i}.bias"] = gbias[:n].clone()
+            if i > 0:
+                w, _ = self._views(self.shadow, i)
+                dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
+        return float(part.double().sum().item()) / B, out
+
+    def logits(self, masks, B, offset=0, sidx=None) -> torch.Tensor:
+        lg, _ = self._forward(masks, B, offset, sidx, self._ws(B))
+        return lg
+
+    def evaluate(self, masks, B, offset=0, sidx=None, chunk: int = 1 << 16) -> dict:
+        tot = np.zeros(8, dtype=np.float64)
+        done = 0
+        while done < B:
+            b = min(chunk, B - done)
+            o = offset + done if sidx is None else 0
+            si = None if sidx is None else sidx[done:done + b]
+            lg = self.logits(masks, b, o, si)
+            tot += FM.draw_metrics(lg, masks, b, loss=self.loss_name, offset=o, sidx=si).double().sum(0).cpu().numpy()
+            done += b
+        if self.group is not None:
+            import torch.distributed as dist
+
+            t = torch.tensor(tot, dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, group=self.group)
+            tot = t.cpu().numpy()
+        cnt = max(tot[7], 1.0)
+        out = {k: float(tot[i] / cnt) for i, k in enumerate(FM.METRIC_NAMES[:-1])}
+        out["count"] = int(tot[7])
+        return out
+
+    # ------------------------------------------------------------------ state
+    def _logical(self, flat: torch.Tensor) -> dict[str, torch.Tensor]:
+        out = {}
+        for i in range(len(self.offsets)):
+            w, b = self._views(flat, i)
+            k, n = self.sizes[i], self.sizes[i + 1]
+            out[f"layers.{i}.weight"] = w[:n, :k]
+            out[f"layers.{i}.bias"] = b[:n]
+        return out
+
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        return {k: v.detach().clone().cpu() for k, v in self._logical(self.params).items()}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.zero_()
+        for k, v in self._logical(self.params).items():
+            v.copy_(sd[k].to(self.device, torch.float32))
+        self.shadow.copy_(self.params)
+
+    def optimizer_state(self) -> dict:
+        return {"m": {k: v.clone().cpu() for k, v in self._logical(self.m).items()},
+                "v": {k: v.clone().cpu() for k, v in self._logical(self.v).items()},
+                "step": int(self.state[0].item()), "hp": self.hp.cpu().tolist()}
+
+    def load_optimizer_state(self, st: dict) -> None:
+        self.m.zero_()
+        self.v.zero_()
+        for name, buf in (("m", self.m), ("v", self.v)):
+            for k, v in self._logical(buf).items():
+                v.copy_(st[name][k].to(self.device, torch.float32))
+        self.state[0] = int(st.get("step", 0))
+        self.state[1] = 0
+
+    def broadcast_parameters(self, src: int = 0) -> None:
+        if self.group is None:
+            return
+        import torch.distributed as dist
+
+        dist.broadcast(self.params, src=src, group=self.group)
+        self.shadow.copy_(self.params)

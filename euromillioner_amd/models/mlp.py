@@ -69,12 +69,7 @@ class DrawMLP(nn.Module):
             from ..ops import linear as LIN
 
             act = {"relu": "relu", "sigmoid": "sigmoid", "identity": "none", "tanh": "tanh"}[self.activation]
-            h = x
-            for i, lin in enumerate(self.layers):
-                last = i == len(self.layers) - 1
-                h = LIN.linear(h, lin.weight, lin.bias, activation="none" if last else act,
-                               compute_dtype=self.compute_dtype)
-            return h
+            return LIN.mlp(x, [lin.weight for lin in self.layers], [lin.bias for lin in self.layers], act)
         h = x.to(self.compute_dtype) if self.compute_dtype != torch.float32 else x
         for i, lin in enumerate(self.layers):
             w, b = lin.weight, lin.bias

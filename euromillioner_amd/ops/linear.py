@@ -1,0 +1,206 @@
+"""Dense layers on the hand-written MFMA GEMM (``csrc/gemm.hip``, K1-K3) + fused loss (K10).
+
+The reference's DL4J ``DenseLayer``/``OutputLayer`` stack (declared in ``pom.xml:62-66``,
+never built) maps onto three GEMM shapes per layer, all served by one kernel template:
+
+=========  ==========================================  ====================  ===========
+pass       math                                         A / B layout          epilogue
+=========  ==========================================  ====================  ===========
+forward    ``Y = act(X W^T + b)``                       X [M,K] / W [N,K]     bias + act
+dgrad      ``dZ_prev = (dZ W) * act'(Y_prev)``          dZ [M,N] / W [N,K]    act backward
+wgrad      ``dW = dZ^T X``  (fp32, optional += )        dZ^T / X              alpha, beta
+=========  ==========================================  ====================  ===========
+
+Tensors handed to the kernel must have unit column stride, a row stride that is a
+multiple of 8 elements and 16-byte aligned storage (one 16-byte vector per lane);
+:func:`aligned` pads a copy when that does not hold (e.g. the 62-wide draw vectors).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+ACTS = {"none": 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
+
+N.register_signatures({
+    "em_gemm_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32,
+                              N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32, N._f32, N._f32,
+                              N._c_void_p]),
+    "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p]),
+    "em_loss_grad": (N._i32, [N._c_void_p, N._i32, N._c_void_p, N._c_void_p, N._i64, N._i64, N._i32, N._f32,
+                              N._c_void_p, N._i32, N._c_void_p, N._c_void_p]),
+})
+
+
+def round8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def is_aligned(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+def aligned(t: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """Return ``t`` (cast to dtype) as a view with a GEMM-friendly layout, copying only if needed."""
+    if t.dtype == dtype and is_aligned(t):
+        return t
+    r, c = t.shape
+    buf = torch.zeros(r, round8(c), dtype=dtype, device=t.device)
+    buf[:, :c] = t
+    return buf[:, :c]
+
+
+def empty_aligned(r: int, c: int, dtype: torch.dtype, device) -> torch.Tensor:
+    return torch.empty(r, round8(c), dtype=dtype, device=device)[:, :c]
+
+
+def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Tensor, M: int, N_: int, K: int,
+         bias: torch.Tensor | None = None, act: str = "none", dact_src: torch.Tensor | None = None,
+         dact: str = "relu", alpha: float = 1.0, beta: float = 0.0) -> torch.Tensor:
+    """Raw K1-K3 launch.  ``a``/``b`` are bf16 in their storage shape; ``out`` fp32 or bf16 [M, N]."""
+    for t, nm in ((a, "a"), (b, "b")):
+        N.check_cuda(t, nm, torch.bfloat16, contiguous=False)
+        if not is_aligned(t):
+            raise ValueError(f"{nm}: needs unit column stride, row stride %8 and 16-byte alignment")
+    N.check_cuda(out, "out", contiguous=False)
+    if out.dtype not in (torch.float32, torch.bfloat16) or out.stride(1) != 1 or tuple(out.shape) != (M, N_):
+        raise ValueError("out must be fp32/bf16 [M, N] with unit column stride")
+    exp_a = (M, K) if a_kc else (K, M)
+    exp_b = (N_, K) if b_kc else (K, N_)
+    if tuple(a.shape) != exp_a or tuple(b.shape) != exp_b:
+        raise ValueError(f"shape mismatch: a {tuple(a.shape)} vs {exp_a}, b {tuple(b.shape)} vs {exp_b}")
+    if bias is not None:
+        N.check_cuda(bias, "bias", torch.float32)
+        if bias.numel() < N_:
+            raise ValueError("bias too short")
+    ldm = 0
+    if dact_src is not None:
+        N.check_cuda(dact_src, "dact_src", torch.bfloat16, contiguous=False)
+        if tuple(dact_src.shape) != (M, N_) or dact_src.stride(1) != 1:
+            raise ValueError("dact_src must be bf16 [M, N] with unit column stride")
+        ldm = dact_src.stride(0)
+    N.call("em_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kc), b.data_ptr(), b.stride(0), int(b_kc),
+           out.data_ptr(), out.stride(0), int(out.dtype == torch.bfloat16), M, N_, K,
+           bias.data_ptr() if bias is not None else None, ACTS[act],
+           dact_src.data_ptr() if dact_src is not None else None, ldm, ACTS[dact] if dact_src is not None else 0,
+           float(alpha), float(beta), N.stream_handle(out.device))
+    return out
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, act: str = "none",
+               out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(x @ w.T + bias)``; x bf16 [M, K], w bf16 [N, K] (nn.Linear layout)."""
+    M, K = x.shape
+    N_ = w.shape[0]
+    if out is None:
+        out = empty_aligned(M, N_, out_dtype, x.device)
+    return gemm(x, True, w, True, out, M, N_, K, bias=bias, act=act)
+
+
+def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """``(dz @ w) * act'(y_prev)``; dz bf16 [M, N], w bf16 [N, K] -> bf16 [M, K]."""
+    M, N_ = dz.shape
+    K = w.shape[1]
+    if out is None:
+        out = empty_aligned(M, K, torch.bfloat16, dz.device)
+    if dact in ("none", "identity"):
+        y_prev = None
+    return gemm(dz, True, w, False, out, M, K, N_, dact_src=y_prev, dact=dact)
+
+
+def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None, alpha: float = 1.0,
+                 beta: float = 0.0) -> torch.Tensor:
+    """``alpha * dz^T @ x (+ beta * out)`` in fp32; dz [M, N], x [M, K] bf16 -> [N, K]."""
+    M, N_ = dz.shape
+    K = x.shape[1]
+    if out is None:
+        out = empty_aligned(N_, K, torch.float32, dz.device)
+    return gemm(dz, False, x, False, out, N_, K, M, alpha=alpha, beta=beta)
+
+
+def colsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
+           scale: float = 1.0) -> torch.Tensor:
+    """Bias gradient: fp32 column sums of a bf16 [M, N] matrix."""
+    N.check_cuda(x, "x", torch.bfloat16, contiguous=False)
+    M, N_ = x.shape
+    if out is None:
+        out = torch.empty(N_, dtype=torch.float32, device=x.device)
+    N.call("em_colsum_bf16", x.data_ptr(), x.stride(0), M, N_, out.data_ptr(), int(accumulate), float(scale),
+           N.stream_handle(x.device))
+    return out
+
+
+def loss_grad(logits: torch.Tensor, masks: torch.Tensor, B: int, loss: str = "softmax", offset: int = 0,
+              sidx: torch.Tensor | None = None, grad_scale: float = 1.0, dz: torch.Tensor | None = None,
+              partials: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """K10: (dz bf16 [B, 64] = grad_scale * dL/dlogits, per-block loss sums [ceil(B/4)])."""
+    from .fused_mlp import LOSS_KINDS, _check_draws
+
+    _check_draws(masks, sidx, B, offset)
+    N.check_cuda(logits, "logits", torch.float32, contiguous=False)
+    if logits.stride(1) != 1 or logits.shape[1] < 62:
+        raise ValueError("logits must be fp32 [B, >=62] with unit column stride")
+    if dz is None:
+        dz = torch.empty(B, 64, dtype=torch.bfloat16, device=logits.device)
+    if partials is None:
+        partials = torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=logits.device)
+    N.call("em_loss_grad", logits.data_ptr(), logits.stride(0), masks.data_ptr(),
+           sidx.data_ptr() if sidx is not None else None, B, offset, LOSS_KINDS[loss], float(grad_scale),
+           dz.data_ptr(), dz.stride(0), partials.data_ptr(), N.stream_handle(logits.device))
+    return dz, partials
+
+
+class _MLPFunction(torch.autograd.Function):
+    """Whole-stack autograd node: saves each layer's bf16 input, fuses act' into dgrad."""
+
+    @staticmethod
+    def forward(ctx, x, act, *wb):
+        ws, bs = wb[0::2], wb[1::2]
+        wq = [aligned(w.detach()) for w in ws]
+        h = aligned(x.detach())
+        inputs = []
+        for i, (w, b) in enumerate(zip(wq, bs)):
+            last = i == len(wq) - 1
+            inputs.append(h)
+            h = linear_fwd(h, w, b.detach().float().contiguous(), "none" if last else act,
+                           torch.float32 if last else torch.bfloat16)
+        ctx.act = act
+        ctx.wq = wq
+        ctx.inputs = inputs
+        ctx.shapes = [tuple(w.shape) for w in ws]
+        return h
+
+    @staticmethod
+    def backward(ctx, gy):
+        dz = aligned(gy)
+        n = len(ctx.wq)
+        grads = [None] * (2 * n)
+        gx = None
+        for i in reversed(range(n)):
+            x_i = ctx.inputs[i]
+            grads[2 * i] = linear_wgrad(dz, x_i)
+            grads[2 * i + 1] = colsum(dz)
+            if i > 0:
+                dz = linear_dgrad(dz, ctx.wq[i], x_i, ctx.act)
+            elif ctx.needs_input_grad[0]:
+                gx = linear_dgrad(dz, ctx.wq[0]).float()
+        ctx.inputs = None
+        return (gx, None, *grads)
+
+
+def mlp(x: torch.Tensor, weights, biases, activation: str = "relu") -> torch.Tensor:
+    """Dense stack on the HIP kernels: hidden layers bf16 + act, last layer fp32 logits."""
+    wb = []
+    for w, b in zip(weights, biases):
+        wb += [w, b]
+    return _MLPFunction.apply(x, activation, *wb)
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, activation: str = "none",
+           compute_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """Single layer (no autograd through the kernel; use :func:`mlp` for training)."""
+    del compute_dtype
+    b = bias.detach().float().contiguous() if bias is not None else None
+    return linear_fwd(aligned(x.detach()), aligned(weight.detach()), b, activation, torch.float32)

@@ -1,0 +1,170 @@
+"""GPU numerics for the MFMA GEMM (K1-K3), colsum, fused loss-grad (K10) and the GEMM-path
+MLPs vs plain PyTorch fp32 references."""
+import pytest
+import torch
+
+from euromillioner_amd.data.draws import DrawSet, multi_hot
+from euromillioner_amd.models import losses as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.bfloat16().float()
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+ACT = {"none": lambda x: x, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 70), (128, 128, 64), (1, 7, 5), (517, 1030, 333)])
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh"])
+def test_forward_nt(M, N, K, act):
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(N, device="cuda", generator=g)
+    y = LIN.linear_fwd(LIN.aligned(x), LIN.aligned(w), b, act, torch.float32)
+    ref = ACT[act](_bf(x) @ _bf(w).t() + b)
+    assert y.shape == (M, N)
+    assert _rel(y, ref) < 2e-3, _rel(y, ref)
+    yb = LIN.linear_fwd(LIN.aligned(x), LIN.aligned(w), b, act, torch.bfloat16)
+    assert _rel(yb, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 70), (64, 8192, 64), (2048, 136, 1000)])
+@pytest.mark.parametrize("dact", ["none", "relu", "sigmoid", "tanh"])
+def test_dgrad_nn(M, N, K, dact):
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(3 + M + N)
+    dz = torch.randn(M, N, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g)
+    y = ACT["sigmoid" if dact == "sigmoid" else "tanh" if dact == "tanh" else "relu"](
+        torch.randn(M, K, device="cuda", generator=g))
+    yq = LIN.aligned(y)
+    out = LIN.linear_dgrad(LIN.aligned(dz), LIN.aligned(w), yq, dact)
+    ref = _bf(dz) @ _bf(w)
+    yf = yq.float()
+    if dact == "relu":
+        ref = ref * (yf > 0)
+    elif dact == "sigmoid":
+        ref = ref * yf * (1 - yf)
+    elif dact == "tanh":
+        ref = ref * (1 - yf * yf)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 62, 64), (4096, 200, 136), (77, 9, 13)])
+def test_wgrad_tn_and_accumulate(M, N, K):
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    dz = torch.randn(M, N, device="cuda", generator=g)
+    x = torch.randn(M, K, device="cuda", generator=g)
+    dzq, xq = LIN.aligned(dz), LIN.aligned(x)
+    gw = LIN.linear_wgrad(dzq, xq)
+    ref = _bf(dz).t() @ _bf(x)
+    assert _rel(gw, ref) < 1e-4, _rel(gw, ref)
+    gw2 = LIN.linear_wgrad(dzq, xq, out=gw.clone(), alpha=0.5, beta=1.0)
+    assert _rel(gw2, 1.5 * ref) < 1e-4
+    cs = LIN.colsum(dzq)
+    assert _rel(cs, _bf(dz).sum(0)) < 1e-5
+
+
+def test_large_square_gemm():
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    a = torch.randn(4096, 4096, device="cuda", generator=g).bfloat16()
+    b = torch.randn(4096, 4096, device="cuda", generator=g).bfloat16()
+    y = LIN.linear_fwd(a, b, None, "none", torch.float32)
+    ref = a.float() @ b.float().t()
+    assert _rel(y, ref) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def data():
+    from euromillioner_amd.ops.fused_mlp import rows_to_masks
+
+    ds = DrawSet.synthetic(n=5000, seed=3, planted=0.6, calendar=False)
+    return ds, rows_to_masks(torch.from_numpy(ds.numbers).cuda())
+
+
+@pytest.mark.parametrize("loss", ["softmax", "bce"])
+def test_loss_grad_kernel(data, loss):
+    from euromillioner_amd.ops import linear as LIN
+
+    ds, masks = data
+    B, off = 1001, 17
+    g = torch.Generator(device="cuda").manual_seed(1)
+    z = (3 * torch.randn(B, 64, device="cuda", generator=g)).requires_grad_()
+    Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).cuda()
+    ref = L.LOSSES[loss](z, Y)
+    ref.backward()
+    dz, part = LIN.loss_grad(z.detach(), masks, B, loss, offset=off, grad_scale=1.0 / B)
+    assert abs(float(part.double().sum()) / B - ref.item()) < 1e-4 * max(1, ref.item())
+    assert _rel(dz[:, :62], z.grad[:, :62]) < 1e-2
+    assert float(dz[:, 62:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "sigmoid"])
+def test_drawmlp_hip_autograd_matches_fp32(data, act):
+    from euromillioner_amd.models.mlp import DrawMLP
+
+    ds, _ = data
+    X = torch.from_numpy(multi_hot(ds.numbers[:700])).float()
+    Y = torch.from_numpy(multi_hot(ds.numbers[1:701])).float()
+    cpu = DrawMLP((62, 96, 40, 62), activation=act, seed=4)
+    gpu = DrawMLP((62, 96, 40, 62), activation=act, seed=4).cuda()
+    lc = cpu.loss(cpu(X), Y)
+    lc.backward()
+    lg = gpu.loss(gpu(X.cuda()), Y.cuda())
+    lg.backward()
+    assert abs(lc.item() - lg.item()) < 1e-2 * max(1, lc.item())
+    for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
+        assert _rel(pg.grad.cpu(), pc.grad) < 5e-2, n
+
+
+@pytest.mark.parametrize("sizes", [(62, 96, 40, 62), (62, 128, 62), (62, 300, 62)])
+def test_gemm_trainer_grads_match_drawmlp(data, sizes):
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+    from euromillioner_amd.models.mlp import DrawMLP
+
+    ds, masks = data
+    B, off = 2048, 5
+    tr = GemmMLPTrainer(sizes, seed=9)
+    ref = DrawMLP(sizes, seed=9)
+    X = torch.from_numpy(multi_hot(ds.numbers[off:off + B])).float()
+    Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).float()
+    l = ref.loss(ref(X), Y)
+    l.backward()
+    lk, gk = tr.grads_only(masks, B, offset=off)
+    assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
+    for n, p in ref.named_parameters():
+        assert _rel(gk[n].cpu(), p.grad) < 5e-2, n
+    # the pads of the flat buffers stay zero
+    sd = tr.state_dict()
+    for n, p in ref.named_parameters():
+        assert torch.equal(sd[n], p.detach())
+
+
+def test_gemm_trainer_learns_planted(data):
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+
+    ds, masks = data
+    tr = GemmMLPTrainer((62, 256, 256, 62), lr=3e-3, seed=0)
+    ntr = 3800
+    first = None
+    for s in range(150):
+        loss = tr.step(masks, ntr, offset=0)
+        if first is None:
+            first = loss.item()
+    assert loss.item() < first
+    ev = tr.evaluate(masks, 1000, offset=ntr)
+    assert ev["acc"] > ev["trivial_acc"], ev
