@@ -250,6 +250,7 @@ class GBDT:
         self.log, self.log_every = log, log_every
         self.trees: TreeArrays | None = None
         self.cuts = None
+        self.num_feature = None
         self.n_tasks = 1
         self.history: list[dict] = []
 
@@ -450,6 +451,7 @@ class GBDT:
             trees.append({"id": k, "task": int(k % self.n_tasks), "nodes": nodes})
         return {"learner": {"objective": self.objective, "base_score": self.base_score,
                             "num_target": self.n_tasks,
+                            "num_feature": len(self.cuts) if self.cuts is not None else self.num_feature,
                             "params": {"eta": self.eta, "max_depth": self.max_depth, "gamma": self.gamma,
                                        "lambda": self.lam, "min_child_weight": self.mcw,
                                        "subsample": self.subsample, "nround": self.nround},
@@ -468,6 +470,7 @@ class GBDT:
                 reg_lambda=p["lambda"], min_child_weight=p["min_child_weight"], base_score=d["base_score"],
                 nround=p["nround"], subsample=p.get("subsample", 1.0), backend="numpy")
         m.n_tasks = d["num_target"]
+        m.num_feature = d.get("num_feature")
         trees = d["gradient_booster"]["model"]["trees"]
         tr = TreeArrays(len(trees), m.max_depth)
         for k, t in enumerate(trees):

@@ -75,3 +75,37 @@ def test_bad_flag_value():
 def test_info():
     rc, out, _ = run(["info"])
     assert rc == 0 and "native" in json.loads(out)
+
+
+def test_cli_train_rf_and_predict(tmp_path, capsys):
+    from euromillioner_amd.cli import main
+
+    ck = str(tmp_path / "rf.npz")
+    rc = main(["train", "--model", "rf", "--device", "cpu", "--n-draws", "600", "--planted", "0.5",
+               "--trees", "5", "--rf-max-depth", "4", "--ckpt", ck])
+    assert rc == 0
+    out = capsys.readouterr().out
+    assert '"model": "rf"' in out
+    rc = main(["predict", "--ckpt", ck, "--n-draws", "600", "--planted", "0.5"])
+    assert rc == 0
+    line = [l for l in capsys.readouterr().out.splitlines() if "*" in l and "{" not in l][0]
+    main_nums, stars = line.split("*")
+    assert len(main_nums.split()) == 5 and len(stars.split()) == 2
+
+
+def test_cli_gbdt_checkpoint_predict(tmp_path, capsys):
+    from euromillioner_amd.cli import main
+
+    ck = str(tmp_path / "g.json")
+    rc = main(["train", "--model", "gbdt", "--device", "cpu", "--n-draws", "300", "--nround", "5",
+               "--ckpt", ck, "--workdir", str(tmp_path)])
+    assert rc == 0
+    rc = main(["predict", "--ckpt", ck, "--n-draws", "300"])
+    assert rc == 0
+    assert '"model": "gbdt"' in capsys.readouterr().out
+
+
+def test_cli_predict_missing_checkpoint_is_data_error(tmp_path):
+    from euromillioner_amd.cli import main
+
+    assert main(["predict", "--ckpt", str(tmp_path / "nope.zip")]) == 3

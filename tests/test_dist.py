@@ -1,0 +1,129 @@
+"""Multi-process data parallelism on the CPU (gloo, 127.0.0.1): DP == single process,
+bucketed == plain all-reduce, tree-parallel forest == single forest, fault injection
+fails loudly instead of hanging, checkpoint resume continues exactly."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "_dist_worker.py")
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port):
+    env = dict(os.environ)
+    env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), OMP_NUM_THREADS="1", PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    return env
+
+
+def _launch(argv, world, timeout=240, cwd=None):
+    port = _port()
+    procs = [subprocess.Popen(argv, env=_env(r, world, port), cwd=cwd or ROOT, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out))
+    return outs
+
+
+def _train_argv(extra):
+    return [sys.executable, "-m", "euromillioner_amd", "train", "--model", "mlp", "--device", "cpu",
+            "--n-draws", "1201", "--planted", "0.7", "--seed", "5", "--eval-every", "0", "--log-level", "WARN"] + extra
+
+
+def _params(path):
+    from euromillioner_amd.ckpt import modelserializer as MS
+
+    ck = MS.load(path)
+    return ck["flat"], ck.get("m"), ck.get("v"), ck.get("extra", {})
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_equals_single_process(tmp_path, world):
+    """Full-batch DP over `world` gloo ranks == one process on the whole batch."""
+    single = str(tmp_path / "single.zip")
+    multi = str(tmp_path / "multi.zip")
+    # 1200 samples -> 840 train: divisible by 2 and 4, so every rank has the same local batch
+    common = ["--steps", "6", "--batch", "840", "--lr", "0.01"]
+    outs = _launch(_train_argv(common + ["--ckpt", single]), 1)
+    assert outs[0][0] == 0, outs[0][1][-2000:]
+    outs = _launch(_train_argv(common + ["--ckpt", multi]), world)
+    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    a, b = _params(single), _params(multi)
+    assert np.allclose(a[0], b[0], atol=2e-6), np.abs(a[0] - b[0]).max()
+    assert np.allclose(a[1], b[1], atol=1e-7) and np.allclose(a[2], b[2], atol=1e-9)
+
+
+@pytest.mark.parametrize("bucket_mb", ["0.01", "25"])
+def test_bucketed_allreduce_equals_plain(tmp_path, bucket_mb):
+    out = str(tmp_path / "b.json")
+    res = _launch([sys.executable, WORKER, "buckets", out, bucket_mb], 2)
+    assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
+    r = json.load(open(out))
+    assert r["max_err"] < 1e-6
+    if bucket_mb == "0.01":
+        assert r["n_buckets"] > 2  # several buckets, launched from the hooks during backward
+
+
+def test_tree_parallel_forest_equals_single(tmp_path):
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.forest import RandomForest, draw_features
+
+    out = str(tmp_path / "f.npz")
+    res = _launch([sys.executable, WORKER, "forest", out], 3)
+    assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
+    z = np.load(out, allow_pickle=False)
+    ds = DrawSet.synthetic(n=900, seed=3, planted=0.5, calendar=False)
+    X, Y, F = draw_features(ds.numbers)
+    rf = RandomForest(n_trees=7, max_depth=4, seed=2, device="cpu").fit(X, Y, F)
+    assert np.array_equal(z["feat"], rf.feat) and np.array_equal(z["value"], rf.value)
+
+
+def test_fault_injection_fails_loudly(tmp_path):
+    """Rank 1 dies at step 2 (exit 17); rank 0 must error out (non-zero) within the timeout."""
+    argv = _train_argv(["--steps", "50", "--batch", "64", "--fault-at-step", "2", "--fault-rank", "1",
+                        "--timeout", "30"])
+    outs = _launch(argv, 2, timeout=200)
+    assert outs[1][0] == 17, outs[1][1][-1500:]
+    assert outs[0][0] != 0, outs[0][1][-1500:]
+
+
+def test_resume_continues_exactly(tmp_path):
+    full = str(tmp_path / "full.zip")
+    part = str(tmp_path / "part.zip")
+    base = ["--batch", "200", "--lr", "0.005"]  # minibatches with shuffling
+    r = _launch(_train_argv(base + ["--steps", "12", "--ckpt", full]), 1)
+    assert r[0][0] == 0, r[0][1][-2000:]
+    r = _launch(_train_argv(base + ["--steps", "5", "--ckpt", part]), 1)
+    assert r[0][0] == 0, r[0][1][-2000:]
+    r = _launch(_train_argv(base + ["--steps", "12", "--ckpt", part, "--resume", part]), 1)
+    assert r[0][0] == 0, r[0][1][-2000:]
+    a, b = _params(full), _params(part)
+    assert b[3]["step"] == 12
+    assert np.allclose(a[0], b[0], atol=1e-6), np.abs(a[0] - b[0]).max()
+    assert np.allclose(a[1], b[1], atol=1e-7)
+
+
+def test_checkpoint_every_writes_intermediate(tmp_path):
+    p = str(tmp_path / "c.zip")
+    r = _launch(_train_argv(["--batch", "256", "--steps", "4", "--ckpt", p, "--ckpt-every", "2"]), 1)
+    assert r[0][0] == 0, r[0][1][-2000:]
+    assert _params(p)[3]["step"] == 4
