@@ -19,6 +19,8 @@
 // ds_read_b128 fragment reads); MN-contiguous tiles are stored [64 k][128] (256-B rows,
 // chunk ^ k&15) and read as MFMA fragments with ds_read_b64_tr_b16.  Block ids are
 // remapped so neighbouring tiles share an XCD's L2 (§5.5 T1, bijective form).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -26,6 +28,11 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand per stage
 constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;
+
+bool getenv_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] == '1';
+}
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
 
@@ -192,28 +199,338 @@ gemm_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict_
   }
 }
 
-// column sums of a bf16 [M][N] matrix into fp32 out[N] (+= if accumulate): bias gradients
-__global__ void colsum_kernel(const __bf16* __restrict__ X, int64_t ldx, int M, int N, float* __restrict__ out,
-                              int accumulate, float scale) {
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;  // 4 row partitions
-  __shared__ float red[4][64];
-  float s = 0.f;
-  if (col < N)
-    for (int m = part; m < M; m += 4) s += (float)X[(int64_t)m * ldx + col];
-  red[part][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (part == 0 && col < N) {
-    const float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x])) * scale;
-    out[col] = accumulate ? out[col] + t : t;
+// ============================================================================================
+// 256x256 NT GEMM (both operands K-contiguous): the large-shape path (wide MLP hidden layers).
+// 8 waves as 2(M) x 4(N), each 128x64 = 4x2 MFMA 32x32x16 tiles (128 accumulator registers);
+// BK = 64; per K-tile each wave issues 4+4 global_load_lds_dwordx4 (1 KiB each, 8 rows) into
+// the other LDS stage while it reads fragments and runs 32 MFMAs on the current one.  The LDS
+// image is lane-linear per instruction (glds writes base + lane*16), so the bank swizzle is
+// applied to the per-lane SOURCE address (cdna_hip_programming.md rule 21): logical chunk c of
+// row r sits at physical chunk c ^ ((r >> 1) & 7) of its 128-B row -- 16 distinct 16-B slots
+// for every ds_read_b128 lane group of the 32x32x16 operand read (MI355X_MICROARCH.md LDS table).
+constexpr int G_BM = 256, G_BN = 256, G_BK = 64, G_NT = 512;
+constexpr int G_TILE = G_BM * G_BK * 2;  // 32 KB per operand per stage
+constexpr int G_LOOP_LDS = 2 * 2 * G_TILE;  // 128 KB: 2 stages x (A, B)
+constexpr int G_EPI_LDS = 8 * 128 * 144;     // epilogue: per-wave 128 x 64 bf16 tile, 144-B rows
+constexpr int G_LDS = G_LOOP_LDS > G_EPI_LDS ? G_LOOP_LDS : G_EPI_LDS;
+
+EM_DEVICE uint32_t g_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// One operand's K-tile piece for this wave: 4 x buffer_load_dwordx4 ... lds (1 KiB = 8 rows each).
+// The descriptor covers the block's 256-row panel; the per-lane part is one 32-bit voffset per
+// row-group parity (the swizzle depends on (row >> 1) & 7), everything else is scalar.
+struct GPanel {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t voff[2];  // per-lane byte offsets for even / odd 8-row groups
+  uint32_t row_bytes;
+};
+
+EM_DEVICE GPanel g_panel(const __bf16* P, int64_t ld, int r0, int lane) {
+  GPanel g;
+  const __bf16* base = P + (int64_t)r0 * ld;
+  g.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
+  const int lr = lane >> 3;  // row within the 8-row group
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int c = (lane & 7) ^ ((4 * par + (lane >> 4)) & 7);  // (row >> 1) & 7 with row = 8g + lr
+    g.voff[par] = (uint32_t)((lr * ld + 8 * c) * 2);
   }
+  g.row_bytes = (uint32_t)(ld * 2);
+  return g;
+}
+
+EM_DEVICE void g_stage(const GPanel& g, int k0, char* lds_tile, int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int grp = wave * 4 + i;
+    const uint32_t soff = (uint32_t)(grp * 8) * g.row_bytes + (uint32_t)k0 * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rsrc, (EM_LDS void*)(lds_tile + grp * 1024), 16, g.voff[i & 1], soff,
+                                             0, 0);
+  }
+}
+
+template <int FN>
+EM_DEVICE float g_fn(float v) {
+  if (FN == ACT_RELU) return fmaxf(v, 0.f);
+  if (FN == ACT_SIGMOID) return 1.f / (1.f + __expf(-v));
+  if (FN == ACT_TANH) return tanhf(v);
+  return v;
+}
+template <int FN>
+EM_DEVICE float g_dfn(float y) {  // activation derivative from the saved output y
+  if (FN == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (FN == ACT_SIGMOID) return y * (1.f - y);
+  return 1.f - y * y;
+}
+
+// OUT_BF16: 1 -> bf16 C (optionally + transposed C^T when HAS_CT), 0 -> fp32 C (+ beta * C_old)
+// FN: activation (DACT = 0, applied to alpha*acc + bias) or activation' (DACT = 1, multiplies
+// alpha*acc by act'(mask[m][n]))
+template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+__global__ void __launch_bounds__(G_NT, 1)
+gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                  void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
+                  const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                  float beta) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = N / G_BN;
+  const int nwg = (M / G_BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  const int ktiles = K / G_BK;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
+  g_stage(pa, 0, smem, wave_s);
+  g_stage(pb, 0, smem + G_TILE, wave_s);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int r = lane & 31, h = lane >> 5;
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const char* la = smem + (kt & 1) * 2 * G_TILE;
+    const char* lb = la + G_TILE;
+    if (kt + 1 < ktiles) {
+      char* na = smem + ((kt + 1) & 1) * 2 * G_TILE;
+      g_stage(pa, (kt + 1) * G_BK, na, wave_s);
+      g_stage(pb, (kt + 1) * G_BK, na + G_TILE, wave_s);
+    }
+#pragma unroll
+    for (int s = 0; s < G_BK / 16; ++s) {
+      bf16x8 a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + 32 * i + r, 2 * s + h));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + 32 * j + r, 2 * s + h));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns column `col`, rows rbase + 8g + e ----
+  // DACT: stage this wave's 128x64 tile of the saved activations through its own 18 KB of the
+  // (now idle) LDS with coalesced 16-B loads, instead of 128 scattered 2-B loads per lane.
+  const __bf16* ylds = reinterpret_cast<const __bf16*>(smem + wave * 128 * 144);
+  if (DACT) {
+    char* yw = smem + wave * 128 * 144;
+    const __bf16* ysrc = mask + (int64_t)(m0 + wm * 128) * ldm + n0 + wn * 64;
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+      const int q = lane + 64 * t;
+      const int row = q >> 3, ch = q & 7;
+      *reinterpret_cast<u32x4*>(yw + row * 144 + ch * 16) =
+          *reinterpret_cast<const u32x4*>(ysrc + (int64_t)row * ldm + ch * 8);
+    }
+    wave_lds_sync();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 64 + 32 * j + r;
+    const float bv = (!DACT && bias) ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rbase = m0 + wm * 128 + 32 * i + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t row = rbase + 8 * g + e;
+          float v = alpha * acc[i][j][4 * g + e];
+          if (DACT) {
+            const int lr = 32 * i + 4 * h + 8 * g + e, lc = 32 * j + r;
+            v *= g_dfn<FN>((float)ylds[lr * 72 + lc]);
+          } else {
+            v = g_fn<FN>(v + bv);
+          }
+          x[e] = v;
+          if (OUT_BF16) {
+            reinterpret_cast<__bf16*>(C)[row * ldc + col] = (__bf16)v;
+          } else {
+            float* cp = reinterpret_cast<float*>(C) + row * ldc + col;
+            *cp = beta != 0.f ? v + beta * *cp : v;
+          }
+        }
+        if (HAS_CT) {  // 4 consecutive rows of C = 8 contiguous bytes of C^T
+          __bf16 t4[4] = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
+          u32x2 pk;
+          __builtin_memcpy(&pk, t4, 8);
+          *reinterpret_cast<u32x2*>(CT + (int64_t)col * ldct + rbase + 8 * g) = pk;
+        }
+      }
+    }
+  }
+}
+
+template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
+             int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
+             int64_t ldm, float alpha, float beta) {
+  static bool attr = false;
+  auto kern = gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(G_NT), G_LDS, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm,
+                     alpha, beta);
+  return 0;
+}
+
+// runtime (out, act/dact, ct) -> one of 15 instantiations
+int g_dispatch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
+               int64_t ldc, int c_bf16, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act,
+               const __bf16* mask, int64_t ldm, int dact, float alpha, float beta) {
+#define EM_G(OB, FN, DA, CTV) \
+  return g_launch<OB, FN, DA, CTV>(grid, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, beta)
+  if (!c_bf16) {
+    if (act != ACT_NONE || mask || CT) return EM_ERR_ARG;
+    EM_G(0, ACT_NONE, 0, 0);
+  }
+  const bool ct = CT != nullptr;
+  if (mask) {
+    if (act != ACT_NONE) return EM_ERR_ARG;
+    switch (dact) {
+      case ACT_RELU: if (ct) EM_G(1, ACT_RELU, 1, 1); else EM_G(1, ACT_RELU, 1, 0);
+      case ACT_SIGMOID: if (ct) EM_G(1, ACT_SIGMOID, 1, 1); else EM_G(1, ACT_SIGMOID, 1, 0);
+      case ACT_TANH: if (ct) EM_G(1, ACT_TANH, 1, 1); else EM_G(1, ACT_TANH, 1, 0);
+      default: return EM_ERR_ARG;
+    }
+  }
+  switch (act) {
+    case ACT_NONE: if (ct) EM_G(1, ACT_NONE, 0, 1); else EM_G(1, ACT_NONE, 0, 0);
+    case ACT_RELU: if (ct) EM_G(1, ACT_RELU, 0, 1); else EM_G(1, ACT_RELU, 0, 0);
+    case ACT_SIGMOID: if (ct) EM_G(1, ACT_SIGMOID, 0, 1); else EM_G(1, ACT_SIGMOID, 0, 0);
+    case ACT_TANH: if (ct) EM_G(1, ACT_TANH, 0, 1); else EM_G(1, ACT_TANH, 0, 0);
+    default: return EM_ERR_ARG;
+  }
+#undef EM_G
+}
+
+// bf16 transpose: dst[c][r] = src[r][c]; 64x64 tiles through LDS, 16-B global accesses
+__global__ void __launch_bounds__(256) transpose_kernel(const __bf16* __restrict__ src, int64_t lds_, int R, int Cc,
+                                                        __bf16* __restrict__ dst, int64_t ldd) {
+  __shared__ __bf16 tile[64][72];
+  const int tiles_c = (Cc + 63) / 64;
+  const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int q = tid + it * 256;  // 512 chunks of 8 elements
+    const int rr = q >> 3, cc = (q & 7) * 8;
+    const int gr = r0 + rr, gc = c0 + cc;
+    if (gr < R && gc + 8 <= Cc) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(src + (int64_t)gr * lds_ + gc);
+      const __bf16* e = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tile[rr][cc + k] = e[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tile[rr][cc + k] = (gr < R && gc + k < Cc) ? src[(int64_t)gr * lds_ + gc + k] : (__bf16)0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int q = tid + it * 256;
+    const int cc = q >> 3, rr = (q & 7) * 8;  // output row = source col
+    const int gc = c0 + cc, gr = r0 + rr;
+    if (gc >= Cc) continue;
+    __bf16 e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = tile[rr + k][cc];
+    if (gr + 8 <= R) {
+      *reinterpret_cast<u32x4*>(dst + (int64_t)gc * ldd + gr) = *reinterpret_cast<const u32x4*>(e);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (gr + k < R) dst[(int64_t)gc * ldd + gr + k] = e[k];
+    }
+  }
+}
+
+// column sums of a bf16 [M][N] matrix (bias gradients), deterministic two-pass:
+// pass 1: block (column group of 512, row chunk of CS_ROWS) -> fp32 partial [chunk][N]
+// pass 2: fixed-order sum over chunks (+ optional accumulate / scale)
+constexpr int CS_ROWS = 512;
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const __bf16* __restrict__ X, int64_t ldx, int M, int N,
+                                                             float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int cg = threadIdx.x & 63, rp = threadIdx.x >> 6;  // 64 column groups of 8 x 4 row phases
+  const int c0 = blockIdx.x * 512 + cg * 8;
+  const int r0 = blockIdx.y * CS_ROWS;
+  const int r1 = min(M, r0 + CS_ROWS);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 + 8 <= N) {
+    for (int rr = r0 + rp; rr < r1; rr += 4) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(X + (int64_t)rr * ldx + c0);
+      const __bf16* e = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += (float)e[k];
+    }
+  } else if (c0 < N) {
+    for (int rr = r0 + rp; rr < r1; rr += 4)
+      for (int k = 0; k < 8 && c0 + k < N; ++k) acc[k] += (float)X[(int64_t)rr * ldx + c0 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rp][cg * 8 + k] = acc[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int col = blockIdx.x * 512 + c;
+    if (col < N) part[(int64_t)blockIdx.y * N + col] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int chunks, int N, float* __restrict__ out,
+                                    int accumulate, float scale) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * N + col];
+  s *= scale;
+  out[col] = accumulate ? out[col] + s : s;
+}
+
+// row sums of a bf16 [R][C] matrix (bias gradients from a transposed dZ copy): one wavefront per row
+__global__ void __launch_bounds__(256) rowsum_kernel(const __bf16* __restrict__ X, int64_t ldx, int R, int Cc,
+                                                     float* __restrict__ out, int accumulate, float scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const __bf16* xr = X + (int64_t)row * ldx;
+  float s = 0.f;
+  int c = lane * 8;
+  for (; c + 8 <= Cc; c += 512) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(xr + c);
+    const __bf16* e = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += (float)e[k];
+  }
+  for (int k = c; k < Cc && k < c + 8; ++k) s += (float)xr[k];
+  s = wave_sum(s) * scale;
+  if (lane == 0) out[row] = accumulate ? out[row] + s : s;
 }
 
 }  // namespace
 
 EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                         int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
-                        int64_t ldm, int dact, float alpha, float beta, hipStream_t stream) {
+                        int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, hipStream_t stream) {
   if (!A || !B || !C || M < 0 || N < 0 || K < 0 || act < 0 || act > 3) return EM_ERR_ARG;
   if (mask && (dact < 1 || dact > 3)) return EM_ERR_ARG;
   if (M == 0 || N == 0) return 0;
@@ -227,6 +544,17 @@ EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int
     (void)hipFuncSetAttribute((const void*)gemm_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = true;
   }
+  const bool big = a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
+                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL");
+  if (big) {
+    const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
+                              ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
+                              beta);
+    if (rc) return rc;
+    EM_CHECK_LAUNCH();
+    return 0;
+  }
+  if (ct) return EM_ERR_ARG;  // the transposed copy is only produced by the 256 path
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const __bf16* a = (const __bf16*)A;
   const __bf16* b = (const __bf16*)B;
@@ -243,11 +571,41 @@ EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int
   return 0;
 }
 
-EM_API int em_colsum_bf16(const void* X, int64_t ldx, int M, int N, float* out, int accumulate, float scale,
+EM_API int em_transpose_bf16(const void* src, int64_t ld_src, int R, int Cc, void* dst, int64_t ld_dst,
+                             hipStream_t stream) {
+  if (!src || !dst || R < 0 || Cc < 0) return EM_ERR_ARG;
+  if ((ld_src & 7) || (ld_dst & 7) || (((uintptr_t)src | (uintptr_t)dst) & 15)) return EM_ERR_ARG;
+  if (R == 0 || Cc == 0) return 0;
+  const int64_t grid = (int64_t)((R + 63) / 64) * ((Cc + 63) / 64);
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (const __bf16*)src, ld_src, R, Cc,
+                     (__bf16*)dst, ld_dst);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_colsum_ws_floats(int M, int N) { return ((M + CS_ROWS - 1) / CS_ROWS) * N; }
+
+EM_API int em_colsum_bf16(const void* X, int64_t ldx, int M, int N, float* out, int accumulate, float scale, float* ws,
                           hipStream_t stream) {
-  if (!X || !out || M < 0 || N < 0) return EM_ERR_ARG;
+  if (!X || !out || !ws || M < 0 || N < 0 || (ldx & 7) || (((uintptr_t)X) & 15)) return EM_ERR_ARG;
   if (N == 0) return 0;
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, (const __bf16*)X, ldx, M, N, out,
+  const int chunks = M > 0 ? (M + CS_ROWS - 1) / CS_ROWS : 0;
+  if (chunks > 0) {
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 511) / 512, chunks), dim3(256), 0, stream, (const __bf16*)X,
+                       ldx, M, N, ws);
+    EM_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, ws, chunks, N, out, accumulate,
+                     scale);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_rowsum_bf16(const void* X, int64_t ldx, int R, int Cc, float* out, int accumulate, float scale,
+                          hipStream_t stream) {
+  if (!X || !out || R < 0 || Cc < 0 || (ldx & 7) || (((uintptr_t)X) & 15)) return EM_ERR_ARG;
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(rowsum_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, (const __bf16*)X, ldx, R, Cc, out,
                      accumulate, scale);
   EM_CHECK_LAUNCH();
   return 0;

@@ -98,15 +98,38 @@ class GemmMLPTrainer:
             f += 2 * kp * np_ * (3 if i > 0 else 2)
         return f
 
+    def _plan(self, B: int) -> dict:
+        """Which layers run the 256-tile NT path for their weight gradient (needs transposed
+        copies of dZ_i and X_i, produced by the neighbouring GEMMs' transposed epilogue)."""
+        P, L = self.padded, len(self.offsets)
+        big_wgrad = [False] * L
+        for i in range(1, L - 1):
+            big_wgrad[i] = (LIN.big_ok(P[i + 1], P[i], B) and LIN.big_ok(B, P[i + 1], P[i + 2])
+                            and LIN.big_ok(B, P[i], P[i - 1]))
+        big_dgrad = [i > 0 and LIN.big_ok(B, P[i], P[i + 1]) for i in range(L)]
+        return {"wgrad": big_wgrad, "dgrad": big_dgrad}
+
     def _ws(self, B: int) -> dict:
         ws = self._ws_cache.get(B)
         if ws is None:
             dev = self.device
+            plan = self._plan(B)
+            L = len(self.offsets)
+            P = self.padded
             ws = {"x": torch.empty(B, 64, dtype=torch.bfloat16, device=dev),
-                  "act": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in self.padded[1:-1]],
-                  "dz": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in self.padded[1:]],
+                  "act": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in P[1:-1]],
+                  "dz": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in P[1:]],
                   "logits": torch.empty(B, 64, dtype=torch.float32, device=dev),
-                  "part": torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=dev)}
+                  "part": torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=dev),
+                  "colsum_ws": torch.empty(max(1, (B + 511) // 512) * max(P), dtype=torch.float32, device=dev),
+                  "plan": plan,
+                  # transposed copies for the big wgrads: X_i^T (= Y_{i-1}^T) and dZ_i^T
+                  "actt": {i: torch.empty(P[i], B, dtype=torch.bfloat16, device=dev)
+                           for i in range(L) if plan["wgrad"][i]},
+                  "dzt": {i: torch.empty(P[i + 1], B, dtype=torch.bfloat16, device=dev)
+                          for i in range(L) if plan["wgrad"][i]},
+                  "wt": {i: torch.empty(P[i], P[i + 1], dtype=torch.bfloat16, device=dev)
+                         for i in range(L) if plan["dgrad"][i]}}
             self._ws_cache = {B: ws}  # keep one batch size resident
         return ws
 
@@ -115,7 +138,7 @@ class GemmMLPTrainer:
     def prepare(draws) -> torch.Tensor:
         return FusedSmallMLP.prepare(draws)
 
-    def _forward(self, masks, B, offset, sidx, ws):
+    def _forward(self, masks, B, offset, sidx, ws, train: bool = False):
         x = FM.onehot(masks, B, offset=offset, which=0, bias=False, sidx=sidx, out=ws["x"])
         h, inputs = x, []
         L = len(self.offsets)
@@ -125,8 +148,33 @@ class GemmMLPTrainer:
             inputs.append(h)
             last = i == L - 1
             out = ws["logits"] if last else ws["act"][i]
-            h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out)
+            ct = ws["actt"].get(i + 1) if train and not last else None  # X_{i+1}^T for layer i+1's wgrad
+            h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out, ct=ct)
         return h, inputs
+
+    def _backward(self, dz, inputs, ws, on_layer_done=None):
+        """Last layer first: wgrad + bias grad into the flat gradient buffer, then dgrad (act' fused)."""
+        plan = ws["plan"]
+        L = len(self.offsets)
+        for i in reversed(range(L)):
+            gw, gbias = self._views(self.grads, i)
+            if plan["wgrad"][i]:
+                LIN.linear_wgrad_nt(ws["dzt"][i], ws["actt"][i], out=gw)
+                LIN.rowsum(ws["dzt"][i], out=gbias)
+            else:
+                LIN.linear_wgrad(dz, inputs[i], out=gw)
+                LIN.colsum(dz, out=gbias, ws=ws["colsum_ws"])
+            if on_layer_done is not None:
+                on_layer_done(i)
+            if i > 0:
+                w, _ = self._views(self.shadow, i)
+                if plan["dgrad"][i]:
+                    wt = LIN.transpose(w, out=ws["wt"][i])
+                    dz = LIN.linear_dgrad_nt(dz, wt, inputs[i], self.activation, out=ws["dz"][i - 1],
+                                             ct=ws["dzt"].get(i - 1))
+                else:
+                    dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
+        return dz
 
     def _check(self, masks, B, offset, sidx):
         if not self._checked:
@@ -139,29 +187,25 @@ class GemmMLPTrainer:
         self._check(masks, B, offset, sidx)
         ws = self._ws(B)
         gb = global_batch if global_batch is not None else B * self.world
-        logits, inputs = self._forward(masks, B, offset, sidx, ws)
+        logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
         dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
                                  grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
         torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
         self.grads[self.P:].mul_(1.0 / gb)
         handles = []
-        dist = None
+        hook = None
         if self.group is not None:
             import torch.distributed as dist
-        L = len(self.offsets)
-        for i in reversed(range(L)):
-            gw, gbias = self._views(self.grads, i)
-            LIN.linear_wgrad(dz, inputs[i], out=gw)
-            LIN.colsum(dz, out=gbias)
-            if dist is not None:
+
+            L = len(self.offsets)
+
+            def hook(i):  # C1: launch this layer's bucket(s) while the remaining backward runs
                 a = self.offsets[i][0]
                 c = self.offsets[i][2] if i < L - 1 else self.P + 1  # the last layer also carries the loss slot
-                for s in range(a, c, self.bucket_elems):
-                    handles.append(dist.all_reduce(self.grads[s:min(c, s + self.bucket_elems)],
+                for s0 in range(a, c, self.bucket_elems):
+                    handles.append(dist.all_reduce(self.grads[s0:min(c, s0 + self.bucket_elems)],
                                                    op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-            if i > 0:
-                w, _ = self._views(self.shadow, i)
-                dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
+        self._backward(dz, inputs, ws, hook)
         for h in handles:
             h.wait()
         FM.adam_flat(self.params, self.grads[:self.P], self.m, self.v, self.hp, self.state, 1.0, shadow=self.shadow)
@@ -170,20 +214,16 @@ class GemmMLPTrainer:
     def grads_only(self, masks, B, offset=0, sidx=None):
         """(loss, {name: grad}) for tests: same kernels, no all-reduce, no update."""
         ws = self._ws(B)
-        logits, inputs = self._forward(masks, B, offset, sidx, ws)
+        logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
         dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx, grad_scale=1.0 / B,
                                  dz=ws["dz"][-1], partials=ws["part"])
+        self._backward(dz, inputs, ws)
         out = {}
-        for i in reversed(range(len(self.offsets))):
+        for i in range(len(self.offsets)):
             gw, gbias = self._views(self.grads, i)
-            LIN.linear_wgrad(dz, inputs[i], out=gw)
-            LIN.colsum(dz, out=gbias)
             k, n = self.sizes[i], self.sizes[i + 1]
             out[f"layers.{i}.weight"] = gw[:n, :k].clone()
             out[f"layers.{i}.bias"] = gbias[:n].clone()
-            if i > 0:
-                w, _ = self._views(self.shadow, i)
-                dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
         return float(part.double().sum().item()) / B, out
 
     def logits(self, masks, B, offset=0, sidx=None) -> torch.Tensor:

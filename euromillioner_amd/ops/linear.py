@@ -26,8 +26,12 @@ ACTS = {"none": 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
 N.register_signatures({
     "em_gemm_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32,
                               N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32, N._f32, N._f32,
-                              N._c_void_p]),
-    "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p]),
+                              N._c_void_p, N._i64, N._c_void_p]),
+    "em_colsum_ws_floats": (N._i32, [N._i32, N._i32]),
+    "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p,
+                                N._c_void_p]),
+    "em_rowsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p]),
+    "em_transpose_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i64, N._c_void_p]),
     "em_loss_grad": (N._i32, [N._c_void_p, N._i32, N._c_void_p, N._c_void_p, N._i64, N._i64, N._i32, N._f32,
                               N._c_void_p, N._i32, N._c_void_p, N._c_void_p]),
 })
@@ -55,10 +59,19 @@ def empty_aligned(r: int, c: int, dtype: torch.dtype, device) -> torch.Tensor:
     return torch.empty(r, round8(c), dtype=dtype, device=device)[:, :c]
 
 
+BIG_M, BIG_N, BIG_K = 256, 256, 64
+
+
+def big_ok(M: int, N_: int, K: int) -> bool:
+    """Shapes the 256x256 NT kernel takes (otherwise the 128x128 any-layout kernel runs)."""
+    return M % BIG_M == 0 and N_ % BIG_N == 0 and K % BIG_K == 0 and K > 0
+
+
 def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Tensor, M: int, N_: int, K: int,
          bias: torch.Tensor | None = None, act: str = "none", dact_src: torch.Tensor | None = None,
-         dact: str = "relu", alpha: float = 1.0, beta: float = 0.0) -> torch.Tensor:
-    """Raw K1-K3 launch.  ``a``/``b`` are bf16 in their storage shape; ``out`` fp32 or bf16 [M, N]."""
+         dact: str = "relu", alpha: float = 1.0, beta: float = 0.0, ct: torch.Tensor | None = None) -> torch.Tensor:
+    """Raw K1-K3 launch.  ``a``/``b`` are bf16 in their storage shape; ``out`` fp32 or bf16 [M, N].
+    ``ct`` (bf16 [N, M], 256-path only) receives a transposed copy of the output."""
     for t, nm in ((a, "a"), (b, "b")):
         N.check_cuda(t, nm, torch.bfloat16, contiguous=False)
         if not is_aligned(t):
@@ -80,22 +93,62 @@ def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Te
         if tuple(dact_src.shape) != (M, N_) or dact_src.stride(1) != 1:
             raise ValueError("dact_src must be bf16 [M, N] with unit column stride")
         ldm = dact_src.stride(0)
+    if ct is not None:
+        N.check_cuda(ct, "ct", torch.bfloat16, contiguous=False)
+        if not (a_kc and b_kc and big_ok(M, N_, K)) or tuple(ct.shape) != (N_, M) or not is_aligned(ct):
+            raise ValueError("ct needs the 256-tile NT path and an aligned bf16 [N, M] buffer")
     N.call("em_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kc), b.data_ptr(), b.stride(0), int(b_kc),
            out.data_ptr(), out.stride(0), int(out.dtype == torch.bfloat16), M, N_, K,
            bias.data_ptr() if bias is not None else None, ACTS[act],
            dact_src.data_ptr() if dact_src is not None else None, ldm, ACTS[dact] if dact_src is not None else 0,
-           float(alpha), float(beta), N.stream_handle(out.device))
+           float(alpha), float(beta), ct.data_ptr() if ct is not None else None, ct.stride(0) if ct is not None else 0,
+           N.stream_handle(out.device))
+    return out
+
+
+def transpose(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 [R, C] -> [C, R] (LDS-tiled, 16-B accesses)."""
+    N.check_cuda(x, "x", torch.bfloat16, contiguous=False)
+    if not is_aligned(x):
+        x = aligned(x)
+    R, Cc = x.shape
+    if out is None:
+        out = empty_aligned(Cc, R, torch.bfloat16, x.device)
+    N.call("em_transpose_bf16", x.data_ptr(), x.stride(0), R, Cc, out.data_ptr(), out.stride(0),
+           N.stream_handle(x.device))
     return out
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, act: str = "none",
-               out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None) -> torch.Tensor:
-    """``act(x @ w.T + bias)``; x bf16 [M, K], w bf16 [N, K] (nn.Linear layout)."""
+               out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None,
+               ct: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(x @ w.T + bias)``; x bf16 [M, K], w bf16 [N, K] (nn.Linear layout); ``ct`` gets the output^T."""
     M, K = x.shape
     N_ = w.shape[0]
     if out is None:
         out = empty_aligned(M, N_, out_dtype, x.device)
-    return gemm(x, True, w, True, out, M, N_, K, bias=bias, act=act)
+    return gemm(x, True, w, True, out, M, N_, K, bias=bias, act=act, ct=ct)
+
+
+def linear_dgrad_nt(dz: torch.Tensor, wt: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",
+                    out: torch.Tensor | None = None, ct: torch.Tensor | None = None) -> torch.Tensor:
+    """dgrad from a transposed weight copy ``wt`` [K, N] (256-tile NT path): ``(dz @ wt.T) * act'(y_prev)``."""
+    M, N_ = dz.shape
+    K = wt.shape[0]
+    if out is None:
+        out = empty_aligned(M, K, torch.bfloat16, dz.device)
+    if dact in ("none", "identity"):
+        y_prev = None
+    return gemm(dz, True, wt, True, out, M, K, N_, dact_src=y_prev, dact=dact, ct=ct)
+
+
+def linear_wgrad_nt(dzt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """wgrad from transposed copies: ``dzt`` [N, M], ``xt`` [K, M] -> fp32 ``dzt @ xt.T`` [N, K]."""
+    N_, M = dzt.shape
+    K = xt.shape[0]
+    if out is None:
+        out = empty_aligned(N_, K, torch.float32, dzt.device)
+    return gemm(dzt, True, xt, True, out, N_, K, M)
 
 
 def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",
@@ -111,23 +164,67 @@ def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None 
 
 
 def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None, alpha: float = 1.0,
-                 beta: float = 0.0) -> torch.Tensor:
-    """``alpha * dz^T @ x (+ beta * out)`` in fp32; dz [M, N], x [M, K] bf16 -> [N, K]."""
+                 beta: float = 0.0, split_k: int | None = None) -> torch.Tensor:
+    """``alpha * dz^T @ x (+ beta * out)`` in fp32; dz [M, N], x [M, K] bf16 -> [N, K].
+
+    Small outputs with a huge reduction (e.g. 64 x 8192 over a 64k batch) are split over K
+    (the batch) into fp32 partial slabs that are summed in a fixed order (deterministic)."""
     M, N_ = dz.shape
     K = x.shape[1]
     if out is None:
         out = empty_aligned(N_, K, torch.float32, dz.device)
-    return gemm(dz, False, x, False, out, N_, K, M, alpha=alpha, beta=beta)
+    tiles = ((N_ + 127) // 128) * ((K + 127) // 128)
+    if split_k is None:
+        split_k = 1
+        if tiles < 256 and M >= 8192:
+            split_k = max(1, min(512 // tiles, M // 4096))
+    if split_k <= 1:
+        return gemm(dz, False, x, False, out, N_, K, M, alpha=alpha, beta=beta)
+    step = (M + split_k - 1) // split_k
+    step = (step + 7) // 8 * 8
+    parts = torch.empty(split_k, N_, round8(K), dtype=torch.float32, device=dz.device)
+    n_used = 0
+    for s in range(split_k):
+        a, b = s * step, min(M, (s + 1) * step)
+        if a >= b:
+            break
+        gemm(dz[a:b], False, x[a:b], False, parts[s, :, :K], N_, K, b - a)
+        n_used += 1
+    red = parts[:n_used, :, :K].sum(0)
+    if beta != 0.0:
+        out.mul_(beta).add_(red, alpha=alpha)
+    else:
+        out.copy_(red.mul_(alpha) if alpha != 1.0 else red)
+    return out
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
-           scale: float = 1.0) -> torch.Tensor:
-    """Bias gradient: fp32 column sums of a bf16 [M, N] matrix."""
+           scale: float = 1.0, ws: torch.Tensor | None = None) -> torch.Tensor:
+    """Bias gradient: fp32 column sums of a bf16 [M, N] matrix (deterministic two-pass)."""
     N.check_cuda(x, "x", torch.bfloat16, contiguous=False)
+    if not is_aligned(x):
+        x = aligned(x)
     M, N_ = x.shape
     if out is None:
         out = torch.empty(N_, dtype=torch.float32, device=x.device)
+    need = max(1, (M + 511) // 512 * N_)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=x.device)
     N.call("em_colsum_bf16", x.data_ptr(), x.stride(0), M, N_, out.data_ptr(), int(accumulate), float(scale),
+           ws.data_ptr(), N.stream_handle(x.device))
+    return out
+
+
+def rowsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
+           scale: float = 1.0) -> torch.Tensor:
+    """fp32 row sums of a bf16 [R, C] matrix (bias gradient from a transposed dZ)."""
+    N.check_cuda(x, "x", torch.bfloat16, contiguous=False)
+    if not is_aligned(x):
+        x = aligned(x)
+    R, Cc = x.shape
+    if out is None:
+        out = torch.empty(R, dtype=torch.float32, device=x.device)
+    N.call("em_rowsum_bf16", x.data_ptr(), x.stride(0), R, Cc, out.data_ptr(), int(accumulate), float(scale),
            N.stream_handle(x.device))
     return out
 

@@ -168,3 +168,81 @@ def test_gemm_trainer_learns_planted(data):
     assert loss.item() < first
     ev = tr.evaluate(masks, 1000, offset=ntr)
     assert ev["acc"] > ev["trivial_acc"], ev
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 256, 4096)])
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh"])
+def test_big_nt_forward_with_transposed_copy(M, N, K, act):
+    from euromillioner_amd.ops import linear as LIN
+
+    assert LIN.big_ok(M, N, K)
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    ct = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
+    y = LIN.linear_fwd(x, w, b, act, torch.bfloat16, ct=ct)
+    ref = ACT[act](x.float() @ w.float().t() + b)
+    assert _rel(y, ref) < 1e-2, _rel(y, ref)
+    assert torch.equal(ct, y.t())
+    y32 = LIN.linear_fwd(x, w, None, "none", torch.float32)
+    assert _rel(y32, x.float() @ w.float().t()) < 1e-5
+
+
+@pytest.mark.parametrize("dact", ["relu", "sigmoid", "tanh"])
+def test_big_nt_dgrad_and_wgrad(dact):
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, N, K = 512, 256, 768
+    dz = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    w = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    y = ACT[dact](torch.randn(M, K, device="cuda", generator=g)).bfloat16()
+    wt = LIN.transpose(w)
+    assert torch.equal(wt, w.t())
+    ct = torch.empty(K, M, dtype=torch.bfloat16, device="cuda")
+    out = LIN.linear_dgrad_nt(dz, wt, y, dact, ct=ct)
+    ref = dz.float() @ w.float()
+    yf = y.float()
+    ref = ref * ((yf > 0).float() if dact == "relu" else yf * (1 - yf) if dact == "sigmoid" else 1 - yf * yf)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    assert torch.equal(ct, out.t())
+    # wgrad through transposed copies: dW = dz^T @ x
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    gw = LIN.linear_wgrad_nt(LIN.transpose(dz), LIN.transpose(x))
+    assert _rel(gw, dz.float().t() @ x.float()) < 1e-5
+    assert _rel(LIN.rowsum(LIN.transpose(dz)), dz.float().sum(0)) < 1e-5
+
+
+def test_wgrad_split_k_and_colsum_big_batch():
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(8)
+    M = 65536
+    dz = torch.randn(M, 64, device="cuda", generator=g).bfloat16()
+    x = torch.randn(M, 200, device="cuda", generator=g).bfloat16()
+    xq = LIN.aligned(x)
+    gw = LIN.linear_wgrad(dz, xq)
+    ref = dz.double().t() @ x.double()
+    assert _rel(gw.double(), ref) < 1e-5
+    assert _rel(LIN.colsum(dz).double(), dz.double().sum(0)) < 1e-5
+
+
+def test_gemm_trainer_big_plan_matches_drawmlp(data):
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+    from euromillioner_amd.models.mlp import DrawMLP
+
+    ds, masks = data
+    sizes, B, off = (62, 512, 256, 62), 1024, 3
+    tr = GemmMLPTrainer(sizes, seed=2)
+    plan = tr._plan(B)
+    assert plan["wgrad"][1] and plan["dgrad"][1] and plan["dgrad"][2]
+    ref = DrawMLP(sizes, seed=2)
+    X = torch.from_numpy(multi_hot(ds.numbers[off:off + B])).float()
+    Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).float()
+    l = ref.loss(ref(X), Y)
+    l.backward()
+    lk, gk = tr.grads_only(masks, B, offset=off)
+    assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
+    for n, p in ref.named_parameters():
+        assert _rel(gk[n].cpu(), p.grad) < 5e-2, n

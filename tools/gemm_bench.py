@@ -50,7 +50,17 @@ def main():
     w1 = torch.randn(H, 64, device=dev, generator=g).bfloat16()
     w3 = torch.randn(64, H, device=dev, generator=g).bfloat16()
     y64 = torch.empty(B, 64, dtype=torch.float32, device=dev)
+    wt = LIN.transpose(w)
+    xt = LIN.transpose(x)
+    ct = torch.empty(H, B, dtype=torch.bfloat16, device=dev)
     cases = [
+        ("fwd_hidden_ct", 2.0 * B * H * H, lambda: LIN.linear_fwd(x, w, bias, "relu", out=y, ct=ct),
+         lambda: torch.relu(torch.nn.functional.linear(x, w))),
+        ("dgrad_hidden_nt", 2.0 * B * H * H, lambda: LIN.linear_dgrad_nt(x, wt, x, "relu", out=y, ct=ct),
+         lambda: (x @ w) * (x > 0)),
+        ("wgrad_hidden_nt", 2.0 * B * H * H, lambda: LIN.linear_wgrad_nt(xt, xt, out=gw),
+         lambda: torch.matmul(x.t(), x, out=None).float()),
+        ("transpose", 2.0 * B * H, lambda: LIN.transpose(x, out=xt), lambda: x.t().contiguous()),
         ("fwd_hidden", 2.0 * B * H * H, lambda: LIN.linear_fwd(x, w, bias, "relu", out=y),
          lambda: torch.relu(torch.nn.functional.linear(x, w))),
         ("dgrad_hidden", 2.0 * B * H * H, lambda: LIN.linear_dgrad(x, w, x, "relu", out=y),
