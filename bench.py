@@ -202,9 +202,14 @@ def main():
         ms = float(t.item())
     loss = float(loss_t.reshape(-1)[0].item()) if loss_t is not None else float("nan")
 
-    ev = {}
+    ev, ev_iid = {}, {}
     if not a.no_eval:
         ev = model.evaluate(draws, n_samples - margin, offset=margin)
+        # the same model on iid draws (no planted structure): must sit at chance
+        n_iid = min(1 << 20, n_samples - margin)
+        iid_nums, _ = generate_draws(n_iid + 1, seed=a.seed + 777 + 1000 * rank, planted=0.0, native=True)
+        iid = rows_to_masks(torch.from_numpy(iid_nums).to(dev))
+        ev_iid = model.evaluate(iid, n_iid, offset=0)
 
     value = B * world / (ms / 1000.0)
     desc = "mlp " + "->".join(str(x) for x in sizes) + " relu, " + (
@@ -232,6 +237,7 @@ def main():
                        "per_gpu_batch": B, "optimizer": "adam", "hipgraph": use_graph},
             "train_loss_last": loss,
             "val": ev,
+            "val_iid": ev_iid,
             **extra,
         }
         print(json.dumps(out))

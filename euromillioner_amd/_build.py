@@ -105,7 +105,7 @@ def _compile(src: str, obj: str, extra=()):
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-march=x86-64-v2", "-Wall", "-Wno-unused-function", "-pthread"]
 
 
-def build_host(force: bool = False, verbose: bool = False) -> str:
+def build_host(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
     """g++ build of csrc/host/*.cpp -> libem_host.so (loads without any GPU/HIP runtime)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
     headers = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
@@ -119,7 +119,7 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
         obj = os.path.join(OBJDIR, "host_" + os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _needs_build(src, obj, headers):
-            cmd = [cxx] + HOST_FLAGS + ["-I", os.path.join(CSRC, "host"), "-c", src, "-o", obj]
+            cmd = [cxx] + HOST_FLAGS + list(extra_flags) + ["-I", os.path.join(CSRC, "host"), "-c", src, "-o", obj]
             p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
             if p.returncode != 0:
                 raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{p.stdout}")
@@ -128,7 +128,7 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     lib = host_lib_path()
     if objs and (force or not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs)):
         tmp = lib + ".tmp"
-        cmd = [cxx, "-shared", "-fPIC", "-pthread", "-o", tmp] + objs
+        cmd = [cxx, "-shared", "-fPIC", "-pthread"] + list(extra_flags) + ["-o", tmp] + objs
         p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if p.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{p.stdout}")
@@ -187,9 +187,16 @@ if __name__ == "__main__":
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--usage", default=None, help="print kernel resource usage for one csrc file")
+    ap.add_argument("--debug", action="store_true",
+                    help="debug build (-g, device asserts kept; run with HIP_LAUNCH_BLOCKING=1 to localise a fault); "
+                         "forces a rebuild -- rebuild without --debug afterwards")
+    ap.add_argument("--host-sanitize", action="store_true",
+                    help="host-only ASan/UBSan build of the C++ host library (GPU sanitizers are unavailable)")
     a = ap.parse_args()
     if a.usage:
         print(resource_usage(a.usage))
     else:
-        print(build_host(force=a.force, verbose=a.verbose))
-        print(build(force=a.force, jobs=a.jobs, verbose=a.verbose))
+        host_flags = ("-fsanitize=address,undefined", "-fno-omit-frame-pointer") if a.host_sanitize else ()
+        print(build_host(force=a.force or a.host_sanitize, verbose=a.verbose, extra_flags=host_flags))
+        dbg = ("-g", "-O1") if a.debug else ()
+        print(build(force=a.force or a.debug, jobs=a.jobs, verbose=a.verbose, extra_flags=dbg))

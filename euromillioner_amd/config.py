@@ -110,12 +110,14 @@ class DistConfig:
     timeout_s: float = 300.0
     fault_at_step: int | None = None  # test-only fault injection
     fault_rank: int | None = None
+    check_sync_every: int = 0  # cross-rank parameter checksum assert every k steps (0 = off)
+    avg_frequency: int = 0  # >0: parameter averaging every k local steps (Spark ParameterAveraging parity)
 
 
 @dataclasses.dataclass
 class CkptConfig:
     path: str | None = None
-    resume: str | None = None
+    resume: str | None = None  # a checkpoint path, or "auto" = ckpt.path if it exists (restart-safe)
     every: int = 0
 
 
@@ -123,6 +125,8 @@ class CkptConfig:
 class LogConfig:
     level: str = "INFO"
     json_metrics: bool = True
+    profile_dir: str | None = None  # torch.profiler chrome trace of a few training steps
+    profile_steps: int = 5
 
 
 @dataclasses.dataclass

@@ -147,3 +147,18 @@ def load_numeric_csv(path: str, skip_header: bool = True, label_column: int | No
     y = out[:, label_column].copy()
     X = np.delete(out, label_column, axis=1)
     return X, y
+
+
+def load_numeric_csv_tensor(path: str, skip_header: bool = True, label_column: int | None = 0, pin: bool = True):
+    """X1: native CSV -> torch tensors in pinned (page-locked) host memory when a GPU is present,
+    ready for an async ``.to(device, non_blocking=True)`` upload."""
+    import torch
+
+    X, y = load_numeric_csv(path, skip_header, label_column)
+    pin = pin and torch.cuda.is_available()
+    tx = torch.from_numpy(X)
+    ty = torch.from_numpy(y) if y is not None else None
+    if pin:
+        tx = tx.pin_memory()
+        ty = ty.pin_memory() if ty is not None else None
+    return tx, ty

@@ -51,6 +51,27 @@ class _Engine:
         raise NotImplementedError
 
 
+def _checksum(flat: torch.Tensor) -> torch.Tensor:
+    """Order-sensitive integer checksum of a float buffer (bit-exact comparison across ranks)."""
+    bits = flat.detach().reshape(-1).view(torch.int32).to(torch.int64)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([bits.sum(), (bits * w).sum()])
+
+
+def check_sync(engine: "_Engine", info: D.DistInfo) -> None:
+    """Race/desync detector: every rank must hold bit-identical parameters."""
+    if not info.is_dist:
+        return
+    c = _checksum(engine.flat_params())
+    if info.backend == "gloo":
+        c = c.cpu()
+    allc = [torch.zeros_like(c) for _ in range(info.world)]
+    torch.distributed.all_gather(allc, c)
+    if any(not torch.equal(allc[0], x) for x in allc[1:]):
+        raise RuntimeError("data-parallel ranks diverged: parameter checksums differ " +
+                           str([x.tolist() for x in allc]))
+
+
 def _sharded_eval(model, masks, offset: int, n: int) -> dict:
     """C3: each rank scores its slice of the validation range; the model all-reduces the sums."""
     if model.group is None:
@@ -100,6 +121,9 @@ class _FusedEngine(_Engine):
     def broadcast(self):
         self.model.broadcast_parameters()
 
+    def flat_params(self):
+        return self.model.params
+
 
 class _GemmEngine(_Engine):
     """Any 62->...->62 stack on the K1-K3 GEMMs + K10 loss + flat Adam."""
@@ -133,6 +157,9 @@ class _GemmEngine(_Engine):
     def broadcast(self):
         self.model.broadcast_parameters()
 
+    def flat_params(self):
+        return self.model.params
+
 
 class _TorchEngine(_Engine):
     """DrawMLP (HIP autograd GEMMs on the GPU, PyTorch on the CPU) + torch.optim.Adam +
@@ -151,6 +178,10 @@ class _TorchEngine(_Engine):
         self.opt = torch.optim.Adam(self.net.parameters(), lr=m.lr, betas=tuple(m.betas), eps=m.eps,
                                     weight_decay=m.weight_decay)
         self.bucketer = GradBucketer(self.net, cfg.dist.bucket_mb, group=info.group, world=info.world)
+        self.avg_k = int(cfg.dist.avg_frequency or 0)
+        if self.avg_k > 0:
+            self.bucketer.enabled = False  # local steps; parameters are averaged every avg_k steps
+        self.n_local = 0
         self.X, self.Y = X, Y
         self.loss_name = m.loss
 
@@ -165,6 +196,9 @@ class _TorchEngine(_Engine):
         loss.backward()
         self.bucketer.finish()
         self.opt.step()
+        self.n_local += 1
+        if self.avg_k > 0 and self.n_local % self.avg_k == 0:
+            self.average_parameters()
         out = loss.detach().reshape(1)
         if self.info.is_dist:
             torch.distributed.all_reduce(out)
@@ -212,6 +246,23 @@ class _TorchEngine(_Engine):
 
     def broadcast(self):
         D.broadcast_module_(self.net, self.info)
+
+    def flat_params(self):
+        return torch.cat([p.detach().reshape(-1).float() for p in self.net.parameters()])
+
+    def average_parameters(self):
+        """Spark ParameterAveragingTrainingMaster parity: mean of params and Adam moments."""
+        if not self.info.is_dist:
+            return
+        with torch.no_grad():
+            for p in self.net.parameters():
+                torch.distributed.all_reduce(p.data)
+                p.data /= self.info.world
+                st = self.opt.state.get(p, {})
+                for k in ("exp_avg", "exp_avg_sq"):
+                    if k in st:
+                        torch.distributed.all_reduce(st[k])
+                        st[k] /= self.info.world
 
 
 # ---------------------------------------------------------------------------------------------
@@ -263,6 +314,13 @@ def load_mlp_checkpoint(path: str) -> dict:
 # ---------------------------------------------------------------------------------------------
 # MLP training
 # ---------------------------------------------------------------------------------------------
+def _export_trace(prof, out_dir: str, rank: int) -> None:
+    os.makedirs(out_dir, exist_ok=True)
+    prof.export_chrome_trace(os.path.join(out_dir, f"trace_rank{rank}.json"))
+    with open(os.path.join(out_dir, f"kernels_rank{rank}.txt"), "w", encoding="utf-8") as f:
+        f.write(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40))
+
+
 def _mlp_sizes(cfg: RunConfig) -> tuple:
     hidden = tuple(int(h) for h in cfg.mlp.hidden)
     if cfg.model == "mlp-wide" and hidden == (128,):
@@ -271,8 +329,8 @@ def _mlp_sizes(cfg: RunConfig) -> tuple:
 
 
 def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
-    if info.device.type != "cuda" or cfg.data.lags != 1:
-        return "torch"
+    if info.device.type != "cuda" or cfg.data.lags != 1 or cfg.dist.avg_frequency:
+        return "torch"  # (parameter averaging runs on the DrawMLP engine)
     if sizes == (62, 128, 62) and cfg.mlp.activation == "relu":
         return "fused"
     return "gemm"
@@ -304,7 +362,10 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
     global_b = local_b * info.world
     steps = m.steps if m.epochs is None else int(m.epochs) * math.ceil(shard / local_b)
 
-    resume = load_mlp_checkpoint(cfg.ckpt.resume) if cfg.ckpt.resume else None
+    resume_path = cfg.ckpt.resume
+    if resume_path == "auto":  # restart-safe (torchrun --max-restarts): continue from ckpt.path if present
+        resume_path = cfg.ckpt.path if cfg.ckpt.path and os.path.exists(cfg.ckpt.path) else None
+    resume = load_mlp_checkpoint(resume_path) if resume_path else None
     if resume is not None:
         if tuple(resume["sizes"]) != tuple(sizes):
             raise ValueError(f"checkpoint sizes {resume['sizes']} != configured {list(sizes)}")
@@ -331,7 +392,7 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
         start_step = int(resume["extra"].get("step", 0))
         if "opt" in resume:
             engine.load_optimizer_state(resume["opt"])
-        log.info(f"resumed from {cfg.ckpt.resume} at step {start_step}")
+        log.info(f"resumed from {resume_path} at step {start_step}")
     log.info(f"mlp {'->'.join(map(str, sizes))} engine={engine.name} device={dev} world={info.world} "
              f"train={margin} (shard {shard}) val={n_samples - margin} batch={global_b} steps={steps}")
 
@@ -341,10 +402,21 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
     ckpt_path = cfg.ckpt.path
     hist = []
     loss_t = None
+    prof = None
+    if cfg.log.profile_dir:  # step timeline (chrome trace) for the first profile_steps steps
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if dev.type == "cuda" else [])
+        prof = profile(activities=acts)
+        prof.__enter__()
     t0 = time.time()
     done = 0
     for step in range(start_step, steps):
         D.maybe_inject_fault(step, info, cfg.dist.fault_at_step, cfg.dist.fault_rank)
+        if prof is not None and step == start_step + cfg.log.profile_steps:
+            prof.__exit__(None, None, None)
+            _export_trace(prof, cfg.log.profile_dir, info.rank)
+            prof = None
         idx, off = None, a + sample_base
         if use_perm:  # epoch-keyed permutation: a resumed run sees the same sample order
             epoch, k = divmod(step, per_epoch)
@@ -355,6 +427,8 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
             idx = perm[k * local_b:(k + 1) * local_b]
         loss_t = engine.step(idx, off, local_b, global_b)
         done += 1
+        if cfg.dist.check_sync_every and (step + 1) % cfg.dist.check_sync_every == 0:
+            check_sync(engine, info)
         last = step == steps - 1
         if (m.eval_every and (step + 1) % m.eval_every == 0) or last:
             ev = engine.evaluate(margin, n_samples - margin) if n_samples > margin else {}
@@ -366,18 +440,25 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
             if info.rank == 0:
                 save_mlp_checkpoint(ckpt_path, engine, cfg, sizes, step + 1)
             D.barrier(info)
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        _export_trace(prof, cfg.log.profile_dir, info.rank)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     secs = time.time() - t0
+    if cfg.dist.check_sync_every:
+        check_sync(engine, info)
     if ckpt_path:
         if info.rank == 0:
             save_mlp_checkpoint(ckpt_path, engine, cfg, sizes, steps)
         D.barrier(info)
     final = hist[-1] if hist else {}
-    return {"model": cfg.model, "engine": engine.name, "sizes": list(sizes), "world": info.world,
+    sps = done * global_b / secs if secs > 0 else None
+    return {"val_acc": final.get("val_acc"), "val_logloss": final.get("val_loss"), "samples_per_sec": sps,
+            "world_size": info.world, "trivial_acc": final.get("val_trivial_acc"), "model": cfg.model, "engine": engine.name, "sizes": list(sizes), "world": info.world,
             "device": str(dev), "steps": steps, "start_step": start_step, "global_batch": global_b,
             "train_samples": margin, "val_samples": n_samples - margin,
-            "samples_per_s": done * global_b / secs if secs > 0 else None, "seconds": round(secs, 3),
+            "seconds": round(secs, 3),
             "loss": final.get("loss"), "val": {k[4:]: v for k, v in final.items() if k.startswith("val_")},
             "history": hist, "checkpoint": ckpt_path}
 

@@ -46,7 +46,7 @@ def _launch(argv, world, timeout=240, cwd=None):
 
 def _train_argv(extra):
     return [sys.executable, "-m", "euromillioner_amd", "train", "--model", "mlp", "--device", "cpu",
-            "--n-draws", "1201", "--planted", "0.7", "--seed", "5", "--eval-every", "0", "--log-level", "WARN"] + extra
+            "--n-draws", "1201", "--planted", "0.7", "--seed", "5", "--eval-every", "0", "--log-level", "INFO"] + extra
 
 
 def _params(path):
@@ -56,7 +56,7 @@ def _params(path):
     return ck["flat"], ck.get("m"), ck.get("v"), ck.get("extra", {})
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_equals_single_process(tmp_path, world):
     """Full-batch DP over `world` gloo ranks == one process on the whole batch."""
     single = str(tmp_path / "single.zip")
@@ -65,11 +65,11 @@ def test_dp_equals_single_process(tmp_path, world):
     common = ["--steps", "6", "--batch", "840", "--lr", "0.01"]
     outs = _launch(_train_argv(common + ["--ckpt", single]), 1)
     assert outs[0][0] == 0, outs[0][1][-2000:]
-    outs = _launch(_train_argv(common + ["--ckpt", multi]), world)
+    outs = _launch(_train_argv(common + ["--ckpt", multi, "--check-sync-every", "2"]), world)
     assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
     a, b = _params(single), _params(multi)
-    assert np.allclose(a[0], b[0], atol=2e-6), np.abs(a[0] - b[0]).max()
-    assert np.allclose(a[1], b[1], atol=1e-7) and np.allclose(a[2], b[2], atol=1e-9)
+    assert np.allclose(a[0], b[0], atol=2e-5), np.abs(a[0] - b[0]).max()  # reduction order differs
+    assert np.allclose(a[1], b[1], atol=1e-6) and np.allclose(a[2], b[2], atol=1e-8)
 
 
 @pytest.mark.parametrize("bucket_mb", ["0.01", "25"])
@@ -127,3 +127,31 @@ def test_checkpoint_every_writes_intermediate(tmp_path):
     r = _launch(_train_argv(["--batch", "256", "--steps", "4", "--ckpt", p, "--ckpt-every", "2"]), 1)
     assert r[0][0] == 0, r[0][1][-2000:]
     assert _params(p)[3]["step"] == 4
+
+
+def test_parameter_averaging_mode_stays_in_sync(tmp_path):
+    """--avg-frequency k (Spark ParameterAveraging parity): local steps, averaged every k; the
+    cross-rank checksum check (--check-sync-every) passes at every averaging point."""
+    p = str(tmp_path / "avg.zip")
+    outs = _launch(_train_argv(["--steps", "8", "--batch", "128", "--avg-frequency", "2",
+                                "--check-sync-every", "2", "--ckpt", p]), 2)
+    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    assert _params(p)[3]["step"] == 8
+
+
+def test_sync_check_detects_divergence(tmp_path):
+    """Local steps that are never averaged diverge; the checker must fail loudly."""
+    outs = _launch(_train_argv(["--steps", "3", "--batch", "128", "--avg-frequency", "1000",
+                                "--check-sync-every", "3"]), 2)
+    assert all(rc != 0 for rc, _ in outs)
+    assert any("diverged" in o for _, o in outs)
+
+
+def test_resume_auto(tmp_path):
+    p = str(tmp_path / "auto.zip")
+    base = ["--batch", "200", "--lr", "0.005", "--ckpt", p, "--resume", "auto"]
+    r = _launch(_train_argv(base + ["--steps", "3"]), 1)  # nothing to resume: fresh start
+    assert r[0][0] == 0, r[0][1][-2000:]
+    r = _launch(_train_argv(base + ["--steps", "6"]), 1)
+    assert r[0][0] == 0 and "resumed from" in r[0][1]
+    assert _params(p)[3]["step"] == 6

@@ -246,3 +246,20 @@ def test_gemm_trainer_big_plan_matches_drawmlp(data):
     assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
     for n, p in ref.named_parameters():
         assert _rel(gk[n].cpu(), p.grad) < 5e-2, n
+
+
+@pytest.mark.parametrize("M,N,K,big", [(256, 512, 256, True), (128, 96, 128, False), (300, 200, 300, False)])
+def test_identity_a_asymmetric_b(M, N, K, big):
+    """A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md 3)."""
+    from euromillioner_amd.ops import linear as LIN
+
+    assert LIN.big_ok(M, N, K) == big
+    n = min(M, K)
+    a = torch.zeros(M, K, device="cuda")
+    a[torch.arange(n), torch.arange(n)] = 1.0
+    # exact small integers, asymmetric: B[n][k] = (3n + 7k) % 17 - 8
+    nn_, kk = torch.meshgrid(torch.arange(N, device="cuda"), torch.arange(K, device="cuda"), indexing="ij")
+    w = ((3 * nn_ + 7 * kk) % 17 - 8).float()
+    y = LIN.linear_fwd(LIN.aligned(a), LIN.aligned(w), None, "none", torch.float32)
+    ref = a @ w.t()
+    assert torch.equal(y, ref)
