@@ -331,6 +331,22 @@ __global__ void gbdt_metric_final(const double* __restrict__ partial, int nb, in
   out[0] = (float)v;
 }
 
+// DP path: fold the per-chunk partial histograms into chunk 0 (fixed order), ready for an all-reduce
+__global__ void gbdt_chunk_reduce(double* __restrict__ partial, int nchunks, int64_t S) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S; e += (int64_t)gridDim.x * blockDim.x) {
+    double acc = 0.0;
+    for (int c = 0; c < nchunks; ++c) acc += partial[(int64_t)c * S + e];
+    partial[e] = acc;
+  }
+}
+
+__global__ void gbdt_metric_sum(const double* __restrict__ partial, int nb, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nb; ++i) s += partial[i];
+  out[0] = s;
+}
+
 inline int grid_for(int64_t total, int bs = 256) {
   int64_t g = (total + bs - 1) / bs;
   if (g > 4096) g = 4096;
@@ -432,6 +448,95 @@ EM_API int em_gbdt_predict(const uint8_t* bins, float* margin, int T, int n, int
   const int NN = (1 << (max_depth + 1)) - 1;
   hipLaunchKernelGGL(gbdt_predict, dim3(grid_for((int64_t)T * n)), dim3(256), 0, stream, bins, margin, T, n, F, NN, k0,
                      k1, status, feat, sbin, leaf);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------- data-parallel (C4) primitives
+// The single-call driver above runs whole rounds on the stream; under data parallelism the host
+// interleaves these per-level steps with an all-reduce of the folded histogram (and of the metric
+// sums), so every rank takes identical split decisions on its own row shard.
+EM_API int em_gbdt_dp_round_begin(int round, int T, int n, int max_depth, const float* margin, const float* Y, float* g,
+                                  float* h, int16_t* node, int obj, float subsample, uint32_t seed, int8_t* status,
+                                  int16_t* feat, uint8_t* sbin, float* gainv, hipStream_t stream) {
+  if (!margin || !Y || !g || !h || !node || !status || T <= 0 || n <= 0 || max_depth < 1 || max_depth > 12)
+    return EM_ERR_ARG;
+  const int NN = (1 << (max_depth + 1)) - 1;
+  const int64_t TN = (int64_t)T * n;
+  hipLaunchKernelGGL(gbdt_round_init, dim3(grid_for((int64_t)T * NN)), dim3(256), 0, stream, status, feat, sbin, gainv,
+                     T * NN, NN);
+  hipLaunchKernelGGL(gbdt_grad, dim3(grid_for(TN)), dim3(256), 0, stream, margin, Y, g, h, node, T, n, obj, subsample,
+                     seed, round);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// histogram of one level folded into partial[0 : T*2^level*F*NB*2]; returns that length in *len_out
+EM_API int em_gbdt_dp_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node,
+                                 int T, int n, int F, int NB, double* partial, int64_t partial_doubles,
+                                 int64_t* len_out, hipStream_t stream) {
+  if (!bins || !g || !h || !node || !partial || !len_out || level < 0 || level > 11) return EM_ERR_ARG;
+  const int chunk = 1024;
+  const int nchunks = (n + chunk - 1) / chunk;
+  const int nodesL = 1 << level;
+  int FT = (int)(65536 / ((int64_t)nodesL * NB * 2 * 8));
+  if (FT > F) FT = F;
+  if (FT > 256) FT = 256;
+  if (FT < 1) return EM_ERR_ARG;
+  const int64_t S = (int64_t)T * nodesL * F * NB * 2;
+  if (S * nchunks > partial_doubles) return EM_ERR_ARG;
+  const int nft = (F + FT - 1) / FT;
+  const int threads = ((FT + 63) / 64) * 64;
+  const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double);
+  hipLaunchKernelGGL(gbdt_hist, dim3(nchunks, T, nft), dim3(threads), lds, stream, bins, g, h, node, partial, T, n, F,
+                     NB, level, chunk, FT);
+  if (nchunks > 1)
+    hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, nchunks, S);
+  EM_CHECK_LAUNCH();
+  *len_out = S;
+  return 0;
+}
+
+EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* hist, int T, int n, int F, int NB,
+                                  int max_depth, int16_t* node, double* Gs, double* Hs, int8_t* status, int16_t* feat,
+                                  uint8_t* sbin, float* gainv, float lam, float mcw, hipStream_t stream) {
+  if (!bins || !hist || !node || !Gs || !Hs || !status || level < 0 || level >= max_depth) return EM_ERR_ARG;
+  const int NN = (1 << (max_depth + 1)) - 1;
+  const int nodesL = 1 << level;
+  const int64_t TN = (int64_t)T * n;
+  hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(64), 0, stream, hist, 1, T, F, NB, level, NN, Gs, Hs, status,
+                     feat, sbin, gainv, (double)lam, (double)mcw);
+  hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
+                     sbin, level);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_gbdt_dp_round_end(int T, int n, int max_depth, float* margin, const int16_t* node, int8_t* status,
+                                int16_t* feat, float* gainv, double* Gs, double* Hs, float* leaf, float* cover,
+                                float lam, float gamma, float eta, hipStream_t stream) {
+  if (!margin || !node || !status || !leaf || T <= 0 || n <= 0) return EM_ERR_ARG;
+  const int NN = (1 << (max_depth + 1)) - 1;
+  const int64_t TN = (int64_t)T * n;
+  hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, stream, T, NN, max_depth, status, feat, gainv,
+                     Gs, Hs, leaf, cover, (double)lam, gamma, (double)eta);
+  hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, stream, margin, node, T, n, NN, status, leaf);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// sum (not mean) of the per-element metric term over [T][n] margins -> out[0] (double)
+EM_API int em_gbdt_metric_sum(const float* margin, const float* Y, int T, int n, int obj, int metric, double* mpart,
+                              double* out, hipStream_t stream) {
+  if (!margin || !Y || !mpart || !out || T <= 0 || n < 0) return EM_ERR_ARG;
+  const int64_t TN = (int64_t)T * n;
+  const int mb = grid_for(TN);
+  if (n > 0) {
+    hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, stream, margin, Y, T, n, obj, metric, mpart);
+    hipLaunchKernelGGL(gbdt_metric_sum, dim3(1), dim3(1), 0, stream, mpart, mb, out);
+  } else {
+    hipLaunchKernelGGL(gbdt_metric_sum, dim3(1), dim3(1), 0, stream, mpart, 0, out);
+  }
   EM_CHECK_LAUNCH();
   return 0;
 }

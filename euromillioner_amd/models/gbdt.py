@@ -65,6 +65,53 @@ def make_cuts(X: np.ndarray, max_bin: int = 256) -> list[np.ndarray]:
     return cuts
 
 
+class _DP:
+    """C4 helper: histogram / sum all-reduce for data-parallel boosting (every rank holds a row
+    shard; identical global sums give identical splits, so trees need no broadcast)."""
+
+    def __init__(self, group):
+        import torch.distributed as dist
+
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+
+    def sum_(self, arr: np.ndarray) -> np.ndarray:
+        import torch
+
+        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64))
+        if self.nccl:
+            t = t.cuda()
+        self.dist.all_reduce(t, group=self.group)
+        return t.cpu().numpy().reshape(np.shape(arr))
+
+    def gather(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+
+def make_cuts_dp(X: np.ndarray, max_bin: int, dp: "_DP") -> list[np.ndarray]:
+    """Global cuts from per-rank value summaries.  Exact (== single-process cuts) whenever a
+    feature has <= 16*max_bin distinct values per rank and <= max_bin globally (true for draw
+    data); otherwise a merged quantile summary."""
+    summaries = []
+    for f in range(X.shape[1]):
+        col = X[:, f]
+        u = np.unique(col[~np.isnan(col)])
+        if len(u) > 16 * max_bin:
+            u = np.unique(np.quantile(u, np.linspace(0, 1, 16 * max_bin)))
+        summaries.append(u)
+    merged = dp.gather(summaries)
+    cols = [np.unique(np.concatenate([m[f] for m in merged])) for f in range(X.shape[1])]
+    width = max((len(c) for c in cols), default=0)
+    Xm = np.full((max(width, 1), X.shape[1]), np.nan)
+    for f, c in enumerate(cols):
+        Xm[:len(c), f] = c
+    return make_cuts(Xm, max_bin)
+
+
 def apply_bins(X: np.ndarray, cuts: list[np.ndarray]) -> np.ndarray:
     """bin index per value: number of cuts strictly below x (x < cut -> left of it)."""
     n, F = X.shape
@@ -288,14 +335,17 @@ class GBDT:
             pass
         return "numpy"
 
-    def fit(self, X: np.ndarray, Y: np.ndarray, evals: dict | None = None):
+    def fit(self, X: np.ndarray, Y: np.ndarray, evals: dict | None = None, group=None):
+        """``group``: a torch.distributed process group -> data-parallel boosting (C4): X/Y and every
+        eval set are this rank's row shard; histograms, node sums and metrics are all-reduced."""
         X = np.asarray(X, dtype=np.float64)
         Y = np.asarray(Y, dtype=np.float64)
         if Y.ndim == 1:
             Y = Y[:, None]
         check_labels(self.objective, Y)
         self.n_tasks = Y.shape[1]
-        self.cuts = make_cuts(X, self.max_bin)
+        dp = _DP(group) if group is not None else None
+        self.cuts = make_cuts_dp(X, self.max_bin, dp) if dp is not None else make_cuts(X, self.max_bin)
         bins = apply_bins(X, self.cuts)
         nbins = max((len(c) for c in self.cuts), default=0) + 1
         evals = evals or {}
@@ -304,13 +354,13 @@ class GBDT:
         if backend == "hip":
             from . import gbdt_hip
 
-            self.trees, self.history = gbdt_hip.fit(self, X, bins, nbins, Y, evals)
+            self.trees, self.history = gbdt_hip.fit(self, X, bins, nbins, Y, evals, dp=dp)
         else:
-            self.trees, self.history = self._fit_numpy(X, bins, nbins, Y, evals)
+            self.trees, self.history = self._fit_numpy(X, bins, nbins, Y, evals, dp=dp)
         self.trees.set_split_values(self.cuts)
         return self
 
-    def _fit_numpy(self, X, bins, nbins, Y, evals):
+    def _fit_numpy(self, X, bins, nbins, Y, evals, dp=None):
         """Oracle, vectorised over tasks and nodes: per level one GEMM of the one-hot bin matrix
         [n, sum(bins)] with (g, h) scattered by (task, node)."""
         n, T = Y.shape
@@ -331,7 +381,8 @@ class GBDT:
         row_feat = np.repeat(np.arange(F), nbf)
         rowseg_start = off[row_feat]
         valid_row = (np.arange(off[-1]) - rowseg_start) < (nbf[row_feat] - 1)  # not the last bin of a feature
-        rng = np.random.default_rng(self.seed)
+        rng = np.random.default_rng(self.seed if dp is None else [self.seed, dp.rank])
+        red = dp.sum_ if dp is not None else (lambda a: a)
         hist = []
         tix = np.arange(T)
         for rnd in range(R):
@@ -348,7 +399,7 @@ class GBDT:
             gain = np.zeros((T, NN))
             Gs = np.zeros((T, NN))
             Hs = np.zeros((T, NN))
-            Gs[:, 0], Hs[:, 0] = g64.sum(0), h64.sum(0)
+            Gs[:, 0], Hs[:, 0] = red(g64.sum(0)), red(h64.sum(0))
             for depth in range(D):
                 first, nl = 2 ** depth - 1, 2 ** depth
                 rel = node - first  # [n, T]
@@ -359,8 +410,8 @@ class GBDT:
                 rows = np.nonzero(act)
                 Zg[rows[0], col[rows]] = g64[rows]
                 Zh[rows[0], col[rows]] = h64[rows]
-                HG = onehot.T @ Zg  # [sum bins, T*nl]
-                HH = onehot.T @ Zh
+                HG = red(onehot.T @ Zg)  # [sum bins, T*nl]; C4: all-reduced under DP
+                HH = red(onehot.T @ Zh)
                 # segmented prefix sums: left sums for "bin <= b" of feature f, all columns at once
                 CG, CH = np.cumsum(HG, axis=0), np.cumsum(HH, axis=0)
                 baseg = np.where(rowseg_start[:, None] > 0, CG[np.maximum(rowseg_start - 1, 0)], 0.0)
@@ -401,16 +452,29 @@ class GBDT:
                     ev_margin[name][:, t] += trees.leaf[kk, _route_bins(trees, kk, eb)].astype(np.float32)
             rec = {"round": rnd}
             for name, (ex, ey) in evals.items():
-                rec[name] = self._metric(np.asarray(ey, np.float64).reshape(len(ex), -1), ev_margin[name])
+                rec[name] = self._metric(np.asarray(ey, np.float64).reshape(len(ex), -1), ev_margin[name], dp)
             hist.append(rec)
             self._log_round(rec)
         return trees, hist
 
-    def _metric(self, y, margin):
+    def _metric(self, y, margin, dp=None):
         from .. import metrics as M
 
         p = transform(self.objective, margin)
-        return M.EVAL_METRICS[self.eval_metric](y, p)
+        if dp is None:
+            return M.EVAL_METRICS[self.eval_metric](y, p)
+        # global mean from per-rank (sum, count): rmse averages squares before the root
+        y = np.asarray(y, np.float64).reshape(-1)
+        p = np.asarray(p, np.float64).reshape(-1)
+        if self.eval_metric == "rmse":
+            loc = float(np.sum((y - p) ** 2))
+        elif self.eval_metric == "error":
+            loc = float(np.sum((p > 0.5).astype(np.float64) != y))
+        else:
+            loc = float(M.logloss(y, p) * y.size) if y.size else 0.0
+        tot = dp.sum_(np.array([loc, float(y.size)]))
+        m = tot[0] / max(tot[1], 1.0)
+        return float(np.sqrt(m)) if self.eval_metric == "rmse" else float(m)
 
     def _log_round(self, rec):
         if self.log is None or (rec["round"] % self.log_every and rec["round"] != self.nround - 1):

@@ -21,6 +21,11 @@ N.register_signatures({
                          _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
     "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
     "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
+    "em_gbdt_dp_round_begin": (_i, [_i, _i, _i, _i, _v, _v, _v, _v, _v, _i, _f, _u32, _v, _v, _v, _v, _v]),
+    "em_gbdt_dp_level_hist": (_i, [_i, _v, _v, _v, _v, _i, _i, _i, _i, _v, _i64, ctypes.POINTER(_i64), _v]),
+    "em_gbdt_dp_level_split": (_i, [_i, _v, _v, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v, _v, _v, _f, _f, _v]),
+    "em_gbdt_dp_round_end": (_i, [_i, _i, _i, _v, _v, _v, _v, _v, _v, _v, _v, _v, _f, _f, _f, _v]),
+    "em_gbdt_metric_sum": (_i, [_v, _v, _i, _i, _i, _i, _v, _v, _v]),
 })
 
 OBJ = {"reg:logistic": 0, "binary:logistic": 0, "reg:squarederror": 1}
@@ -31,7 +36,7 @@ def _dev():
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25):
+def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     dev = _dev()
     n, F = bins.shape
     T = Y.shape[1]
@@ -73,7 +78,10 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25):
     cover = torch.zeros_like(leaf)
     hist = torch.zeros(R * (1 + len(ev_names)), dtype=torch.float32, device=dev)
     history = []
-    r0 = 0
+    if dp is not None:
+        _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, nbins, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
+                       mpart, status, feat, sbin, leaf, gain, cover, history, stream)
+    r0 = R if dp is not None else 0
     while r0 < R:
         r1 = min(R, r0 + rounds_per_call)
         N.call("em_gbdt_fit", d_bins.data_ptr(), d_Y.data_ptr(), n, F, nbins, T, margin.data_ptr(), ev_structs,
@@ -100,6 +108,57 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25):
     trees.cover[:] = cover.view(R * T, NN).cpu().numpy().astype(np.float64)
     model._device_trees = (status, feat, sbin, leaf)
     return trees, history
+
+
+def _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, nbins, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
+                   mpart, status, feat, sbin, leaf, gain, cover, history, stream):
+    """C4: per-level histogram all-reduce between the HIP hist and split kernels (stream-ordered,
+    no host sync inside a round); metric sums are all-reduced and read back once at the end."""
+    import torch.distributed as dist
+
+    R, D = model.nround, model.max_depth
+    NN = 2 ** (D + 1) - 1
+    dev = d_bins.device
+    seed = (model.seed + 0x9E3779B9 * dp.rank) & 0xFFFFFFFF
+    msum = torch.zeros(R, max(1, len(ev_names)), 2, dtype=torch.float64, device=dev)
+    S = ctypes.c_int64(0)
+    obj, met = OBJ[model.objective], MET[model.eval_metric]
+
+    def off(t, k):  # pointer to round-k slice of a [R*T*NN] buffer
+        return t.data_ptr() + k * T * NN * t.element_size()
+
+    for rnd in range(R):
+        N.call("em_gbdt_dp_round_begin", rnd, T, n, D, margin.data_ptr(), d_Y.data_ptr(), g.data_ptr(), h.data_ptr(),
+               node.data_ptr(), obj, model.subsample, seed, off(status, rnd), off(feat, rnd), off(sbin, rnd),
+               off(gain, rnd), stream)
+        for level in range(D):
+            N.call("em_gbdt_dp_level_hist", level, d_bins.data_ptr(), g.data_ptr(), h.data_ptr(), node.data_ptr(), T, n,
+                   F, nbins, partial.data_ptr(), partial.numel(), ctypes.byref(S), stream)
+            dist.all_reduce(partial[:S.value], group=dp.group)
+            N.call("em_gbdt_dp_level_split", level, d_bins.data_ptr(), partial.data_ptr(), T, n, F, nbins, D,
+                   node.data_ptr(), Gs.data_ptr(), Hs.data_ptr(), off(status, rnd), off(feat, rnd), off(sbin, rnd),
+                   off(gain, rnd), model.lam, model.mcw, stream)
+        N.call("em_gbdt_dp_round_end", T, n, D, margin.data_ptr(), node.data_ptr(), off(status, rnd), off(feat, rnd),
+               off(gain, rnd), Gs.data_ptr(), Hs.data_ptr(), off(leaf, rnd), off(cover, rnd), model.lam, model.gamma,
+               model.eta, stream)
+        for j, name in enumerate(ev_names):
+            db, dy, em = ev_keep[3 * j:3 * j + 3]
+            ne = db.shape[0]
+            N.call("em_gbdt_predict", db.data_ptr(), em.data_ptr(), T, ne, F, D, rnd * T, rnd * T + T,
+                   status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), stream)
+            N.call("em_gbdt_metric_sum", em.data_ptr(), dy.data_ptr(), T, ne, obj, met, mpart.data_ptr(),
+                   msum[rnd, j, :1].data_ptr(), stream)
+            msum[rnd, j, 1] = float(T * ne)
+    if ev_names:
+        dist.all_reduce(msum, group=dp.group)
+    ms = msum.cpu().numpy()
+    for rnd in range(R):
+        rec = {"round": rnd}
+        for j, name in enumerate(ev_names):
+            v = ms[rnd, j, 0] / max(ms[rnd, j, 1], 1.0)
+            rec[name] = float(np.sqrt(v)) if model.eval_metric == "rmse" else float(v)
+        history.append(rec)
+        model._log_round(rec)
 
 
 def predict_margin(model, X):

@@ -111,16 +111,25 @@ def run_reference_pipeline(cfg: RunConfig, out=None) -> dict:
     mk = dict(nround=g.nround, reg_lambda=g.reg_lambda, min_child_weight=g.min_child_weight,
               base_score=g.base_score, max_bin=g.max_bin, backend=_gbdt_backend(cfg), log=log,
               log_every=max(1, g.nround // 20))
-    watches = {"train": (Xtr, Ytr), "test": (Xva, Yva)}
-    booster = GBDT.from_params(cfg.gbdt_params(), **mk).fit(Xtr, Ytr, evals=watches)
+    # data-parallel boosting (C4) under torchrun: row shards, all-reduced histograms, identical trees
+    from .parallel import dist as D
+
+    info = D.init(cfg.dist.backend, cfg.dist.timeout_s, device="cpu" if _gbdt_backend(cfg) == "numpy" else cfg.device)
+    group = info.group if info.is_dist else None
+    a, b = D.shard_range(len(Xtr), info)
+    va, vb = D.shard_range(len(Xva), info)
+    watches = {"train": (Xtr[a:b], Ytr[a:b]), "test": (Xva[va:vb], Yva[va:vb])}
+    booster = GBDT.from_params(cfg.gbdt_params(), **mk).fit(Xtr[a:b], Ytr[a:b], evals=watches, group=group)
     p_train = booster.predict(Xtr)
     if cfg.reference_compat:
-        booster_test = GBDT.from_params(cfg.gbdt_params(), **mk).fit(Xva, Yva, evals=watches)  # D-f
+        booster_test = GBDT.from_params(cfg.gbdt_params(), **mk).fit(Xva[va:vb], Yva[va:vb], evals=watches,
+                                                                      group=group)  # D-f
         p_val = booster_test.predict(Xva)
     else:
         p_val = booster.predict(Xva)
     compat = M.check_predicts(p_train, p_val)
-    (out.write if out else print)(str(compat).lower() + ("\n" if out else ""))  # Main.java:143 prints the boolean
+    if info.rank == 0:
+        (out.write if out else print)(str(compat).lower() + ("\n" if out else ""))  # Main.java:143 prints the boolean
     res = {"pipeline": "reference", "target": target, "n_draws": len(ds), "n_train": int(margin),
            "n_val": int(n - margin), "backend": booster.backend_used, "check_predicts": compat,
            "train_" + g.eval_metric: booster.history[-1].get("train") if booster.history else None,
@@ -130,9 +139,11 @@ def run_reference_pipeline(cfg: RunConfig, out=None) -> dict:
         margins = booster.predict_margin(Xva)
         res["val"] = M.draw_metrics(margins, Yva, loss="bce")
         res["chance"] = M.chance_levels()
-    if cfg.ckpt.path:
+    res["world_size"] = info.world
+    if cfg.ckpt.path and info.rank == 0:
         booster.save(cfg.ckpt.path)
         res["checkpoint"] = cfg.ckpt.path
+    D.shutdown(info)
     return res
 
 

@@ -62,6 +62,31 @@ def case_forest(out):
     dist.destroy_process_group()
 
 
+def case_gbdt(out):
+    """Data-parallel boosting (C4): each rank fits on its row shard with all-reduced histograms."""
+    import numpy as np
+
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.gbdt import GBDT
+    from euromillioner_amd.parallel.dist import DistInfo, shard_range
+    from euromillioner_amd.pipeline import gbdt_dataset
+    from euromillioner_amd import config as C
+
+    rank, world = _init()
+    ds = DrawSet.synthetic(n=700, seed=4, planted=0.6, calendar=True)
+    X, Y, _ = gbdt_dataset(ds, C.RunConfig())
+    Y = Y[:, :6]
+    n_tr = 500
+    a, b = shard_range(n_tr, DistInfo(rank, world))
+    va, vb = shard_range(len(X) - n_tr, DistInfo(rank, world))
+    m = GBDT(eta=0.5, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=8, backend="numpy")
+    m.fit(X[a:b], Y[a:b], evals={"test": (X[n_tr + va:n_tr + vb], Y[n_tr + va:n_tr + vb])}, group=dist.group.WORLD)
+    if rank == 0:
+        np.savez(out, feat=m.trees.feat, sbin=m.trees.sbin, leaf=m.trees.leaf,
+                 hist=np.array([h["test"] for h in m.history]))
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     case = sys.argv[1]
     globals()["case_" + case](*sys.argv[2:])

@@ -155,3 +155,36 @@ def test_resume_auto(tmp_path):
     r = _launch(_train_argv(base + ["--steps", "6"]), 1)
     assert r[0][0] == 0 and "resumed from" in r[0][1]
     assert _params(p)[3]["step"] == 6
+
+
+def test_data_parallel_gbdt_equals_single(tmp_path):
+    """C4: histogram all-reduce over 2 ranks == one process on the concatenated rows."""
+    from euromillioner_amd import config as C
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.gbdt import GBDT
+    from euromillioner_amd.pipeline import gbdt_dataset
+
+    out = str(tmp_path / "g.npz")
+    res = _launch([sys.executable, WORKER, "gbdt", out], 2)
+    assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
+    z = np.load(out, allow_pickle=False)
+    ds = DrawSet.synthetic(n=700, seed=4, planted=0.6, calendar=True)
+    X, Y, _ = gbdt_dataset(ds, C.RunConfig())
+    Y = Y[:, :6]
+    m = GBDT(eta=0.5, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=8, backend="numpy")
+    m.fit(X[:500], Y[:500], evals={"test": (X[500:], Y[500:])})
+    assert np.array_equal(z["feat"], m.trees.feat) and np.array_equal(z["sbin"], m.trees.sbin)
+    assert np.allclose(z["leaf"], m.trees.leaf, atol=1e-6)
+    assert np.allclose(z["hist"], [h["test"] for h in m.history], atol=1e-6)
+
+
+def test_cli_pipeline_data_parallel(tmp_path):
+    """`euromillioner run` under 2 ranks: DP boosting, only rank 0 prints the checkPredicts line."""
+    argv = [sys.executable, "-m", "euromillioner_amd", "run", "--device", "cpu", "--n-draws", "400", "--nround", "4",
+            "--workdir", str(tmp_path)]
+    outs = _launch(argv, 2)
+    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    lines0 = [l for l in outs[0][1].splitlines() if l.strip() in ("true", "false")]
+    lines1 = [l for l in outs[1][1].splitlines() if l.strip() in ("true", "false")]
+    assert len(lines0) == 1 and not lines1
+    assert '"world_size": 2' in outs[0][1]

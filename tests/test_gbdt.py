@@ -126,3 +126,36 @@ def test_hip_engine_multitask():
     b = G.GBDT(nround=8, eta=0.5, backend="hip").fit(X[:15000], Y[:15000])
     assert np.array_equal(a.trees.feat, b.trees.feat)
     assert np.allclose(a.predict(X[15000:]), b.predict(X[15000:], backend="hip"), atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hip_dp_primitives_match_single_call():
+    """The data-parallel HIP path (per-level hist -> all-reduce -> split) on a 1-rank RCCL group
+    reproduces the fused multi-round driver exactly (C4 plumbing on one GPU)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from euromillioner_amd import config as C
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.gbdt import GBDT
+    from euromillioner_amd.pipeline import gbdt_dataset
+
+    ds = DrawSet.synthetic(n=900, seed=8, planted=0.6, calendar=True)
+    X, Y, _ = gbdt_dataset(ds, C.RunConfig())
+    Y = Y[:, :5]
+    kw = dict(eta=0.7, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=12, backend="hip")
+    ref = GBDT(**kw).fit(X[:600], Y[:600], evals={"test": (X[600:], Y[600:])})
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        dp = GBDT(**kw).fit(X[:600], Y[:600], evals={"test": (X[600:], Y[600:])}, group=dist.group.WORLD)
+    finally:
+        dist.destroy_process_group()
+    assert np.array_equal(dp.trees.feat, ref.trees.feat) and np.array_equal(dp.trees.sbin, ref.trees.sbin)
+    assert np.array_equal(dp.trees.leaf, ref.trees.leaf)
+    assert np.allclose([h["test"] for h in dp.history], [h["test"] for h in ref.history], rtol=1e-6)
