@@ -56,11 +56,14 @@ EM_DEVICE void mlp_pack_one(int p, float val, uint8_t* img) {
 // to finish (ticket) publishes step+1.  So one launch = one Adam step, with no host round-trip,
 // and the whole train step can be replayed from a hipGraph.
 EM_DEVICE int adam_begin(int* state) { return __hip_atomic_load(&state[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1; }
+// No release fence: the parameters/moments are consumed by later launches (a kernel boundary
+// publishes them); the ticket only orders the step counter, whose read in adam_begin has already
+// returned (its value fed the bias correction) before this block draws its ticket.  An agent-scope
+// release here is an L2 writeback per block (cdna_hip_programming.md 5, "3.9x slower").
 EM_DEVICE void adam_end(int* state, int t) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const int tk = __hip_atomic_fetch_add(&state[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const int tk = __hip_atomic_fetch_add(&state[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tk == (int)gridDim.x - 1) {
       __hip_atomic_store(&state[0], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&state[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -84,16 +87,16 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
   const int p = blockIdx.x * AS_P + tx;
   float g = 0.f;
   if (mode != 2) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (p < P) {
       int sl = ty;
-      for (; sl + 3 * AS_G < nslab; sl += 4 * AS_G) {
+      for (; sl + 7 * AS_G < nslab; sl += 8 * AS_G) {  // 8 independent loads in flight per thread
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] += slabs[(size_t)(sl + k * AS_G) * stride + p];
+        for (int k = 0; k < 8; ++k) acc[k] += slabs[(size_t)(sl + k * AS_G) * stride + p];
       }
       for (; sl < nslab; sl += AS_G) acc[0] += slabs[(size_t)sl * stride + p];
     }
-    part[ty][tx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    part[ty][tx] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     __syncthreads();
     if (ty == 0) {
       float t = 0.f;
