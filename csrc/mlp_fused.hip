@@ -28,6 +28,8 @@
 //   * dW accumulators (2 x 8 tiles x 16 regs = 256 regs) stay in AGPRs for the
 //     whole launch; one wave per SIMD.  The 4 waves are summed through LDS at
 //     the end and each workgroup writes ONE fp32 slab (deterministic; no atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -453,6 +455,385 @@ mlp_fused_train_kernel(const uint64_t* __restrict__ masks, const int32_t* __rest
   if (tid == 0) loss_slabs[blockIdx.x] = LOSSS[0] + LOSSS[1] + LOSSS[2] + LOSSS[3];
 }
 
+// ============================================================================================
+// v4: hidden-split wave pairs, two waves per SIMD.
+//
+// v3 keeps the whole dW (256 AGPRs) in every wave, so a CU runs one wave per SIMD and the
+// serial F1 -> relu -> F2 -> loss -> B1 -> mask -> dW chain of a tile leaves the matrix pipe idle
+// most of the time (PMC: MFMA busy 21 %, waiting 48 %).  v4 runs 8 waves (4 pairs) per CU.  The two
+// waves of a pair work on the SAME 32-sample tile and split the hidden layer: role rho owns hidden
+// units [64 rho, 64 rho + 64) and output tile u = rho, so each holds half of dW2 and of dW1T
+// (128 AGPRs) and does half of the MFMAs (40 per tile).  Per tile the pair exchanges through LDS:
+//   (1) the partial logits of the partner's output tile (4 KB fp32),
+//   (2) the per-sample softmax statistics (online-softmax merge: max and scaled sum),
+//   (3) the bf16 dZ2 fragments of its output tile (for B1) + its half of the D2 image.
+// Synchronisation is per pair through LDS counters (no workgroup barrier in the loop), so the two
+// waves that share a SIMD belong to different pairs and fill each other's dependency stalls.
+// Every spin is bounded: a broken protocol produces NaN losses, never a hung GPU.
+constexpr int V4_PAIR_BYTES = 25152;  // X 4K | D2 4K | H0 4K | H1 4K | XB0 4K | XB1 4K | stats 2x256 | flags 64
+constexpr int V4_PX = 0, V4_PD2 = 4096, V4_PH = 8192, V4_PXB = 16384, V4_PST = 24576, V4_PFL = 25088;
+static_assert(V4_PST + 2 * 256 <= V4_PFL && V4_PFL + 64 <= V4_PAIR_BYTES, "v4 pair layout");
+constexpr int V4_BASE = IMG_BYTES + LUT_BYTES;
+constexpr int V4_LOOP_LDS = V4_BASE + 4 * V4_PAIR_BYTES;
+constexpr int V4_RED = 65536;  // epilogue fp32 dW image [16384]
+constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 4096);
+#ifndef V4_SLEEP
+#define V4_SLEEP 0
+#endif
+constexpr int V4_SPIN_LIMIT = V4_SLEEP ? (1 << 22) : (1 << 24);
+static_assert(V4_LDS <= 163840, "v4 LDS budget");
+
+EM_DEVICE void pair_signal(char* smem, uint32_t flag_off, int value) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_store(reinterpret_cast<int*>(smem + flag_off), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// returns false if the partner never arrived (protocol bug): the caller poisons its loss
+EM_DEVICE bool pair_wait(const char* smem, uint32_t flag_off, int target) {
+  int spins = 0;
+  while (__hip_atomic_load(reinterpret_cast<const int*>(smem + flag_off), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    if (V4_SLEEP) __builtin_amdgcn_s_sleep(1);
+    if (++spins > V4_SPIN_LIMIT) return false;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return true;
+}
+
+// class of output o = 32 RHO + oo0(i) + 4h: 0 main, 1 star, 2 pad
+template <int RHO>
+EM_DEVICE int v4_cls(int i, int h) {
+  const int o = 32 * RHO + oo0(i) + 4 * h;
+  return o < 50 ? 0 : (o < 62 ? 1 : 2);
+}
+
+template <int LOSS, int RHO>
+EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int r, int h, int lane, int q4, int p4,
+                       int g1, uint64_t imask, uint64_t tmask, bool valid, int& sig, bool& ok, f32x16 (&dW2)[2][2],
+                       f32x16 (&dW1T)[2][2], float (&db2)[16], float& loss_acc) {
+  constexpr int PR = 1 - RHO;
+  const uint32_t XB = PB + V4_PX, DB = PB + V4_PD2, HB = PB + V4_PH + RHO * 4096;
+  const uint32_t MYX = PB + V4_PXB + RHO * 4096, PAX = PB + V4_PXB + PR * 4096;
+  const uint32_t MYFL = PB + V4_PFL + RHO * 4, PAFL = PB + V4_PFL + PR * 4;
+  (void)pairw;
+
+  bf16x8 xf[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xf[q] = lut_frag(lut, imask, q, h);
+
+  // ---- F1 (own hidden half) -> relu -> hT (B of F2) + own H image [32 samples][64 hid] ----
+  bf16x8 hT[2][2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int t = 2 * RHO + tt;
+    f32x16 a1 = f32x16{};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a1 = mfma32(lds_frag(smem, w1t_off(32 * t + r, 2 * q + h)), xf[q], a1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      hT[tt][q] = relu_pack(a1, q);
+      const u32x4 d = __builtin_bit_cast(u32x4, hT[tt][q]);
+      *reinterpret_cast<u32x2*>(smem + HB + r * 128 + ((((4 * tt + 2 * q) ^ (r & 7))) << 4) + h * 8) =
+          u32x2{d[0], d[1]};
+      *reinterpret_cast<u32x2*>(smem + HB + r * 128 + ((((4 * tt + 2 * q + 1) ^ (r & 7))) << 4) + h * 8) =
+          u32x2{d[2], d[3]};
+    }
+  }
+
+  // ---- F2 partial over the own hidden half, both output tiles ----
+  f32x16 zp[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    zp[u] = f32x16{};
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        zp[u] = mfma32(lds_frag(smem, w2p_off(32 * u + r, (2 * (2 * RHO + tt) + q) * 2 + h)), hT[tt][q], zp[u]);
+  }
+
+  // ---- exchange (1): give the partner its output tile's partial, take ours ----
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<f32x4*>(smem + MYX + (g * 64 + lane) * 16) =
+        f32x4{zp[PR][4 * g + 0], zp[PR][4 * g + 1], zp[PR][4 * g + 2], zp[PR][4 * g + 3]};
+  pair_signal(smem, MYFL, ++sig);
+  ok &= pair_wait(smem, PAFL, sig);
+  f32x16 z = zp[RHO];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 o = *reinterpret_cast<const f32x4*>(smem + PAX + (g * 64 + lane) * 16);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * RHO + 8 * g + 4 * h) * 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[4 * g + k] += o[k] + b[k];
+  }
+  if (RHO == 0) {  // the pair-shared X image [32 samples][64 feat]; the partner is past its previous tile
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<bf16x8*>(smem + XB + r * 128 + ((((2 * q + h) ^ (r & 7))) << 4)) = xf[q];
+  }
+
+  // ---- loss on the own output tile ----
+  const uint32_t tmh = (uint32_t)(tmask >> (32 * RHO)) >> (4 * h);
+  float dz[16];
+  if (LOSS == 0) {
+    const int nm = __builtin_popcountll(tmask & MAIN_BITS), ns = __builtin_popcountll(tmask & STAR_BITS);
+    const float inv_m = nm ? 1.f / (float)nm : 0.f, inv_s = ns ? 1.f / (float)ns : 0.f;
+    float mx_m = -3.0e38f, mx_s = -3.0e38f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v4_cls<RHO>(i, h);
+      mx_m = (c == 0) ? fmaxf(mx_m, z[i]) : mx_m;
+      if (RHO == 1) mx_s = (c == 1) ? fmaxf(mx_s, z[i]) : mx_s;
+    }
+    mx_m = fmaxf(mx_m, __shfl_xor(mx_m, 32));
+    if (RHO == 1) mx_s = fmaxf(mx_s, __shfl_xor(mx_s, 32));
+    float s_m = 0.f, s_s = 0.f, zt = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v4_cls<RHO>(i, h);
+      const float e = __expf(z[i] - ((RHO == 1 && c == 1) ? mx_s : mx_m));
+      const float ee = (c == 2) ? 0.f : e;
+      dz[i] = ee;
+      s_m += (c == 0) ? ee : 0.f;
+      if (RHO == 1) s_s += (c == 1) ? ee : 0.f;
+      const bool t = (tmh >> oo0(i)) & 1u;
+      zt += t ? z[i] * (c == 0 ? inv_m : inv_s) : 0.f;
+    }
+    s_m += __shfl_xor(s_m, 32);
+    if (RHO == 1) s_s += __shfl_xor(s_s, 32);
+    // exchange (2): online-softmax merge of the main-group statistics
+    if (h == 0) *reinterpret_cast<float2*>(smem + PB + V4_PST + RHO * 256 + r * 8) = float2{mx_m, s_m};
+    pair_signal(smem, MYFL, ++sig);
+    ok &= pair_wait(smem, PAFL, sig);
+    const float2 ps = *reinterpret_cast<const float2*>(smem + PB + V4_PST + PR * 256 + r * 8);
+    const float M = fmaxf(mx_m, ps.x);
+    const float S = s_m * __expf(mx_m - M) + ps.y * __expf(ps.x - M);
+    const float f_m = nm ? __expf(mx_m - M) / S : 0.f;
+    const float f_s = (RHO == 1 && ns) ? 1.f / s_s : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v4_cls<RHO>(i, h);
+      const bool t = (tmh >> oo0(i)) & 1u;
+      const float pr = dz[i] * (c == 0 ? f_m : f_s);
+      const float y = t ? (c == 0 ? inv_m : inv_s) : 0.f;
+      dz[i] = (valid && c != 2) ? pr - y : 0.f;
+    }
+    float l = -zt;
+    if (RHO == 1 && h == 0) l += (nm ? M + __logf(S) : 0.f) + (ns ? mx_s + __logf(s_s) : 0.f);
+    loss_acc += valid ? l : 0.f;
+  } else {
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v4_cls<RHO>(i, h);
+      const float v = z[i];
+      const float y = ((tmh >> oo0(i)) & 1u) ? 1.f : 0.f;
+      const float en = __expf(-fabsf(v));
+      const float pr = v >= 0.f ? 1.f / (1.f + en) : en / (1.f + en);
+      const float sp = fmaxf(v, 0.f) + __logf(1.f + en);
+      const bool okc = valid && c != 2;
+      dz[i] = okc ? (pr - y) : 0.f;
+      l += okc ? (sp - y * v) : 0.f;
+    }
+    loss_acc += l;
+    pair_signal(smem, MYFL, ++sig);  // keeps the exchange-buffer reuse below ordered
+    ok &= pair_wait(smem, PAFL, sig);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) db2[i] += dz[i];
+  bf16x8 dzf[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    dzf[q] = pack8(dz[8 * q + 0], dz[8 * q + 1], dz[8 * q + 2], dz[8 * q + 3], dz[8 * q + 4], dz[8 * q + 5],
+                   dz[8 * q + 6], dz[8 * q + 7]);
+  // exchange (3): dZ2 fragments (lane-for-lane dump into our exchange buffer; the partner has read
+  // its partial from it, which it did before its signal (2)) + our half of the D2 image
+#pragma unroll
+  for (int q = 0; q < 2; ++q) *reinterpret_cast<bf16x8*>(smem + MYX + (q * 64 + lane) * 16) = dzf[q];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 f = __builtin_bit_cast(u32x4, dzf[g >> 1]);
+    *reinterpret_cast<u32x2*>(smem + DB + r * 128 + ((((4 * RHO + g) ^ (r & 7))) << 4) + h * 8) =
+        u32x2{f[2 * (g & 1)], f[2 * (g & 1) + 1]};
+  }
+  pair_signal(smem, MYFL, ++sig);
+  ok &= pair_wait(smem, PAFL, sig);
+  bf16x8 dzp[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) dzp[q] = *reinterpret_cast<const bf16x8*>(smem + PAX + (q * 64 + lane) * 16);
+
+  // ---- B1: dH = dZ2·W2ᵀ for the own hidden half; dZ1 = dH * (Z1 > 0) ----
+  bf16x8 hR[2][2], dz1[2][2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int t = 2 * RHO + tt;
+    f32x16 aD = f32x16{};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        aD = mfma32(u == RHO ? dzf[q] : dzp[q], lds_frag(smem, w2q_off(32 * t + r, (2 * u + q) * 2 + h)), aD);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      hR[tt][q] = tr_frag<0>(smem, HB, 32 * tt, q, h, q4, p4, g1);
+      dz1[tt][q] = mask_by(hR[tt][q], aD, q);
+    }
+  }
+
+  // ---- dW2[own hid][out] += Hᵀ·dZ2 ; dW1ᵀ[own hid][feat] += dZ1ᵀ·X ----
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bf16x8 bd = tr_frag<0>(smem, DB, 32 * u, q, h, q4, p4, g1);
+      const bf16x8 bx = tr_frag<0>(smem, XB, 32 * u, q, h, q4, p4, g1);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        mfma_acc_agpr(dW2[tt][u], hR[tt][q], bd);
+        mfma_acc_agpr(dW1T[tt][u], dz1[tt][q], bx);
+      }
+    }
+  wave_lds_sync();  // own H image is rewritten by the next tile
+}
+
+// One role's whole persistent loop + its share of the epilogue reduction.  Instantiated per role so
+// the AGPR-pinned dW accumulators never cross a role branch (a merge point would force copies).
+template <int LOSS, int RHO>
+EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                       int offset, int pair, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const char* lut = smem + IMG_BYTES;
+  const uint32_t PB = V4_BASE + pair * V4_PAIR_BYTES;
+  f32x16 dW2[2][2], dW1T[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      dW2[t][u] = f32x16{};
+      dW1T[t][u] = f32x16{};
+    }
+  float db2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) db2[i] = 0.f;
+  float loss_acc = 0.f;
+  int sig = 0;
+  bool ok = true;
+
+  const int ntiles = (B + 31) / 32;
+  const int npairs = gridDim.x * 4;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
+  auto fetch = [&](int tile, uint64_t& mi, uint64_t& mt) {
+    const int s = tile * 32 + r;
+    mi = 0;
+    mt = 0;
+    if (tile < ntiles && s < B) {
+      const int idx = sidx ? sidx[s] : (offset + s);
+      mi = masks[idx];
+      mt = masks[idx + 1];
+    }
+  };
+  const int first = blockIdx.x * 4 + pair;
+  uint64_t nin, ntg;
+  fetch(first, nin, ntg);
+  for (int tile = first; tile < ntiles; tile += npairs) {
+    const int s = tile * 32 + r;
+    const bool valid = s < B;
+    const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
+    const uint64_t tmask = valid ? ntg : 0ull;
+    fetch(tile + npairs, nin, ntg);
+    v4_tile<LOSS, RHO>(smem, lut, PB, pair, r, h, lane, q4, p4, g1, imask, tmask, valid, sig, ok, dW2, dW1T, db2,
+                       loss_acc);
+  }
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // asm MFMA (AGPR D) -> v_accvgpr_read hazard
+
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float v = db2[i];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o);
+    db2[i] = v;
+  }
+  float lsum = wave_sum(loss_acc);
+  if (!ok) lsum = __builtin_nanf("");
+  __syncthreads();  // every wave is out of the loop: the loop's LDS is free
+  float* RED = reinterpret_cast<float*>(smem);  // [16 tiles][4 g][64 lanes][4]: tiles 0..7 dW2, 8..15 dW1T
+  float* DB2S = reinterpret_cast<float*>(smem + V4_RED);          // [4 pairs][64]
+  float* LOSSS = reinterpret_cast<float*>(smem + V4_RED + 1024);  // [8]
+  if (r == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) DB2S[pair * 64 + 32 * RHO + oo0(i) + 4 * h] = db2[i];
+  }
+  if (lane == 0) LOSSS[2 * pair + RHO] = lsum;
+  // the same number of barriers in both role instantiations (wave-uniform branch)
+  for (int stage = 0; stage < 4; ++stage) {
+    if (pair == stage) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int which = 0; which < 2; ++which) {
+            const f32x16& acc = which ? dW1T[tt][u] : dW2[tt][u];
+            const int T = 8 * which + 2 * (2 * RHO + tt) + u;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              f32x4* p = reinterpret_cast<f32x4*>(RED + ((T * 4 + g) * 64 + lane) * 4);
+              f32x4 v = {acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+              if (stage) v += *p;
+              *p = v;
+            }
+          }
+    }
+    __syncthreads();
+  }
+}
+
+template <int LOSS>
+__global__ void __launch_bounds__(512, 1)
+mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
+                          const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                          float* __restrict__ loss_slabs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pair = wave >> 1, rho = wave & 1;
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
+    u32x4* dst = reinterpret_cast<u32x4*>(smem);
+    for (int i = tid; i < IMG_BYTES / 16; i += 512) dst[i] = src[i];
+  }
+  fill_lut(smem + IMG_BYTES, tid);
+  if (lane < 2) reinterpret_cast<int*>(smem + V4_BASE + pair * V4_PAIR_BYTES + V4_PFL)[lane] = 0;
+  __syncthreads();
+  if (rho == 0)
+    v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane);
+  else
+    v4_body<LOSS, 1>(smem, masks, sidx, B, offset, pair, lane);
+
+  const float* RED = reinterpret_cast<const float*>(smem);
+  const float* DB2S = reinterpret_cast<const float*>(smem + V4_RED);
+  const float* LOSSS = reinterpret_cast<const float*>(smem + V4_RED + 1024);
+  float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
+  for (int e = tid; e < 16 * 4 * 64; e += 512) {
+    const int T = e >> 8, g = (e >> 6) & 3, l = e & 63, hh = l >> 5, rr = l & 31;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + e * 4);
+    const int c0 = 32 * ((T & 7) >> 1) + 8 * g + 4 * hh;  // hidden rows c0..c0+3
+    const int col = 32 * (T & 1) + rr;
+    if (T < 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) slab[P_W2 + (c0 + k) * OUT + col] = v[k];
+    } else {
+      *reinterpret_cast<f32x4*>(slab + P_W1 + col * HID + c0) = v;
+    }
+  }
+  if (tid < 64) slab[P_B2 + tid] = DB2S[tid] + DB2S[64 + tid] + DB2S[128 + tid] + DB2S[192 + tid];
+  if (tid == 0) {
+    float l = 0.f;
+    for (int w = 0; w < 8; ++w) l += LOSSS[w];
+    loss_slabs[blockIdx.x] = l;
+  }
+}
+
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
 __global__ void __launch_bounds__(256)
 mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
@@ -537,7 +918,23 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
                               TRAIN_LDS);
     attr_set = true;
   }
-  if (loss_kind == 0)
+  static int use_v3 = -1;
+  if (use_v3 < 0) {
+    const char* e = std::getenv("EM_FUSED_V3");
+    use_v3 = (e && e[0] == '1') ? 1 : 0;
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v4_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V4_LDS);
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v4_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V4_LDS);
+  }
+  if (!use_v3) {
+    if (loss_kind == 0)
+      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<0>, dim3(nslab), dim3(512), V4_LDS, stream, draws, sidx, (int)B,
+                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+    else
+      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<1>, dim3(nslab), dim3(512), V4_LDS, stream, draws, sidx, (int)B,
+                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+  } else if (loss_kind == 0)
     hipLaunchKernelGGL(mlp_fused_train_kernel<0>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, (int)B, (int)offset,
                        (const uint8_t*)wimg, slabs, loss_slabs);
   else
