@@ -116,8 +116,16 @@ template <int A_KC, int B_KC>
 __global__ void __launch_bounds__(NT, 2)
 gemm_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb, void* __restrict__ C,
             int64_t ldc, int c_bf16, int M, int N, int K, const float* __restrict__ bias, int act,
-            const __bf16* __restrict__ mask, int64_t ldm, int dact, float alpha, float beta) {
+            const __bf16* __restrict__ mask, int64_t ldm, int dact, float alpha, float beta, int kstep,
+            int64_t c_split) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (gridDim.y > 1) {  // split-K: slice blockIdx.y of the reduction into its own fp32/bf16 partial output
+    const int k0 = blockIdx.y * kstep;
+    A += A_KC ? (int64_t)k0 : (int64_t)k0 * lda;
+    B += B_KC ? (int64_t)k0 : (int64_t)k0 * ldb;
+    K = min(kstep, K - k0);
+    C = reinterpret_cast<char*>(C) + (int64_t)blockIdx.y * c_split * (c_bf16 ? 2 : 4);
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
@@ -211,7 +219,7 @@ gemm_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict_
 constexpr int G_BM = 256, G_BN = 256, G_BK = 64, G_NT = 512;
 constexpr int G_TILE = G_BM * G_BK * 2;  // 32 KB per operand per stage
 constexpr int G_LOOP_LDS = 2 * 2 * G_TILE;  // 128 KB: 2 stages x (A, B)
-constexpr int G_EPI_LDS = 8 * 128 * 144;     // epilogue: per-wave 128 x 64 bf16 tile, 144-B rows
+constexpr int G_EPI_LDS = 8 * (64 * 80 + 32 * 144);  // epilogue: per-wave transposed 64x32 tile + 32x64 Y block
 constexpr int G_LDS = G_LOOP_LDS > G_EPI_LDS ? G_LOOP_LDS : G_EPI_LDS;
 
 EM_DEVICE uint32_t g_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -323,58 +331,85 @@ gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
     __syncthreads();
   }
 
-  // ---- epilogue: lane owns column `col`, rows rbase + 8g + e ----
-  // DACT: stage this wave's 128x64 tile of the saved activations through its own 18 KB of the
-  // (now idle) LDS with coalesced 16-B loads, instead of 128 scattered 2-B loads per lane.
-  const __bf16* ylds = reinterpret_cast<const __bf16*>(smem + wave * 128 * 144);
-  if (DACT) {
-    char* yw = smem + wave * 128 * 144;
-    const __bf16* ysrc = mask + (int64_t)(m0 + wm * 128) * ldm + n0 + wn * 64;
-#pragma unroll 4
-    for (int t = 0; t < 16; ++t) {
-      const int q = lane + 64 * t;
-      const int row = q >> 3, ch = q & 7;
-      *reinterpret_cast<u32x4*>(yw + row * 144 + ch * 16) =
-          *reinterpret_cast<const u32x4*>(ysrc + (int64_t)row * ldm + ch * 8);
+  // ---- epilogue, one 32-row block of this wave's 128x64 tile at a time ----
+  // bf16 outputs go through a per-wave transposed LDS tile T[64 cols][32 rows] (ds_write_b64 of 4
+  // consecutive rows per lane), then leave as 16-B coalesced stores: C rows via ds_read_b64_tr_b16
+  // pairs (8 consecutive columns of one row), C^T rows straight from T.  DACT stages the matching
+  // 32x64 block of the saved activations with 16-B loads.
+  constexpr int TS = 80;                    // bytes per T row (32 bf16 + pad)
+  constexpr int YS = 144;                   // bytes per staged Y row (64 bf16 + pad)
+  constexpr int WEPI = 64 * TS + 32 * YS;   // per-wave epilogue bytes
+  char* tb = smem + wave * WEPI;
+  char* yb = tb + 64 * TS;
+  const int colw = n0 + wn * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // unrolled: acc[i] must stay statically indexed (no scratch)
+    const int rowb = m0 + wm * 128 + 32 * i;  // first row of this block
+    if (DACT) {
+      const __bf16* ysrc = mask + (int64_t)rowb * ldm + colw;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int q = lane + 64 * t;
+        const int row = q >> 3, ch = q & 7;
+        *reinterpret_cast<u32x4*>(yb + row * YS + ch * 16) =
+            *reinterpret_cast<const u32x4*>(ysrc + (int64_t)row * ldm + ch * 8);
+      }
+      wave_lds_sync();
     }
-    wave_lds_sync();
-  }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 64 + 32 * j + r;
-    const float bv = (!DACT && bias) ? bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rbase = m0 + wm * 128 + 32 * i + 4 * h;
+    for (int j = 0; j < 2; ++j) {
+      const int lc = 32 * j + r;
+      const float bv = (!DACT && bias) ? bias[colw + lc] : 0.f;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float x[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int64_t row = rbase + 8 * g + e;
+          const int lr = 8 * g + 4 * h + e;
           float v = alpha * acc[i][j][4 * g + e];
           if (DACT) {
-            const int lr = 32 * i + 4 * h + 8 * g + e, lc = 32 * j + r;
-            v *= g_dfn<FN>((float)ylds[lr * 72 + lc]);
+            v *= g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
           } else {
             v = g_fn<FN>(v + bv);
           }
           x[e] = v;
-          if (OUT_BF16) {
-            reinterpret_cast<__bf16*>(C)[row * ldc + col] = (__bf16)v;
-          } else {
-            float* cp = reinterpret_cast<float*>(C) + row * ldc + col;
+          if (!OUT_BF16) {
+            float* cp = reinterpret_cast<float*>(C) + (int64_t)(rowb + lr) * ldc + colw + lc;
             *cp = beta != 0.f ? v + beta * *cp : v;
           }
         }
-        if (HAS_CT) {  // 4 consecutive rows of C = 8 contiguous bytes of C^T
+        if (OUT_BF16) {
           __bf16 t4[4] = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
           u32x2 pk;
           __builtin_memcpy(&pk, t4, 8);
-          *reinterpret_cast<u32x2*>(CT + (int64_t)col * ldct + rbase + 8 * g) = pk;
+          *reinterpret_cast<u32x2*>(tb + lc * TS + (8 * g + 4 * h) * 2) = pk;
         }
       }
     }
+    if (OUT_BF16) {
+      wave_lds_sync();
+      // C: group gg of 16 lanes covers rows 16*(gg&1)..+15, columns cb..cb+7 with cb = 8*(gg>>1) + 16*it
+      const int gg = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int cb = 8 * (gg >> 1) + 16 * it;
+        const int r0 = 16 * (gg & 1);
+        const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * TS + (r0 + 4 * p4) * 2));
+        const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * TS + (r0 + 4 * p4) * 2));
+        const bf16x8 v8 = cat_tr(lo, hi);
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + r0 + i16) * ldc + colw + cb) = v8;
+      }
+      if (HAS_CT) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = lane + 64 * k;
+          const int col = q >> 2, part = q & 3;
+          *reinterpret_cast<u32x4*>(CT + (int64_t)(colw + col) * ldct + rowb + part * 8) =
+              *reinterpret_cast<const u32x4*>(tb + col * TS + part * 16);
+        }
+      }
+    }
+    wave_lds_sync();  // T / Y blocks are rewritten by the next block
   }
 }
 
@@ -528,9 +563,33 @@ __global__ void __launch_bounds__(256) rowsum_kernel(const __bf16* __restrict__ 
 
 }  // namespace
 
+static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
+                     int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
+                     int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, int splits, int kstep,
+                     int64_t c_split, hipStream_t stream);
+
 EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                         int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
                         int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, hipStream_t stream) {
+  return gemm_impl(A, lda, a_kc, B, ldb, b_kc, C, ldc, c_bf16, M, N, K, bias, act, mask, ldm, dact, alpha, beta, ct,
+                   ldct, 1, K, 0, stream);
+}
+
+// Split-K on the any-layout kernel: `splits` slices of `kstep` (multiple of 64) along K, slice s writing
+// C + s * c_split (elements).  For small outputs with a huge reduction (64 x 8192 over a 64k batch).
+EM_API int em_gemm_bf16_splitk(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
+                               int64_t ldc, int c_bf16, int M, int N, int K, float alpha, int splits, int kstep,
+                               int64_t c_split, hipStream_t stream) {
+  if (splits < 1 || splits > 65535 || kstep <= 0 || (kstep & 63) || (int64_t)splits * kstep < K || c_split < 0)
+    return EM_ERR_ARG;
+  return gemm_impl(A, lda, a_kc, B, ldb, b_kc, C, ldc, c_bf16, M, N, K, nullptr, 0, nullptr, 0, 0, alpha, 0.f,
+                   nullptr, 0, splits, kstep, c_split, stream);
+}
+
+static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
+                     int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
+                     int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, int splits, int kstep,
+                     int64_t c_split, hipStream_t stream) {
   if (!A || !B || !C || M < 0 || N < 0 || K < 0 || act < 0 || act > 3) return EM_ERR_ARG;
   if (mask && (dact < 1 || dact > 3)) return EM_ERR_ARG;
   if (M == 0 || N == 0) return 0;
@@ -544,7 +603,7 @@ EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int
     (void)hipFuncSetAttribute((const void*)gemm_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = true;
   }
-  const bool big = a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
+  const bool big = splits == 1 && a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
                    (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL");
   if (big) {
     const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
@@ -560,8 +619,8 @@ EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int
   const __bf16* b = (const __bf16*)B;
   const __bf16* mk = (const __bf16*)mask;
 #define EM_GEMM_LAUNCH(AK, BKC)                                                                                        \
-  hipLaunchKernelGGL((gemm_kernel<AK, BKC>), dim3(grid), dim3(NT), LDS_BYTES, stream, a, lda, b, ldb, C, ldc, c_bf16, M, \
-                     N, K, bias, act, mk, ldm, dact, alpha, beta)
+  hipLaunchKernelGGL((gemm_kernel<AK, BKC>), dim3(grid, splits), dim3(NT), LDS_BYTES, stream, a, lda, b, ldb, C, ldc,   \
+                     c_bf16, M, N, K, bias, act, mk, ldm, dact, alpha, beta, kstep, c_split)
   if (a_kc && b_kc) EM_GEMM_LAUNCH(1, 1);
   else if (a_kc && !b_kc) EM_GEMM_LAUNCH(1, 0);
   else if (!a_kc && !b_kc) EM_GEMM_LAUNCH(0, 0);

@@ -477,6 +477,9 @@ constexpr int V4_BASE = IMG_BYTES + LUT_BYTES;
 constexpr int V4_LOOP_LDS = V4_BASE + 4 * V4_PAIR_BYTES;
 constexpr int V4_RED = 65536;  // epilogue fp32 dW image [16384]
 constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 4096);
+#ifndef V4_STAGGER
+#define V4_STAGGER 80
+#endif
 #ifndef V4_SLEEP
 #define V4_SLEEP 0
 #endif
@@ -805,6 +808,13 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   fill_lut(smem + IMG_BYTES, tid);
   if (lane < 2) reinterpret_cast<int*>(smem + V4_BASE + pair * V4_PAIR_BYTES + V4_PFL)[lane] = 0;
   __syncthreads();
+  // waves 4-7 share SIMDs with waves 0-3 (other pairs): start them half a tile later so the two
+  // co-resident waves do not hit their MFMA and VALU phases in lockstep (MI355X_MICROARCH.md,
+  // "Two waves per SIMD" item 9), and give the younger half static priority (item 4)
+  if (V4_STAGGER && wave >= 4) {
+    __builtin_amdgcn_s_sleep(V4_STAGGER);  // ~64 cycles per unit
+    __builtin_amdgcn_s_setprio(1);
+  }
   if (rho == 0)
     v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane);
   else

@@ -27,6 +27,8 @@ N.register_signatures({
     "em_gemm_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32,
                               N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32, N._f32, N._f32,
                               N._c_void_p, N._i64, N._c_void_p]),
+    "em_gemm_bf16_splitk": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64,
+                                     N._i32, N._i32, N._i32, N._i32, N._f32, N._i32, N._i32, N._i64, N._c_void_p]),
     "em_colsum_ws_floats": (N._i32, [N._i32, N._i32]),
     "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p,
                                 N._c_void_p]),
@@ -177,24 +179,25 @@ def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
     if split_k is None:
         split_k = 1
         if tiles < 256 and M >= 8192:
-            split_k = max(1, min(512 // tiles, M // 4096))
+            split_k = max(1, min((1024 + tiles - 1) // tiles, M // 1024))
     if split_k <= 1:
         return gemm(dz, False, x, False, out, N_, K, M, alpha=alpha, beta=beta)
-    step = (M + split_k - 1) // split_k
-    step = (step + 7) // 8 * 8
-    parts = torch.empty(split_k, N_, round8(K), dtype=torch.float32, device=dz.device)
-    n_used = 0
-    for s in range(split_k):
-        a, b = s * step, min(M, (s + 1) * step)
-        if a >= b:
-            break
-        gemm(dz[a:b], False, x[a:b], False, parts[s, :, :K], N_, K, b - a)
-        n_used += 1
-    red = parts[:n_used, :, :K].sum(0)
+    for t, nm in ((dz, "dz"), (x, "x")):
+        N.check_cuda(t, nm, torch.bfloat16, contiguous=False)
+        if not is_aligned(t):
+            raise ValueError(f"{nm}: needs an aligned bf16 layout")
+    kstep = ((M + split_k - 1) // split_k + 63) // 64 * 64
+    split_k = (M + kstep - 1) // kstep
+    Kp = round8(K)
+    parts = torch.empty(split_k, N_, Kp, dtype=torch.float32, device=dz.device)
+    # one launch: blockIdx.y = K-slice -> its own fp32 partial [N, K]; then a fixed-order sum
+    N.call("em_gemm_bf16_splitk", dz.data_ptr(), dz.stride(0), 0, x.data_ptr(), x.stride(0), 0, parts.data_ptr(), Kp,
+           0, N_, K, M, float(alpha), split_k, kstep, N_ * Kp, N.stream_handle(dz.device))
+    red = parts[:, :, :K].sum(0)
     if beta != 0.0:
-        out.mul_(beta).add_(red, alpha=alpha)
+        out.mul_(beta).add_(red)
     else:
-        out.copy_(red.mul_(alpha) if alpha != 1.0 else red)
+        out.copy_(red)
     return out
 
 
