@@ -46,3 +46,47 @@ def test_rf_on_gpu():
     res = train(_cfg(**{"model": "rf", "rf.n_trees": 20, "rf.max_depth": 6}))
     assert res["backend"] == "hip" and res["trees"] == 20
     assert res["val"]["hits_main"] > 0.5
+
+
+def _nccl_world1():
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    return dist
+
+
+@pytest.mark.parametrize("engine", ["fused", "gemm"])
+def test_dp_code_path_on_one_rank_matches_local(engine):
+    """The RCCL data-parallel step (fused: slab-reduce -> all-reduce -> Adam; GEMM trainer:
+    per-layer async bucket all-reduce) on a 1-rank group equals the local step bit for bit."""
+    import torch
+
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds = DrawSet.synthetic(n=9000, seed=5, planted=0.7, calendar=False)
+    masks = FusedSmallMLP.prepare(torch.from_numpy(ds.numbers).cuda())
+    make = (lambda g: FusedSmallMLP("cuda", seed=1, lr=3e-3, process_group=g)) if engine == "fused" else \
+        (lambda g: GemmMLPTrainer((62, 256, 256, 62), "cuda", seed=1, lr=3e-3, process_group=g, bucket_mb=0.05))
+    local = make(None)
+    for k in range(4):
+        local.step(masks, 2048, offset=1000 * k)
+    dist = _nccl_world1()
+    try:
+        dp = make(dist.group.WORLD)
+        dp.broadcast_parameters()
+        for k in range(4):
+            loss = dp.step(masks, 2048, offset=1000 * k)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert torch.isfinite(loss).all()
+    assert torch.allclose(dp.params, local.params, atol=1e-6, rtol=0), float((dp.params - local.params).abs().max())
