@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""GBDT engine benchmark: the reference configuration (Main.java:113-138: gbtree, eta 1, depth 3,
+gamma 1, reg:logistic, logloss watch, 500 rounds) on the reference-sized draw history
+(~1.33k draws, 62 next-draw boosters), HIP engine vs the numpy oracle, plus a large synthetic
+draw set to show device throughput.  One JSON line per case."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from euromillioner_amd import config as C
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.gbdt import GBDT
+    from euromillioner_amd.pipeline import gbdt_dataset
+
+    cfg = C.RunConfig()
+    cases = [("reference_calendar", None, 500, True), ("synthetic_262k", 262145, 50, False)]
+    for name, n, rounds, with_numpy in cases:
+        ds = DrawSet.synthetic(n=n, seed=0, planted=0.5)
+        X, Y, _ = gbdt_dataset(ds, cfg)
+        m = int(0.7 * len(X))
+        res = {"case": name, "rows": m, "features": X.shape[1], "tasks": Y.shape[1], "rounds": rounds}
+        for be in (["hip", "numpy"] if with_numpy else ["hip"]):
+            g = GBDT.from_params(cfg.gbdt_params(), nround=rounds, backend=be)
+            t0 = time.perf_counter()
+            g.fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
+            dt = time.perf_counter() - t0
+            res[f"{be}_s"] = round(dt, 3)
+            res[f"{be}_test_logloss"] = g.history[-1]["test"]
+            res[f"{be}_trees_per_s"] = round(rounds * Y.shape[1] / dt, 1)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
