@@ -547,6 +547,13 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     zp[u] = f32x16{};
+    if (u == RHO) {  // b2 rides in as the accumulator init of the own output tile
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * RHO + 8 * g + 4 * h) * 4);
+        zp[u][4 * g + 0] = b[0]; zp[u][4 * g + 1] = b[1]; zp[u][4 * g + 2] = b[2]; zp[u][4 * g + 3] = b[3];
+      }
+    }
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -565,9 +572,8 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const f32x4 o = *reinterpret_cast<const f32x4*>(smem + PAX + (g * 64 + lane) * 16);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * RHO + 8 * g + 4 * h) * 4);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) z[4 * g + k] += o[k] + b[k];
+    for (int k = 0; k < 4; ++k) z[4 * g + k] += o[k];
   }
   if (RHO == 0) {  // the pair-shared X image [32 samples][64 feat]; the partner is past its previous tile
 #pragma unroll
@@ -577,6 +583,9 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 
   // ---- loss on the own output tile ----
   const uint32_t tmh = (uint32_t)(tmask >> (32 * RHO)) >> (4 * h);
+  float yb[16];  // target bits of the lane's 16 outputs, as 0/1 floats (one v_bfe + cvt each)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) yb[i] = (float)((tmh >> oo0(i)) & 1u);
   float dz[16];
   if (LOSS == 0) {
     const int nm = __builtin_popcountll(tmask & MAIN_BITS), ns = __builtin_popcountll(tmask & STAR_BITS);
@@ -599,8 +608,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
       dz[i] = ee;
       s_m += (c == 0) ? ee : 0.f;
       if (RHO == 1) s_s += (c == 1) ? ee : 0.f;
-      const bool t = (tmh >> oo0(i)) & 1u;
-      zt += t ? z[i] * (c == 0 ? inv_m : inv_s) : 0.f;
+      zt += yb[i] * z[i] * (c == 0 ? inv_m : inv_s);
     }
     s_m += __shfl_xor(s_m, 32);
     if (RHO == 1) s_s += __shfl_xor(s_s, 32);
@@ -616,10 +624,8 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = v4_cls<RHO>(i, h);
-      const bool t = (tmh >> oo0(i)) & 1u;
-      const float pr = dz[i] * (c == 0 ? f_m : f_s);
-      const float y = t ? (c == 0 ? inv_m : inv_s) : 0.f;
-      dz[i] = (valid && c != 2) ? pr - y : 0.f;
+      const float v = dz[i] * (c == 0 ? f_m : f_s) - yb[i] * (c == 0 ? inv_m : inv_s);
+      dz[i] = (valid && c != 2) ? v : 0.f;
     }
     float l = -zt;
     if (RHO == 1 && h == 0) l += (nm ? M + __logf(S) : 0.f) + (ns ? mx_s + __logf(s_s) : 0.f);
@@ -630,7 +636,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     for (int i = 0; i < 16; ++i) {
       const int c = v4_cls<RHO>(i, h);
       const float v = z[i];
-      const float y = ((tmh >> oo0(i)) & 1u) ? 1.f : 0.f;
+      const float y = yb[i];
       const float en = __expf(-fabsf(v));
       const float pr = v >= 0.f ? 1.f / (1.f + en) : en / (1.f + en);
       const float sp = fmaxf(v, 0.f) + __logf(1.f + en);
