@@ -92,16 +92,43 @@ __global__ void gbdt_hist(const uint8_t* __restrict__ bins, const float* __restr
   if (active)
     for (int i = 0; i < per; ++i) hist[fl * per + i] = 0.0;
   const int r0 = c * chunk, r1 = min(n, r0 + chunk);
+  // the chunk's per-row (node, g, h) are shared by every feature thread: stage them in LDS once
+  // (coalesced), after the per-thread histograms (chunk <= 1024 rows -> 12 KB)
+  float* sg = reinterpret_cast<float*>(smem + (size_t)FT * per * sizeof(double));
+  float* sh = sg + chunk;
+  int16_t* sn = reinterpret_cast<int16_t*>(sh + chunk);
+  const int64_t base = (int64_t)t * n;
+  for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
+    sg[r - r0] = g[base + r];
+    sh[r - r0] = h[base + r];
+    sn[r - r0] = (int16_t)(node[base + r] - first);
+  }
+  __syncthreads();
   if (active) {
     double* my = hist + fl * per;
-    const int64_t base = (int64_t)t * n;
-    for (int r = r0; r < r1; ++r) {
-      const int nd = node[base + r] - first;
+    int r = r0;
+    // 8 rows per step: the 8 bin loads are issued before any update (memory-level parallelism);
+    // the updates stay in row order, so the sums are bitwise those of the plain loop
+    for (; r + 8 <= r1; r += 8) {
+      int b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) b[u] = bins[(int64_t)(r + u) * F + f];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int nd = sn[r + u - r0];
+        if (nd < 0 || nd >= nodesL) continue;
+        double* e = my + (nd * NB + b[u]) * 2;
+        e[0] += (double)sg[r + u - r0];
+        e[1] += (double)sh[r + u - r0];
+      }
+    }
+    for (; r < r1; ++r) {
+      const int nd = sn[r - r0];
       if (nd < 0 || nd >= nodesL) continue;
       const int b = bins[(int64_t)r * F + f];
       double* e = my + (nd * NB + b) * 2;
-      e[0] += (double)g[base + r];
-      e[1] += (double)h[base + r];
+      e[0] += (double)sg[r - r0];
+      e[1] += (double)sh[r - r0];
     }
   }
   __syncthreads();
@@ -393,7 +420,7 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
       // feature tile so that FT * nodesL * NB * 2 floats fit in 64 KB of LDS
-      int FT = (int)(65536 / ((int64_t)nodesL * NB * 2 * 8));
+      int FT = (int)((65536 - 10240) / ((int64_t)nodesL * NB * 2 * 8));  // + 10 KB row staging <= 64 KB
       if (FT > F) FT = F;
       if (FT > 256) FT = 256;
       if (FT < 1) return EM_ERR_ARG;  // nodesL * NB too large for one thread's LDS slice
@@ -401,7 +428,7 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
       if (need > partial_doubles) return EM_ERR_ARG;
       const int nft = (F + FT - 1) / FT;
       const int threads = ((FT + 63) / 64) * 64;
-      const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double);
+      const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double) + (size_t)chunk * 10;
       hipLaunchKernelGGL(gbdt_hist, dim3(nchunks, T, nft), dim3(threads), lds, stream, bins, g, h, node, partial, T, n,
                          F, NB, level, chunk, FT);
       hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(64), 0, stream, partial, nchunks, T, F, NB, level, NN, Gs,
@@ -479,7 +506,7 @@ EM_API int em_gbdt_dp_level_hist(int level, const uint8_t* bins, const float* g,
   const int chunk = 1024;
   const int nchunks = (n + chunk - 1) / chunk;
   const int nodesL = 1 << level;
-  int FT = (int)(65536 / ((int64_t)nodesL * NB * 2 * 8));
+  int FT = (int)((65536 - 10240) / ((int64_t)nodesL * NB * 2 * 8));  // + 10 KB row staging <= 64 KB
   if (FT > F) FT = F;
   if (FT > 256) FT = 256;
   if (FT < 1) return EM_ERR_ARG;
@@ -487,7 +514,7 @@ EM_API int em_gbdt_dp_level_hist(int level, const uint8_t* bins, const float* g,
   if (S * nchunks > partial_doubles) return EM_ERR_ARG;
   const int nft = (F + FT - 1) / FT;
   const int threads = ((FT + 63) / 64) * 64;
-  const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double);
+  const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double) + (size_t)chunk * 10;
   hipLaunchKernelGGL(gbdt_hist, dim3(nchunks, T, nft), dim3(threads), lds, stream, bins, g, h, node, partial, T, n, F,
                      NB, level, chunk, FT);
   if (nchunks > 1)

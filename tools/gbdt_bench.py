@@ -23,12 +23,17 @@ def main():
 
     cfg = C.RunConfig()
     cases = [("reference_calendar", None, 500, True), ("synthetic_262k", 262145, 50, False)]
+    only = sys.argv[1] if len(sys.argv) > 1 else None
     for name, n, rounds, with_numpy in cases:
+        if only and only not in name:
+            continue
         ds = DrawSet.synthetic(n=n, seed=0, planted=0.5)
         X, Y, _ = gbdt_dataset(ds, cfg)
         m = int(0.7 * len(X))
         res = {"case": name, "rows": m, "features": X.shape[1], "tasks": Y.shape[1], "rounds": rounds}
-        for be in (["hip", "numpy"] if with_numpy else ["hip"]):
+        for be in (["hip", "numpy"] if with_numpy and not only else ["hip"]):
+            if be == "hip":  # exclude one-time GPU context / code-object load from the timing
+                GBDT.from_params(cfg.gbdt_params(), nround=2, backend=be).fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
             g = GBDT.from_params(cfg.gbdt_params(), nround=rounds, backend=be)
             t0 = time.perf_counter()
             g.fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
