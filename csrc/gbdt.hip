@@ -21,8 +21,17 @@
 namespace {
 
 constexpr float KRT_EPS = 1e-6f;
-enum { OBJ_LOGISTIC = 0, OBJ_SQERR = 1 };
-enum { MET_LOGLOSS = 0, MET_RMSE = 1, MET_ERROR = 2 };
+enum { OBJ_LOGISTIC = 0, OBJ_SQERR = 1, OBJ_SOFTMAX = 2 };
+enum { MET_LOGLOSS = 0, MET_RMSE = 1, MET_ERROR = 2, MET_MLOGLOSS = 3, MET_MERROR = 4 };
+
+// multi:softprob over the T class margins of row r ([T][n] layout), sequential class order
+EM_DEVICE float softmax_p(const float* __restrict__ margin, int T, int n, int r, int t) {
+  float mx = margin[r];
+  for (int k = 1; k < T; ++k) mx = fmaxf(mx, margin[(int64_t)k * n + r]);
+  float s = 0.f;
+  for (int k = 0; k < T; ++k) s += expf(margin[(int64_t)k * n + r] - mx);
+  return expf(margin[(int64_t)t * n + r] - mx) / s;
+}
 
 EM_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
@@ -63,6 +72,10 @@ __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restr
       const float p = 1.f / (1.f + expf(-m));
       gg = p - y;
       hh = fmaxf(p * (1.f - p), 1e-16f);
+    } else if (obj == OBJ_SOFTMAX) {  // XGBoost SoftmaxMultiClassObj: g = p - y, h = max(2p(1-p), eps)
+      const float p = softmax_p(margin, T, n, r, t);
+      gg = p - y;
+      hh = fmaxf(2.f * p * (1.f - p), 1e-16f);
     } else {
       gg = m - y;
       hh = 1.f;
@@ -321,9 +334,25 @@ __global__ void gbdt_predict(const uint8_t* __restrict__ bins, float* __restrict
 __global__ void __launch_bounds__(256)
 gbdt_metric(const float* __restrict__ margin, const float* __restrict__ Y, int T, int n, int obj, int metric,
             double* __restrict__ partial) {
-  const int64_t total = (int64_t)T * n;
+  const bool rowwise = metric >= MET_MLOGLOSS;  // multi-class metrics: one term per row
+  const int64_t total = rowwise ? (int64_t)n : (int64_t)T * n;
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    if (rowwise) {
+      const int r = (int)i;
+      int lab = 0, am = 0;
+      for (int k = 0; k < T; ++k) {
+        if (Y[(int64_t)r * T + k] > 0.5f) lab = k;
+        if (margin[(int64_t)k * n + r] > margin[(int64_t)am * n + r]) am = k;
+      }
+      if (metric == MET_MLOGLOSS) {
+        const double p = (double)softmax_p(margin, T, n, r, lab);
+        acc += -log(fmax(p, 1e-16));
+      } else {
+        acc += (am != lab) ? 1.0 : 0.0;
+      }
+      continue;
+    }
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
     const float m = margin[i], y = Y[(int64_t)r * T + t];
     const float p = obj == OBJ_LOGISTIC ? 1.f / (1.f + expf(-m)) : m;
@@ -442,8 +471,8 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
     // metrics (train + evals)
     const int mb_train = grid_for(TN);
     hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, stream, margin, Y, T, n, obj, metric, mpart);
-    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(1), 0, stream, mpart, mb_train, TN, metric,
-                       hist_out + (int64_t)round * (1 + n_evals));
+    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(1), 0, stream, mpart, mb_train,
+                       metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, hist_out + (int64_t)round * (1 + n_evals));
     for (int e = 0; e < n_evals; ++e) {
       const int64_t TE = (int64_t)T * evals[e].n;
       const int64_t k0 = (int64_t)round * T;
@@ -452,7 +481,8 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
       const int mb = grid_for(TE);
       hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, stream, evals[e].margin, evals[e].Y, T, evals[e].n, obj,
                          metric, mpart);
-      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(1), 0, stream, mpart, mb, TE, metric,
+      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(1), 0, stream, mpart, mb,
+                         metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric,
                          hist_out + (int64_t)round * (1 + n_evals) + 1 + e);
     }
     EM_CHECK_LAUNCH();

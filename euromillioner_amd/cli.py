@@ -32,10 +32,11 @@ _FLAGS = {
     "--to-date": "data.to_date", "--html-table-class": "data.html_table_class", "--train-pct": "data.train_pct",
     "--date-format": "data.date_format", "--label-column": "data.label_column", "--n-draws": "data.n_draws",
     "--seed": "data.seed", "--planted": "data.planted", "--lags": "data.lags", "--workdir": "data.workdir",
+    "--header": "data.header", "--fetch-jitter-ms": "data.fetch_jitter_ms",
     "--eta": "gbdt.eta", "--max-depth": "gbdt.max_depth", "--objective": "gbdt.objective",
     "--subsample": "gbdt.subsample", "--nthread": "gbdt.nthread", "--gamma": "gbdt.gamma",
     "--eval-metric": "gbdt.eval_metric", "--nround": "gbdt.nround", "--lambda": "gbdt.reg_lambda",
-    "--min-child-weight": "gbdt.min_child_weight", "--target": "gbdt.target", "--max-bin": "gbdt.max_bin",
+    "--min-child-weight": "gbdt.min_child_weight", "--num-class": "gbdt.num_class", "--target": "gbdt.target", "--max-bin": "gbdt.max_bin",
     "--trees": "rf.n_trees", "--rf-max-depth": "rf.max_depth", "--min-samples-leaf": "rf.min_samples_leaf",
     "--feature-subset": "rf.feature_subset",
     "--hidden": "mlp.hidden", "--activation": "mlp.activation", "--loss": "mlp.loss", "--lr": "mlp.lr",

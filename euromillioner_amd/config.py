@@ -48,7 +48,9 @@ class DataConfig:
     seed: int = 0
     planted: float = 0.0  # synthetic Markov structure strength (0 = iid draws)
     lags: int = 1
-    workdir: str | None = None
+    workdir: str | None = None  # where the emn*.csv split files go (None: a temp dir, removed afterwards; D-h)
+    header: str = "auto"  # CSV header handling: auto | yes | no (D-b / D-c)
+    fetch_jitter_ms: int = 0  # Main.java:53-54 random pre-fetch sleep; accepted for parity, no network here
 
 
 @dataclasses.dataclass
@@ -68,6 +70,7 @@ class GBDTConfig:
     min_child_weight: float = 1.0  # XGBoost default
     base_score: float = 0.5  # XGBoost default
     max_bin: int = 256
+    num_class: int = 0  # multi:softprob / multi:softmax (0 = max label + 1)
     target: str = "next-draw"  # next-draw (62 boosters) | reference (label_column of the raw features; D-d)
     device: str = "auto"  # auto | cuda | cpu
 
@@ -149,9 +152,12 @@ class RunConfig:
     def gbdt_params(self) -> dict:
         """The reference's XGBoost parameter map (Main.java:113-126)."""
         g = self.gbdt
-        return {"booster": g.booster, "eta": g.eta, "max_depth": g.max_depth, "predictor": g.predictor,
-                "objective": g.objective, "subsample": g.subsample, "silent": g.silent, "nthread": g.nthread,
-                "gamma": g.gamma, "eval_metric": g.eval_metric}
+        p = {"booster": g.booster, "eta": g.eta, "max_depth": g.max_depth, "predictor": g.predictor,
+             "objective": g.objective, "subsample": g.subsample, "silent": g.silent, "nthread": g.nthread,
+             "gamma": g.gamma, "eval_metric": g.eval_metric}
+        if g.objective.startswith("multi:"):
+            p["num_class"] = g.num_class
+        return p
 
 
 def _coerce(cur: Any, val: Any, typ: Any = None):

@@ -45,8 +45,9 @@ def write_draws_csv(path: str, ds: DrawSet) -> None:
             w.writerow(row)
 
 
-def read_draws_csv(path: str) -> DrawSet:
-    """Our CSV (with ``date`` column), the reference's 11 columns with a header, or headerless 11/12 cols."""
+def read_draws_csv(path: str, header: bool | None = None) -> DrawSet:
+    """Our CSV (with ``date`` column), the reference's 11 columns with a header, or headerless 11/12 cols.
+    ``header``: None = detect, True/False = force (``--header yes|no``)."""
     with open(path, newline="", encoding="utf-8") as f:
         rows = [r for r in csv.reader(f) if any(c.strip() for c in r)]
     if not rows:
@@ -60,7 +61,7 @@ def read_draws_csv(path: str) -> DrawSet:
         except ValueError:
             return False
 
-    has_header = not all(numeric(c) for c in head if c) or "date" in head
+    has_header = (not all(numeric(c) for c in head if c) or "date" in head) if header is None else bool(header)
     body = rows[1:] if has_header else rows
     nums, dates = [], []
     for r in body:

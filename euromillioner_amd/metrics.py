@@ -52,7 +52,25 @@ def error_rate(y: np.ndarray, p: np.ndarray) -> float:
     return float(np.mean((p > 0.5).astype(np.float64) != y)) if y.size else float("nan")
 
 
-EVAL_METRICS = {"logloss": logloss, "rmse": rmse, "error": error_rate}
+def mlogloss(y: np.ndarray, p: np.ndarray, eps: float = 1e-16) -> float:
+    """XGBoost ``mlogloss``: y one-hot (or class ids) [n, K], p class probabilities [n, K]."""
+    p = np.asarray(p, dtype=np.float64)
+    y = np.asarray(y)
+    lab = y.reshape(-1).astype(np.int64) if y.ndim == 1 else np.argmax(y, axis=1)
+    if p.shape[0] == 0:
+        return float("nan")
+    return float(-np.mean(np.log(np.maximum(p[np.arange(len(p)), lab], eps))))
+
+
+def merror(y: np.ndarray, p: np.ndarray) -> float:
+    """XGBoost ``merror``: fraction of rows whose arg-max class is wrong."""
+    p = np.asarray(p)
+    y = np.asarray(y)
+    lab = y.reshape(-1).astype(np.int64) if y.ndim == 1 else np.argmax(y, axis=1)
+    return float(np.mean(np.argmax(p, axis=1) != lab)) if len(p) else float("nan")
+
+
+EVAL_METRICS = {"logloss": logloss, "rmse": rmse, "error": error_rate, "mlogloss": mlogloss, "merror": merror}
 
 
 def _topk_mask(z: np.ndarray, k: int) -> np.ndarray:

@@ -41,7 +41,8 @@ import math
 import numpy as np
 
 KRT_EPS = 1e-6
-OBJECTIVES = ("reg:logistic", "binary:logistic", "reg:squarederror")
+OBJECTIVES = ("reg:logistic", "binary:logistic", "reg:squarederror", "multi:softprob", "multi:softmax")
+MULTI = ("multi:softprob", "multi:softmax")
 
 
 # ----------------------------------------------------------------------------- binning
@@ -180,11 +181,35 @@ def base_margin_for(objective: str, base_score: float) -> float:
     return float(base_score)
 
 
+def softmax_rows(margin: np.ndarray) -> np.ndarray:
+    """Row softmax over the class margins in float32, classes summed in order (== the HIP kernel)."""
+    m = np.asarray(margin, dtype=np.float32)
+    mx = m[:, :1].copy()
+    for k in range(1, m.shape[1]):
+        mx = np.maximum(mx, m[:, k:k + 1])
+    e = np.exp(m - mx)
+    s = np.zeros_like(mx)
+    for k in range(m.shape[1]):
+        s += e[:, k:k + 1]
+    return e / s
+
+
 def transform(objective: str, margin: np.ndarray) -> np.ndarray:
-    return _sigmoid(margin) if objective in ("reg:logistic", "binary:logistic") else margin
+    if objective in ("reg:logistic", "binary:logistic"):
+        return _sigmoid(margin)
+    if objective in MULTI:
+        return softmax_rows(margin)
+    return margin
 
 
-def check_labels(objective: str, y: np.ndarray) -> None:
+def check_labels(objective: str, y: np.ndarray, num_class: int = 0) -> None:
+    if objective in MULTI:
+        yy = np.asarray(y).reshape(-1)
+        if np.any(np.isnan(yy)) or np.any(yy < 0) or np.any(yy != np.floor(yy)) or \
+                (num_class and np.any(yy >= num_class)):
+            # XGBoost: SoftmaxMultiClassObj -> "label must be in [0, num_class)"
+            raise ValueError("multi-class labels must be integers in [0, num_class)")
+        return
     if objective in ("reg:logistic", "binary:logistic"):
         if np.any((y < 0) | (y > 1)) or np.any(np.isnan(y)):
             # XGBoost: LogisticRegression::CheckLabel -> XGBoostError
@@ -197,6 +222,9 @@ def gradients(objective: str, margin: np.ndarray, y: np.ndarray):
         return p - y, np.maximum(p * (p.dtype.type(1) - p), p.dtype.type(1e-16))
     if objective == "reg:squarederror":
         return margin - y, np.ones_like(margin)
+    if objective in MULTI:  # y one-hot [n, K]
+        p = softmax_rows(margin)
+        return p - y, np.maximum(np.float32(2) * p * (np.float32(1) - p), np.float32(1e-16))
     raise ValueError(f"unsupported objective {objective}")
 
 
@@ -286,13 +314,16 @@ class GBDT:
 
     def __init__(self, eta=1.0, max_depth=3, objective="reg:logistic", subsample=1.0, gamma=1.0,
                  reg_lambda=1.0, min_child_weight=1.0, base_score=0.5, nround=500, max_bin=256,
-                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1):
+                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1, num_class=0):
         if objective not in OBJECTIVES:
             raise ValueError(f"objective must be one of {OBJECTIVES}")
         self.eta, self.max_depth, self.objective = float(eta), int(max_depth), objective
         self.subsample, self.gamma, self.lam = float(subsample), float(gamma), float(reg_lambda)
         self.mcw, self.base_score, self.nround = float(min_child_weight), float(base_score), int(nround)
         self.max_bin, self.eval_metric, self.seed = int(max_bin), eval_metric, int(seed)
+        self.num_class = int(num_class)
+        if objective in MULTI and eval_metric in ("logloss", "error"):
+            self.eval_metric = "m" + eval_metric  # XGBoost's multi-class defaults: mlogloss / merror
         self.backend = backend
         self.log, self.log_every = log, log_every
         self.trees: TreeArrays | None = None
@@ -312,7 +343,7 @@ class GBDT:
                     gamma=float(p.get("gamma", 0.0)), reg_lambda=float(p.get("lambda", 1.0)),
                     min_child_weight=float(p.get("min_child_weight", 1.0)),
                     base_score=float(p.get("base_score", 0.5)), eval_metric=p.get("eval_metric", "logloss"),
-                    nround=nround)
+                    nround=nround, num_class=int(p.get("num_class", 0)))
         args.update(kw)
         return cls(**args)
 
@@ -340,11 +371,24 @@ class GBDT:
         eval set are this rank's row shard; histograms, node sums and metrics are all-reduced."""
         X = np.asarray(X, dtype=np.float64)
         Y = np.asarray(Y, dtype=np.float64)
+        dp = _DP(group) if group is not None else None
+        if self.objective in MULTI:  # class ids -> one booster per class on one-hot targets
+            y = Y.reshape(-1)
+            ev_y = {k: np.asarray(ey, np.float64).reshape(-1) for k, (_, ey) in (evals or {}).items()}
+            for v in (y, *ev_y.values()):
+                check_labels(self.objective, v, self.num_class)
+            if not self.num_class:  # XGBoost requires num_class; 0 = infer (global max under DP)
+                top = max([float(v.max()) for v in (y, *ev_y.values()) if v.size] or [0.0])
+                if dp is not None:
+                    top = float(dp.sum_(np.eye(dp.world)[dp.rank] * top).max())  # all-gather of per-rank maxima
+                self.num_class = int(top) + 1
+            eye = np.eye(self.num_class, dtype=np.float64)
+            Y = eye[y.astype(np.int64)]
+            evals = {k: (ex, eye[ev_y[k].astype(np.int64)]) for k, (ex, _) in (evals or {}).items()}
         if Y.ndim == 1:
             Y = Y[:, None]
         check_labels(self.objective, Y)
         self.n_tasks = Y.shape[1]
-        dp = _DP(group) if group is not None else None
         self.cuts = make_cuts_dp(X, self.max_bin, dp) if dp is not None else make_cuts(X, self.max_bin)
         bins = apply_bins(X, self.cuts)
         nbins = max((len(c) for c in self.cuts), default=0) + 1
@@ -466,6 +510,12 @@ class GBDT:
         # global mean from per-rank (sum, count): rmse averages squares before the root
         y = np.asarray(y, np.float64).reshape(-1)
         p = np.asarray(p, np.float64).reshape(-1)
+        if self.eval_metric in ("mlogloss", "merror"):
+            yy = np.asarray(y, np.float64).reshape(-1, self.n_tasks)
+            pp = np.asarray(p, np.float64).reshape(-1, self.n_tasks)
+            loc = float(M.EVAL_METRICS[self.eval_metric](yy, pp) * len(yy)) if len(yy) else 0.0
+            tot = dp.sum_(np.array([loc, float(len(yy))]))
+            return float(tot[0] / max(tot[1], 1.0))
         if self.eval_metric == "rmse":
             loc = float(np.sum((y - p) ** 2))
         elif self.eval_metric == "error":
@@ -494,8 +544,12 @@ class GBDT:
         return predict_margin_values(self.trees, X, task, self.n_tasks, self.base_margin)
 
     def predict(self, X: np.ndarray, backend: str | None = None) -> np.ndarray:
-        """Like Booster.predict: float32 [n, T] (reg:logistic -> probabilities)."""
-        return transform(self.objective, self.predict_margin(X, backend)).astype(np.float32)
+        """Like Booster.predict: float32 [n, T] (reg:logistic -> probabilities; multi:softprob ->
+        class probabilities; multi:softmax -> the predicted class id, shape [n])."""
+        p = transform(self.objective, self.predict_margin(X, backend)).astype(np.float32)
+        if self.objective == "multi:softmax":
+            return np.argmax(p, axis=1).astype(np.float32)
+        return p
 
     # ------------------------------------------------------------------ persistence
     def to_json(self) -> dict:
@@ -514,7 +568,7 @@ class GBDT:
                 nodes.append(nd)
             trees.append({"id": k, "task": int(k % self.n_tasks), "nodes": nodes})
         return {"learner": {"objective": self.objective, "base_score": self.base_score,
-                            "num_target": self.n_tasks,
+                            "num_target": self.n_tasks, "num_class": self.num_class,
                             "num_feature": len(self.cuts) if self.cuts is not None else self.num_feature,
                             "params": {"eta": self.eta, "max_depth": self.max_depth, "gamma": self.gamma,
                                        "lambda": self.lam, "min_child_weight": self.mcw,
@@ -534,6 +588,7 @@ class GBDT:
                 reg_lambda=p["lambda"], min_child_weight=p["min_child_weight"], base_score=d["base_score"],
                 nround=p["nround"], subsample=p.get("subsample", 1.0), backend="numpy")
         m.n_tasks = d["num_target"]
+        m.num_class = int(d.get("num_class", 0))
         m.num_feature = d.get("num_feature")
         trees = d["gradient_booster"]["model"]["trees"]
         tr = TreeArrays(len(trees), m.max_depth)

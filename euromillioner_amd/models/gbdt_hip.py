@@ -28,8 +28,8 @@ N.register_signatures({
     "em_gbdt_metric_sum": (_i, [_v, _v, _i, _i, _i, _i, _v, _v, _v]),
 })
 
-OBJ = {"reg:logistic": 0, "binary:logistic": 0, "reg:squarederror": 1}
-MET = {"logloss": 0, "rmse": 1, "error": 2}
+OBJ = {"reg:logistic": 0, "binary:logistic": 0, "reg:squarederror": 1, "multi:softprob": 2, "multi:softmax": 2}
+MET = {"logloss": 0, "rmse": 1, "error": 2, "mlogloss": 3, "merror": 4}
 
 
 def _dev():
@@ -148,7 +148,7 @@ def _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, nbins, T, margin, ev_names, ev_
                    status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), stream)
             N.call("em_gbdt_metric_sum", em.data_ptr(), dy.data_ptr(), T, ne, obj, met, mpart.data_ptr(),
                    msum[rnd, j, :1].data_ptr(), stream)
-            msum[rnd, j, 1] = float(T * ne)
+            msum[rnd, j, 1] = float(ne if met >= 3 else T * ne)
     if ev_names:
         dist.all_reduce(msum, group=dp.group)
     ms = msum.cpu().numpy()

@@ -39,7 +39,10 @@ def load_draws(cfg: RunConfig) -> DrawSet:
     elif d.source == "csv":
         from .data.csv_io import read_draws_csv
 
-        ds = read_draws_csv(_need(d.path))
+        hdr = {"auto": None, "yes": True, "no": False}.get(str(d.header).lower())
+        if hdr is None and str(d.header).lower() != "auto":
+            raise ValueError("--header must be auto, yes or no")
+        ds = read_draws_csv(_need(d.path), header=hdr)
     elif d.source == "reference-csv":
         from .data.csv_io import read_reference_csv, reference_records_to_drawset
 
@@ -93,8 +96,13 @@ def run_reference_pipeline(cfg: RunConfig, out=None) -> dict:
     ds = load_draws(cfg)
     log.info(f"loaded {len(ds)} draws from {cfg.data.source} "
              f"({ds.meta.get('planted', 0.0) if cfg.data.source == 'synthetic' else 'n/a'} planted)")
-    workdir = cfg.data.workdir or tempfile.mkdtemp(prefix="emn_")
-    os.makedirs(workdir, exist_ok=True)
+    tmp = None
+    if cfg.data.workdir:
+        workdir = cfg.data.workdir
+        os.makedirs(workdir, exist_ok=True)
+    else:  # D-h: the reference leaks its temp CSVs; ours are removed when the run ends
+        tmp = tempfile.TemporaryDirectory(prefix="emn_")
+        workdir = tmp.name
     X, Y, target = gbdt_dataset(ds, cfg)
     n = len(X)
     margin = positional_split(n, cfg.data.train_pct)
@@ -132,8 +140,8 @@ def run_reference_pipeline(cfg: RunConfig, out=None) -> dict:
         (out.write if out else print)(str(compat).lower() + ("\n" if out else ""))  # Main.java:143 prints the boolean
     res = {"pipeline": "reference", "target": target, "n_draws": len(ds), "n_train": int(margin),
            "n_val": int(n - margin), "backend": booster.backend_used, "check_predicts": compat,
-           "train_" + g.eval_metric: booster.history[-1].get("train") if booster.history else None,
-           "val_" + g.eval_metric: booster.history[-1].get("test") if booster.history else None,
+           "train_" + booster.eval_metric: booster.history[-1].get("train") if booster.history else None,
+           "val_" + booster.eval_metric: booster.history[-1].get("test") if booster.history else None,
            "seconds": round(time.time() - t0, 3), "workdir": workdir}
     if target == "next-draw" and len(Xva):
         margins = booster.predict_margin(Xva)
@@ -144,6 +152,9 @@ def run_reference_pipeline(cfg: RunConfig, out=None) -> dict:
         booster.save(cfg.ckpt.path)
         res["checkpoint"] = cfg.ckpt.path
     D.shutdown(info)
+    if tmp is not None:
+        tmp.cleanup()
+        res["workdir"] = None
     return res
 
 

@@ -62,7 +62,7 @@ def case_forest(out):
     dist.destroy_process_group()
 
 
-def case_gbdt(out):
+def case_gbdt(out, objective="reg:logistic"):
     """Data-parallel boosting (C4): each rank fits on its row shard with all-reduced histograms."""
     import numpy as np
 
@@ -76,10 +76,14 @@ def case_gbdt(out):
     ds = DrawSet.synthetic(n=700, seed=4, planted=0.6, calendar=True)
     X, Y, _ = gbdt_dataset(ds, C.RunConfig())
     Y = Y[:, :6]
+    if objective.startswith("multi:"):  # class = first of the 6 numbers drawn (0 = none); rank 1 never sees 6
+        Y = np.where(Y.any(1), np.argmax(Y, 1) + 1, 0).astype(np.float64)
+        if rank == 1:
+            Y = np.minimum(Y, 5)
     n_tr = 500
     a, b = shard_range(n_tr, DistInfo(rank, world))
     va, vb = shard_range(len(X) - n_tr, DistInfo(rank, world))
-    m = GBDT(eta=0.5, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=8, backend="numpy")
+    m = GBDT(eta=0.5, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=8, backend="numpy", objective=objective)
     m.fit(X[a:b], Y[a:b], evals={"test": (X[n_tr + va:n_tr + vb], Y[n_tr + va:n_tr + vb])}, group=dist.group.WORLD)
     if rank == 0:
         np.savez(out, feat=m.trees.feat, sbin=m.trees.sbin, leaf=m.trees.leaf,

@@ -109,3 +109,15 @@ def test_cli_predict_missing_checkpoint_is_data_error(tmp_path):
     from euromillioner_amd.cli import main
 
     assert main(["predict", "--ckpt", str(tmp_path / "nope.zip")]) == 3
+
+
+def test_pipeline_cleans_temp_workdir(capsys):
+    """D-h: without --workdir the split CSVs live in a temp dir that is removed afterwards."""
+    import json as _json
+
+    from euromillioner_amd.cli import main
+
+    assert main(["run", "--device", "cpu", "--n-draws", "200", "--nround", "2"]) == 0
+    out = capsys.readouterr().out
+    js = [l for l in out.splitlines() if l.startswith("{")]
+    assert js and _json.loads(js[-1])["workdir"] is None

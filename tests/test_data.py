@@ -155,3 +155,13 @@ def test_html_date_format_english():
 
     assert parse_date("Fri, Jun 12, 2020") == dt.date(2020, 6, 12)
     assert parse_date("Tue,  May 10, 2011") == dt.date(2011, 5, 10)
+
+
+def test_csv_header_flag(tmp_path):
+    from euromillioner_amd.data.csv_io import read_draws_csv
+
+    p = tmp_path / "h.csv"
+    p.write_text("5,1,3,2020,1,2,3,4,5,6,7\n4,2,4,2020,8,9,10,11,12,1,2\n")
+    assert len(read_draws_csv(str(p))) == 2  # detected: no header
+    assert len(read_draws_csv(str(p), header=True)) == 1  # forced: first row is a header
+    assert len(read_draws_csv(str(p), header=False)) == 2

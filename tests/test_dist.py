@@ -157,22 +157,31 @@ def test_resume_auto(tmp_path):
     assert _params(p)[3]["step"] == 6
 
 
-def test_data_parallel_gbdt_equals_single(tmp_path):
-    """C4: histogram all-reduce over 2 ranks == one process on the concatenated rows."""
+@pytest.mark.parametrize("objective", ["reg:logistic", "multi:softprob"])
+def test_data_parallel_gbdt_equals_single(tmp_path, objective):
+    """C4: histogram all-reduce over 2 ranks == one process on the concatenated rows (multi-class:
+    num_class inferred from the global label maximum, mlogloss from global row sums)."""
     from euromillioner_amd import config as C
     from euromillioner_amd.data.draws import DrawSet
     from euromillioner_amd.models.gbdt import GBDT
+    from euromillioner_amd.parallel.dist import DistInfo, shard_range
     from euromillioner_amd.pipeline import gbdt_dataset
 
     out = str(tmp_path / "g.npz")
-    res = _launch([sys.executable, WORKER, "gbdt", out], 2)
+    res = _launch([sys.executable, WORKER, "gbdt", out, objective], 2)
     assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
     z = np.load(out, allow_pickle=False)
     ds = DrawSet.synthetic(n=700, seed=4, planted=0.6, calendar=True)
     X, Y, _ = gbdt_dataset(ds, C.RunConfig())
     Y = Y[:, :6]
-    m = GBDT(eta=0.5, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=8, backend="numpy")
+    if objective.startswith("multi:"):
+        Y = np.where(Y.any(1), np.argmax(Y, 1) + 1, 0).astype(np.float64)
+        for lo, hi in (shard_range(500, DistInfo(1, 2)), [500 + v for v in shard_range(200, DistInfo(1, 2))]):
+            Y[lo:hi] = np.minimum(Y[lo:hi], 5)
+    m = GBDT(eta=0.5, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=8, backend="numpy", objective=objective)
     m.fit(X[:500], Y[:500], evals={"test": (X[500:], Y[500:])})
+    if objective.startswith("multi:"):
+        assert m.num_class == 7 and z["leaf"].shape == m.trees.leaf.shape
     assert np.array_equal(z["feat"], m.trees.feat) and np.array_equal(z["sbin"], m.trees.sbin)
     assert np.allclose(z["leaf"], m.trees.leaf, atol=1e-6)
     assert np.allclose(z["hist"], [h["test"] for h in m.history], atol=1e-6)

@@ -101,6 +101,68 @@ def test_json_roundtrip(tmp_path):
     assert np.array_equal(m.predict(X), m2.predict(X))
 
 
+def _multi_data(n=700, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 6))
+    y = (X[:, 0] > 0).astype(np.int64) + 2 * (X[:, 1] > 0.4) + (X[:, 2] > 1.2)
+    return X, np.minimum(y, 3).astype(np.float64)
+
+
+@pytest.mark.parametrize("obj", ["multi:softprob", "multi:softmax"])
+def test_multiclass_softmax_learns(obj, tmp_path):
+    X, y = _multi_data()
+    m = G.GBDT(objective=obj, nround=25, eta=0.3, gamma=0.0, backend="numpy").fit(
+        X[:500], y[:500], evals={"test": (X[500:], y[500:])})
+    assert m.num_class == 4 and m.n_tasks == 4 and m.eval_metric == "mlogloss"
+    assert m.history[-1]["test"] < 0.5 * m.history[0]["test"]
+    p = m.predict(X[500:])
+    if obj == "multi:softprob":
+        assert p.shape == (200, 4) and np.allclose(p.sum(1), 1.0, atol=1e-5)
+        p = np.argmax(p, 1)
+    assert np.mean(p == y[500:]) > 0.85
+    m.save(str(tmp_path / "m.json"))
+    m2 = G.GBDT.load(str(tmp_path / "m.json"))
+    assert m2.num_class == 4 and np.array_equal(m2.predict(X[500:]), m.predict(X[500:]))
+
+
+def test_multiclass_first_round_gradients_by_hand():
+    """Round-0 margins are base_score for every class -> p = 1/K, g = 1/K - y, h = 2/K (1 - 1/K)."""
+    y1 = np.eye(3)[[0, 2, 1]].astype(np.float32)
+    g, h = G.gradients("multi:softprob", np.full((3, 3), 0.5, np.float32), y1)
+    assert np.allclose(g, 1 / 3 - y1) and np.allclose(h, 2 / 3 * (2 / 3))
+
+
+def test_multiclass_rejects_bad_labels():
+    X, y = _multi_data(50)
+    with pytest.raises(ValueError):
+        G.GBDT(objective="multi:softprob", nround=1, backend="numpy").fit(X, y + 0.5)
+    with pytest.raises(ValueError):
+        G.GBDT(objective="multi:softprob", num_class=2, nround=1, backend="numpy").fit(X, y)
+
+
+def test_multiclass_metrics():
+    from euromillioner_amd import metrics as M
+
+    p = np.array([[0.7, 0.2, 0.1], [0.1, 0.1, 0.8]])
+    assert abs(M.mlogloss(np.array([0, 1]), p) - (-(np.log(0.7) + np.log(0.1)) / 2)) < 1e-12
+    assert M.merror(np.array([0, 1]), p) == 0.5
+    assert M.merror(np.eye(3)[[0, 2]], p) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obj", ["multi:softprob", "multi:softmax"])
+def test_hip_multiclass_matches_oracle(obj):
+    X, y = _multi_data(3000, seed=2)
+    kw = dict(objective=obj, nround=15, eta=0.3, gamma=0.0, max_depth=3)
+    a = G.GBDT(backend="numpy", **kw).fit(X[:2000], y[:2000], evals={"test": (X[2000:], y[2000:])})
+    b = G.GBDT(backend="hip", **kw).fit(X[:2000], y[:2000], evals={"test": (X[2000:], y[2000:])})
+    assert b.backend_used == "hip"
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-4)
+    assert np.allclose(a.predict(X[2000:]), b.predict(X[2000:], backend="hip"), atol=1e-4)
+    assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-4
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("obj", ["reg:logistic", "reg:squarederror"])
 def test_hip_engine_matches_oracle(obj):
