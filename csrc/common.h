@@ -41,12 +41,19 @@ EM_DEVICE float bf2f(__bf16 b) { return (float)b; }
 
 EM_DEVICE float bf16_bits_to_f32(uint16_t u) { return __builtin_bit_cast(float, ((uint32_t)u) << 16); }
 
-// 8 f32 -> bf16x8 fragment
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// 2 f32 -> packed bf16 pair: ONE v_cvt_pk_bf16_f32 (element-wise (__bf16) casts compile to two
+// single-lane converts plus a v_perm_b32 on ROCm 7.2)
+EM_DEVICE uint32_t pack2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
+
+// 8 f32 -> bf16x8 fragment (4 v_cvt_pk_bf16_f32)
 EM_DEVICE bf16x8 pack8(float a0, float a1, float a2, float a3, float a4, float a5, float a6, float a7) {
-  bf16x8 r;
-  r[0] = (__bf16)a0; r[1] = (__bf16)a1; r[2] = (__bf16)a2; r[3] = (__bf16)a3;
-  r[4] = (__bf16)a4; r[5] = (__bf16)a5; r[6] = (__bf16)a6; r[7] = (__bf16)a7;
-  return r;
+  const u32x4 d = {pack2(a0, a1), pack2(a2, a3), pack2(a4, a5), pack2(a6, a7)};
+  return __builtin_bit_cast(bf16x8, d);
 }
 
 // Expand 8 mask bits into 8 bf16 {0,1} values (element j = bit j).

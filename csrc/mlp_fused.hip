@@ -175,17 +175,20 @@ EM_DEVICE bf16x8 relu_pack(const f32x16& a, int q) {
   return __builtin_bit_cast(bf16x8, d);
 }
 
-// dZ1 = dH * (Z1 > 0) on packed bf16: the relu'd H fragment is 0 exactly where Z1 <= 0
+// dZ1 = dH * (Z1 > 0) on packed bf16: the relu'd H fragment is 0 exactly where Z1 <= 0 and a
+// positive bf16 (bits 0x0001..0x7f7f) otherwise, so min_u16(h, 1) is the 0/1 mask and a 16-bit
+// integer multiply applies it (v_pk_min_u16 + v_pk_mul_lo_u16 per two values)
 EM_DEVICE bf16x8 mask_by(const bf16x8 hfrag, const f32x16& a, int q) {
   const bf16x8 p = pack8(a[8 * q + 0], a[8 * q + 1], a[8 * q + 2], a[8 * q + 3], a[8 * q + 4], a[8 * q + 5],
                          a[8 * q + 6], a[8 * q + 7]);
   u32x4 d = __builtin_bit_cast(u32x4, p);
   const u32x4 hh = __builtin_bit_cast(u32x4, hfrag);
+  // (inline asm: written in C the compiler re-derives a compare + select per 16-bit half)
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t x = hh[k];
-    const s16x2 m = ((s16x2){0, 0} - as_s16x2(x)) >> (s16x2){15, 15};
-    d[k] &= as_u32(m);
+    uint32_t m;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(hh[k]), "s"(0x00010001u));
+    asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(d[k]) : "v"(d[k]), "v"(m));
   }
   return __builtin_bit_cast(bf16x8, d);
 }
@@ -474,7 +477,8 @@ constexpr int V4_PAIR_BYTES = 25152;  // X 4K | D2 4K | H0 4K | H1 4K | XB0 4K |
 constexpr int V4_PX = 0, V4_PD2 = 4096, V4_PH = 8192, V4_PXB = 16384, V4_PST = 24576, V4_PFL = 25088;
 static_assert(V4_PST + 2 * 256 <= V4_PFL && V4_PFL + 64 <= V4_PAIR_BYTES, "v4 pair layout");
 constexpr int V4_BASE = IMG_BYTES + LUT_BYTES;
-constexpr int V4_LOOP_LDS = V4_BASE + 4 * V4_PAIR_BYTES;
+constexpr int V4_YLUT = V4_BASE + 4 * V4_PAIR_BYTES;  // 16 x f32x4: target nibble -> 4 {0,1} floats
+constexpr int V4_LOOP_LDS = V4_YLUT + 256;
 constexpr int V4_RED = 65536;  // epilogue fp32 dW image [16384]
 constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 4096);
 #ifndef V4_STAGGER
@@ -582,14 +586,26 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
   }
 
   // ---- loss on the own output tile ----
+  // target bits of the lane's 16 outputs as 0/1 floats: register group g holds outputs
+  // 8g + 4h .. +3 of the tile = one nibble of the target mask -> one ds_read_b128 of a 16-entry table
   const uint32_t tmh = (uint32_t)(tmask >> (32 * RHO)) >> (4 * h);
-  float yb[16];  // target bits of the lane's 16 outputs, as 0/1 floats (one v_bfe + cvt each)
+  float yb[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) yb[i] = (float)((tmh >> oo0(i)) & 1u);
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + V4_YLUT + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+    yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
+  }
   float dz[16];
   if (LOSS == 0) {
-    const int nm = __builtin_popcountll(tmask & MAIN_BITS), ns = __builtin_popcountll(tmask & STAR_BITS);
-    const float inv_m = nm ? 1.f / (float)nm : 0.f, inv_s = ns ? 1.f / (float)ns : 0.f;
+    // VALU-lean grouped softmax: exponentials as exp2(z·log2e − max·log2e) (one fma + v_exp each),
+    // reciprocals with v_rcp, and no per-element validity select -- an invalid (padding) sample has
+    // an all-zero target mask, so nm = ns = 0 zeroes its factors and hence its dZ and loss.
+    constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+    const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
+    const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
+    const int ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
+    const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
+    const float inv_s = (RHO == 1 && ns) ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
     float mx_m = -3.0e38f, mx_s = -3.0e38f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -599,16 +615,21 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     }
     mx_m = fmaxf(mx_m, __shfl_xor(mx_m, 32));
     if (RHO == 1) mx_s = fmaxf(mx_s, __shfl_xor(mx_s, 32));
-    float s_m = 0.f, s_s = 0.f, zt = 0.f;
+    const float nmL = -mx_m * L2E, nsL = -mx_s * L2E;
+    float s_m = 0.f, s_s = 0.f, zt_m = 0.f, zt_s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = v4_cls<RHO>(i, h);
-      const float e = __expf(z[i] - ((RHO == 1 && c == 1) ? mx_s : mx_m));
+      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z[i], L2E, (RHO == 1 && c == 1) ? nsL : nmL));
       const float ee = (c == 2) ? 0.f : e;
       dz[i] = ee;
+      // branch-free: c is a compile-time constant except for the two registers straddling 50/62
       s_m += (c == 0) ? ee : 0.f;
-      if (RHO == 1) s_s += (c == 1) ? ee : 0.f;
-      zt += yb[i] * z[i] * (c == 0 ? inv_m : inv_s);
+      zt_m = __builtin_fmaf((c == 0) ? yb[i] : 0.f, z[i], zt_m);
+      if (RHO == 1) {
+        s_s += (c == 1) ? ee : 0.f;
+        zt_s = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z[i], zt_s);
+      }
     }
     s_m += __shfl_xor(s_m, 32);
     if (RHO == 1) s_s += __shfl_xor(s_s, 32);
@@ -618,18 +639,19 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     ok &= pair_wait(smem, PAFL, sig);
     const float2 ps = *reinterpret_cast<const float2*>(smem + PB + V4_PST + PR * 256 + r * 8);
     const float M = fmaxf(mx_m, ps.x);
-    const float S = s_m * __expf(mx_m - M) + ps.y * __expf(ps.x - M);
-    const float f_m = nm ? __expf(mx_m - M) / S : 0.f;
-    const float f_s = (RHO == 1 && ns) ? 1.f / s_s : 0.f;
+    const float sc_own = __builtin_amdgcn_exp2f((mx_m - M) * L2E);
+    const float S = s_m * sc_own + ps.y * __builtin_amdgcn_exp2f((ps.x - M) * L2E);
+    const float f_m = nm ? sc_own * __builtin_amdgcn_rcpf(S) : 0.f;
+    const float f_s = (RHO == 1 && ns) ? __builtin_amdgcn_rcpf(s_s) : 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = v4_cls<RHO>(i, h);
-      const float v = dz[i] * (c == 0 ? f_m : f_s) - yb[i] * (c == 0 ? inv_m : inv_s);
-      dz[i] = (valid && c != 2) ? v : 0.f;
+      dz[i] = (c == 2) ? 0.f : __builtin_fmaf(dz[i], c == 0 ? f_m : f_s, -yb[i] * (c == 0 ? inv_m : inv_s));
     }
-    float l = -zt;
-    if (RHO == 1 && h == 0) l += (nm ? M + __logf(S) : 0.f) + (ns ? mx_s + __logf(s_s) : 0.f);
-    loss_acc += valid ? l : 0.f;
+    float l = -(zt_m * inv_m + zt_s * inv_s);
+    if (RHO == 1 && h == 0)
+      l += (nm ? M + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
+    loss_acc += l;
   } else {
     float l = 0.f;
 #pragma unroll
@@ -812,6 +834,7 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
     for (int i = tid; i < IMG_BYTES / 16; i += 512) dst[i] = src[i];
   }
   fill_lut(smem + IMG_BYTES, tid);
+  if (tid < 64) reinterpret_cast<float*>(smem + V4_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
   if (lane < 2) reinterpret_cast<int*>(smem + V4_BASE + pair * V4_PAIR_BYTES + V4_PFL)[lane] = 0;
   __syncthreads();
   // waves 4-7 share SIMDs with waves 0-3 (other pairs): start them half a tile later so the two
