@@ -516,7 +516,7 @@ EM_DEVICE int v4_cls(int i, int h) {
 template <int LOSS, int RHO>
 EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int r, int h, int lane, int q4, int p4,
                        int g1, uint64_t imask, uint64_t tmask, bool valid, int& sig, bool& ok, f32x16 (&dW2)[2][2],
-                       f32x16 (&dW1T)[2][2], float (&db2)[16], float& loss_acc) {
+                       f32x16 (&dW1T)[2][2], f32x16& db2, const bf16x8 ones, float& loss_acc) {
   constexpr int PR = 1 - RHO;
   const uint32_t XB = PB + V4_PX, DB = PB + V4_PD2, HB = PB + V4_PH + RHO * 4096;
   const uint32_t MYX = PB + V4_PXB + RHO * 4096, PAX = PB + V4_PXB + PR * 4096;
@@ -546,39 +546,33 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     }
   }
 
-  // ---- F2 partial over the own hidden half, both output tiles ----
-  f32x16 zp[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    zp[u] = f32x16{};
-    if (u == RHO) {  // b2 rides in as the accumulator init of the own output tile
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * RHO + 8 * g + 4 * h) * 4);
-        zp[u][4 * g + 0] = b[0]; zp[u][4 * g + 1] = b[1]; zp[u][4 * g + 2] = b[2]; zp[u][4 * g + 3] = b[3];
-      }
-    }
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        zp[u] = mfma32(lds_frag(smem, w2p_off(32 * u + r, (2 * (2 * RHO + tt) + q) * 2 + h)), hT[tt][q], zp[u]);
-  }
-
-  // ---- exchange (1): give the partner its output tile's partial, take ours ----
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    *reinterpret_cast<f32x4*>(smem + MYX + (g * 64 + lane) * 16) =
-        f32x4{zp[PR][4 * g + 0], zp[PR][4 * g + 1], zp[PR][4 * g + 2], zp[PR][4 * g + 3]};
+  // ---- exchange (1): the H images.  Each wave computes the FULL logits of its own output tile:
+  // its own hidden half from registers, the partner's half read back as B fragments from the
+  // partner's H image (two ds_read_b64 each) -- no fp32 partial-sum round trip through LDS ----
   pair_signal(smem, MYFL, ++sig);
-  ok &= pair_wait(smem, PAFL, sig);
-  f32x16 z = zp[RHO];
+  f32x16 z;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 o = *reinterpret_cast<const f32x4*>(smem + PAX + (g * 64 + lane) * 16);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) z[4 * g + k] += o[k];
+  for (int g = 0; g < 4; ++g) {  // b2 rides in as the accumulator init
+    const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * RHO + 8 * g + 4 * h) * 4);
+    z[4 * g + 0] = b[0]; z[4 * g + 1] = b[1]; z[4 * g + 2] = b[2]; z[4 * g + 3] = b[3];
   }
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      z = mfma32(lds_frag(smem, w2p_off(32 * RHO + r, (2 * (2 * RHO + tt) + q) * 2 + h)), hT[tt][q], z);
+  ok &= pair_wait(smem, PAFL, sig);
+  const uint32_t PHB = PB + V4_PH + PR * 4096;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + PHB + r * 128 + (((4 * tt + 2 * q) ^ (r & 7)) << 4) + h * 8);
+      const u32x2 hi =
+          *reinterpret_cast<const u32x2*>(smem + PHB + r * 128 + (((4 * tt + 2 * q + 1) ^ (r & 7)) << 4) + h * 8);
+      const bf16x8 pT = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      z = mfma32(lds_frag(smem, w2p_off(32 * RHO + r, (2 * (2 * PR + tt) + q) * 2 + h)), pT, z);
+    }
   if (RHO == 0) {  // the pair-shared X image [32 samples][64 feat]; the partner is past its previous tile
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -653,15 +647,17 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
       l += (nm ? M + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
     loss_acc += l;
   } else {
+    constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
     float l = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = v4_cls<RHO>(i, h);
       const float v = z[i];
       const float y = yb[i];
-      const float en = __expf(-fabsf(v));
-      const float pr = v >= 0.f ? 1.f / (1.f + en) : en / (1.f + en);
-      const float sp = fmaxf(v, 0.f) + __logf(1.f + en);
+      const float en = __builtin_amdgcn_exp2f(-fabsf(v) * L2E);  // stable sigmoid / softplus
+      const float rp = __builtin_amdgcn_rcpf(1.f + en);
+      const float pr = v >= 0.f ? rp : en * rp;
+      const float sp = fmaxf(v, 0.f) + __builtin_amdgcn_logf(1.f + en) * LN2;
       const bool okc = valid && c != 2;
       dz[i] = okc ? (pr - y) : 0.f;
       l += okc ? (sp - y * v) : 0.f;
@@ -670,8 +666,6 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     pair_signal(smem, MYFL, ++sig);  // keeps the exchange-buffer reuse below ordered
     ok &= pair_wait(smem, PAFL, sig);
   }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) db2[i] += dz[i];
   bf16x8 dzf[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q)
@@ -723,6 +717,9 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
         mfma_acc_agpr(dW2[tt][u], hR[tt][q], bd);
         mfma_acc_agpr(dW1T[tt][u], dz1[tt][q], bx);
       }
+      // db2 of the own output tile on the matrix pipe: ones(32 x samples) · dZ2 (every row of the
+      // accumulator is the column sum) instead of 16 VALU adds per tile
+      if (u == RHO) db2 = mfma32(ones, bd, db2);
     }
   wave_lds_sync();  // own H image is rewritten by the next tile
 }
@@ -743,9 +740,8 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
       dW2[t][u] = f32x16{};
       dW1T[t][u] = f32x16{};
     }
-  float db2[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) db2[i] = 0.f;
+  f32x16 db2 = f32x16{};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   float loss_acc = 0.f;
   int sig = 0;
   bool ok = true;
@@ -773,27 +769,17 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
     const uint64_t tmask = valid ? ntg : 0ull;
     fetch(tile + npairs, nin, ntg);
     v4_tile<LOSS, RHO>(smem, lut, PB, pair, r, h, lane, q4, p4, g1, imask, tmask, valid, sig, ok, dW2, dW1T, db2,
-                       loss_acc);
+                       ones, loss_acc);
   }
   asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // asm MFMA (AGPR D) -> v_accvgpr_read hazard
 
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    float v = db2[i];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o);
-    db2[i] = v;
-  }
   float lsum = wave_sum(loss_acc);
   if (!ok) lsum = __builtin_nanf("");
   __syncthreads();  // every wave is out of the loop: the loop's LDS is free
   float* RED = reinterpret_cast<float*>(smem);  // [16 tiles][4 g][64 lanes][4]: tiles 0..7 dW2, 8..15 dW1T
   float* DB2S = reinterpret_cast<float*>(smem + V4_RED);          // [4 pairs][64]
   float* LOSSS = reinterpret_cast<float*>(smem + V4_RED + 1024);  // [8]
-  if (r == 0) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) DB2S[pair * 64 + 32 * RHO + oo0(i) + 4 * h] = db2[i];
-  }
+  if (h == 0) DB2S[pair * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
   if (lane == 0) LOSSS[2 * pair + RHO] = lsum;
   // the same number of barriers in both role instantiations (wave-uniform branch)
   for (int stage = 0; stage < 4; ++stage) {
