@@ -478,7 +478,8 @@ constexpr int V4_PX = 0, V4_PD2 = 4096, V4_PH = 8192, V4_PXB = 16384, V4_PST = 2
 static_assert(V4_PST + 2 * 256 <= V4_PFL && V4_PFL + 64 <= V4_PAIR_BYTES, "v4 pair layout");
 constexpr int V4_BASE = IMG_BYTES + LUT_BYTES;
 constexpr int V4_YLUT = V4_BASE + 4 * V4_PAIR_BYTES;  // 16 x f32x4: target nibble -> 4 {0,1} floats
-constexpr int V4_LOOP_LDS = V4_YLUT + 256;
+constexpr int V4_XLUT = V4_YLUT + 256;  // 16 x 8 B: input nibble -> 4 bf16 {0,1}
+constexpr int V4_LOOP_LDS = V4_XLUT + 128;
 constexpr int V4_RED = 65536;  // epilogue fp32 dW image [16384]
 constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 4096);
 #ifndef V4_STAGGER
@@ -513,6 +514,35 @@ EM_DEVICE int v4_cls(int i, int h) {
   return o < 50 ? 0 : (o < 62 ? 1 : 2);
 }
 
+// v4 pair images [32 samples][64 cols] bf16, 128-B rows.  Row r XORs its 16-B chunk index with
+// fr(r) and (H, D2 only) its 8-B half with gr(r), chosen so that every access of the tile is
+// conflict-free under the CDNA4 banking rules (tools/lds_conflicts.py): the per-row 8-B writes
+// (16-lane groups, 32 banks) need (fr, gr) injective on rows 0-15, the partner's 8-B row reads
+// (32-lane groups, 64 banks) injective on each row parity, and the transposing reads (4 rows x 64 B
+// per 32-lane group) need fr's top bit to follow row bit 1.  The X image is written in whole 16-B
+// chunks, so it keeps gr = 0.
+EM_DEVICE uint32_t v4_fr(int r) { return ((r ^ (r >> 4)) & 1) | (((r >> 2) & 1) << 1) | (((r >> 1) & 1) << 2); }
+EM_DEVICE uint32_t v4_gr(int r) { return (r >> 3) & 1; }
+template <bool G>
+EM_DEVICE uint32_t v4_img(uint32_t base, int row, int col) {
+  const uint32_t c = (uint32_t)(((col >> 3) ^ v4_fr(row)) << 4);
+  return base + row * 128 + c + (G ? (((((col >> 2) & 1) ^ v4_gr(row)) << 3) + (col & 3) * 2) : (col & 7) * 2);
+}
+template <bool G>
+EM_DEVICE bf16x8 v4_tr_frag(const char* smem, uint32_t base, int colbase, int q, int h, int q4, int p4, int g1) {
+  const int col = colbase + 16 * g1 + 4 * p4;
+  const int r0 = 16 * q + 4 * h + q4;
+  return cat_tr(lds_tr16(smem, v4_img<G>(base, r0, col)), lds_tr16(smem, v4_img<G>(base, r0 + 8, col)));
+}
+// X fragments from a 16-entry nibble table (4 bf16 {0,1} per entry, 128 B): two ds_read_b64 per
+// fragment; distinct entries never share a bank, unlike a 256-entry byte table
+EM_DEVICE bf16x8 v4_xfrag(const char* smem, uint32_t w, int q) {
+  const int sh = 16 * (q & 1);
+  const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + V4_XLUT + (__builtin_amdgcn_ubfe(w, sh, 4) << 3));
+  const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + V4_XLUT + (__builtin_amdgcn_ubfe(w, sh + 4, 4) << 3));
+  return __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+}
+
 template <int LOSS, int RHO>
 EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int r, int h, int lane, int q4, int p4,
                        int g1, uint64_t imask, uint64_t tmask, bool valid, int& sig, bool& ok, f32x16 (&dW2)[2][2],
@@ -522,10 +552,12 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
   const uint32_t MYX = PB + V4_PXB + RHO * 4096, PAX = PB + V4_PXB + PR * 4096;
   const uint32_t MYFL = PB + V4_PFL + RHO * 4, PAFL = PB + V4_PFL + PR * 4;
   (void)pairw;
+  (void)lut;
 
   bf16x8 xf[4];
+  const uint32_t wlo = (uint32_t)imask >> (8 * h), whi = (uint32_t)(imask >> 32) >> (8 * h);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) xf[q] = lut_frag(lut, imask, q, h);
+  for (int q = 0; q < 4; ++q) xf[q] = v4_xfrag(smem, q < 2 ? wlo : whi, q);
 
   // ---- F1 (own hidden half) -> relu -> hT (B of F2) + own H image [32 samples][64 hid] ----
   bf16x8 hT[2][2];
@@ -539,10 +571,8 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     for (int q = 0; q < 2; ++q) {
       hT[tt][q] = relu_pack(a1, q);
       const u32x4 d = __builtin_bit_cast(u32x4, hT[tt][q]);
-      *reinterpret_cast<u32x2*>(smem + HB + r * 128 + ((((4 * tt + 2 * q) ^ (r & 7))) << 4) + h * 8) =
-          u32x2{d[0], d[1]};
-      *reinterpret_cast<u32x2*>(smem + HB + r * 128 + ((((4 * tt + 2 * q + 1) ^ (r & 7))) << 4) + h * 8) =
-          u32x2{d[2], d[3]};
+      *reinterpret_cast<u32x2*>(smem + v4_img<true>(HB, r, 32 * tt + 16 * q + 4 * h)) = u32x2{d[0], d[1]};
+      *reinterpret_cast<u32x2*>(smem + v4_img<true>(HB, r, 32 * tt + 16 * q + 8 + 4 * h)) = u32x2{d[2], d[3]};
     }
   }
 
@@ -567,16 +597,15 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
   for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + PHB + r * 128 + (((4 * tt + 2 * q) ^ (r & 7)) << 4) + h * 8);
-      const u32x2 hi =
-          *reinterpret_cast<const u32x2*>(smem + PHB + r * 128 + (((4 * tt + 2 * q + 1) ^ (r & 7)) << 4) + h * 8);
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + v4_img<true>(PHB, r, 32 * tt + 16 * q + 4 * h));
+      const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + v4_img<true>(PHB, r, 32 * tt + 16 * q + 8 + 4 * h));
       const bf16x8 pT = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
       z = mfma32(lds_frag(smem, w2p_off(32 * RHO + r, (2 * (2 * PR + tt) + q) * 2 + h)), pT, z);
     }
   if (RHO == 0) {  // the pair-shared X image [32 samples][64 feat]; the partner is past its previous tile
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<bf16x8*>(smem + XB + r * 128 + ((((2 * q + h) ^ (r & 7))) << 4)) = xf[q];
+      *reinterpret_cast<bf16x8*>(smem + v4_img<false>(XB, r, 16 * q + 8 * h)) = xf[q];
   }
 
   // ---- loss on the own output tile ----
@@ -678,7 +707,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const u32x4 f = __builtin_bit_cast(u32x4, dzf[g >> 1]);
-    *reinterpret_cast<u32x2*>(smem + DB + r * 128 + ((((4 * RHO + g) ^ (r & 7))) << 4) + h * 8) =
+    *reinterpret_cast<u32x2*>(smem + v4_img<true>(DB, r, 32 * RHO + 8 * g + 4 * h)) =
         u32x2{f[2 * (g & 1)], f[2 * (g & 1) + 1]};
   }
   pair_signal(smem, MYFL, ++sig);
@@ -700,7 +729,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
         aD = mfma32(u == RHO ? dzf[q] : dzp[q], lds_frag(smem, w2q_off(32 * t + r, (2 * u + q) * 2 + h)), aD);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      hR[tt][q] = tr_frag<0>(smem, HB, 32 * tt, q, h, q4, p4, g1);
+      hR[tt][q] = v4_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
       dz1[tt][q] = mask_by(hR[tt][q], aD, q);
     }
   }
@@ -710,8 +739,8 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const bf16x8 bd = tr_frag<0>(smem, DB, 32 * u, q, h, q4, p4, g1);
-      const bf16x8 bx = tr_frag<0>(smem, XB, 32 * u, q, h, q4, p4, g1);
+      const bf16x8 bd = v4_tr_frag<true>(smem, DB, 32 * u, q, h, q4, p4, g1);
+      const bf16x8 bx = v4_tr_frag<false>(smem, XB, 32 * u, q, h, q4, p4, g1);
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         mfma_acc_agpr(dW2[tt][u], hR[tt][q], bd);
@@ -821,6 +850,10 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   }
   fill_lut(smem + IMG_BYTES, tid);
   if (tid < 64) reinterpret_cast<float*>(smem + V4_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
+  if (tid < 32) {  // nibble n = tid >> 1, dword tid & 1 holds elements 2(tid&1), 2(tid&1)+1
+    const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
+    reinterpret_cast<uint32_t*>(smem + V4_XLUT)[tid] = (((n >> b) & 1u) ? 0x3F80u : 0u) | (((n >> (b + 1)) & 1u) ? 0x3F800000u : 0u);
+  }
   if (lane < 2) reinterpret_cast<int*>(smem + V4_BASE + pair * V4_PAIR_BYTES + V4_PFL)[lane] = 0;
   __syncthreads();
   // waves 4-7 share SIMDs with waves 0-3 (other pairs): start them half a tile later so the two
