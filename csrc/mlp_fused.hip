@@ -483,7 +483,10 @@ constexpr int V4_LOOP_LDS = V4_XLUT + 128;
 constexpr int V4_RED = 65536;  // epilogue fp32 dW image [16384]
 constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 4096);
 #ifndef V4_STAGGER
-#define V4_STAGGER 80
+#define V4_STAGGER 0
+#endif
+#ifndef V4_PRIO
+#define V4_PRIO 0
 #endif
 #ifndef V4_SLEEP
 #define V4_SLEEP 0
@@ -513,6 +516,27 @@ EM_DEVICE int v4_cls(int i, int h) {
   const int o = 32 * RHO + oo0(i) + 4 * h;
   return o < 50 ? 0 : (o < 62 ? 1 : 2);
 }
+
+// Diagnostic phase timers (build with --define V4_STAMPS=1; tools/fused_phases.py reads them):
+// s_memtime deltas summed per phase per wave, written after the dW slab into spare slab floats.
+// They force an lgkmcnt drain at every mark, so they perturb what they measure (+~10 %).
+#ifndef V4_STAMPS
+#define V4_STAMPS 0
+#endif
+struct V4Stamps {
+  uint64_t last = 0;
+  uint64_t acc[10] = {};
+  EM_DEVICE void start() {
+    if (V4_STAMPS) last = __builtin_amdgcn_s_memtime();
+  }
+  EM_DEVICE void mark(int k) {
+    if (V4_STAMPS) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc[k] += t - last;
+      last = t;
+    }
+  }
+};
 
 // v4 pair images [32 samples][64 cols] bf16, 128-B rows.  Row r XORs its 16-B chunk index with
 // fr(r) and (H, D2 only) its 8-B half with gr(r), chosen so that every access of the tile is
@@ -546,7 +570,7 @@ EM_DEVICE bf16x8 v4_xfrag(const char* smem, uint32_t w, int q) {
 template <int LOSS, int RHO>
 EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int r, int h, int lane, int q4, int p4,
                        int g1, uint64_t imask, uint64_t tmask, bool valid, int& sig, bool& ok, f32x16 (&dW2)[2][2],
-                       f32x16 (&dW1T)[2][2], f32x16& db2, const bf16x8 ones, float& loss_acc) {
+                       f32x16 (&dW1T)[2][2], f32x16& db2, const bf16x8 ones, float& loss_acc, V4Stamps& st) {
   constexpr int PR = 1 - RHO;
   const uint32_t XB = PB + V4_PX, DB = PB + V4_PD2, HB = PB + V4_PH + RHO * 4096;
   const uint32_t MYX = PB + V4_PXB + RHO * 4096, PAX = PB + V4_PXB + PR * 4096;
@@ -579,6 +603,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
   // ---- exchange (1): the H images.  Each wave computes the FULL logits of its own output tile:
   // its own hidden half from registers, the partner's half read back as B fragments from the
   // partner's H image (two ds_read_b64 each) -- no fp32 partial-sum round trip through LDS ----
+  st.mark(0);
   pair_signal(smem, MYFL, ++sig);
   f32x16 z;
 #pragma unroll
@@ -591,7 +616,9 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 #pragma unroll
     for (int q = 0; q < 2; ++q)
       z = mfma32(lds_frag(smem, w2p_off(32 * RHO + r, (2 * (2 * RHO + tt) + q) * 2 + h)), hT[tt][q], z);
+  st.mark(1);
   ok &= pair_wait(smem, PAFL, sig);
+  st.mark(2);
   const uint32_t PHB = PB + V4_PH + PR * 4096;
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt)
@@ -608,6 +635,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
       *reinterpret_cast<bf16x8*>(smem + v4_img<false>(XB, r, 16 * q + 8 * h)) = xf[q];
   }
 
+  st.mark(3);
   // ---- loss on the own output tile ----
   // target bits of the lane's 16 outputs as 0/1 floats: register group g holds outputs
   // 8g + 4h .. +3 of the tile = one nibble of the target mask -> one ds_read_b128 of a 16-entry table
@@ -658,8 +686,10 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     if (RHO == 1) s_s += __shfl_xor(s_s, 32);
     // exchange (2): online-softmax merge of the main-group statistics
     if (h == 0) *reinterpret_cast<float2*>(smem + PB + V4_PST + RHO * 256 + r * 8) = float2{mx_m, s_m};
+    st.mark(4);
     pair_signal(smem, MYFL, ++sig);
     ok &= pair_wait(smem, PAFL, sig);
+    st.mark(5);
     const float2 ps = *reinterpret_cast<const float2*>(smem + PB + V4_PST + PR * 256 + r * 8);
     const float M = fmaxf(mx_m, ps.x);
     const float sc_own = __builtin_amdgcn_exp2f((mx_m - M) * L2E);
@@ -710,54 +740,98 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
     *reinterpret_cast<u32x2*>(smem + v4_img<true>(DB, r, 32 * RHO + 8 * g + 4 * h)) =
         u32x2{f[2 * (g & 1)], f[2 * (g & 1) + 1]};
   }
+  st.mark(6);
   pair_signal(smem, MYFL, ++sig);
+
+  // ---- work that needs only our own dZ2 half, issued before waiting for the partner's:
+  // B1 over the own output tile, dW2 for the own output columns, db2 ----
+  // (BCE keeps the old order: its longer loss code leaves no registers for the early accumulators)
+  bf16x8 hR[2][2], dz1[2][2];
+  f32x16 aD[2];
+  if (LOSS == 0) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * RHO + tt;
+      aD[tt] = f32x16{};
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        aD[tt] = mfma32(dzf[q], lds_frag(smem, w2q_off(32 * t + r, (2 * RHO + q) * 2 + h)), aD[tt]);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) hR[tt][q] = v4_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bf16x8 bd = v4_tr_frag<true>(smem, DB, 32 * RHO, q, h, q4, p4, g1);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) mfma_acc_agpr(dW2[tt][RHO], hR[tt][q], bd);
+      // db2 of the own output tile on the matrix pipe: ones(32 x samples) · dZ2 (every row of the
+      // accumulator is the column sum) instead of 16 VALU adds per tile
+      db2 = mfma32(ones, bd, db2);
+    }
+  }
   ok &= pair_wait(smem, PAFL, sig);
+  if (LOSS != 0) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * RHO + tt;
+      aD[tt] = f32x16{};
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        aD[tt] = mfma32(dzf[q], lds_frag(smem, w2q_off(32 * t + r, (2 * RHO + q) * 2 + h)), aD[tt]);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) hR[tt][q] = v4_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bf16x8 bd = v4_tr_frag<true>(smem, DB, 32 * RHO, q, h, q4, p4, g1);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) mfma_acc_agpr(dW2[tt][RHO], hR[tt][q], bd);
+      // db2 of the own output tile on the matrix pipe: ones(32 x samples) · dZ2 (every row of the
+      // accumulator is the column sum) instead of 16 VALU adds per tile
+      db2 = mfma32(ones, bd, db2);
+    }
+  }
+  st.mark(7);
   bf16x8 dzp[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) dzp[q] = *reinterpret_cast<const bf16x8*>(smem + PAX + (q * 64 + lane) * 16);
 
-  // ---- B1: dH = dZ2·W2ᵀ for the own hidden half; dZ1 = dH * (Z1 > 0) ----
-  bf16x8 hR[2][2], dz1[2][2];
+  // ---- B1 (partner's output tile): dH = dZ2·W2ᵀ for the own hidden half; dZ1 = dH * (Z1 > 0) ----
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int t = 2 * RHO + tt;
-    f32x16 aD = f32x16{};
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int q = 0; q < 2; ++q)
+      aD[tt] = mfma32(dzp[q], lds_frag(smem, w2q_off(32 * t + r, (2 * PR + q) * 2 + h)), aD[tt]);
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        aD = mfma32(u == RHO ? dzf[q] : dzp[q], lds_frag(smem, w2q_off(32 * t + r, (2 * u + q) * 2 + h)), aD);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      hR[tt][q] = v4_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
-      dz1[tt][q] = mask_by(hR[tt][q], aD, q);
-    }
+    for (int q = 0; q < 2; ++q) dz1[tt][q] = mask_by(hR[tt][q], aD[tt], q);
   }
 
-  // ---- dW2[own hid][out] += Hᵀ·dZ2 ; dW1ᵀ[own hid][feat] += dZ1ᵀ·X ----
+  st.mark(8);
+  // ---- dW2[own hid][partner out] += Hᵀ·dZ2 ; dW1ᵀ[own hid][feat] += dZ1ᵀ·X ----
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const bf16x8 bd = v4_tr_frag<true>(smem, DB, 32 * PR, q, h, q4, p4, g1);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) mfma_acc_agpr(dW2[tt][PR], hR[tt][q], bd);
+  }
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const bf16x8 bd = v4_tr_frag<true>(smem, DB, 32 * u, q, h, q4, p4, g1);
       const bf16x8 bx = v4_tr_frag<false>(smem, XB, 32 * u, q, h, q4, p4, g1);
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        mfma_acc_agpr(dW2[tt][u], hR[tt][q], bd);
-        mfma_acc_agpr(dW1T[tt][u], dz1[tt][q], bx);
-      }
-      // db2 of the own output tile on the matrix pipe: ones(32 x samples) · dZ2 (every row of the
-      // accumulator is the column sum) instead of 16 VALU adds per tile
-      if (u == RHO) db2 = mfma32(ones, bd, db2);
+      for (int tt = 0; tt < 2; ++tt) mfma_acc_agpr(dW1T[tt][u], dz1[tt][q], bx);
     }
   wave_lds_sync();  // own H image is rewritten by the next tile
+  st.mark(9);
 }
 
 // One role's whole persistent loop + its share of the epilogue reduction.  Instantiated per role so
 // the AGPR-pinned dW accumulators never cross a role branch (a merge point would force copies).
 template <int LOSS, int RHO>
 EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                       int offset, int pair, int lane) {
+                       int offset, int pair, int lane, float* slab_spare) {
   const int r = lane & 31, h = lane >> 5;
   const char* lut = smem + IMG_BYTES;
   const uint32_t PB = V4_BASE + pair * V4_PAIR_BYTES;
@@ -788,9 +862,11 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
       mt = masks[idx + 1];
     }
   };
+  V4Stamps st;
   const int first = blockIdx.x * 4 + pair;
   uint64_t nin, ntg;
   fetch(first, nin, ntg);
+  st.start();
   for (int tile = first; tile < ntiles; tile += npairs) {
     const int s = tile * 32 + r;
     const bool valid = s < B;
@@ -798,12 +874,18 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
     const uint64_t tmask = valid ? ntg : 0ull;
     fetch(tile + npairs, nin, ntg);
     v4_tile<LOSS, RHO>(smem, lut, PB, pair, r, h, lane, q4, p4, g1, imask, tmask, valid, sig, ok, dW2, dW1T, db2,
-                       ones, loss_acc);
+                       ones, loss_acc, st);
   }
   asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // asm MFMA (AGPR D) -> v_accvgpr_read hazard
 
   float lsum = wave_sum(loss_acc);
   if (!ok) lsum = __builtin_nanf("");
+  if (V4_STAMPS && lane < 10) {  // phase cycles of this wave -> spare slab floats
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) v = (lane == k) ? st.acc[k] : v;
+    slab_spare[(2 * pair + RHO) * 16 + lane] = (float)v;
+  }
   __syncthreads();  // every wave is out of the loop: the loop's LDS is free
   float* RED = reinterpret_cast<float*>(smem);  // [16 tiles][4 g][64 lanes][4]: tiles 0..7 dW2, 8..15 dW1T
   float* DB2S = reinterpret_cast<float*>(smem + V4_RED);          // [4 pairs][64]
@@ -859,14 +941,13 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   // waves 4-7 share SIMDs with waves 0-3 (other pairs): start them half a tile later so the two
   // co-resident waves do not hit their MFMA and VALU phases in lockstep (MI355X_MICROARCH.md,
   // "Two waves per SIMD" item 9), and give the younger half static priority (item 4)
-  if (V4_STAGGER && wave >= 4) {
-    __builtin_amdgcn_s_sleep(V4_STAGGER);  // ~64 cycles per unit
-    __builtin_amdgcn_s_setprio(1);
-  }
+  if (V4_STAGGER && wave >= 4) __builtin_amdgcn_s_sleep(V4_STAGGER);  // ~64 cycles per unit
+  if (V4_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
   if (rho == 0)
-    v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane);
+    v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane, slab_spare);
   else
-    v4_body<LOSS, 1>(smem, masks, sidx, B, offset, pair, lane);
+    v4_body<LOSS, 1>(smem, masks, sidx, B, offset, pair, lane, slab_spare);
 
   const float* RED = reinterpret_cast<const float*>(smem);
   const float* DB2S = reinterpret_cast<const float*>(smem + V4_RED);

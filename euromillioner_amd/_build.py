@@ -190,6 +190,8 @@ if __name__ == "__main__":
     ap.add_argument("--debug", action="store_true",
                     help="debug build (-g, device asserts kept; run with HIP_LAUNCH_BLOCKING=1 to localise a fault); "
                          "forces a rebuild -- rebuild without --debug afterwards")
+    ap.add_argument("--define", action="append", default=[], metavar="NAME=VALUE",
+                    help="extra -D for the HIP sources (kernel tuning sweeps); forces a rebuild")
     ap.add_argument("--host-sanitize", action="store_true",
                     help="host-only ASan/UBSan build of the C++ host library (GPU sanitizers are unavailable)")
     a = ap.parse_args()
@@ -199,4 +201,5 @@ if __name__ == "__main__":
         host_flags = ("-fsanitize=address,undefined", "-fno-omit-frame-pointer") if a.host_sanitize else ()
         print(build_host(force=a.force or a.host_sanitize, verbose=a.verbose, extra_flags=host_flags))
         dbg = ("-g", "-O1") if a.debug else ()
-        print(build(force=a.force or a.debug, jobs=a.jobs, verbose=a.verbose, extra_flags=dbg))
+        defs = tuple("-D" + d for d in a.define)
+        print(build(force=a.force or a.debug or bool(defs), jobs=a.jobs, verbose=a.verbose, extra_flags=dbg + defs))
