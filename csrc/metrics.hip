@@ -134,9 +134,10 @@ __global__ void rows_to_masks_kernel(const uint8_t* __restrict__ rows, int64_t n
 }
 
 // K14: feature masks -> multi-hot bf16 [B][64] (optional constant-1 bias feature at 62)
+template <typename T>
 __global__ void onehot_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int64_t B,
-                              int64_t offset, int which, int with_bias, __bf16* __restrict__ out) {
-  // one thread per (sample, 8-feature chunk): 16-byte stores
+                              int64_t offset, int which, int with_bias, T* __restrict__ out) {
+  // one thread per (sample, 8-feature chunk): 16-byte (bf16) / 2x16-byte (fp32) stores
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * 8) return;
   const int64_t s = e >> 3;
@@ -144,15 +145,23 @@ __global__ void onehot_kernel(const uint64_t* __restrict__ masks, const int32_t*
   const int64_t idx = (sidx ? (int64_t)sidx[s] : offset + s) + which;
   uint64_t m = masks[idx] & (MAIN_BITS | STAR_BITS);
   if (with_bias) m |= 1ull << 62;
-  *reinterpret_cast<bf16x8*>(out + s * 64 + c * 8) = bits_to_bf16x8((uint32_t)(m >> (8 * c)) & 0xFFu);
+  const uint32_t b = (uint32_t)(m >> (8 * c)) & 0xFFu;
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<bf16x8*>(out + s * 64 + c * 8) = bits_to_bf16x8(b);
+  } else {
+    f32x4* o = reinterpret_cast<f32x4*>(out + s * 64 + c * 8);
+    o[0] = f32x4{(float)(b & 1u), (float)((b >> 1) & 1u), (float)((b >> 2) & 1u), (float)((b >> 3) & 1u)};
+    o[1] = f32x4{(float)((b >> 4) & 1u), (float)((b >> 5) & 1u), (float)((b >> 6) & 1u), (float)((b >> 7) & 1u)};
+  }
 }
 
 // K10: loss + dL/dlogits for the GEMM-path MLPs.  One wavefront per sample, lane j = output j
 // (62 live lanes; 62/63 are padding and get dz = 0).  dz is written bf16 (the next GEMM's
 // operand) already scaled by grad_scale (1/global_batch); per-block loss sums -> partials.
+template <typename T>  // dz element type: __bf16 (bf16 GEMM path) or float (fp32 path)
 __global__ void loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __restrict__ masks,
                                  const int32_t* __restrict__ sidx, int64_t B, int64_t offset, int loss_kind,
-                                 float grad_scale, __bf16* __restrict__ dz, int ldz, float* __restrict__ partials) {
+                                 float grad_scale, T* __restrict__ dz, int ldz, float* __restrict__ partials) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __shared__ float red[4];
   const int64_t s = (int64_t)blockIdx.x * 4 + w;
@@ -186,7 +195,7 @@ __global__ void loss_grad_kernel(const float* __restrict__ logits, int ld, const
       const float l = fmaxf(z, 0.f) - z * y + __logf(1.f + __expf(-fabsf(z)));
       loss = wave_sum(live ? l : 0.f) * (1.f / 62.f);
     }
-    dz[s * ldz + lane] = (__bf16)(g * grad_scale);
+    dz[s * ldz + lane] = (T)(g * grad_scale);
   }
   if (lane == 0) red[w] = loss;
   __syncthreads();
@@ -219,8 +228,19 @@ EM_API int em_onehot_encode(const uint64_t* draws, const int32_t* sidx, int64_t 
   if (!draws || !out || B < 0) return EM_ERR_ARG;
   if (B == 0) return 0;
   const int64_t n = B * 8;
-  hipLaunchKernelGGL(onehot_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, draws, sidx, B, offset,
-                     which, with_bias, (__bf16*)out);
+  hipLaunchKernelGGL(onehot_kernel<__bf16>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, draws, sidx, B,
+                     offset, which, with_bias, (__bf16*)out);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_onehot_encode_f32(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset, int which,
+                                int with_bias, float* out, hipStream_t stream) {
+  if (!draws || !out || B < 0) return EM_ERR_ARG;
+  if (B == 0) return 0;
+  const int64_t n = B * 8;
+  hipLaunchKernelGGL(onehot_kernel<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, draws, sidx, B,
+                     offset, which, with_bias, out);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -231,8 +251,20 @@ EM_API int em_loss_grad(const float* logits, int ld, const uint64_t* masks, cons
   if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
     return EM_ERR_ARG;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(loss_grad_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks, sidx,
-                     B, offset, loss_kind, grad_scale, (__bf16*)dz, ldz, partials);
+  hipLaunchKernelGGL(loss_grad_kernel<__bf16>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks,
+                     sidx, B, offset, loss_kind, grad_scale, (__bf16*)dz, ldz, partials);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+EM_API int em_loss_grad_f32(const float* logits, int ld, const uint64_t* masks, const int32_t* sidx, int64_t B,
+                            int64_t offset, int loss_kind, float grad_scale, float* dz, int ldz, float* partials,
+                            hipStream_t stream) {
+  if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
+    return EM_ERR_ARG;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(loss_grad_kernel<float>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks,
+                     sidx, B, offset, loss_kind, grad_scale, dz, ldz, partials);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -231,6 +231,32 @@ def apply_env(cfg: RunConfig, environ=None) -> None:
             continue
 
 
+# enumerated fields: a typo must be a configuration error (exit 2), not a silently ignored value
+CHOICES = {
+    "model": ("gbdt", "rf", "mlp", "mlp-wide"),
+    "device": ("auto", "cuda", "cpu"),
+    "data.source": ("synthetic", "csv", "html", "reference-csv"),
+    "gbdt.objective": ("reg:logistic", "binary:logistic", "reg:squarederror", "multi:softprob", "multi:softmax"),
+    "gbdt.eval_metric": ("logloss", "rmse", "error", "mlogloss", "merror"),
+    "gbdt.device": ("auto", "cuda", "cpu"),
+    "rf.device": ("auto", "cuda", "cpu"),
+    "mlp.activation": ("relu", "sigmoid", "tanh"),
+    "mlp.loss": ("softmax", "bce"),
+    "mlp.dtype": ("bf16", "fp32"),
+    "dist.backend": ("auto", "nccl", "gloo"),
+}
+
+
+def validate(cfg: RunConfig) -> RunConfig:
+    for dotted, allowed in CHOICES.items():
+        obj: Any = cfg
+        for part in dotted.split("."):
+            obj = getattr(obj, part)
+        if obj not in allowed:
+            raise ValueError(f"{dotted}={obj!r}: expected one of {', '.join(allowed)}")
+    return cfg
+
+
 def build_config(file: str | None = None, overrides: dict | None = None, environ=None) -> RunConfig:
     cfg = RunConfig()
     if file:
@@ -239,4 +265,4 @@ def build_config(file: str | None = None, overrides: dict | None = None, environ
     for k, v in (overrides or {}).items():
         if v is not None:
             set_path(cfg, k, v)
-    return cfg
+    return validate(cfg)

@@ -314,7 +314,7 @@ class GBDT:
 
     def __init__(self, eta=1.0, max_depth=3, objective="reg:logistic", subsample=1.0, gamma=1.0,
                  reg_lambda=1.0, min_child_weight=1.0, base_score=0.5, nround=500, max_bin=256,
-                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1, num_class=0):
+                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1, num_class=0, nthread=0):
         if objective not in OBJECTIVES:
             raise ValueError(f"objective must be one of {OBJECTIVES}")
         self.eta, self.max_depth, self.objective = float(eta), int(max_depth), objective
@@ -322,6 +322,7 @@ class GBDT:
         self.mcw, self.base_score, self.nround = float(min_child_weight), float(base_score), int(nround)
         self.max_bin, self.eval_metric, self.seed = int(max_bin), eval_metric, int(seed)
         self.num_class = int(num_class)
+        self.nthread = int(nthread)  # XGBoost nthread (Main.java:122): CPU threads of the numpy engine (0 = all)
         if objective in MULTI and eval_metric in ("logloss", "error"):
             self.eval_metric = "m" + eval_metric  # XGBoost's multi-class defaults: mlogloss / merror
         self.backend = backend
@@ -343,7 +344,7 @@ class GBDT:
                     gamma=float(p.get("gamma", 0.0)), reg_lambda=float(p.get("lambda", 1.0)),
                     min_child_weight=float(p.get("min_child_weight", 1.0)),
                     base_score=float(p.get("base_score", 0.5)), eval_metric=p.get("eval_metric", "logloss"),
-                    nround=nround, num_class=int(p.get("num_class", 0)))
+                    nround=nround, num_class=int(p.get("num_class", 0)), nthread=int(p.get("nthread", 0)))
         args.update(kw)
         return cls(**args)
 
@@ -400,7 +401,10 @@ class GBDT:
 
             self.trees, self.history = gbdt_hip.fit(self, X, bins, nbins, Y, evals, dp=dp)
         else:
-            self.trees, self.history = self._fit_numpy(X, bins, nbins, Y, evals, dp=dp)
+            from threadpoolctl import threadpool_limits
+
+            with threadpool_limits(limits=self.nthread or None):  # X3: the reference's OpenMP nthread
+                self.trees, self.history = self._fit_numpy(X, bins, nbins, Y, evals, dp=dp)
         self.trees.set_split_values(self.cuts)
         return self
 

@@ -21,6 +21,9 @@ Per step (all on the current HIP stream, no host sync):
 Flat layout per layer (padded: input and output 62 -> 64, hidden to multiples of 8; the
 pads stay exactly zero): ``W [N_pad, K_pad]`` (nn.Linear orientation) then ``b [N_pad]``;
 one extra slot at the end carries the step loss through the same all-reduce.
+
+``dtype="fp32"`` (``--dtype fp32``) runs the same step in fp32 end to end on the exact-fp32 MFMA
+GEMM (``csrc/gemm_f32.hip``): fp32 activations and dL/dZ, no bf16 shadow.
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ import torch
 
 from ..ops import fused_mlp as FM
 from ..ops import linear as LIN
+from ..ops import linear_f32 as LF
 from ..ops import _native as N
 from .mlp import DrawMLP, FusedSmallMLP
 
@@ -40,7 +44,7 @@ def _pad(n: int) -> int:
 class GemmMLPTrainer:
     def __init__(self, sizes=(62, 8192, 8192, 62), device="cuda", activation: str = "relu", loss: str = "softmax",
                  lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
-                 state_dict: dict | None = None, process_group=None, bucket_mb: float = 25.0):
+                 state_dict: dict | None = None, process_group=None, bucket_mb: float = 25.0, dtype: str = "bf16"):
         if sizes[0] != 62 or sizes[-1] != 62:
             raise ValueError("draw MLPs are 62-in / 62-out")
         if activation not in ("relu", "tanh", "sigmoid"):
@@ -49,6 +53,10 @@ class GemmMLPTrainer:
             raise ValueError("sigmoid needs hidden sizes that are multiples of 8 (sigmoid(0) != 0 on pads)")
         if loss not in FM.LOSS_KINDS:
             raise ValueError(f"loss must be one of {list(FM.LOSS_KINDS)}")
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError("dtype must be bf16 or fp32")
+        self.dtype = dtype
+        self.f32 = dtype == "fp32"
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("GemmMLPTrainer runs on the GPU (use DrawMLP on the CPU)")
@@ -68,7 +76,8 @@ class GemmMLPTrainer:
         self.grads = torch.zeros(self.P + 1, dtype=torch.float32, device=dev)
         self.m = torch.zeros(self.P, dtype=torch.float32, device=dev)
         self.v = torch.zeros(self.P, dtype=torch.float32, device=dev)
-        self.shadow = torch.zeros(self.P, dtype=torch.bfloat16, device=dev)
+        # bf16 copy of the weights the bf16 GEMMs read (refreshed by the fused Adam); fp32 reads params
+        self.shadow = None if self.f32 else torch.zeros(self.P, dtype=torch.bfloat16, device=dev)
         self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
         self.state = torch.zeros(2, dtype=torch.int32, device=dev)
         if state_dict is None:
@@ -111,6 +120,16 @@ class GemmMLPTrainer:
 
     def _ws(self, B: int) -> dict:
         ws = self._ws_cache.get(B)
+        if ws is None and self.f32:
+            dev, P = self.device, self.padded
+            f = torch.float32
+            ws = {"x": torch.empty(B, 64, dtype=f, device=dev),
+                  "act": [torch.empty(B, n, dtype=f, device=dev) for n in P[1:-1]],
+                  "dz": [torch.empty(B, n, dtype=f, device=dev) for n in P[1:]],
+                  "logits": torch.empty(B, 64, dtype=f, device=dev),
+                  "part": torch.empty(max((B + 3) // 4, 1), dtype=f, device=dev),
+                  "parts": {}}
+            self._ws_cache = {B: ws}
         if ws is None:
             dev = self.device
             plan = self._plan(B)
@@ -139,6 +158,17 @@ class GemmMLPTrainer:
         return FusedSmallMLP.prepare(draws)
 
     def _forward(self, masks, B, offset, sidx, ws, train: bool = False):
+        if self.f32:
+            h = LF.onehot(masks, B, offset=offset, which=0, sidx=sidx, out=ws["x"])
+            inputs = []
+            L = len(self.offsets)
+            for i in range(L):
+                w, bf = self._views(self.params, i)
+                inputs.append(h)
+                last = i == L - 1
+                h = LF.linear_fwd(h, w, bf, "none" if last else self.activation,
+                                  out=ws["logits"] if last else ws["act"][i])
+            return h, inputs
         x = FM.onehot(masks, B, offset=offset, which=0, bias=False, sidx=sidx, out=ws["x"])
         h, inputs = x, []
         L = len(self.offsets)
@@ -154,8 +184,19 @@ class GemmMLPTrainer:
 
     def _backward(self, dz, inputs, ws, on_layer_done=None):
         """Last layer first: wgrad + bias grad into the flat gradient buffer, then dgrad (act' fused)."""
-        plan = ws["plan"]
         L = len(self.offsets)
+        if self.f32:
+            for i in reversed(range(L)):
+                gw, gbias = self._views(self.grads, i)
+                LF.linear_wgrad(dz, inputs[i], out=gw, parts_cache=ws["parts"])
+                torch.sum(dz, dim=0, out=gbias)
+                if on_layer_done is not None:
+                    on_layer_done(i)
+                if i > 0:
+                    w, _ = self._views(self.params, i)
+                    dz = LF.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
+            return dz
+        plan = ws["plan"]
         for i in reversed(range(L)):
             gw, gbias = self._views(self.grads, i)
             if plan["wgrad"][i]:
@@ -188,8 +229,8 @@ class GemmMLPTrainer:
         ws = self._ws(B)
         gb = global_batch if global_batch is not None else B * self.world
         logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
-        dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
-                                 grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
+        dz, part = (LF if self.f32 else LIN).loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
+                                                       grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
         torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
         self.grads[self.P:].mul_(1.0 / gb)
         handles = []
@@ -215,8 +256,8 @@ class GemmMLPTrainer:
         """(loss, {name: grad}) for tests: same kernels, no all-reduce, no update."""
         ws = self._ws(B)
         logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
-        dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx, grad_scale=1.0 / B,
-                                 dz=ws["dz"][-1], partials=ws["part"])
+        dz, part = (LF if self.f32 else LIN).loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
+                                                       grad_scale=1.0 / B, dz=ws["dz"][-1], partials=ws["part"])
         self._backward(dz, inputs, ws)
         out = {}
         for i in range(len(self.offsets)):
@@ -268,7 +309,8 @@ class GemmMLPTrainer:
         self.params.zero_()
         for k, v in self._logical(self.params).items():
             v.copy_(sd[k].to(self.device, torch.float32))
-        self.shadow.copy_(self.params)
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)
 
     def optimizer_state(self) -> dict:
         return {"m": {k: v.clone().cpu() for k, v in self._logical(self.m).items()},
@@ -290,4 +332,5 @@ class GemmMLPTrainer:
         import torch.distributed as dist
 
         dist.broadcast(self.params, src=src, group=self.group)
-        self.shadow.copy_(self.params)
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)

@@ -136,7 +136,7 @@ class _GemmEngine(_Engine):
         m = cfg.mlp
         self.model = GemmMLPTrainer(sizes, info.device, activation=m.activation, loss=m.loss, lr=m.lr,
                                     betas=tuple(m.betas), eps=m.eps, weight_decay=m.weight_decay, state_dict=sd,
-                                    process_group=info.group, bucket_mb=cfg.dist.bucket_mb)
+                                    process_group=info.group, bucket_mb=cfg.dist.bucket_mb, dtype=m.dtype)
         self.masks = masks
 
     def step(self, idx, offset, B, global_batch):
@@ -173,7 +173,10 @@ class _TorchEngine(_Engine):
 
         m = cfg.mlp
         self.info = info
-        self.net = DrawMLP(sizes, activation=m.activation, loss=m.loss).to(info.device)
+        # --dtype fp32 on the GPU: plain fp32 layers (the HIP autograd GEMMs are bf16).  The CPU
+        # plumbing path (BASELINE config 1) always computes in fp32.
+        self.net = DrawMLP(sizes, activation=m.activation, loss=m.loss,
+                           use_hip=False if m.dtype == "fp32" else None).to(info.device)
         self.net.load_state_dict(sd)
         self.opt = torch.optim.Adam(self.net.parameters(), lr=m.lr, betas=tuple(m.betas), eps=m.eps,
                                     weight_decay=m.weight_decay)
@@ -331,8 +334,8 @@ def _mlp_sizes(cfg: RunConfig) -> tuple:
 def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
     if info.device.type != "cuda" or cfg.data.lags != 1 or cfg.dist.avg_frequency:
         return "torch"  # (parameter averaging runs on the DrawMLP engine)
-    if sizes == (62, 128, 62) and cfg.mlp.activation == "relu":
-        return "fused"
+    if sizes == (62, 128, 62) and cfg.mlp.activation == "relu" and cfg.mlp.dtype == "bf16":
+        return "fused"  # the single-launch kernel is bf16; --dtype fp32 takes the fp32 MFMA GEMM engine
     return "gemm"
 
 

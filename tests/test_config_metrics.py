@@ -75,3 +75,16 @@ def test_log4j_line_format():
     import re
 
     assert re.match(r"^\d{4}-\d\d-\d\d \d\d:\d\d:\d\d WARN  Main - Could not access URL - x$", line), line
+
+
+@pytest.mark.parametrize("key,val", [("mlp.dtype", "fp16"), ("model", "cnn"), ("gbdt.objective", "rank:pairwise"),
+                                     ("data.source", "web")])
+def test_enumerated_fields_are_validated(key, val):
+    with pytest.raises(ValueError):
+        C.build_config(None, {key: val}, environ={})
+
+
+def test_cli_rejects_bad_dtype_with_exit_2():
+    from euromillioner_amd.cli import main
+
+    assert main(["train", "--model", "mlp", "--dtype", "fp16", "--device", "cpu"]) == 2
