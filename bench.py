@@ -95,6 +95,10 @@ def main():
     ap.add_argument("--model", default="mlp", choices=["mlp", "mlp-wide"],
                     help="mlp = 62->128->62 (headline, fused kernel); mlp-wide = 62->8192->8192->62 (GEMM path)")
     ap.add_argument("--hidden", default=None, help="GEMM-path hidden sizes, e.g. 8192,8192")
+    ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
+                    help="DP gradient all-reduce of the fused path: xgmi = one-shot peer-memory reduction fused "
+                         "into Adam (hipGraph-replayable); rccl = torch.distributed all_reduce; auto = xgmi if the "
+                         "node passes its self-test")
     a = ap.parse_args()
     if a.model == "mlp-wide":
         if a.batch == 1 << 20:
@@ -143,7 +147,7 @@ def main():
         def step(i):
             return model.step(draws, B, offset=(i % n_off) * B)
     elif a.impl == "fused":
-        model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group)
+        model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group, comm=a.comm)
         model.broadcast_parameters()
 
         def step(i):
@@ -154,7 +158,7 @@ def main():
         def step(i):
             return model.step((i % n_off) * B)
 
-    use_graph = bool(a.graph) and world == 1
+    use_graph = bool(a.graph) and (world == 1 or getattr(model, "graph_safe", False))
     graph = None
     loss_t = None
     for i in range(a.warmup):
@@ -196,6 +200,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1000.0 / a.steps
+    if hasattr(model, "check_comm"):
+        model.check_comm()  # an xGMI peer wait that timed out is an error, not a fast step
     if world > 1:
         t = torch.tensor([ms], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -234,14 +240,18 @@ def main():
             "data": "synthetic (seeded Euromillions draws, planted Markov p=%.2f; random-init weights)" % a.planted,
             "config": {"model": desc,
                        "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
-                       "per_gpu_batch": B, "optimizer": "adam", "hipgraph": use_graph},
+                       "per_gpu_batch": B, "optimizer": "adam", "hipgraph": use_graph,
+                       "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none")},
             "train_loss_last": loss,
             "val": ev,
             "val_iid": ev_iid,
             **extra,
         }
         print(json.dumps(out))
+    if hasattr(model, "close"):
+        model.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

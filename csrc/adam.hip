@@ -12,6 +12,7 @@
 // straight 48 KB copy).  Modes let DP insert an RCCL all-reduce between the slab
 // reduction and the update.
 #include "common.h"
+#include "xgmi.h"
 
 namespace {
 
@@ -71,6 +72,29 @@ EM_DEVICE void adam_end(int* state, int t) {
   }
 }
 
+// torch.optim.Adam update of parameter p with gradient g (pad slots of the MLP image pinned to 0)
+EM_DEVICE void adam_apply(int p, float g, int tstep, float* __restrict__ params, float* __restrict__ m,
+                          float* __restrict__ v, const float* __restrict__ hp, uint8_t* __restrict__ mlp_img) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+  const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
+  if (mlp_img && mlp_pad_slot(p)) {
+    params[p] = 0.f;
+    m[p] = 0.f;
+    v[p] = 0.f;
+    mlp_pack_one(p, 0.f, mlp_img);
+  } else {
+    float w = params[p];
+    g += wd * w;
+    const float mm = b1 * m[p] + (1.f - b1) * g;
+    const float vv = b2 * v[p] + (1.f - b2) * g * g;
+    m[p] = mm;
+    v[p] = vv;
+    w -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
+    params[p] = w;
+    if (mlp_img) mlp_pack_one(p, w, mlp_img);
+  }
+}
+
 // 16 threads per parameter (slab-split, all loads issued up front), 64 parameters per 1024-thread block.
 // The slab reduction is latency-bound (16 MB spread over 256 slabs): every thread keeps its 16
 // loads in flight at once.
@@ -79,8 +103,13 @@ __global__ void __launch_bounds__(AS_P * AS_G)
 adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, float grad_scale, float* __restrict__ params,
                  float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io, const float* __restrict__ hp,
                  int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img, const float* __restrict__ loss_slabs,
-                 float* __restrict__ loss_out, float loss_scale) {
+                 float* __restrict__ loss_out, float loss_scale, int* __restrict__ xg_hdr, float* __restrict__ xg_data,
+                 int xg_cap) {
   const int tstep = (mode != 1) ? adam_begin(state) : 0;
+  if (xg_hdr) {  // mode 1 producer for the xGMI all-reduce: [grad | loss] into this rank's next slot
+    grad_io = xg_produce_slot(xg_hdr, xg_data, xg_cap);
+    loss_out = grad_io + P;
+  }
   // hp = {lr, beta1, beta2, eps, weight_decay}; state = {step, ticket} (device ints, graph-replay safe)
   __shared__ float part[AS_G][AS_P];
   const int tx = threadIdx.x % AS_P, ty = threadIdx.x / AS_P;
@@ -117,26 +146,25 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
     if (ty == 0 && p < P) grad_io[p] = g;
     return;
   }
-  if (ty == 0 && p < P) {
-    const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
-    const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
-    if (mlp_img && mlp_pad_slot(p)) {
-      params[p] = 0.f;
-      m[p] = 0.f;
-      v[p] = 0.f;
-      mlp_pack_one(p, 0.f, mlp_img);
-    } else {
-      float w = params[p];
-      g += wd * w;
-      const float mm = b1 * m[p] + (1.f - b1) * g;
-      const float vv = b2 * v[p] + (1.f - b2) * g * g;
-      m[p] = mm;
-      v[p] = vv;
-      w -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
-      params[p] = w;
-      if (mlp_img) mlp_pack_one(p, w, mlp_img);
-    }
+  if (ty == 0 && p < P) adam_apply(p, g, tstep, params, m, v, hp, mlp_img);
+  adam_end(state, tstep);
+}
+
+// xGMI consumer (xgmi.h): g = sum over ranks of slot[s&1][p] (rank order), then the same Adam
+// update as mode 2.  Element P of the slot carries the loss.  256 threads, one parameter each.
+constexpr int AX_B = 256;
+__global__ void __launch_bounds__(AX_B)
+adam_xgmi_kernel(XgmiDesc d, int P, float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
+                 const float* __restrict__ hp, int* __restrict__ state, uint8_t* __restrict__ mlp_img,
+                 float* __restrict__ loss_out) {
+  const int s = xg_next_seq(d.my_hdr);
+  const int tstep = adam_begin(state);
+  if (xg_publish_and_wait(d, s)) {
+    const int p = blockIdx.x * AX_B + threadIdx.x;
+    if (p < P) adam_apply(p, xg_sum(d, s, p), tstep, params, m, v, hp, mlp_img);
+    else if (p == P && loss_out) loss_out[0] = xg_sum(d, s, P);
   }
+  xg_finish(d, s);
   adam_end(state, tstep);
 }
 
@@ -196,13 +224,31 @@ adam_flat_kernel(float* __restrict__ params, const float* __restrict__ grad, flo
 
 EM_API int em_adam_slab(const float* slabs, int nslab, int P, int stride, float grad_scale, float* params, float* m, float* v,
                         float* grad_io, const float* hp, int* state, int mode, void* mlp_img, const float* loss_slabs,
-                        float* loss_out, float loss_scale, hipStream_t stream) {
-  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0 || stride < P)) || (mode != 0 && !grad_io)) return EM_ERR_ARG;
+                        float* loss_out, float loss_scale, void* xgmi, hipStream_t stream) {
+  XgmiComm* xc = static_cast<XgmiComm*>(xgmi);
+  if (xc && (mode != 1 || xc->desc.cap < P + 1)) return EM_ERR_ARG;
+  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0 || stride < P)) || (mode != 0 && !grad_io && !xc)) return EM_ERR_ARG;
   if (mode != 1 && (!params || !m || !v || !hp || !state)) return EM_ERR_ARG;
   if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
   const int nb = (P + AS_P - 1) / AS_P;
   hipLaunchKernelGGL(adam_slab_kernel, dim3(nb), dim3(AS_P * AS_G), 0, stream, slabs, nslab, P, stride, grad_scale, params, m, v,
-                     grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale);
+                     grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale,
+                     xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// Adam step whose gradient is the xGMI all-reduce of every rank's slot (see xgmi.h);
+// loss_out (optional) receives the reduced element P.
+EM_API int em_adam_xgmi(void* xgmi, int P, float* params, float* m, float* v, const float* hp, int* state, void* mlp_img,
+                        float* loss_out, hipStream_t stream) {
+  XgmiComm* xc = static_cast<XgmiComm*>(xgmi);
+  if (!xc || !xc->connected || P <= 0 || xc->desc.cap < P + 1 || !params || !m || !v || !hp || !state) return EM_ERR_ARG;
+  if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
+  const int nb = (P + 1 + AX_B - 1) / AX_B;
+  if (nb > 256) return EM_ERR_ARG;  // consumer grid must stay co-resident (blocks spin on peer flags)
+  hipLaunchKernelGGL(adam_xgmi_kernel, dim3(nb), dim3(AX_B), 0, stream, xc->desc, P, params, m, v, hp, state,
+                     (uint8_t*)mlp_img, loss_out);
   EM_CHECK_LAUNCH();
   return 0;
 }

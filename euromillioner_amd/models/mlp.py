@@ -92,7 +92,7 @@ class FusedSmallMLP:
 
     def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
-                 state_dict: dict | None = None, process_group=None):
+                 state_dict: dict | None = None, process_group=None, comm: str = "auto"):
         from ..ops import fused_mlp as FM
         from ..ops import _native as N
 
@@ -124,6 +124,17 @@ class FusedSmallMLP:
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
         FM.pack(self.params, self.img)
         self._checked = False
+        # DP gradient all-reduce: "xgmi" = one-shot peer-memory reduction fused into the Adam
+        # kernel (parallel/xgmi.py), "rccl" = torch.distributed all_reduce between two Adam
+        # launches; "auto" = xgmi when the node supports it (verified collectively), else rccl.
+        if comm not in ("auto", "xgmi", "rccl"):
+            raise ValueError("comm must be auto, xgmi or rccl")
+        self.xgmi = None
+        if process_group is not None and comm != "rccl":
+            from ..parallel.xgmi import XgmiComm
+
+            self.xgmi = XgmiComm.create(process_group, dev, P + 1, required=(comm == "xgmi"))
+        self.comm = "xgmi" if self.xgmi is not None else ("rccl" if process_group is not None else "none")
 
     # ------------------------------------------------------------------ training
     @property
@@ -162,6 +173,12 @@ class FusedSmallMLP:
             FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=0,
                          img=self.img, loss_slabs=self.loss_slabs, loss_out=self.loss_out, loss_scale=lscale)
             return self.loss_out
+        if self.xgmi is not None:  # producer -> own xGMI slot; consumer = all-reduce + Adam, no host sync
+            FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=1,
+                         loss_slabs=self.loss_slabs, loss_scale=lscale, xgmi=self.xgmi.handle)
+            FM.adam_xgmi(self.xgmi.handle, self.params, self.m, self.v, self.hp, self.state, img=self.img,
+                         loss_out=self.loss_out)
+            return self.loss_out
         import torch.distributed as dist
 
         loss_view = self.grad_io[FM.P_TOTAL:]
@@ -171,6 +188,22 @@ class FusedSmallMLP:
         FM.adam_slab(None, 0, 1.0, self.params, self.m, self.v, self.hp, self.state, mode=2, grad_io=self.grad_io,
                      img=self.img)
         return loss_view
+
+    @property
+    def graph_safe(self) -> bool:
+        """True when a step has no host-side collective (single GPU or xGMI) -> hipGraph-replayable."""
+        return self.group is None or self.xgmi is not None
+
+    def check_comm(self) -> None:
+        """Raise if an xGMI wait timed out (synchronises)."""
+        if self.xgmi is not None:
+            self.xgmi.check()
+
+    def close(self) -> None:
+        if self.xgmi is not None:
+            torch.cuda.synchronize(self.device)
+            self.xgmi.close()
+            self.xgmi = None
 
     def grads(self, draws: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None):
         """(mean loss, flat gradient) without updating — for tests / gradient checks."""

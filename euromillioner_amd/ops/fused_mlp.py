@@ -141,7 +141,9 @@ def forward_logits(draws: torch.Tensor, B: int, img: torch.Tensor, out: torch.Te
 def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params: torch.Tensor, m: torch.Tensor,
               v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor, mode: int = 0, grad_io: torch.Tensor | None = None,
               img: torch.Tensor | None = None, loss_slabs: torch.Tensor | None = None,
-              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0) -> None:
+              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0, xgmi: int | None = None) -> None:
+    """mode 0: slab reduce + Adam; mode 1: slab reduce -> grad_io (or, with ``xgmi``, this rank's
+    next xGMI slot); mode 2: Adam from grad_io."""
     P = params.numel()
     stride = slabs.shape[1] if slabs is not None else P
     N.call("em_adam_slab", slabs.data_ptr() if slabs is not None else None, int(nslab), int(P), int(stride),
@@ -149,7 +151,18 @@ def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params:
            params.data_ptr(), m.data_ptr(), v.data_ptr(), grad_io.data_ptr() if grad_io is not None else None,
            hp.data_ptr(), state.data_ptr(), int(mode), img.data_ptr() if img is not None else None,
            loss_slabs.data_ptr() if loss_slabs is not None else None,
-           loss_out.data_ptr() if loss_out is not None else None, float(loss_scale), N.stream_handle(params.device))
+           loss_out.data_ptr() if loss_out is not None else None, float(loss_scale), xgmi,
+           N.stream_handle(params.device))
+
+
+def adam_xgmi(xgmi: int, params: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor,
+              state: torch.Tensor, img: torch.Tensor | None = None, loss_out: torch.Tensor | None = None) -> None:
+    """Adam step on the xGMI all-reduce (rank-order sum) of every rank's staged [grad | loss]."""
+    from ..parallel import xgmi as _xg  # noqa: F401  (registers the em_xgmi_* signatures)
+
+    N.call("em_adam_xgmi", xgmi, params.numel(), params.data_ptr(), m.data_ptr(), v.data_ptr(), hp.data_ptr(),
+           state.data_ptr(), img.data_ptr() if img is not None else None,
+           loss_out.data_ptr() if loss_out is not None else None, N.stream_handle(params.device))
 
 
 def adam_flat(params: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor,
