@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--model", default="mlp", choices=["mlp", "mlp-wide"],
                     help="mlp = 62->128->62 (headline, fused kernel); mlp-wide = 62->8192->8192->62 (GEMM path)")
     ap.add_argument("--hidden", default=None, help="GEMM-path hidden sizes, e.g. 8192,8192")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks sharing one GPU)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="DP gradient all-reduce of the fused path: xgmi = one-shot peer-memory reduction fused "
                          "into Adam (hipGraph-replayable); rccl = torch.distributed all_reduce; auto = xgmi if the "
@@ -109,6 +111,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(torch.cuda.device_count(), 1)  # (identity on a node with >= N GPUs)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
@@ -117,7 +120,10 @@ def main():
 
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", timeout=datetime.timedelta(minutes=10), device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", timeout=datetime.timedelta(minutes=10), device_id=dev)
+        else:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
         group = dist.group.WORLD
 
     from euromillioner_amd.data.synthetic import generate_draws
