@@ -34,6 +34,11 @@ bool getenv_flag(const char* name) {
   return v && v[0] == '1';
 }
 
+bool getenv_flag_off(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] == '0';
+}
+
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
 
 EM_DEVICE uint32_t kc_off(int row, int chunk) { return row * 128 + (((chunk ^ (row & 7))) << 4); }     // [128][64]
@@ -274,64 +279,14 @@ EM_DEVICE float g_dfn(float y) {  // activation derivative from the saved output
 // OUT_BF16: 1 -> bf16 C (optionally + transposed C^T when HAS_CT), 0 -> fp32 C (+ beta * C_old)
 // FN: activation (DACT = 0, applied to alpha*acc + bias) or activation' (DACT = 1, multiplies
 // alpha*acc by act'(mask[m][n]))
+// Epilogue shared by the 256x256 kernels: acc[4][2] = this wave's 128x64 tile (wm, wn) of the
+// block tile at (m0, n0); LDS (>= G_EPI_LDS bytes) is free when called.
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
-__global__ void __launch_bounds__(G_NT, 1)
-gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
-                  void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
-                  const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = N / G_BN;
-  const int nwg = (M / G_BM) * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
-  const int ktiles = K / G_BK;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
-  g_stage(pa, 0, smem, wave_s);
-  g_stage(pb, 0, smem + G_TILE, wave_s);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
+EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, int wm, int wn, int m0, int n0,
+                          void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
+                          const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                          float beta) {
   const int r = lane & 31, h = lane >> 5;
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const char* la = smem + (kt & 1) * 2 * G_TILE;
-    const char* lb = la + G_TILE;
-    if (kt + 1 < ktiles) {
-      char* na = smem + ((kt + 1) & 1) * 2 * G_TILE;
-      g_stage(pa, (kt + 1) * G_BK, na, wave_s);
-      g_stage(pb, (kt + 1) * G_BK, na + G_TILE, wave_s);
-    }
-#pragma unroll
-    for (int s = 0; s < G_BK / 16; ++s) {
-      bf16x8 a[4], b[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + 32 * i + r, 2 * s + h));
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + 32 * j + r, 2 * s + h));
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- epilogue, one 32-row block of this wave's 128x64 tile at a time ----
   // bf16 outputs go through a per-wave transposed LDS tile T[64 cols][32 rows] (ds_write_b64 of 4
   // consecutive rows per lane), then leave as 16-B coalesced stores: C rows via ds_read_b64_tr_b16
   // pairs (8 consecutive columns of one row), C^T rows straight from T.  DACT stages the matching
@@ -414,13 +369,239 @@ gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
 }
 
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+__global__ void __launch_bounds__(G_NT, 1)
+gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                  void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
+                  const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                  float beta) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = N / G_BN;
+  const int nwg = (M / G_BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  const int ktiles = K / G_BK;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
+  g_stage(pa, 0, smem, wave_s);
+  g_stage(pb, 0, smem + G_TILE, wave_s);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int r = lane & 31, h = lane >> 5;
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const char* la = smem + (kt & 1) * 2 * G_TILE;
+    const char* lb = la + G_TILE;
+    if (kt + 1 < ktiles) {
+      char* na = smem + ((kt + 1) & 1) * 2 * G_TILE;
+      g_stage(pa, (kt + 1) * G_BK, na, wave_s);
+      g_stage(pb, (kt + 1) * G_BK, na + G_TILE, wave_s);
+    }
+#pragma unroll
+    for (int s = 0; s < G_BK / 16; ++s) {
+      bf16x8 a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + 32 * i + r, 2 * s + h));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + 32 * j + r, 2 * s + h));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
+                                         alpha, beta);
+}
+
+// ============================================================================================
+// 256x256 NT GEMM, ping-pong schedule (default large-shape path; the kernel above stays behind
+// EM_GEMM_PP=0 for A/B).  Same tile, waves, LDS image and epilogue; the K loop is restructured so
+// that the two waves sharing each SIMD alternate roles (cdna_hip_programming.md §5 "256² 8-phase
+// template", MI355X_MICROARCH.md "Two waves per SIMD"):
+//   * G0 = waves 0-3 (A rows 0-127), G1 = waves 4-7 (A rows 128-255); G1 starts one barrier late,
+//     so in every barrier interval ("slot") one group runs MFMAs while the other reads fragments
+//     and issues staging -> matrix work beside memory work on every SIMD.
+//   * a phase = one 64x32 quadrant of the wave's 128x64 tile over one K-tile (8 MFMA 32x32x16);
+//     quadrants qn-major: (qm, qn) = (0,0) (1,0) (0,1) (1,1), the B fragments of (0,qn) are reused
+//     by (1,qn) (40 instead of 48 ds_read_b128 per wave per K-tile).
+//   * LDS holds 2 K-tiles (64 KB each: A 32 KB | B 32 KB).  A K-tile is staged as 8 units of 64 rows
+//     (8 KB: 2 buffer_load...lds per thread of ONE group): A0..A3 = A rows 64u.., and B units by
+//     the quadrant half they feed: B(lo, p) = rows {(2p+b)*64 + 0..31}, B(hi, p) = {(2p+b)*64 + 32..63}.
+//   * one unit per slot; unit of K-tile kt issued in slot 8kt + o: B(lo,0) -12, B(lo,1) -11, A0 -10,
+//     A2 -9, A1 -8, A3 -7, B(hi,0) -6, B(hi,1) -5 (residue r = slot & 7 picks the unit).
+//     Each load segment issues its unit then waits vmcnt(6): the unit its group issued 3 load
+//     segments (6 slots) earlier has landed, and becomes readable after the barrier that follows.
+//   Hazards (slot numbers relative to 8kt; G0 reads phase g in slot 2g-1, G1 in slot 2g):
+//     RAW: unit issued at o is readable from o+7 <= its first read (B lo -1, A0 -1, A2 0, A1 1,
+//          A3 2, B hi 3).
+//     WAR: the same unit of K-tile kt-2 was last read at (B lo 2, A0 3, A2 4, A1 5, A3 6, B hi 4)-16;
+//          each reader retires its reads (lgkmcnt(0)) before the barrier that ends its next slot,
+//          so a restage 2 slots after the last read is safe: every o above is >= last + 2 - 16.
+__device__ __forceinline__ void pp_stage_unit(const GPanel& g, int k0, char* lds_op, int first_grp, bool split_b,
+                                               int hsel, int pair, int wi) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = 2 * wi + i;  // this wave's row-group of the unit's 8
+    const int grp = split_b ? (2 * pair + (j >> 2)) * 8 + hsel * 4 + (j & 3) : first_grp + j;
+    const uint32_t soff = (uint32_t)(grp * 8) * g.row_bytes + (uint32_t)k0 * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rsrc, (EM_LDS void*)(lds_op + grp * 1024), 16, g.voff[grp & 1], soff,
+                                             0, 0);
+  }
+}
+
+// issue the unit scheduled for slot s (wave-uniform); false when it belongs past the last K-tile
+__device__ __forceinline__ bool pp_stage_slot(const GPanel& pa, const GPanel& pb, char* smem, int s, int ktiles,
+                                               int wi) {
+  const int r = s & 7, w = s >> 3;  // arithmetic shift: s = -1 -> w = -1, r = 7
+  const int kt = w + (r < 4 ? 1 : 2);
+  if (kt >= ktiles) return false;
+  char* buf = smem + (kt & 1) * 2 * G_TILE;
+  const int k0 = kt * G_BK;
+  switch (r) {
+    case 0: pp_stage_unit(pa, k0, buf, 8, false, 0, 0, wi); break;            // A1
+    case 1: pp_stage_unit(pa, k0, buf, 24, false, 0, 0, wi); break;           // A3
+    case 2: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 1, 0, wi); break;    // B(hi,0)
+    case 3: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 1, 1, wi); break;    // B(hi,1)
+    case 4: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 0, 0, wi); break;    // B(lo,0)
+    case 5: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 0, 1, wi); break;    // B(lo,1)
+    case 6: pp_stage_unit(pa, k0, buf, 0, false, 0, 0, wi); break;            // A0
+    default: pp_stage_unit(pa, k0, buf, 16, false, 0, 0, wi); break;          // A2
+  }
+  return true;
+}
+
+template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+__global__ void __launch_bounds__(G_NT, 1)
+gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                  void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
+                  const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                  float beta) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = N / G_BN;
+  const int nwg = (M / G_BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  const int ktiles = K / G_BK;
+  const int nph = 4 * ktiles;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int wi = wave_s & 3;
+  const bool g1 = wave_s >= 4;
+  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
+  // prologue: K-tile 0 by all waves, then the K-tile-1 units of slots -4 (G1), -3 (G0), -2 (G1)
+  g_stage(pa, 0, smem, wave_s);
+  g_stage(pb, 0, smem + G_TILE, wave_s);
+  if (g1) {
+    const bool a = pp_stage_slot(pa, pb, smem, -4, ktiles, wi);
+    const bool b = pp_stage_slot(pa, pb, smem, -2, ktiles, wi);
+    if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (pp_stage_slot(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8 fa[2][4], fb[4];
+  // load segment of phase g (slot `slot`): fragments for phase g (if any), stage, wait, barrier
+  auto load_seg = [&](int g, int slot) {
+    if (g < nph) {
+      const int kt = g >> 2, q = g & 3, qm = q & 1, qn = q >> 1;
+      const char* la = smem + (kt & 1) * 2 * G_TILE;
+      const char* lb = la + G_TILE;
+      if (qm == 0) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) fb[ks] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + qn * 32 + r, 2 * ks + h));
+      }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          fa[ii][ks] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + qm * 64 + 32 * ii + r, 2 * ks + h));
+    }
+    if (pp_stage_slot(pa, pb, smem, slot, ktiles, wi)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // MFMA segment of phase g: quadrant (qm, qn) += A frags x B frags over the K-tile
+  auto mfma_seg = [&](int q) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        f32x16& c = acc[2 * (q & 1) + ii][q >> 1];
+        c = mfma32(fa[ii][ks], fb[ks], c);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if (!g1) {
+    load_seg(0, -1);
+    for (int kt = 0; kt < ktiles; ++kt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int g = 4 * kt + q;
+        mfma_seg(q);
+        load_seg(g + 1, 2 * g + 1);
+      }
+    }
+  } else {
+    __builtin_amdgcn_s_barrier();  // the stagger: G1 sits out slot -1
+    for (int kt = 0; kt < ktiles; ++kt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int g = 4 * kt + q;
+        load_seg(g, 2 * g);
+        mfma_seg(q);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
+                                         alpha, beta);
+}
+
+template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
              int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
              int64_t ldm, float alpha, float beta) {
   static bool attr = false;
-  auto kern = gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
+  static const bool pp = !getenv_flag_off("EM_GEMM_PP");
+  auto kern = pp ? gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT> : gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     attr = true;
   }
   hipLaunchKernelGGL(kern, grid, dim3(G_NT), G_LDS, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm,

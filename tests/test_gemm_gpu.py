@@ -263,3 +263,23 @@ def test_identity_a_asymmetric_b(M, N, K, big):
     y = LIN.linear_fwd(LIN.aligned(a), LIN.aligned(w), None, "none", torch.float32)
     ref = a @ w.t()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("M,N", [(256, 256), (768, 512), (2048, 1024)])
+def test_big_nt_schedule_race_screen(M, N):
+    """The 256x256 ping-pong K loop (gemm.hip gemm256_pp_kernel) at 1..40 K-tiles: every tail of its
+    staging schedule, fp32 output vs the fp32 product of the same bf16 operands, and bitwise
+    repeatable over 8 launches (a mis-ordered LDS-DMA read shows up as a non-repeatable tile)."""
+    from euromillioner_amd.ops import linear as LIN
+
+    for K in (64, 128, 192, 320, 2560):
+        assert LIN.big_ok(M, N, K)
+        g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+        x = torch.rand(M, K, device="cuda", generator=g).mul(2).sub(1).bfloat16()
+        w = torch.rand(N, K, device="cuda", generator=g).mul(2).sub(1).bfloat16()
+        ref = x.double() @ w.double().t()
+        first = LIN.linear_fwd(x, w, None, "none", torch.float32)
+        assert float((first.double() - ref).abs().max()) < 1e-4 * K ** 0.5, (M, N, K)
+        for _ in range(7):
+            again = LIN.linear_fwd(x, w, None, "none", torch.float32)
+            assert torch.equal(again, first), (M, N, K)
