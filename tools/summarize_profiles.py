@@ -58,7 +58,9 @@ def main():
                 f.write(json.dumps(j) + "\n")
     f1 = pmc("fused_pmc", "mlp_fused_train")
     f2 = pmc("fused_pmc2", "mlp_fused_train")
-    w = pmc("wide_pmc", "gemm256_nt_kernel<1, 1, 0, 0>")
+    w = pmc("wide_pmc", "gemm256_pp_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_nt_kernel<1, 1, 0, 0>")
+    wcyc = w.get("GRBM_GUI_ACTIVE", 0) / 8.0
+    w_busy = w.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(1.0, 1024 * wcyc) if wcyc else float("nan")
     head = last_json("bench_headline.log")[-1]
     torch_b = last_json("bench_torch.log")[-1]
     wide = last_json("bench_wide.log")[-1]
@@ -97,8 +99,8 @@ def main():
         "",
         stats_table("wide", 12),
         "",
-        f"256x256 NT GEMM (forward 8192^2 layer) PMC: MFMA busy cycles {w.get('SQ_VALU_MFMA_BUSY_CYCLES', 0):.3g}, "
-        f"FETCH_SIZE {w.get('FETCH_SIZE', 0):.3g} KB",
+        f"256x256 ping-pong GEMM (8192^2 layer, per dispatch) PMC: MFMA busy {w_busy:.2f} of SIMD-cycles, "
+        f"{w.get('SQ_INSTS_MFMA', 0):.3g} MFMA insts, FETCH_SIZE {w.get('FETCH_SIZE', 0) / 1024:.0f} MB",
         "",
         "GEMM micro-benchmark vs torch.matmul (hipBLASLt), same GPU: see `gemm_bench.jsonl`.",
         "",
@@ -106,7 +108,7 @@ def main():
         "",
         stats_table("rf", 6),
         "",
-        "## GBDT (reference config: 500 rounds x 62 boosters, depth 3)",
+        "## GBDT (tools/gbdt_bench.py: reference config 500 rounds x 62 boosters on ~930 rows, then 50 rounds on 183k synthetic rows; depth 3)",
         "",
         stats_table("gbdt", 10),
         "",
