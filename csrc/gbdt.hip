@@ -90,159 +90,196 @@ __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restr
   }
 }
 
-// grid (nchunks, T, nftiles); block = FT threads (one per feature of the tile, padded to 64)
-// partial: [nchunks][T][nodesL][F][NB][2]
-__global__ void gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
-                          const int16_t* __restrict__ node, double* __restrict__ partial, int T, int n, int F, int NB,
-                          int level, int chunk, int FT) {
+// ---------------------------------------------------------------- K8 histogram (compact cells)
+// Cells: feature f owns bins [foff[f], foff[f+1]) of a compact axis of C = foff[F] cells (a one-hot
+// lag feature has 2 cells, "day" 31 ...), so a (task, node) histogram of the reference features is
+// ~200 cells (3 KB of double pairs) instead of F x max_bins.
+// Work split (deterministic, no atomics): block = (row chunk, task, tile); tile = FT features x NTn
+// nodes.  Thread (p, fl) owns feature f0 + fl for the p-th contiguous sub-range of the chunk's rows
+// and accumulates its private LDS copy in row order; the P copies are folded in p order and the
+// chunks by gbdt_chunk_reduce in chunk order.  Two features that induce the same partition of the
+// rows therefore get bit-identical sums (exact gain ties keep breaking towards the lower feature).
+// Per row a thread does one 16-B LDS read-modify-write; the chain is latency-bound per thread and is
+// hidden by occupancy: the tile plan keeps the LDS footprint <= ~48 KB (3+ blocks per CU).
+constexpr int HIST_MAX_CHUNK = 1024;
+constexpr int HIST_LDS_BUDGET = 36 * 1024;  // per-block histogram copies (+ 10 B/row staging)
+
+__global__ void __launch_bounds__(256)
+gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
+          const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
+          int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* hist = reinterpret_cast<double*>(smem);  // sums in double, like XGBoost's GradStats
   const int nodesL = 1 << level, first = nodesL - 1;
-  const int c = blockIdx.x, t = blockIdx.y, f0 = blockIdx.z * FT;
-  const int fl = threadIdx.x, f = f0 + fl;
-  const int per = nodesL * NB * 2;
-  const bool active = fl < FT && f < F;
-  if (active)
-    for (int i = 0; i < per; ++i) hist[fl * per + i] = 0.0;
+  const int c = blockIdx.x, t = blockIdx.y;
+  const int nft = (F + FT - 1) / FT;
+  const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
+  const int f0 = ft * FT, f1 = min(F, f0 + FT), n0 = nt * NTn;
+  const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
+  double* hist = reinterpret_cast<double*>(smem);  // [P][NTn][ldsC][2]
+  const int per = NTn * ldsC * 2;
+  for (int i = threadIdx.x; i < P * per; i += blockDim.x) hist[i] = 0.0;
   const int r0 = c * chunk, r1 = min(n, r0 + chunk);
-  // the chunk's per-row (node, g, h) are shared by every feature thread: stage them in LDS once
-  // (coalesced), after the per-thread histograms (chunk <= 1024 rows -> 12 KB)
-  float* sg = reinterpret_cast<float*>(smem + (size_t)FT * per * sizeof(double));
+  float* sg = reinterpret_cast<float*>(smem + (size_t)P * per * sizeof(double));
   float* sh = sg + chunk;
   int16_t* sn = reinterpret_cast<int16_t*>(sh + chunk);
   const int64_t base = (int64_t)t * n;
   for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
     sg[r - r0] = g[base + r];
     sh[r - r0] = h[base + r];
-    sn[r - r0] = (int16_t)(node[base + r] - first);
+    sn[r - r0] = (int16_t)(node[base + r] - first - n0);  // tile-relative node (outside -> skipped)
   }
   __syncthreads();
-  if (active) {
-    double* my = hist + fl * per;
-    int r = r0;
-    // 8 rows per step: the 8 bin loads are issued before any update (memory-level parallelism);
-    // the updates stay in row order, so the sums are bitwise those of the plain loop
-    for (; r + 8 <= r1; r += 8) {
+  const int nth = f1 - f0;
+  const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
+  if (p < P) {
+    const int f = f0 + fl;
+    double* my = hist + (size_t)p * per + (foff[f] - c0) * 2;
+    const int len = r1 - r0, sub = (len + P - 1) / P;
+    const int a0 = min(len, p * sub), a1 = min(len, a0 + sub);
+    const uint8_t* col = bins + (int64_t)r0 * F + f;
+    int r = a0;
+    // 8 bin loads in flight, then the 8 updates in row order (sums bitwise = the plain loop)
+    for (; r + 8 <= a1; r += 8) {
       int b[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) b[u] = bins[(int64_t)(r + u) * F + f];
+      for (int u = 0; u < 8; ++u) b[u] = col[(int64_t)(r + u) * F];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int nd = sn[r + u - r0];
-        if (nd < 0 || nd >= nodesL) continue;
-        double* e = my + (nd * NB + b[u]) * 2;
-        e[0] += (double)sg[r + u - r0];
-        e[1] += (double)sh[r + u - r0];
+        const int nd = sn[r + u];
+        if ((unsigned)nd >= (unsigned)NTn) continue;
+        double* e = my + (nd * ldsC + b[u]) * 2;
+        e[0] += (double)sg[r + u];
+        e[1] += (double)sh[r + u];
       }
     }
-    for (; r < r1; ++r) {
-      const int nd = sn[r - r0];
-      if (nd < 0 || nd >= nodesL) continue;
-      const int b = bins[(int64_t)r * F + f];
-      double* e = my + (nd * NB + b) * 2;
-      e[0] += (double)sg[r - r0];
-      e[1] += (double)sh[r - r0];
+    for (; r < a1; ++r) {
+      const int nd = sn[r];
+      if ((unsigned)nd >= (unsigned)NTn) continue;
+      double* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
+      e[0] += (double)sg[r];
+      e[1] += (double)sh[r];
     }
   }
   __syncthreads();
-  if (active) {
-    double* out = partial + ((int64_t)c * T + t) * (int64_t)nodesL * F * NB * 2;
-    for (int nd = 0; nd < nodesL; ++nd)
-      for (int b = 0; b < NB; ++b) {
-        const double* e = hist + fl * per + (nd * NB + b) * 2;
-        double* o = out + (((int64_t)nd * F + f) * NB + b) * 2;
-        o[0] = e[0];
-        o[1] = e[1];
-      }
+  // fold the P copies (p order) and write this chunk's cells: partial [nchunks][T][nodesL][C][2]
+  double* out = partial + ((int64_t)c * T + t) * (int64_t)nodesL * C * 2;
+  const int nn = min(NTn, nodesL - n0);
+  for (int i = threadIdx.x; i < nn * Ct; i += blockDim.x) {
+    const int nd = i / Ct, cc = i - nd * Ct;
+    double sgv = 0.0, shv = 0.0;
+    for (int q = 0; q < P; ++q) {
+      const double* e = hist + (size_t)q * per + (nd * ldsC + cc) * 2;
+      sgv += e[0];
+      shv += e[1];
+    }
+    double* o = out + ((int64_t)(n0 + nd) * C + c0 + cc) * 2;
+    o[0] = sgv;
+    o[1] = shv;
   }
 }
 
-// one 64-thread block per (task, node of this level)
-// G/H: [T][NN] node totals (in: this level's nodes; out: their children)
-__global__ void gbdt_split(const double* __restrict__ partial, int nchunks, int T, int F, int NB, int level, int NN,
-                           double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
-                           int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam,
-                           double mcw) {
+// fold the per-chunk histograms into chunk 0 in chunk order (single-GPU and DP paths alike)
+__global__ void gbdt_chunk_reduce(double* __restrict__ partial, int nchunks, int64_t S) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S; e += (int64_t)gridDim.x * blockDim.x) {
+    double acc = partial[e];
+    for (int c = 1; c < nchunks; ++c) acc += partial[(int64_t)c * S + e];
+    partial[e] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- K9 split scan
+// one block (64..256 threads) per (task, node of this level).  hist: [T][nodesL][C][2] (folded).
+// Thread <-> feature: a sequential left-sum over the feature's bins (bin order), XGBoost loss_chg
+// at every candidate "bin <= b", first maximum kept; then a block arg-max where the larger gain
+// wins and equal gains go to the lower feature == numpy's first argmax in (feature, bin) order.
+__global__ void __launch_bounds__(256)
+gbdt_split(const double* __restrict__ hist, const int* __restrict__ foff, int T, int F, int C, int level, int NN,
+           double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status, int16_t* __restrict__ feat,
+           uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw) {
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
-  const int lane = threadIdx.x;
   int8_t* st = status + (int64_t)t * NN;
-  if (st[i] != 2) return;
-  const int64_t tstride = (int64_t)nodesL * F * NB * 2;
-  // node totals: the root sums feature 0 over all bins; other nodes were set by the parent split
-  double Gn, Hn;
-  if (level == 0) {
-    double sg = 0.0, sh = 0.0;
-    for (int b = lane; b < NB; b += 64)
-      for (int c = 0; c < nchunks; ++c) {
-        const double* e = partial + ((int64_t)c * T + t) * tstride + ((int64_t)0 * NB + b) * 2;
-        sg += e[0];
-        sh += e[1];
+  if (st[i] != 2) return;  // block-uniform
+  const double* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
+  __shared__ double sGn[2];
+  __shared__ double rv[4];
+  __shared__ int rf[4], rb[4];
+  __shared__ double rgl[4], rhl[4];
+  if (threadIdx.x == 0) {
+    double Gn, Hn;
+    if (level == 0) {  // root totals: feature 0's cells in bin order
+      Gn = 0.0;
+      Hn = 0.0;
+      for (int c = foff[0]; c < foff[1]; ++c) {
+        Gn += hs[2 * c];
+        Hn += hs[2 * c + 1];
       }
-    Gn = wave_sum_d(sg);
-    Hn = wave_sum_d(sh);
-    if (lane == 0) {
       G[(int64_t)t * NN] = Gn;
       H[(int64_t)t * NN] = Hn;
+    } else {
+      Gn = G[(int64_t)t * NN + i];
+      Hn = H[(int64_t)t * NN + i];
     }
-  } else {
-    Gn = G[(int64_t)t * NN + i];
-    Hn = H[(int64_t)t * NN + i];
+    sGn[0] = Gn;
+    sGn[1] = Hn;
   }
+  __syncthreads();
+  const double Gn = sGn[0], Hn = sGn[1];
   const double root = Gn * Gn / (Hn + lam);
   double best = -INFINITY, bGL = 0.0, bHL = 0.0;
-  int bf = -1, bb = 0;
-  for (int f = 0; f < F; ++f) {
-    double carry_g = 0.0, carry_h = 0.0;
-    for (int b0 = 0; b0 < NB; b0 += 64) {
-      const int b = b0 + lane;
-      double hg = 0.0, hh = 0.0;
-      if (b < NB)
-        for (int c = 0; c < nchunks; ++c) {
-          const double* e = partial + ((int64_t)c * T + t) * tstride + (((int64_t)nd * F + f) * NB + b) * 2;
-          hg += e[0];
-          hh += e[1];
-        }
-      // inclusive prefix scan across the wave
-      double sg = hg, sh = hh;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double ug = __shfl_up(sg, o), uh = __shfl_up(sh, o);
-        if (lane >= o) {
-          sg += ug;
-          sh += uh;
-        }
-      }
-      const double GL = carry_g + sg, HL = carry_h + sh;
+  int bf = 0x7fffffff, bb = 0;
+  for (int f = threadIdx.x; f < F; f += blockDim.x) {
+    const int ca = foff[f], cb = foff[f + 1];
+    double GL = 0.0, HL = 0.0;
+    for (int c = ca; c < cb - 1; ++c) {  // the last bin is never a candidate (nothing to its right)
+      GL += hs[2 * c];
+      HL += hs[2 * c + 1];
       const double GR = Gn - GL, HR = Hn - HL;
-      double gn = -INFINITY;
-      if (b < NB - 1 && HL >= mcw && HR >= mcw) gn = GL * GL / (HL + lam) + GR * GR / (HR + lam) - root;
-      // wave arg-max: larger gain wins; ties -> lower bin (lane)
-      double bv = gn;
-      int bl = lane;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(bv, o);
-        const int ol = __shfl_xor(bl, o);
-        if (ov > bv || (ov == bv && ol < bl)) {
-          bv = ov;
-          bl = ol;
+      if (HL >= mcw && HR >= mcw) {
+        const double gn = GL * GL / (HL + lam) + GR * GR / (HR + lam) - root;
+        if (gn > best) {  // strict: the lower bin of this feature keeps ties
+          best = gn;
+          bf = f;
+          bb = c - ca;
+          bGL = GL;
+          bHL = HL;
         }
       }
-      const double wGL = __shfl(GL, bl), wHL = __shfl(HL, bl);
-      if (bv > best) {  // strict: earlier (feature, bin) wins ties
-        best = bv;
-        bf = f;
-        bb = b0 + bl;
-        bGL = wGL;
-        bHL = wHL;
-      }
-      carry_g = __shfl(GL, 63);
-      carry_h = __shfl(HL, 63);
+    }
+  }
+  // block arg-max: larger gain, then lower feature (a thread's features ascend with its loop)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(best, o), ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
+    const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o);
+    if (ov > best || (ov == best && of < bf)) {
+      best = ov;
+      bf = of;
+      bb = ob;
+      bGL = ogl;
+      bHL = ohl;
     }
   }
   if (lane == 0) {
-    if (bf >= 0 && best > KRT_EPS) {
+    rv[w] = best;
+    rf[w] = bf;
+    rb[w] = bb;
+    rgl[w] = bGL;
+    rhl[w] = bHL;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int k = 1; k < nw; ++k)
+      if (rv[k] > best || (rv[k] == best && rf[k] < bf)) {
+        best = rv[k];
+        bf = rf[k];
+        bb = rb[k];
+        bGL = rgl[k];
+        bHL = rhl[k];
+      }
+    if (bf < F && best > KRT_EPS) {
       st[i] = 1;
       feat[(int64_t)t * NN + i] = (int16_t)bf;
       sbin[(int64_t)t * NN + i] = (uint8_t)bb;
@@ -377,30 +414,35 @@ gbdt_metric(const float* __restrict__ margin, const float* __restrict__ Y, int T
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-__global__ void gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int metric,
-                                  float* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// fixed-order block reduction of the per-block metric partials (256 threads: strided sequential
+// sums, then a tree) -- deterministic, and ~50x faster than one thread walking 4096 doubles
+EM_DEVICE double block_sum_partials(const double* __restrict__ partial, int nb) {
+  __shared__ double red[256];
   double s = 0.0;
-  for (int i = 0; i < nb; ++i) s += partial[i];
-  double v = s / (double)(count > 0 ? count : 1);
-  if (metric == MET_RMSE) v = sqrt(v);
-  out[0] = (float)v;
+  for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  return red[0];
 }
 
-// DP path: fold the per-chunk partial histograms into chunk 0 (fixed order), ready for an all-reduce
-__global__ void gbdt_chunk_reduce(double* __restrict__ partial, int nchunks, int64_t S) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S; e += (int64_t)gridDim.x * blockDim.x) {
-    double acc = 0.0;
-    for (int c = 0; c < nchunks; ++c) acc += partial[(int64_t)c * S + e];
-    partial[e] = acc;
+__global__ void __launch_bounds__(256)
+gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int metric, float* __restrict__ out) {
+  const double s = block_sum_partials(partial, nb);
+  if (threadIdx.x == 0) {
+    double v = s / (double)(count > 0 ? count : 1);
+    if (metric == MET_RMSE) v = sqrt(v);
+    out[0] = (float)v;
   }
 }
 
-__global__ void gbdt_metric_sum(const double* __restrict__ partial, int nb, double* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < nb; ++i) s += partial[i];
-  out[0] = s;
+__global__ void __launch_bounds__(256)
+gbdt_metric_sum(const double* __restrict__ partial, int nb, double* __restrict__ out) {
+  const double s = block_sum_partials(partial, nb);
+  if (threadIdx.x == 0) out[0] = s;
 }
 
 inline int grid_for(int64_t total, int bs = 256) {
@@ -411,6 +453,81 @@ inline int grid_for(int64_t total, int bs = 256) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ host-side histogram plan
+namespace {
+struct HistPlan {
+  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads;
+  size_t lds;
+};
+
+// Tile plan of one level: widest feature tile (then fewest node tiles) whose P private copies fit
+// the LDS budget; P (row phases, 1..4) fills a 256-thread block when F is small.  Chunks are sized
+// so a level launches ~4096 blocks (all 256 CUs busy even for the reference's ~930 rows).
+bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
+  const int nodesL = 1 << level;
+  for (int NTn = nodesL; NTn >= 1; NTn >>= 1) {
+    for (int FT = F < 256 ? F : 256;; FT = (FT + 1) / 2) {
+      int maxC = 0;
+      for (int f0 = 0; f0 < F; f0 += FT) {
+        const int f1 = f0 + FT < F ? f0 + FT : F;
+        maxC = foff[f1] - foff[f0] > maxC ? foff[f1] - foff[f0] : maxC;
+      }
+      int P = 256 / FT;
+      P = P > 4 ? 4 : (P < 1 ? 1 : P);
+      for (; P >= 1; --P)
+        if ((int64_t)P * NTn * maxC * 16 <= HIST_LDS_BUDGET) break;
+      if (P >= 1) {
+        pl.FT = FT;
+        pl.NTn = NTn;
+        pl.P = P;
+        pl.ldsC = maxC;
+        pl.nft = (F + FT - 1) / FT;
+        pl.ntn = nodesL / NTn;
+        pl.threads = ((FT * P + 63) / 64) * 64;
+        const int64_t per_chunk = (int64_t)T * pl.nft * pl.ntn;
+        const int64_t want = (4096 + per_chunk - 1) / per_chunk;
+        int64_t chunk = (n + want - 1) / want;
+        chunk = chunk < 64 ? 64 : (chunk > HIST_MAX_CHUNK ? HIST_MAX_CHUNK : chunk);
+        pl.chunk = (int)chunk;
+        pl.nchunks = (int)((n + chunk - 1) / chunk);
+        pl.lds = (size_t)P * NTn * maxC * 16 + (((size_t)chunk * 10 + 15) & ~(size_t)15);
+        return true;
+      }
+      if (FT == 1) break;
+    }
+  }
+  return false;
+}
+
+int64_t partial_need(int level, int n, int T, int F, const int* foff) {
+  HistPlan pl;
+  if (!plan_hist(level, n, T, F, foff, pl)) return -1;
+  return (int64_t)pl.nchunks * T * (1 << level) * foff[F] * 2;
+}
+
+// K8 for one level: per-chunk histograms, then folded into partial[0 : T*nodesL*C*2]
+int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
+                      int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
+                      hipStream_t stream) {
+  HistPlan pl;
+  if (!plan_hist(level, n, T, F, foff_h, pl)) return EM_ERR_ARG;
+  const int C = foff_h[F];
+  const int64_t S = (int64_t)T * (1 << level) * C * 2;
+  if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
+  hipLaunchKernelGGL(gbdt_hist, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g, h,
+                     node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC);
+  if (pl.nchunks > 1) hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
+  return 0;
+}
+
+bool valid_foff(const int* foff, int F) {
+  if (!foff || foff[0] != 0) return false;
+  for (int f = 0; f < F; ++f)
+    if (foff[f + 1] - foff[f] < 1 || foff[f + 1] - foff[f] > 256) return false;
+  return true;
+}
+}  // namespace
+
 // ------------------------------------------------------------------ C ABI
 struct EmGbdtEval {
   const uint8_t* bins;  // [n][F]
@@ -419,21 +536,34 @@ struct EmGbdtEval {
   int n;
 };
 
+// doubles of histogram scratch the driver needs (max over the levels of a depth-D tree); -1 = unsupported
+EM_API int64_t em_gbdt_partial_doubles(int n, int T, int F, const int* foff, int max_depth) {
+  if (n <= 0 || T <= 0 || F <= 0 || max_depth < 1 || max_depth > 12 || !valid_foff(foff, F)) return -1;
+  int64_t need = 0;
+  for (int l = 0; l < max_depth; ++l) {
+    const int64_t v = partial_need(l, n, T, F, foff);
+    if (v < 0) return -1;
+    need = v > need ? v : need;
+  }
+  return need;
+}
+
 // Trains rounds [r0, r1).  Tree arrays hold ALL rounds: [R*T][NN] (tree k = round*T + task).
-// scratch: g, h [T][n]; node int16 [T][n]; partial (see gbdt_hist); G, H [T][NN]; mpart double[4096]
+// foff_h / foff_d: feature -> first compact histogram cell, [F+1] (host copy for the plan, device copy
+// for the kernels); feature f has foff[f+1]-foff[f] bins.
+// scratch: g, h [T][n]; node int16 [T][n]; partial (em_gbdt_partial_doubles); G, H [T][NN]; mpart double[4096]
 // hist_out: float [R][1 + n_evals] (metric of train + each eval set after each round)
-EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB, int T, float* margin,
-                       const EmGbdtEval* evals, int n_evals, int r0, int r1, int max_depth, int obj, int metric,
-                       float eta, float lam, float gamma, float mcw, float subsample, uint32_t seed, float* g, float* h,
-                       int16_t* node, double* partial, int64_t partial_doubles, double* Gs, double* Hs, double* mpart,
-                       int8_t* status, int16_t* feat, uint8_t* sbin, float* leaf, float* gainv, float* cover,
-                       float* hist_out, hipStream_t stream) {
-  if (!bins || !Y || !margin || n <= 0 || F <= 0 || NB < 1 || NB > 256 || T <= 0 || max_depth < 1 ||
+EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const int* foff_h, const int* foff_d, int T,
+                       float* margin, const EmGbdtEval* evals, int n_evals, int r0, int r1, int max_depth, int obj,
+                       int metric, float eta, float lam, float gamma, float mcw, float subsample, uint32_t seed,
+                       float* g, float* h, int16_t* node, double* partial, int64_t partial_doubles, double* Gs,
+                       double* Hs, double* mpart, int8_t* status, int16_t* feat, uint8_t* sbin, float* leaf,
+                       float* gainv, float* cover, float* hist_out, hipStream_t stream) {
+  if (!bins || !Y || !margin || n <= 0 || F <= 0 || !valid_foff(foff_h, F) || !foff_d || T <= 0 || max_depth < 1 ||
       max_depth > 12 || r0 < 0 || r1 < r0)
     return EM_ERR_ARG;
   const int NN = (1 << (max_depth + 1)) - 1;
-  const int chunk = 1024;
-  const int nchunks = (n + chunk - 1) / chunk;
+  const int C = foff_h[F];
   const int64_t TN = (int64_t)T * n;
   for (int round = r0; round < r1; ++round) {
     int8_t* st = status + (int64_t)round * T * NN;
@@ -448,19 +578,11 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
                        seed, round);
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
-      // feature tile so that FT * nodesL * NB * 2 floats fit in 64 KB of LDS
-      int FT = (int)((65536 - 10240) / ((int64_t)nodesL * NB * 2 * 8));  // + 10 KB row staging <= 64 KB
-      if (FT > F) FT = F;
-      if (FT > 256) FT = 256;
-      if (FT < 1) return EM_ERR_ARG;  // nodesL * NB too large for one thread's LDS slice
-      const int64_t need = (int64_t)nchunks * T * nodesL * F * NB * 2;
-      if (need > partial_doubles) return EM_ERR_ARG;
-      const int nft = (F + FT - 1) / FT;
-      const int threads = ((FT + 63) / 64) * 64;
-      const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double) + (size_t)chunk * 10;
-      hipLaunchKernelGGL(gbdt_hist, dim3(nchunks, T, nft), dim3(threads), lds, stream, bins, g, h, node, partial, T, n,
-                         F, NB, level, chunk, FT);
-      hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(64), 0, stream, partial, nchunks, T, F, NB, level, NN, Gs,
+      const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles,
+                                       stream);
+      if (rc) return rc;
+      const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
+      hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), 0, stream, partial, foff_d, T, F, C, level, NN, Gs,
                          Hs, st, fe, sb, gn, (double)lam, (double)mcw);
       hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, st, fe, sb,
                          level);
@@ -471,7 +593,7 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
     // metrics (train + evals)
     const int mb_train = grid_for(TN);
     hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, stream, margin, Y, T, n, obj, metric, mpart);
-    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(1), 0, stream, mpart, mb_train,
+    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, stream, mpart, mb_train,
                        metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, hist_out + (int64_t)round * (1 + n_evals));
     for (int e = 0; e < n_evals; ++e) {
       const int64_t TE = (int64_t)T * evals[e].n;
@@ -481,7 +603,7 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, int NB
       const int mb = grid_for(TE);
       hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, stream, evals[e].margin, evals[e].Y, T, evals[e].n, obj,
                          metric, mpart);
-      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(1), 0, stream, mpart, mb,
+      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, stream, mpart, mb,
                          metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric,
                          hist_out + (int64_t)round * (1 + n_evals) + 1 + e);
     }
@@ -528,41 +650,32 @@ EM_API int em_gbdt_dp_round_begin(int round, int T, int n, int max_depth, const 
   return 0;
 }
 
-// histogram of one level folded into partial[0 : T*2^level*F*NB*2]; returns that length in *len_out
+// histogram of one level folded into partial[0 : T*2^level*C*2]; returns that length in *len_out
 EM_API int em_gbdt_dp_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node,
-                                 int T, int n, int F, int NB, double* partial, int64_t partial_doubles,
-                                 int64_t* len_out, hipStream_t stream) {
-  if (!bins || !g || !h || !node || !partial || !len_out || level < 0 || level > 11) return EM_ERR_ARG;
-  const int chunk = 1024;
-  const int nchunks = (n + chunk - 1) / chunk;
-  const int nodesL = 1 << level;
-  int FT = (int)((65536 - 10240) / ((int64_t)nodesL * NB * 2 * 8));  // + 10 KB row staging <= 64 KB
-  if (FT > F) FT = F;
-  if (FT > 256) FT = 256;
-  if (FT < 1) return EM_ERR_ARG;
-  const int64_t S = (int64_t)T * nodesL * F * NB * 2;
-  if (S * nchunks > partial_doubles) return EM_ERR_ARG;
-  const int nft = (F + FT - 1) / FT;
-  const int threads = ((FT + 63) / 64) * 64;
-  const size_t lds = (size_t)FT * nodesL * NB * 2 * sizeof(double) + (size_t)chunk * 10;
-  hipLaunchKernelGGL(gbdt_hist, dim3(nchunks, T, nft), dim3(threads), lds, stream, bins, g, h, node, partial, T, n, F,
-                     NB, level, chunk, FT);
-  if (nchunks > 1)
-    hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, nchunks, S);
+                                 int T, int n, int F, const int* foff_h, const int* foff_d, double* partial,
+                                 int64_t partial_doubles, int64_t* len_out, hipStream_t stream) {
+  if (!bins || !g || !h || !node || !partial || !len_out || level < 0 || level > 11 || !valid_foff(foff_h, F) ||
+      !foff_d)
+    return EM_ERR_ARG;
+  const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles, stream);
+  if (rc) return rc;
   EM_CHECK_LAUNCH();
-  *len_out = S;
+  *len_out = (int64_t)T * (1 << level) * foff_h[F] * 2;
   return 0;
 }
 
-EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* hist, int T, int n, int F, int NB,
-                                  int max_depth, int16_t* node, double* Gs, double* Hs, int8_t* status, int16_t* feat,
-                                  uint8_t* sbin, float* gainv, float lam, float mcw, hipStream_t stream) {
-  if (!bins || !hist || !node || !Gs || !Hs || !status || level < 0 || level >= max_depth) return EM_ERR_ARG;
+EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* hist, int T, int n, int F,
+                                  const int* foff_d, int C, int max_depth, int16_t* node, double* Gs, double* Hs,
+                                  int8_t* status, int16_t* feat, uint8_t* sbin, float* gainv, float lam, float mcw,
+                                  hipStream_t stream) {
+  if (!bins || !hist || !node || !Gs || !Hs || !status || !foff_d || C < F || level < 0 || level >= max_depth)
+    return EM_ERR_ARG;
   const int NN = (1 << (max_depth + 1)) - 1;
   const int nodesL = 1 << level;
   const int64_t TN = (int64_t)T * n;
-  hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(64), 0, stream, hist, 1, T, F, NB, level, NN, Gs, Hs, status,
-                     feat, sbin, gainv, (double)lam, (double)mcw);
+  const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
+  hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), 0, stream, hist, foff_d, T, F, C, level, NN, Gs, Hs,
+                     status, feat, sbin, gainv, (double)lam, (double)mcw);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
                      sbin, level);
   EM_CHECK_LAUNCH();
@@ -590,9 +703,9 @@ EM_API int em_gbdt_metric_sum(const float* margin, const float* Y, int T, int n,
   const int mb = grid_for(TN);
   if (n > 0) {
     hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, stream, margin, Y, T, n, obj, metric, mpart);
-    hipLaunchKernelGGL(gbdt_metric_sum, dim3(1), dim3(1), 0, stream, mpart, mb, out);
+    hipLaunchKernelGGL(gbdt_metric_sum, dim3(1), dim3(256), 0, stream, mpart, mb, out);
   } else {
-    hipLaunchKernelGGL(gbdt_metric_sum, dim3(1), dim3(1), 0, stream, mpart, 0, out);
+    hipLaunchKernelGGL(gbdt_metric_sum, dim3(1), dim3(256), 0, stream, mpart, 0, out);
   }
   EM_CHECK_LAUNCH();
   return 0;

@@ -17,13 +17,14 @@ class _Eval(ctypes.Structure):
 
 
 N.register_signatures({
-    "em_gbdt_fit": (_i, [_v, _v, _i, _i, _i, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f, _f,
-                         _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
+    "em_gbdt_fit": (_i, [_v, _v, _i, _i, _v, _v, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f,
+                         _f, _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
+    "em_gbdt_partial_doubles": (_i64, [_i, _i, _i, _v, _i]),
     "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
     "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
     "em_gbdt_dp_round_begin": (_i, [_i, _i, _i, _i, _v, _v, _v, _v, _v, _i, _f, _u32, _v, _v, _v, _v, _v]),
-    "em_gbdt_dp_level_hist": (_i, [_i, _v, _v, _v, _v, _i, _i, _i, _i, _v, _i64, ctypes.POINTER(_i64), _v]),
-    "em_gbdt_dp_level_split": (_i, [_i, _v, _v, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v, _v, _v, _f, _f, _v]),
+    "em_gbdt_dp_level_hist": (_i, [_i, _v, _v, _v, _v, _i, _i, _i, _v, _v, _v, _i64, ctypes.POINTER(_i64), _v]),
+    "em_gbdt_dp_level_split": (_i, [_i, _v, _v, _i, _i, _i, _v, _i, _i, _v, _v, _v, _v, _v, _v, _v, _f, _f, _v]),
     "em_gbdt_dp_round_end": (_i, [_i, _i, _i, _v, _v, _v, _v, _v, _v, _v, _v, _v, _f, _f, _f, _v]),
     "em_gbdt_metric_sum": (_i, [_v, _v, _i, _i, _i, _i, _v, _v, _v]),
 })
@@ -36,14 +37,30 @@ def _dev():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+class _Cells:
+    """Compact histogram axis: feature f owns bins [off[f], off[f+1]) (host array for the native
+    tile planner, device copy for the kernels)."""
+
+    def __init__(self, cuts, dev):
+        nbf = np.array([len(c) + 1 for c in cuts], dtype=np.int64)
+        if (nbf > 256).any():
+            raise ValueError("GPU GBDT supports at most 256 bins per feature")
+        self.host = np.ascontiguousarray(np.concatenate([[0], np.cumsum(nbf)]).astype(np.int32))
+        self.dev = torch.from_numpy(self.host).to(dev)
+        self.C = int(self.host[-1])
+
+    @property
+    def hp(self):
+        return self.host.ctypes.data
+
+
 def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     dev = _dev()
     n, F = bins.shape
     T = Y.shape[1]
     R, D = model.nround, model.max_depth
     NN = 2 ** (D + 1) - 1
-    if nbins > 256:
-        raise ValueError("GPU GBDT supports at most 256 bins per feature")
+    cells = _Cells(model.cuts, dev)
     d_bins = torch.from_numpy(np.ascontiguousarray(bins, dtype=np.uint8)).to(dev)
     d_Y = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float32)).to(dev)
     margin = torch.empty(T * n, dtype=torch.float32, device=dev)
@@ -64,8 +81,9 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     g = torch.empty(T * n, dtype=torch.float32, device=dev)
     h = torch.empty_like(g)
     node = torch.empty(T * n, dtype=torch.int16, device=dev)
-    nchunks = (n + 1023) // 1024
-    pdoubles = nchunks * T * (2 ** (D - 1)) * F * nbins * 2
+    pdoubles = N.query("em_gbdt_partial_doubles", n, T, F, cells.hp, D)
+    if pdoubles < 0:
+        raise ValueError(f"GPU GBDT: no histogram tile plan for depth {D} with {cells.C} bins")
     partial = torch.empty(max(pdoubles, 1), dtype=torch.float64, device=dev)
     Gs = torch.zeros(T * NN, dtype=torch.float64, device=dev)
     Hs = torch.zeros_like(Gs)
@@ -79,12 +97,13 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     hist = torch.zeros(R * (1 + len(ev_names)), dtype=torch.float32, device=dev)
     history = []
     if dp is not None:
-        _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, nbins, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
+        _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, cells, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
                        mpart, status, feat, sbin, leaf, gain, cover, history, stream)
     r0 = R if dp is not None else 0
     while r0 < R:
         r1 = min(R, r0 + rounds_per_call)
-        N.call("em_gbdt_fit", d_bins.data_ptr(), d_Y.data_ptr(), n, F, nbins, T, margin.data_ptr(), ev_structs,
+        N.call("em_gbdt_fit", d_bins.data_ptr(), d_Y.data_ptr(), n, F, cells.hp, cells.dev.data_ptr(), T,
+               margin.data_ptr(), ev_structs,
                len(ev_names), r0, r1, D, OBJ[model.objective], MET[model.eval_metric], model.eta, model.lam,
                model.gamma, model.mcw, model.subsample, model.seed & 0xFFFFFFFF, g.data_ptr(), h.data_ptr(),
                node.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
@@ -110,7 +129,7 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     return trees, history
 
 
-def _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, nbins, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
+def _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, cells, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
                    mpart, status, feat, sbin, leaf, gain, cover, history, stream):
     """C4: per-level histogram all-reduce between the HIP hist and split kernels (stream-ordered,
     no host sync inside a round); metric sums are all-reduced and read back once at the end."""
@@ -133,9 +152,10 @@ def _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, nbins, T, margin, ev_names, ev_
                off(gain, rnd), stream)
         for level in range(D):
             N.call("em_gbdt_dp_level_hist", level, d_bins.data_ptr(), g.data_ptr(), h.data_ptr(), node.data_ptr(), T, n,
-                   F, nbins, partial.data_ptr(), partial.numel(), ctypes.byref(S), stream)
+                   F, cells.hp, cells.dev.data_ptr(), partial.data_ptr(), partial.numel(), ctypes.byref(S), stream)
             dist.all_reduce(partial[:S.value], group=dp.group)
-            N.call("em_gbdt_dp_level_split", level, d_bins.data_ptr(), partial.data_ptr(), T, n, F, nbins, D,
+            N.call("em_gbdt_dp_level_split", level, d_bins.data_ptr(), partial.data_ptr(), T, n, F,
+                   cells.dev.data_ptr(), cells.C, D,
                    node.data_ptr(), Gs.data_ptr(), Hs.data_ptr(), off(status, rnd), off(feat, rnd), off(sbin, rnd),
                    off(gain, rnd), model.lam, model.mcw, stream)
         N.call("em_gbdt_dp_round_end", T, n, D, margin.data_ptr(), node.data_ptr(), off(status, rnd), off(feat, rnd),

@@ -118,6 +118,14 @@ def call(name: str, *args) -> None:
         raise RuntimeError(f"{name}: HIP error {rc}")
 
 
+def query(name: str, *args):
+    """Call a native function whose return value is data (a size, a count), not a status code."""
+    fn = getattr(lib(), name, None)
+    if fn is None:
+        raise NativeUnavailable(f"symbol {name} missing from {_build.lib_path()} (rebuild)")
+    return fn(*args)
+
+
 def cu_count(device: torch.device | int | None = None) -> int:
     return torch.cuda.get_device_properties(device if device is not None else torch.cuda.current_device()).multi_processor_count
 
