@@ -56,41 +56,6 @@ __device__ inline int xbit(const uint64_t* __restrict__ X, int W, int64_t row, i
   return (int)((X[row * W + (f >> 6)] >> (f & 63)) & 1ull);
 }
 
-// root row lists: rows with non-zero bootstrap weight, compacted per tree (one block per tree)
-__global__ void rf_init_rows(int64_t N, int T, int bootstrap, uint64_t seed, int t_off, int32_t* __restrict__ rows,
-                             int32_t* __restrict__ seg, int nodes) {
-  const int t = blockIdx.x;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __shared__ int wcnt[4];
-  __shared__ int base;
-  if (threadIdx.x == 0) base = 0;
-  __syncthreads();
-  int32_t* out = rows + (int64_t)t * N;
-  for (int64_t c = 0; c < N; c += RF_NT) {
-    const int64_t r = c + threadIdx.x;
-    const bool keep = r < N && row_weight(bootstrap, seed, t + t_off, r) > 0;
-    const uint64_t bal = __ballot(keep);
-    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-    if (lane == 0) wcnt[wv] = __builtin_popcountll(bal);
-    __syncthreads();
-    int off = base;
-    for (int i = 0; i < wv; ++i) off += wcnt[i];
-    if (keep) out[off + pre] = (int32_t)r;
-    __syncthreads();
-    if (threadIdx.x == 0) base += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-    __syncthreads();
-  }
-  int32_t* s = seg + (int64_t)t * nodes * 2;
-  for (int i = 1 + threadIdx.x; i < nodes; i += RF_NT) {  // everything below the root starts absent
-    s[2 * i] = 0;
-    s[2 * i + 1] = -1;
-  }
-  if (threadIdx.x == 0) {
-    s[0] = 0;
-    s[1] = base;
-  }
-}
-
 struct RfParams {
   const uint64_t* X;
   const uint64_t* Y;
@@ -102,95 +67,184 @@ struct RfParams {
   float* value;   // [T][nodes][64]
   double* gain;   // [T][nodes]
   float* cover;   // [T][nodes] weighted count
+  int16_t* cand;  // [T][2^max_depth][k] candidate features of the current level's nodes
+  uint32_t* acc;  // [T][2^max_depth][rec] per-node integer sums of the current level (see rec_words)
+  int32_t* lrc;   // [T][2^max_depth][2] partition counters (left, right) of the current level
 };
 
-__global__ void __launch_bounds__(RF_NT) rf_hist_split(RfParams p, const int32_t* __restrict__ rows, int level) {
+// per-node record of integer sums: S[64] (sum of w*y_j), n (sum of w), 3 pad, cnt[kp] (sum of w*x_f
+// per candidate), hist[k][64] (sum of w*x_f*y_j) -- exact, so block partials merge with atomics in
+// any order and the split decision is independent of row order and of the block count
+__host__ __device__ inline int rec_words(int k) { return 68 + ((k + 3) & ~3) + 64 * k; }
+
+// Root row lists: rows with non-zero bootstrap weight, compacted per tree by (blocks x tree)
+// workgroups; each 256-row chunk reserves its output range with one atomic (row order inside a list
+// is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
+__global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, int32_t* __restrict__ rows) {
+  const int t = blockIdx.y, B = gridDim.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ int wcnt[4];
+  __shared__ int base;
+  int32_t* out = rows + (int64_t)t * p.N;
+  const int64_t r0 = p.N * blockIdx.x / B, r1 = p.N * (blockIdx.x + 1) / B;
+  for (int64_t c = r0; c < r1; c += RF_NT) {
+    const int64_t r = c + threadIdx.x;
+    const bool keep = r < r1 && row_weight(p.bootstrap, p.seed, t + p.t_off, r) > 0;
+    const uint64_t bal = __ballot(keep);
+    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+    if (lane == 0) wcnt[wv] = __builtin_popcountll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) base = atomicAdd(&p.lrc[(int64_t)t * 2], wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3]);
+    __syncthreads();
+    int off = base;
+    for (int i = 0; i < wv; ++i) off += wcnt[i];
+    if (keep) out[off + pre] = (int32_t)r;
+    __syncthreads();
+  }
+}
+
+// One thread per (tree, node of this level): child segments from the parent's partition counters,
+// then the node's candidate features (partial Fisher-Yates on a hashed stream, as the oracle).
+__global__ void rf_level_prep(RfParams p, int level) {
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)p.T * nodesL) return;
+  const int t = (int)(gid / nodesL), nd = (int)(gid - (int64_t)t * nodesL), node = first + nd;
+  int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
+  int start = 0, count = -1;
+  if (level == 0) {
+    count = p.lrc[(int64_t)t * 2];
+  } else {
+    const int parent = (node - 1) >> 1, pnd = parent - ((nodesL >> 1) - 1);
+    const int32_t* ps = p.seg + ((int64_t)t * p.nodes + parent) * 2;
+    if (ps[1] >= 0 && p.feat[(int64_t)t * p.nodes + parent] >= 0) {
+      const int lc = p.lrc[((int64_t)t * (nodesL >> 1) + pnd) * 2];
+      const bool left = ((node - 1) & 1) == 0;
+      start = left ? ps[0] : ps[0] + lc;
+      count = left ? lc : ps[1] - lc;
+    }
+  }
+  sg[0] = start;
+  sg[1] = count;
+  if (count < 0 || level >= p.max_depth) return;
+  int arr[RF_MAXF];
+  for (int i = 0; i < p.F; ++i) arr[i] = i;
+  const int kk = p.k_feat < p.F ? p.k_feat : p.F;
+  int16_t* co = p.cand + ((int64_t)t * nodesL + nd) * p.k_feat;
+  for (int i = 0; i < kk; ++i) {
+    const uint64_t h = hash3(p.seed ^ 0x5EEDF00Dull, ((uint64_t)(t + p.t_off) << 32) | (uint64_t)node, (uint64_t)i);
+    const int j = i + (int)(h % (uint64_t)(p.F - i));
+    const int tmp = arr[i];
+    arr[i] = arr[j];
+    arr[j] = tmp;
+    co[i] = (int16_t)arr[i];
+  }
+}
+
+// K8: (blocks x nodes x trees) workgroups; block b of a node sums its slice of the node's row list
+// into LDS (integer atomics on set bits only: y bits for S, candidate x bits for cnt/hist), then
+// merges into the node record (plain stores when one block owns the node, else global atomics).
+__global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const int32_t* __restrict__ rows, int level) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* hist = lds;                       // [F][64]
-  uint32_t* cnt = hist + p.F * 64;            // [F]
-  uint32_t* S = cnt + p.F;                    // [4 waves][64]
-  __shared__ uint32_t nw[4];
-  __shared__ int cand[RF_MAXF];
-  __shared__ double bgain[4];
-  __shared__ int bfeat[4];
-  const int t = blockIdx.y;
-  const int node = (1 << level) - 1 + blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int t = blockIdx.z, nd = blockIdx.y, B = gridDim.x;
+  const int node = first + nd;
   const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
   const int start = sg[0], count = sg[1];
-  int16_t* fo = p.feat + (int64_t)t * p.nodes + node;
-  if (count < 0) {  // absent node (below a leaf)
-    if (tid == 0) *fo = -2;
-    return;
+  if (count < 0) return;
+  const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
+  uint32_t* S = lds;                // [64]
+  uint32_t* nn = lds + 64;          // [1] (+3 pad)
+  uint32_t* cnt = lds + 68;         // [kp]
+  uint32_t* hist = cnt + kp;        // [k][64]
+  __shared__ int16_t slot[RF_MAXF];
+  __shared__ uint64_t cmask[RF_MAXF / 64];
+  const bool split = level < p.max_depth;
+  for (int i = threadIdx.x; i < rec; i += blockDim.x) lds[i] = 0u;
+  for (int i = threadIdx.x; i < p.F; i += blockDim.x) slot[i] = -1;
+  if (threadIdx.x < RF_MAXF / 64) cmask[threadIdx.x] = 0ull;
+  __syncthreads();
+  const int kk = k < p.F ? k : p.F;
+  if (split && threadIdx.x == 0) {
+    const int16_t* co = p.cand + ((int64_t)t * nodesL + nd) * k;
+    for (int i = 0; i < kk; ++i) {
+      slot[co[i]] = (int16_t)i;
+      cmask[co[i] >> 6] |= 1ull << (co[i] & 63);
+    }
   }
-  for (int i = tid; i < p.F * 64 + p.F + 4 * 64; i += RF_NT) lds[i] = 0u;
   __syncthreads();
   const int32_t* rl = rows + (int64_t)t * p.N + start;
+  const int i0 = (int)((int64_t)count * blockIdx.x / B), i1 = (int)((int64_t)count * (blockIdx.x + 1) / B);
   uint32_t my_n = 0;
-  for (int i = tid; i < count; i += RF_NT) {
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int64_t r = rl[i];
     const uint32_t w = (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
-    if (!w) continue;
     my_n += w;
     const uint64_t y = p.Y[r] & ((1ull << 62) - 1);
     uint64_t yy = y;
     while (yy) {
-      const int j = __builtin_ctzll(yy);
+      atomicAdd(&S[__builtin_ctzll(yy)], w);
       yy &= yy - 1;
-      atomicAdd(&S[wv * 64 + j], w);
     }
+    if (!split) continue;
     for (int wd = 0; wd < p.W; ++wd) {
-      uint64_t xx = p.X[r * p.W + wd];
+      uint64_t xx = p.X[r * p.W + wd] & cmask[wd];
       while (xx) {
-        const int f = wd * 64 + __builtin_ctzll(xx);
+        const int sl = slot[wd * 64 + __builtin_ctzll(xx)];
         xx &= xx - 1;
-        if (f >= p.F) break;
-        atomicAdd(&cnt[f], w);
+        atomicAdd(&cnt[sl], w);
         uint64_t y2 = y;
         while (y2) {
-          const int j = __builtin_ctzll(y2);
+          atomicAdd(&hist[sl * 64 + __builtin_ctzll(y2)], w);
           y2 &= y2 - 1;
-          atomicAdd(&hist[f * 64 + j], w);
         }
       }
     }
   }
-  // weighted node size
-  uint32_t nsum = my_n;
-  for (int o = 32; o > 0; o >>= 1) nsum += __shfl_xor(nsum, o);
-  if (lane == 0) nw[wv] = nsum;
-  // candidate features (partial Fisher-Yates on a hashed stream), by one thread
-  if (tid == 0) {
-    for (int i = 0; i < p.F; ++i) cand[i] = i;
-    for (int i = 0; i < p.k_feat && i < p.F; ++i) {
-      const uint64_t h = hash3(p.seed ^ 0x5EEDF00Dull, ((uint64_t)(t + p.t_off) << 32) | (uint64_t)node, (uint64_t)i);
-      const int j = i + (int)(h % (uint64_t)(p.F - i));
-      const int tmp = cand[i];
-      cand[i] = cand[j];
-      cand[j] = tmp;
-    }
-  }
+  for (int o = 32; o > 0; o >>= 1) my_n += __shfl_xor(my_n, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(nn, my_n);
   __syncthreads();
-  const uint32_t n = nw[0] + nw[1] + nw[2] + nw[3];
-  // node record: weighted mean of the outputs (leaf value / diagnostics)
-  const uint32_t Sj = lane < 62 ? S[lane] + S[64 + lane] + S[128 + lane] + S[192 + lane] : 0u;
-  if (wv == 0) {
-    float* vo = p.value + ((int64_t)t * p.nodes + node) * 64;
-    vo[lane] = (n > 0 && lane < 62) ? (float)((double)Sj / (double)n) : 0.f;
+  uint32_t* dst = p.acc + ((int64_t)t * nodesL + nd) * rec;
+  const int used = split ? rec : 68;
+  if (B == 1) {
+    for (int i = threadIdx.x; i < used; i += blockDim.x) dst[i] = lds[i];
+  } else {
+    for (int i = threadIdx.x; i < used; i += blockDim.x)
+      if (lds[i]) atomicAdd(&dst[i], lds[i]);
   }
-  if (tid == 0) p.cover[(int64_t)t * p.nodes + node] = (float)n;
+}
+
+// K9: one wavefront per (tree, node): node record (weighted mean outputs, cover) and the split scan
+// over the candidates (lane j = output j): gain = SL2/nL + SR2/nR - S2/n from exact integers.
+__global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int t = blockIdx.y, nd = blockIdx.x, node = first + nd;
+  const int lane = threadIdx.x;
+  const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
+  int16_t* fo = p.feat + (int64_t)t * p.nodes + node;
+  if (sg[1] < 0) {
+    if (lane == 0) *fo = -2;
+    return;
+  }
+  const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
+  const uint32_t* A = p.acc + ((int64_t)t * nodesL + nd) * rec;
+  const uint32_t n = A[64];
+  const uint32_t Sj = lane < 62 ? A[lane] : 0u;
+  float* vo = p.value + ((int64_t)t * p.nodes + node) * 64;
+  vo[lane] = (n > 0 && lane < 62) ? (float)((double)Sj / (double)n) : 0.f;
+  if (lane == 0) p.cover[(int64_t)t * p.nodes + node] = (float)n;
   const bool can_split = level < p.max_depth && n >= (uint32_t)(2 * p.min_leaf) && n > 0;
   double best = 0.0;
   int bf = -1;
   if (can_split) {
-    // S2 = sum_j S_j^2 (exact integer)
     uint64_t s2 = (uint64_t)Sj * Sj;
     for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
-    const int kk = p.k_feat < p.F ? p.k_feat : p.F;
-    for (int c = wv; c < kk; c += 4) {
-      const int f = cand[c];
-      const uint32_t nR = cnt[f], nL = n - nR;
-      const uint32_t SR = lane < 62 ? hist[f * 64 + lane] : 0u;
+    const int kk = k < p.F ? k : p.F;
+    const int16_t* co = p.cand + ((int64_t)t * nodesL + nd) * k;
+    for (int c = 0; c < kk; ++c) {
+      const int f = co[c];
+      const uint32_t nR = A[68 + c], nL = n - nR;
+      const uint32_t SR = lane < 62 ? A[68 + kp + c * 64 + lane] : 0u;
       const uint32_t SL = Sj - SR;
       uint64_t aL = (uint64_t)SL * SL, aR = (uint64_t)SR * SR;
       for (int o = 32; o > 0; o >>= 1) {
@@ -204,60 +258,36 @@ __global__ void __launch_bounds__(RF_NT) rf_hist_split(RfParams p, const int32_t
         bf = f;
       }
     }
-    if (lane == 0) {
-      bgain[wv] = best;
-      bfeat[wv] = bf;
-    }
+    // a split must reduce impurity by more than rounding noise
+    if (bf >= 0 && !(best > 1e-9 * (1.0 + best))) bf = -1;
   }
-  __syncthreads();
-  if (tid == 0) {
-    int f = -1;
-    double g = 0.0;
-    if (can_split) {
-      for (int i = 0; i < 4; ++i) {
-        if (bfeat[i] < 0) continue;
-        if (f < 0 || bgain[i] > g || (bgain[i] == g && bfeat[i] < f)) {
-          g = bgain[i];
-          f = bfeat[i];
-        }
-      }
-      // a split must reduce impurity by more than rounding noise
-      if (f >= 0 && !(g > 1e-9 * (1.0 + g))) f = -1;
-    }
-    *fo = (int16_t)f;
-    p.gain[(int64_t)t * p.nodes + node] = f >= 0 ? g : 0.0;
+  if (lane == 0) {
+    *fo = (int16_t)bf;
+    p.gain[(int64_t)t * p.nodes + node] = bf >= 0 ? best : 0.0;
   }
 }
 
-// children row lists: left (x_f = 0) fills from the segment start, right from its end
+// K10: children row lists, (blocks x nodes x trees) workgroups: left rows (x_f = 0) fill the parent
+// segment from its start, right rows from its end; every 256-row chunk reserves its ranges with one
+// atomic per side on the node's counters (lrc), which rf_level_prep turns into the child segments.
 __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t* __restrict__ rin,
                                                       int32_t* __restrict__ rout, int level) {
-  const int t = blockIdx.y;
-  const int node = (1 << level) - 1 + blockIdx.x;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int t = blockIdx.z, nd = blockIdx.y, B = gridDim.x, node = first + nd;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
   const int start = sg[0], count = sg[1];
   const int f = p.feat[(int64_t)t * p.nodes + node];
-  const bool has_children = 2 * node + 2 < p.nodes;
-  if (f < 0 || count < 0) {
-    if (threadIdx.x == 0 && has_children) {
-      int32_t* c = p.seg + ((int64_t)t * p.nodes + 2 * node + 1) * 2;
-      c[0] = 0; c[1] = -1; c[2] = 0; c[3] = -1;
-    }
-    return;
-  }
+  if (f < 0 || count < 0) return;
   __shared__ int lc[4], rc[4];
   __shared__ int lbase, rbase;
-  if (threadIdx.x == 0) {
-    lbase = 0;
-    rbase = 0;
-  }
-  __syncthreads();
+  int32_t* ctr = p.lrc + ((int64_t)t * nodesL + nd) * 2;
   const int32_t* ri = rin + (int64_t)t * p.N + start;
   int32_t* ro = rout + (int64_t)t * p.N + start;
-  for (int c = 0; c < count; c += RF_NT) {
+  const int i0 = (int)((int64_t)count * blockIdx.x / B), i1 = (int)((int64_t)count * (blockIdx.x + 1) / B);
+  for (int c = i0; c < i1; c += blockDim.x) {
     const int i = c + threadIdx.x;
-    const bool live = i < count;
+    const bool live = i < i1;
     const int32_t r = live ? ri[i] : 0;
     const bool right = live && xbit(p.X, p.W, r, f);
     const bool left = live && !right;
@@ -269,6 +299,16 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t*
       rc[wv] = __builtin_popcountll(br);
     }
     __syncthreads();
+    if (threadIdx.x == 0) {
+      int tl = 0, tr = 0;
+      for (int k = 0; k < nwv; ++k) {
+        tl += lc[k];
+        tr += rc[k];
+      }
+      lbase = atomicAdd(&ctr[0], tl);
+      rbase = atomicAdd(&ctr[1], tr);
+    }
+    __syncthreads();
     int lo = lbase, roff = rbase;
     for (int k = 0; k < wv; ++k) {
       lo += lc[k];
@@ -277,38 +317,39 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t*
     if (left) ro[lo + pl] = r;
     if (right) ro[count - 1 - (roff + pr)] = r;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      lbase += lc[0] + lc[1] + lc[2] + lc[3];
-      rbase += rc[0] + rc[1] + rc[2] + rc[3];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0 && has_children) {
-    int32_t* ch = p.seg + ((int64_t)t * p.nodes + 2 * node + 1) * 2;
-    ch[0] = start;
-    ch[1] = lbase;
-    ch[2] = start + lbase;
-    ch[3] = rbase;
   }
 }
 
-// mean of leaf vectors over trees: one wavefront per row, lane j = output j
-__global__ void rf_predict(const uint64_t* __restrict__ X, int W, int64_t N, const int16_t* __restrict__ feat,
-                           const float* __restrict__ value, int T, int nodes, int out_logit, float* __restrict__ out,
-                           int ldo) {
+// K11: mean leaf vector over trees, one wavefront per row.  The traversals run lane-parallel
+// (lane l walks tree t0 + l: 8 dependent loads per 64 trees instead of per tree), then lane j
+// (= output j) gathers the 64 trees' leaf values through wave shuffles of the leaf indices.
+// NOTE (ROCm 7.2): holding the row's feature words in registers and picking one with a per-lane
+// select chain + 64-bit shift produced wrong bits for ~3 % of rows on gfx950; reading the bit
+// through xbit() (an L1-resident load) is exact -- tests/test_forest.py checks the deep-tree case.
+__global__ void __launch_bounds__(256) rf_predict(const uint64_t* __restrict__ X, int W, int64_t N,
+                                                  const int16_t* __restrict__ feat, const float* __restrict__ value,
+                                                  int T, int nodes, int out_logit, float* __restrict__ out, int ldo) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (r >= N) return;
   float acc = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const int16_t* ft = feat + (int64_t)t * nodes;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
     int nd = 0;
-    int f = ft[0];
-    while (f >= 0) {
-      nd = 2 * nd + 1 + xbit(X, W, r, f);
-      f = ft[nd];
+    if (t < T) {
+      const int16_t* ft = feat + (int64_t)t * nodes;
+      int f = ft[0];
+      while (f >= 0) {
+        nd = 2 * nd + 1 + xbit(X, W, r, f);
+        f = ft[nd];
+      }
     }
-    acc += value[((int64_t)t * nodes + nd) * 64 + lane];
+    const int cnt = T - t0 < 64 ? T - t0 : 64;
+    const float* vb = value + (int64_t)t0 * nodes * 64 + lane;
+    for (int k = 0; k < cnt; ++k) {
+      const int ndk = __shfl(nd, k);
+      acc += vb[((int64_t)k * nodes + ndk) * 64];
+    }
   }
   float pr = T > 0 ? acc / (float)T : 0.f;
   if (out_logit) {
@@ -324,34 +365,64 @@ __global__ void rf_predict(const uint64_t* __restrict__ X, int W, int64_t N, con
 
 EM_API int em_rf_nodes(int max_depth) { return (1 << (max_depth + 1)) - 1; }
 
-EM_API int em_rf_lds_bytes(int F) { return (F * 64 + F + 4 * 64) * 4; }
+// per-level launch shape: blocks per node from the average node size (>= 4096 rows per block)
+static void rf_shape(int64_t N, int level, int& B, int& nt) {
+  const int64_t avg = N / (1ll << level);
+  int64_t b = avg / 4096;
+  B = (int)(b < 1 ? 1 : (b > 64 ? 64 : b));
+  nt = avg >= 2048 ? RF_NT : 64;
+}
 
-// Native level-wise driver: all T trees advance one level per (hist_split, partition) pair.
+EM_API int64_t em_rf_acc_words(int T, int max_depth, int k_feat) {
+  if (T < 1 || max_depth < 0 || max_depth > 14 || k_feat < 1 || k_feat > RF_MAXF) return -1;
+  return (int64_t)T * (1ll << max_depth) * rec_words(k_feat);
+}
+
+// Native level-wise driver: all T trees advance one level per (prep, hist, split, partition) round.
+// scratch: cand int16 [T][2^D][k], acc uint32 [em_rf_acc_words], lrc int32 [T][2^D][2]
 EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int F, int T, int max_depth, int k_feat,
                      int min_leaf, int bootstrap, uint64_t seed, int t_off, int32_t* rows_a, int32_t* rows_b,
-                     int32_t* seg, int16_t* feat, float* value, double* gain, float* cover, hipStream_t stream) {
-  if (!X || !Y || !rows_a || !rows_b || !seg || !feat || !value || !gain || !cover) return EM_ERR_ARG;
+                     int32_t* seg, int16_t* feat, float* value, double* gain, float* cover, int16_t* cand,
+                     uint32_t* acc, int32_t* lrc, hipStream_t stream) {
+  if (!X || !Y || !rows_a || !rows_b || !seg || !feat || !value || !gain || !cover || !cand || !acc || !lrc)
+    return EM_ERR_ARG;
   if (W < 1 || F < 1 || F > RF_MAXF || F > 64 * W || T < 1 || max_depth < 0 || max_depth > 14 || k_feat < 1 ||
-      min_leaf < 1 || N < 1 || N >= (1ll << 31))
+      k_feat > RF_MAXF || min_leaf < 1 || N < 1 || N >= (1ll << 31))
     return EM_ERR_ARG;
   const int nodes = (1 << (max_depth + 1)) - 1;
-  const int lds = em_rf_lds_bytes(F);
+  const int rec = rec_words(k_feat);
+  const size_t lds = (size_t)rec * 4;
+  if (lds > 160 * 1024 - 8192) return EM_ERR_ARG;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)rf_hist_split, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+    (void)hipFuncSetAttribute((const void*)rf_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
     attr = true;
   }
-  RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain, cover};
-  hipLaunchKernelGGL(rf_init_rows, dim3(T), dim3(RF_NT), 0, stream, N, T, bootstrap, seed, t_off, rows_a, seg, nodes);
+  RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
+             cover, cand, acc, lrc};
+  (void)hipMemsetAsync(lrc, 0, (size_t)T * 2 * sizeof(int32_t), stream);
+  {
+    int B, nt;
+    rf_shape(N, 0, B, nt);
+    hipLaunchKernelGGL(rf_init_rows, dim3(B, T), dim3(RF_NT), 0, stream, p, rows_a);
+  }
   EM_CHECK_LAUNCH();
   int32_t* rin = rows_a;
   int32_t* rout = rows_b;
+  const int64_t kept = bootstrap ? (N * 632) / 1000 : N;  // expected rows per tree (Poisson(1): 1 - 1/e)
   for (int level = 0; level <= max_depth; ++level) {
-    const dim3 grid(1u << level, (unsigned)T);
-    hipLaunchKernelGGL(rf_hist_split, grid, dim3(RF_NT), lds, stream, p, rin, level);
+    const int nodesL = 1 << level;
+    int B, nt;
+    rf_shape(kept, level, B, nt);
+    const int64_t tn = (int64_t)T * nodesL;
+    hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level);
+    if (B > 1) (void)hipMemsetAsync(acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
+    hipLaunchKernelGGL(rf_hist, dim3(B, nodesL, T), dim3(nt), lds, stream, p, rin, level);
+    hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level);
     EM_CHECK_LAUNCH();
     if (level == max_depth) break;
-    hipLaunchKernelGGL(rf_partition, grid, dim3(RF_NT), 0, stream, p, rin, rout, level);
+    (void)hipMemsetAsync(lrc, 0, (size_t)tn * 2 * sizeof(int32_t), stream);
+    hipLaunchKernelGGL(rf_partition, dim3(B, nodesL, T), dim3(nt), 0, stream, p, rin, rout, level);
     EM_CHECK_LAUNCH();
     int32_t* tmp = rin;
     rin = rout;

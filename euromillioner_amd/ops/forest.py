@@ -9,10 +9,10 @@ from . import _native as N
 
 N.register_signatures({
     "em_rf_nodes": (N._i32, [N._i32]),
-    "em_rf_lds_bytes": (N._i32, [N._i32]),
+    "em_rf_acc_words": (N._i64, [N._i32, N._i32, N._i32]),
     "em_rf_fit": (N._i32, [N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32, N._i32, N._i32, N._i32, N._i32, N._i32,
                            N.ctypes.c_uint64, N._i32, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p,
-                           N._c_void_p, N._c_void_p, N._c_void_p]),
+                           N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p]),
     "em_rf_predict": (N._i32, [N._c_void_p, N._i32, N._i64, N._c_void_p, N._c_void_p, N._i32, N._i32, N._i32,
                                N._c_void_p, N._i32, N._c_void_p]),
 })
@@ -42,10 +42,18 @@ def fit(X: np.ndarray | torch.Tensor, Y: np.ndarray | torch.Tensor, F: int, t_of
     value = torch.zeros(T, nodes, 64, dtype=torch.float32, device=dev)
     gain = torch.zeros(T, nodes, dtype=torch.float64, device=dev)
     cover = torch.zeros(T, nodes, dtype=torch.float32, device=dev)
+    # per-level scratch: candidate lists, per-node integer sums, partition counters
+    acc_words = N.query("em_rf_acc_words", T, max_depth, k)
+    if acc_words < 0:
+        raise ValueError("unsupported forest shape (trees / depth / candidate count)")
+    cand = torch.empty(T, 1 << max_depth, k, dtype=torch.int16, device=dev)
+    acc = torch.empty(acc_words, dtype=torch.int32, device=dev)
+    lrc = torch.empty(T, 1 << max_depth, 2, dtype=torch.int32, device=dev)
     N.call("em_rf_fit", Xd.data_ptr(), W, Yd.data_ptr(), n, F, T, max_depth, k, min_leaf, int(bootstrap),
            int(seed) & 0xFFFFFFFFFFFFFFFF, int(t_off), rows_a.data_ptr(), rows_b.data_ptr(), seg.data_ptr(),
-           feat.data_ptr(), value.data_ptr(), gain.data_ptr(), cover.data_ptr(), N.stream_handle(dev))
-    del rows_a, rows_b
+           feat.data_ptr(), value.data_ptr(), gain.data_ptr(), cover.data_ptr(), cand.data_ptr(), acc.data_ptr(),
+           lrc.data_ptr(), N.stream_handle(dev))
+    del rows_a, rows_b, cand, acc, lrc
     if return_device:
         return feat, value, gain, cover
     return feat.cpu().numpy(), value.cpu().numpy(), gain.cpu().numpy(), cover.cpu().numpy()

@@ -106,3 +106,47 @@ def test_hip_forest_matches_oracle(depth, subset, boot, lags):
     assert np.array_equal(gpu.cover[live], cpu.cover[live])
     pd = gpu.predict_proba_device(X[:700]).cpu().numpy()[:, :62]
     assert np.allclose(pd, cpu.predict_proba(X[:700]), atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_hip_forest_predict_many_trees():
+    """> 64 trees: the lane-parallel traversal runs in two passes (lanes = trees t0 .. t0+63)."""
+    ds = DrawSet.synthetic(n=2000, seed=4, planted=0.7, calendar=False)
+    X, Y, F = draw_features(ds.numbers, 1)
+    gpu = RandomForest(n_trees=100, max_depth=4, seed=3, device="cuda")
+    gpu.fit(X, Y, F)
+    assert gpu.backend_used == "hip"
+    pd = gpu.predict_proba_device(X[:500]).cpu().numpy()[:, :62]
+    cpu = RandomForest(n_trees=100, max_depth=4, seed=3, device="cpu")
+    cpu.fit(X, Y, F)
+    assert np.array_equal(gpu.feat, cpu.feat)
+    assert np.allclose(pd, cpu.predict_proba(X[:500]), atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [4, 8])
+def test_hip_forest_predict_matches_torch_traversal(depth):
+    """Deep trees on 20k rows: GPU predict == a plain torch traversal of the same device arrays."""
+    import torch
+
+    from euromillioner_amd.data.draws import mask_bits
+    from euromillioner_amd.data.synthetic import generate_draws
+    from euromillioner_amd.ops import forest as K
+
+    nums, _ = generate_draws(20001, seed=0, planted=0.9, native=False)
+    md = torch.from_numpy(mask_bits(nums).view(np.int64)).cuda()
+    n_tr = 14000
+    feat, value, _, _ = K.fit(md[:n_tr].reshape(-1, 1).contiguous(), md[1:n_tr + 1].contiguous(), 62, 0, 70, depth,
+                              8, 1, True, 0, return_device=True)
+    Xv = md[n_tr:20000].reshape(-1, 1).contiguous()
+    p = K.predict(Xv, feat, value, depth)
+    x = Xv[:, 0]
+    acc = torch.zeros(Xv.shape[0], 64, device=x.device)
+    for t in range(feat.shape[0]):
+        nd = torch.zeros(Xv.shape[0], dtype=torch.long, device=x.device)
+        for _ in range(depth + 1):
+            f = feat[t][nd].long()
+            nd = torch.where(f >= 0, 2 * nd + 1 + ((x >> f.clamp(min=0)) & 1), nd)
+        acc += value[t][nd]
+    ref = acc / feat.shape[0]
+    assert torch.allclose(p[:, :62], ref[:, :62], atol=1e-6)
