@@ -590,14 +590,229 @@ gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
                                          alpha, beta);
 }
 
+// --------------------------------------------------------------------------------------------
+// The same ping-pong K loop on v_mfma_f32_16x16x32_bf16 (16 cycles, 16x16 output per instruction).
+// Same LDS image, staging units, slot schedule and quadrant order; per phase a wave runs
+// 4 (rows) x 2 (cols) x 2 (k-steps of 32) = 16 MFMAs instead of 8 of the 32x32x16 form.  The
+// 16x16x32 shape sustains a higher clock under load for the same cycles per FLOP
+// (MI355X_MICROARCH.md, matrix-core notes), which is where its gain comes from.
+// Fragment reads: lane l takes row (l & 15) of a 16-row block and the 16-B chunk 4*ks + (l >> 4)
+// of the 128-B row; with the (row >> 1) & 7 chunk swizzle each 16-lane group of a ds_read_b128
+// hits 16 distinct 16-B slots (conflict-free, as for the 32-row reads).
+// Accumulators acc[mb][nb] (mb = 16-row block 0..7 of the wave's 128 rows, nb = 16-col block 0..3):
+// lane l holds rows 4*(l >> 4) + e, column l & 15.
+EM_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// g_epilogue for the 16x16 accumulator layout: per 32-row block i the lane's values land in the
+// same transposed per-wave LDS tile T[64 cols][32 rows] (4 consecutive rows = one 8-B write), so
+// everything after the tile is shared with the 32x32 form.
+// acc[mb][nb0 + nb] (nb = 0..3) is the wave's 128 x 64 block at rows rowbase.., cols colw..
+template <int OUT_BF16, int FN, int DACT, int HAS_CT, int NBT>
+EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave, int lane, int rowbase, int colw,
+                            void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
+                            const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                            float beta) {
+  constexpr int TS = 80;
+  constexpr int YS = 144;
+  constexpr int WEPI = 64 * TS + 32 * YS;
+  char* tb = smem + wave * WEPI;
+  char* yb = tb + 64 * TS;
+  const int c16 = lane & 15, r4 = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rowb = rowbase + 32 * i;
+    if (DACT) {
+      const __bf16* ysrc = mask + (int64_t)rowb * ldm + colw;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int q = lane + 64 * t;
+        const int row = q >> 3, ch = q & 7;
+        *reinterpret_cast<u32x4*>(yb + row * YS + ch * 16) =
+            *reinterpret_cast<const u32x4*>(ysrc + (int64_t)row * ldm + ch * 8);
+      }
+      wave_lds_sync();
+    }
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int lc = 16 * nb + c16;
+      const float bv = (!DACT && bias) ? bias[colw + lc] : 0.f;
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        const f32x4& a = acc[2 * i + tm][nb0 + nb];
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lr = 16 * tm + r4 + e;
+          float v = alpha * a[e];
+          if (DACT) {
+            v *= g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
+          } else {
+            v = g_fn<FN>(v + bv);
+          }
+          x[e] = v;
+          if (!OUT_BF16) {
+            float* cp = reinterpret_cast<float*>(C) + (int64_t)(rowb + lr) * ldc + colw + lc;
+            *cp = beta != 0.f ? v + beta * *cp : v;
+          }
+        }
+        if (OUT_BF16) {
+          u32x2 pk = {pack2(x[0], x[1]), pack2(x[2], x[3])};
+          *reinterpret_cast<u32x2*>(tb + lc * TS + (16 * tm + r4) * 2) = pk;
+        }
+      }
+    }
+    if (OUT_BF16) {
+      wave_lds_sync();
+      const int gg = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int cb = 8 * (gg >> 1) + 16 * it;
+        const int r0 = 16 * (gg & 1);
+        const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * TS + (r0 + 4 * p4) * 2));
+        const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * TS + (r0 + 4 * p4) * 2));
+        const bf16x8 v8 = cat_tr(lo, hi);
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + r0 + i16) * ldc + colw + cb) = v8;
+      }
+      if (HAS_CT) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = lane + 64 * k;
+          const int col = q >> 2, part = q & 3;
+          *reinterpret_cast<u32x4*>(CT + (int64_t)(colw + col) * ldct + rowb + part * 8) =
+              *reinterpret_cast<const u32x4*>(tb + col * TS + part * 16);
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+__global__ void __launch_bounds__(G_NT, 1)
+gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                    void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
+                    const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                    float beta) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = N / G_BN;
+  const int nwg = (M / G_BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  const int ktiles = K / G_BK;
+  const int nph = 4 * ktiles;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int wi = wave_s & 3;
+  const bool g1 = wave_s >= 4;
+  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
+  g_stage(pa, 0, smem, wave_s);
+  g_stage(pb, 0, smem + G_TILE, wave_s);
+  if (g1) {
+    const bool a = pp_stage_slot(pa, pb, smem, -4, ktiles, wi);
+    const bool b = pp_stage_slot(pa, pb, smem, -2, ktiles, wi);
+    if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (pp_stage_slot(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  const int r16 = lane & 15, c4 = lane >> 4;
+  // fragment registers: both A halves (qm) stay resident across their two quadrants, so a K-tile
+  // reads A once and B once (24 ds_read_b128 per wave instead of 40): phase 0 reads A(qm 0) + B(qn 0),
+  // phase 1 A(qm 1), phase 2 B(qn 1), phase 3 nothing.  Reads only move earlier than in the 32x32
+  // schedule (first reads unchanged), so the staging slots' RAW / WAR analysis above still holds.
+  bf16x8 fa[2][4][2], fb[2][2];
+  auto load_seg = [&](int g, int slot) {
+    if (g < nph) {
+      const int kt = g >> 2, q = g & 3;
+      const char* la = smem + (kt & 1) * 2 * G_TILE;
+      const char* lb = la + G_TILE;
+      if (q == 0 || q == 2) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            fb[jj][ks] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + (q >> 1) * 32 + 16 * jj + r16, 4 * ks + c4));
+      }
+      if (q < 2) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            fa[q][ii][ks] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + q * 64 + 16 * ii + r16, 4 * ks + c4));
+      }
+    }
+    if (pp_stage_slot(pa, pb, smem, slot, ktiles, wi)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  auto mfma_seg = [&](int q) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x4& c = acc[4 * (q & 1) + ii][2 * (q >> 1) + jj];
+          c = mfma16(fa[q & 1][ii][ks], fb[jj][ks], c);
+        }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if (!g1) {
+    load_seg(0, -1);
+    for (int kt = 0; kt < ktiles; ++kt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int g = 4 * kt + q;
+        mfma_seg(q);
+        load_seg(g + 1, 2 * g + 1);
+      }
+    }
+  } else {
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < ktiles; ++kt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int g = 4 * kt + q;
+        load_seg(g, 2 * g);
+        mfma_seg(q);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  g_epilogue16<OUT_BF16, FN, DACT, HAS_CT, 4>(acc, 0, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, C, ldc, CT,
+                                              ldct, bias, mask, ldm, alpha, beta);
+}
+
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
              int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
              int64_t ldm, float alpha, float beta) {
   static bool attr = false;
   static const bool pp = !getenv_flag_off("EM_GEMM_PP");
-  auto kern = pp ? gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT> : gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
+  static const bool m16 = !getenv_flag_off("EM_GEMM_MFMA16");
+  auto kern = pp ? (m16 ? gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT> : gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>)
+                 : gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
   if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     (void)hipFuncSetAttribute((const void*)gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     (void)hipFuncSetAttribute((const void*)gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>,
