@@ -58,7 +58,7 @@ def main():
                 f.write(json.dumps(j) + "\n")
     f1 = pmc("fused_pmc", "mlp_fused_train")
     f2 = pmc("fused_pmc2", "mlp_fused_train")
-    w = pmc("wide_pmc", "gemm256_pp_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_nt_kernel<1, 1, 0, 0>")
+    w = pmc("wide_pmc", "gemm256_pp16_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_pp_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_nt_kernel<1, 1, 0, 0>")
     wcyc = w.get("GRBM_GUI_ACTIVE", 0) / 8.0
     w_busy = w.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(1.0, 1024 * wcyc) if wcyc else float("nan")
     head = last_json("bench_headline.log")[-1]
