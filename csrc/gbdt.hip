@@ -101,7 +101,8 @@ __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restr
 // rows therefore get bit-identical sums (exact gain ties keep breaking towards the lower feature).
 // Per row a thread does one 16-B LDS read-modify-write; the chain is latency-bound per thread and is
 // hidden by occupancy: the tile plan keeps the LDS footprint <= ~48 KB (3+ blocks per CU).
-constexpr int HIST_MAX_CHUNK = 1024;
+constexpr int HIST_MAX_CHUNK = 1024;        // rows staged in LDS per piece
+constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // doubles of per-chunk partials (1 GiB) per level
 constexpr int HIST_LDS_BUDGET = 36 * 1024;  // per-block histogram copies (+ 10 B/row staging)
 
 __global__ void __launch_bounds__(256)
@@ -117,47 +118,54 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
   double* hist = reinterpret_cast<double*>(smem);  // [P][NTn][ldsC][2]
   const int per = NTn * ldsC * 2;
-  for (int i = threadIdx.x; i < P * per; i += blockDim.x) hist[i] = 0.0;
-  const int r0 = c * chunk, r1 = min(n, r0 + chunk);
+  for (int i = threadIdx.x; i < P * per; i += blockDim.x) hist[i] = 0.0;  // (ordered by the loop's first barrier)
   float* sg = reinterpret_cast<float*>(smem + (size_t)P * per * sizeof(double));
-  float* sh = sg + chunk;
-  int16_t* sn = reinterpret_cast<int16_t*>(sh + chunk);
+  float* sh = sg + HIST_MAX_CHUNK;
+  int16_t* sn = reinterpret_cast<int16_t*>(sh + HIST_MAX_CHUNK);
   const int64_t base = (int64_t)t * n;
-  for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
-    sg[r - r0] = g[base + r];
-    sh[r - r0] = h[base + r];
-    sn[r - r0] = (int16_t)(node[base + r] - first - n0);  // tile-relative node (outside -> skipped)
-  }
-  __syncthreads();
   const int nth = f1 - f0;
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
-  if (p < P) {
-    const int f = f0 + fl;
-    double* my = hist + (size_t)p * per + (foff[f] - c0) * 2;
-    const int len = r1 - r0, sub = (len + P - 1) / P;
-    const int a0 = min(len, p * sub), a1 = min(len, a0 + sub);
-    const uint8_t* col = bins + (int64_t)r0 * F + f;
-    int r = a0;
-    // 8 bin loads in flight, then the 8 updates in row order (sums bitwise = the plain loop)
-    for (; r + 8 <= a1; r += 8) {
-      int b[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) b[u] = col[(int64_t)(r + u) * F];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int nd = sn[r + u];
-        if ((unsigned)nd >= (unsigned)NTn) continue;
-        double* e = my + (nd * ldsC + b[u]) * 2;
-        e[0] += (double)sg[r + u];
-        e[1] += (double)sh[r + u];
-      }
+  const int f = f0 + (p < P ? fl : 0);
+  double* my = hist + (size_t)(p < P ? p : 0) * per + (foff[f] - c0) * 2;
+  // the block's rows [c*chunk, +chunk) in staged pieces of <= HIST_MAX_CHUNK rows: per piece the
+  // rows' (node, g, h) go to LDS once (shared by every feature thread), then thread (p, fl) adds
+  // the p-th contiguous part of the piece to its copy in row order
+  const int rb = c * chunk, re = min(n, rb + chunk);
+  for (int r0 = rb; r0 < re; r0 += HIST_MAX_CHUNK) {
+    const int r1 = min(re, r0 + HIST_MAX_CHUNK);
+    __syncthreads();  // the previous piece's staging is consumed
+    for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
+      sg[r - r0] = g[base + r];
+      sh[r - r0] = h[base + r];
+      sn[r - r0] = (int16_t)(node[base + r] - first - n0);  // tile-relative node (outside -> skipped)
     }
-    for (; r < a1; ++r) {
-      const int nd = sn[r];
-      if ((unsigned)nd >= (unsigned)NTn) continue;
-      double* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
-      e[0] += (double)sg[r];
-      e[1] += (double)sh[r];
+    __syncthreads();
+    if (p < P) {
+      const int len = r1 - r0, sub = (len + P - 1) / P;
+      const int a0 = min(len, p * sub), a1 = min(len, a0 + sub);
+      const uint8_t* col = bins + (int64_t)r0 * F + f;
+      int r = a0;
+      // 8 bin loads in flight, then the 8 updates in row order (sums bitwise = the plain loop)
+      for (; r + 8 <= a1; r += 8) {
+        int b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = col[(int64_t)(r + u) * F];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int nd = sn[r + u];
+          if ((unsigned)nd >= (unsigned)NTn) continue;
+          double* e = my + (nd * ldsC + b[u]) * 2;
+          e[0] += (double)sg[r + u];
+          e[1] += (double)sh[r + u];
+        }
+      }
+      for (; r < a1; ++r) {
+        const int nd = sn[r];
+        if ((unsigned)nd >= (unsigned)NTn) continue;
+        double* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
+        e[0] += (double)sg[r];
+        e[1] += (double)sh[r];
+      }
     }
   }
   __syncthreads();
@@ -484,13 +492,18 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
         pl.nft = (F + FT - 1) / FT;
         pl.ntn = nodesL / NTn;
         pl.threads = ((FT * P + 63) / 64) * 64;
+        // chunks: ~4096 blocks per level, >= 64 rows each, and the per-chunk partials within the cap
         const int64_t per_chunk = (int64_t)T * pl.nft * pl.ntn;
-        const int64_t want = (4096 + per_chunk - 1) / per_chunk;
+        const int64_t S = (int64_t)T * nodesL * foff[F] * 2;
+        if (S > HIST_PARTIAL_CAP) return false;
+        int64_t want = (4096 + per_chunk - 1) / per_chunk;
+        const int64_t cap = HIST_PARTIAL_CAP / S;
+        want = want > cap ? cap : want;
         int64_t chunk = (n + want - 1) / want;
-        chunk = chunk < 64 ? 64 : (chunk > HIST_MAX_CHUNK ? HIST_MAX_CHUNK : chunk);
+        chunk = chunk < 64 ? 64 : chunk;
         pl.chunk = (int)chunk;
         pl.nchunks = (int)((n + chunk - 1) / chunk);
-        pl.lds = (size_t)P * NTn * maxC * 16 + (((size_t)chunk * 10 + 15) & ~(size_t)15);
+        pl.lds = (size_t)P * NTn * maxC * 16 + (size_t)HIST_MAX_CHUNK * 10;
         return true;
       }
       if (FT == 1) break;

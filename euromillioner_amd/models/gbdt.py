@@ -399,8 +399,16 @@ class GBDT:
         if backend == "hip":
             from . import gbdt_hip
 
-            self.trees, self.history = gbdt_hip.fit(self, X, bins, nbins, Y, evals, dp=dp)
-        else:
+            try:
+                self.trees, self.history = gbdt_hip.fit(self, X, bins, nbins, Y, evals, dp=dp)
+            except gbdt_hip.PlanUnsupported as e:
+                if self.backend != "auto":
+                    raise
+                from .. import log as L
+
+                L.get("GBDT").warning("%s; training on the numpy engine", e)
+                backend = self.backend_used = "numpy"
+        if backend != "hip":
             from threadpoolctl import threadpool_limits
 
             with threadpool_limits(limits=self.nthread or None):  # X3: the reference's OpenMP nthread

@@ -37,6 +37,10 @@ def _dev():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+class PlanUnsupported(ValueError):
+    """The device engine has no histogram plan for this shape (per-level histograms too large)."""
+
+
 class _Cells:
     """Compact histogram axis: feature f owns bins [off[f], off[f+1]) (host array for the native
     tile planner, device copy for the kernels)."""
@@ -44,7 +48,7 @@ class _Cells:
     def __init__(self, cuts, dev):
         nbf = np.array([len(c) + 1 for c in cuts], dtype=np.int64)
         if (nbf > 256).any():
-            raise ValueError("GPU GBDT supports at most 256 bins per feature")
+            raise PlanUnsupported("GPU GBDT supports at most 256 bins per feature")
         self.host = np.ascontiguousarray(np.concatenate([[0], np.cumsum(nbf)]).astype(np.int32))
         self.dev = torch.from_numpy(self.host).to(dev)
         self.C = int(self.host[-1])
@@ -83,7 +87,7 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     node = torch.empty(T * n, dtype=torch.int16, device=dev)
     pdoubles = N.query("em_gbdt_partial_doubles", n, T, F, cells.hp, D)
     if pdoubles < 0:
-        raise ValueError(f"GPU GBDT: no histogram tile plan for depth {D} with {cells.C} bins")
+        raise PlanUnsupported(f"GPU GBDT: no histogram plan for depth {D} x {cells.C} bins x {T} tasks")
     partial = torch.empty(max(pdoubles, 1), dtype=torch.float64, device=dev)
     Gs = torch.zeros(T * NN, dtype=torch.float64, device=dev)
     Hs = torch.zeros_like(Gs)

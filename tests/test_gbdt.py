@@ -221,3 +221,46 @@ def test_hip_dp_primitives_match_single_call():
     assert np.array_equal(dp.trees.feat, ref.trees.feat) and np.array_equal(dp.trees.sbin, ref.trees.sbin)
     assert np.array_equal(dp.trees.leaf, ref.trees.leaf)
     assert np.allclose([h["test"] for h in dp.history], [h["test"] for h in ref.history], rtol=1e-6)
+
+
+def test_native_hist_plan_bounds():
+    """The GBDT device planner (host C++, runs without a GPU): small shapes plan, the per-chunk
+    partial buffer stays under its 1 GiB cap for deep 256-bin trees, and impossible shapes are
+    refused (-1) instead of asking for terabytes."""
+    import numpy as np
+    import pytest
+
+    from euromillioner_amd.ops import _native as N
+
+    if not N.available():
+        pytest.skip("native library not built")
+    from euromillioner_amd.models import gbdt_hip  # noqa: F401  (registers the signatures)
+
+    def need(n, T, F, nb, D):
+        off = np.concatenate([[0], np.cumsum([nb] * F)]).astype(np.int32)
+        return N.query("em_gbdt_partial_doubles", n, T, F, off.ctypes.data, D)
+
+    assert 0 < need(928, 62, 66, 3, 3) <= 1 << 27
+    assert 0 < need(183500, 62, 66, 7, 3) <= 1 << 27
+    assert 0 < need(100000, 62, 66, 256, 6) <= 1 << 27
+    assert need(100000, 62, 66, 256, 12) == -1
+    off = np.array([0, 2, 300], dtype=np.int32)  # a feature with 298 bins is not supported
+    assert N.query("em_gbdt_partial_doubles", 1000, 1, 2, off.ctypes.data, 3) == -1
+
+
+@pytest.mark.gpu
+def test_hip_engine_deep_many_bins_matches_oracle():
+    """Continuous features (256 bins each) on depth-6 trees: the device planner tiles features and
+    nodes and stages rows in several LDS pieces per chunk; trees still match the numpy oracle."""
+    rng = np.random.default_rng(7)
+    n = 6000
+    X = rng.normal(size=(n, 12))
+    y = ((X[:, 0] + 0.5 * X[:, 3] * X[:, 5] + 0.3 * rng.normal(size=n)) > 0).astype(np.float64)
+    kw = dict(nround=6, max_depth=6, eta=0.5, gamma=0.0, min_child_weight=0.5)
+    a = G.GBDT(backend="numpy", **kw).fit(X[:4500], y[:4500], evals={"test": (X[4500:], y[4500:])})
+    b = G.GBDT(backend="hip", **kw).fit(X[:4500], y[:4500], evals={"test": (X[4500:], y[4500:])})
+    assert b.backend_used == "hip"
+    assert np.array_equal(a.trees.status, b.trees.status)
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)
+    assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-5
