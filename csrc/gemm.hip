@@ -229,6 +229,20 @@ constexpr int G_LDS = G_LOOP_LDS > G_EPI_LDS ? G_LOOP_LDS : G_EPI_LDS;
 
 EM_DEVICE uint32_t g_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
+// (XCD-contiguous) block id -> output tile, grouped GM tile-rows at a time: the ~32 blocks an XCD
+// runs at once form a GM x (32/GM) super-tile, so each A panel slice is shared by 32/GM blocks and
+// each B panel slice by GM blocks in that XCD's L2 (GM = 8: ~12 GB of panel traffic per 65536 x 8192
+// x 8192 GEMM instead of ~33 GB with whole tile-rows, whose 32 distinct B panels miss L2)
+EM_DEVICE void g_tile(int bid, int tiles_m, int tiles_n, int& m0, int& n0) {
+  constexpr int GM = 8;
+  const int per = GM * tiles_n;
+  const int grp = bid / per, first = grp * GM;
+  const int gm = tiles_m - first < GM ? tiles_m - first : GM;
+  const int in = bid - grp * per;
+  m0 = (first + in % gm) * G_BM;
+  n0 = (in / gm) * G_BN;
+}
+
 // One operand's K-tile piece for this wave: 4 x buffer_load_dwordx4 ... lds (1 KiB = 8 rows each).
 // The descriptor covers the block's 256-row panel; the per-lane part is one 32-bit voffset per
 // row-group parity (the swizzle depends on (row >> 1) & 7), everything else is scalar.
@@ -380,7 +394,8 @@ gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   const int tiles_n = N / G_BN;
   const int nwg = (M / G_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
-  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  int m0, n0;
+  g_tile(bid, M / G_BM, tiles_n, m0, n0);
   const int ktiles = K / G_BK;
 
   f32x16 acc[4][2];
@@ -498,7 +513,8 @@ gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   const int tiles_n = N / G_BN;
   const int nwg = (M / G_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
-  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  int m0, n0;
+  g_tile(bid, M / G_BM, tiles_n, m0, n0);
   const int ktiles = K / G_BK;
   const int nph = 4 * ktiles;
 
@@ -701,7 +717,8 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   const int tiles_n = N / G_BN;
   const int nwg = (M / G_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
-  const int m0 = (bid / tiles_n) * G_BM, n0 = (bid % tiles_n) * G_BN;
+  int m0, n0;
+  g_tile(bid, M / G_BM, tiles_n, m0, n0);
   const int ktiles = K / G_BK;
   const int nph = 4 * ktiles;
 
