@@ -1,6 +1,7 @@
 """numpy oracle for the random forest engine (``csrc/forest.hip``): the same level-wise
 algorithm with the same hashes and the same double-precision gain expression, so the
-GPU forest can be compared array-for-array (CPU backend and test reference)."""
+GPU forest can be compared array-for-array (CPU backend and test reference).  The forest is
+declared, never built, by the reference (``/root/reference/pom.xml:56-61``)."""
 from __future__ import annotations
 
 import numpy as np

@@ -1,4 +1,9 @@
-"""Device side of :mod:`euromillioner_amd.models.gbdt`: buffers + calls into ``csrc/gbdt.hip``."""
+"""Device side of :mod:`euromillioner_amd.models.gbdt`: buffers + calls into ``csrc/gbdt.hip``.
+
+Replaces the reference's ``XGBoost.train`` / ``Booster.predict`` JNI calls
+(``/root/reference/src/main/java/com/euromillioner/Main.java:136-141``):
+all rounds and levels run on the stream from the native driver ``em_gbdt_fit``; under data
+parallelism (C4) the per-level histogram is all-reduced between the hist and split kernels."""
 from __future__ import annotations
 
 import ctypes

@@ -4,6 +4,10 @@ and the CPU path of the framework.
 ``grouped_softmax_ce``: the 62 outputs are two categorical groups — 50 main numbers
 and 12 stars — each trained with cross-entropy against the normalised multi-hot
 target (5 ones / 5, 2 ones / 2).  ``bce``: independent sigmoids, mean over 62.
+
+The reference has no neural loss at all (its learner is XGBoost ``reg:logistic`` with
+``logloss``, ``/root/reference/src/main/java/com/euromillioner/Main.java:119,124``); these are
+the DL4J-style heads of SURVEY.md §2.4 N5.
 """
 from __future__ import annotations
 

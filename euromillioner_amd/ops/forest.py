@@ -1,5 +1,8 @@
 """Python face of the random-forest kernels (``csrc/forest.hip``: K8 hist, K9 split scan,
-K10 partition, K11 predict) and their native level-wise driver ``em_rf_fit``."""
+K10 partition, K11 predict) and their native level-wise driver ``em_rf_fit``.
+
+The reference only declares Spark MLlib's RandomForest (``/root/reference/pom.xml:56-61``,
+``README.md:6``); SURVEY.md §2.4 N7 / BASELINE config 4 define the 100-tree one-hot forest."""
 from __future__ import annotations
 
 import numpy as np

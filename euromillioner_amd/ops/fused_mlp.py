@@ -1,5 +1,6 @@
 """Python face of the fused small-MLP kernels (``csrc/mlp_fused.hip``, ``csrc/adam.hip``,
-``csrc/metrics.hip``).
+``csrc/metrics.hip``): the 62->128->62 MLP the reference declares through DL4J but never builds
+(``/root/reference/pom.xml:62-66``, ``README.md:2,6``; BASELINE.json configs 1-3).
 
 Flat fp32 parameter layout (``P = 16448`` floats; the pads stay exactly 0):
 
