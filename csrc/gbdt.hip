@@ -201,14 +201,33 @@ __global__ void gbdt_chunk_reduce(double* __restrict__ partial, int nchunks, int
 // at every candidate "bin <= b", first maximum kept; then a block arg-max where the larger gain
 // wins and equal gains go to the lower feature == numpy's first argmax in (feature, bin) order.
 __global__ void __launch_bounds__(256)
-gbdt_split(const double* __restrict__ hist, const int* __restrict__ foff, int T, int F, int C, int level, int NN,
-           double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status, int16_t* __restrict__ feat,
-           uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw) {
+gbdt_split(const double* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
+           int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
+           int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
   int8_t* st = status + (int64_t)t * NN;
   if (st[i] != 2) return;  // block-uniform
   const double* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
+  if (nchunks > 1) {  // per-chunk partials: fold this node's cells into LDS in chunk order (== gbdt_chunk_reduce)
+    double* fold = reinterpret_cast<double*>(smem);
+    for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
+      double acc = hs[e];
+      int c = 1;
+      for (; c + 8 <= nchunks; c += 8) {  // 8 independent loads in flight, added in chunk order
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = hs[(int64_t)(c + u) * cstride + e];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+      for (; c < nchunks; ++c) acc += hs[(int64_t)c * cstride + e];
+      fold[e] = acc;
+    }
+    __syncthreads();
+    hs = fold;
+  }
   __shared__ double sGn[2];
   __shared__ double rv[4];
   __shared__ int rf[4], rb[4];
@@ -519,9 +538,12 @@ int64_t partial_need(int level, int n, int T, int F, const int* foff) {
 }
 
 // K8 for one level: per-chunk histograms, then folded into partial[0 : T*nodesL*C*2]
+// fold = false leaves the per-chunk partials for gbdt_split to fold (small chunk counts); *nchunks_out
+// = the number of partial copies left in `partial` (1 after a fold)
+constexpr int SPLIT_FOLD_MAX_CHUNKS = 32, SPLIT_FOLD_MAX_LDS = 32 * 1024;
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
-                      hipStream_t stream) {
+                      bool fold, int* nchunks_out, hipStream_t stream) {
   HistPlan pl;
   if (!plan_hist(level, n, T, F, foff_h, pl)) return EM_ERR_ARG;
   const int C = foff_h[F];
@@ -529,7 +551,10 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
   if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
   hipLaunchKernelGGL(gbdt_hist, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g, h,
                      node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC);
-  if (pl.nchunks > 1) hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
+  const bool split_folds = !fold && pl.nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
+  if (pl.nchunks > 1 && !split_folds)
+    hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
+  *nchunks_out = split_folds ? pl.nchunks : 1;
   return 0;
 }
 
@@ -591,12 +616,14 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
                        seed, round);
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
+      int nch = 1;
       const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles,
-                                       stream);
+                                       false, &nch, stream);
       if (rc) return rc;
-      const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
-      hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), 0, stream, partial, foff_d, T, F, C, level, NN, Gs,
-                         Hs, st, fe, sb, gn, (double)lam, (double)mcw);
+      const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
+      const int64_t cstride = (int64_t)T * nodesL * C * 2;
+      hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), nch > 1 ? (size_t)C * 16 : 0, stream, partial, nch,
+                         cstride, foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw);
       hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, st, fe, sb,
                          level);
     }
@@ -670,7 +697,9 @@ EM_API int em_gbdt_dp_level_hist(int level, const uint8_t* bins, const float* g,
   if (!bins || !g || !h || !node || !partial || !len_out || level < 0 || level > 11 || !valid_foff(foff_h, F) ||
       !foff_d)
     return EM_ERR_ARG;
-  const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles, stream);
+  int nch = 1;
+  const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles, true,
+                                   &nch, stream);
   if (rc) return rc;
   EM_CHECK_LAUNCH();
   *len_out = (int64_t)T * (1 << level) * foff_h[F] * 2;
@@ -687,8 +716,8 @@ EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* 
   const int nodesL = 1 << level;
   const int64_t TN = (int64_t)T * n;
   const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
-  hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), 0, stream, hist, foff_d, T, F, C, level, NN, Gs, Hs,
-                     status, feat, sbin, gainv, (double)lam, (double)mcw);
+  hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C, level,
+                     NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
                      sbin, level);
   EM_CHECK_LAUNCH();
