@@ -974,6 +974,129 @@ __global__ void __launch_bounds__(256) rowsum_kernel(const __bf16* __restrict__ 
   if (lane == 0) out[row] = accumulate ? out[row] + s : s;
 }
 
+// ============================================================================================
+// Skinny weight gradient: C = alpha * P^T Q (+ beta C) with P [K][J <= 64] and Q [K][W] both
+// row-major over the batch K (the wide MLP's first and last layers: 64 x 8192 over 65536 rows).
+// The 128x128 any-layout kernel wastes half its MFMAs on the 64-wide side and hides its global
+// latency poorly; this path reads the W-wide operand exactly once, streaming it through a 3-stage
+// buffer_load...lds ring.  Block = (256-column tile of Q, K-slice); 4 waves, each a 64 x 64 output
+// (2 x 2 MFMA 32x32x16 tiles); fragments via ds_read_b64_tr_b16 from [64 k][128 col] images
+// (frag<0>, the MC layout of the any-layout kernel).  Each K-slice writes an fp32 partial; a
+// fixed-order reduce sums the slices (deterministic) and writes C or C^T.
+constexpr int SK_WT = 256, SK_STAGES = 3;
+constexpr int SK_IMG = 64 * 256;             // one [64 k][128 col] bf16 image, 16 KB
+constexpr int SK_STAGE = 3 * SK_IMG;         // P image (64 of its 128 columns used) + 2 Q images
+constexpr int SK_LDS = SK_STAGES * SK_STAGE;  // 144 KB
+
+struct SkPanel {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t voff[4];
+  uint32_t row_bytes;
+};
+// one buffer_load...lds writes 1 KB = 4 image rows lane-linearly (row 4g + (L >> 4), physical
+// 16-B chunk L & 15); the mc_off swizzle (chunk ^ (k & 15)) is applied to the source chunk, so
+// the per-lane offset depends on g mod 4
+EM_DEVICE SkPanel sk_panel(const __bf16* base, int64_t ld, int64_t bytes, int lane) {
+  SkPanel p;
+  p.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(bytes < 0x7FFFFFFF ? bytes : 0x7FFFFFFF),
+                                             0x00020000);
+  const int lr = lane >> 4, pc = lane & 15;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int c = pc ^ ((4 * g4 + lr) & 15);
+    p.voff[g4] = (uint32_t)((lr * ld + 8 * c) * 2);
+  }
+  p.row_bytes = (uint32_t)(ld * 2);
+  return p;
+}
+// this wave's 4 of the image's 16 row groups; k0 relative to the panel base, col0 in elements
+EM_DEVICE void sk_stage_img(const SkPanel& p, int k0, int col0, char* img, int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int g = wave * 4 + i;
+    const uint32_t soff = (uint32_t)(k0 + 4 * g) * p.row_bytes + (uint32_t)col0 * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (EM_LDS void*)(img + g * 1024), 16, p.voff[g & 3], soff, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(256, 1)
+wgrad_skinny_kernel(const __bf16* __restrict__ P, int64_t ldp, const __bf16* __restrict__ Q, int64_t ldq, int K,
+                    int W, int kstep, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w0 = blockIdx.x * SK_WT, s = blockIdx.y;
+  const int kb = s * kstep, ke = min(K, kb + kstep);
+  const int T = (ke - kb) / 64;
+  const SkPanel pp = sk_panel(P + (int64_t)kb * ldp, ldp, ((int64_t)(K - kb) * ldp) * 2, lane);
+  const SkPanel pq = sk_panel(Q + (int64_t)kb * ldq + w0, ldq, ((int64_t)(K - kb) * ldq - w0) * 2, lane);
+  auto stage = [&](int t) {
+    char* st = smem + (t % SK_STAGES) * SK_STAGE;
+    sk_stage_img(pp, t * 64, 0, st, wave);
+    sk_stage_img(pq, t * 64, 0, st + SK_IMG, wave);
+    sk_stage_img(pq, t * 64, 128, st + 2 * SK_IMG, wave);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  if (T > 0) stage(0);
+  if (T > 1) {
+    stage(1);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // tile 0 landed, tile 1 in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  const int r = lane & 31;
+  const int qimg = SK_IMG * (1 + (wave >> 1)), qc = (wave & 1) * 64;
+  for (int t = 0; t < T; ++t) {
+    // the slot of tile t-1 is free: every wave consumed its fragments before the last barrier
+    if (t + 2 < T) stage(t + 2);
+    const char* st = smem + (t % SK_STAGES) * SK_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 a0 = frag<0>(st, r, ks, lane), a1 = frag<0>(st, 32 + r, ks, lane);
+      const bf16x8 b0 = frag<0>(st + qimg, qc + r, ks, lane), b1 = frag<0>(st + qimg, qc + 32 + r, ks, lane);
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+    }
+    if (t + 2 < T) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");  // tile t+1 landed
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // fp32 partial of this K-slice: part[s][j][w] (j = P column 0..63)
+  const int h = lane >> 5;
+  float* ps = part + (int64_t)s * 64 * W;
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int wt = 0; wt < 2; ++wt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int j = 32 * jt + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const int w = w0 + (wave >> 1) * 128 + qc + 32 * wt + r;
+        ps[(int64_t)j * W + w] = acc[jt][wt][v];
+      }
+}
+
+// fixed-order sum over the K-slices; C [J][W] (trans = 0) or C^T [W][J] (trans = 1)
+__global__ void __launch_bounds__(256)
+wgrad_skinny_reduce_kernel(const float* __restrict__ part, int S, int J, int W, float* __restrict__ C, int64_t ldc,
+                           int trans, float alpha, float beta) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)J * W) return;
+  const int j = (int)(e / W), w = (int)(e - (int64_t)j * W);
+  float acc = 0.f;
+  for (int s = 0; s < S; ++s) acc += part[((int64_t)s * 64 + j) * W + w];
+  acc *= alpha;
+  float* o = trans ? C + (int64_t)w * ldc + j : C + (int64_t)j * ldc + w;
+  *o = beta != 0.f ? acc + beta * *o : acc;
+}
+
 }  // namespace
 
 static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
@@ -1079,6 +1202,33 @@ EM_API int em_rowsum_bf16(const void* X, int64_t ldx, int R, int Cc, float* out,
   if (R == 0) return 0;
   hipLaunchKernelGGL(rowsum_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, (const __bf16*)X, ldx, R, Cc, out,
                      accumulate, scale);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// C = alpha * P^T Q (+ beta C): P bf16 [K][J <= 64] (ldp), Q bf16 [K][W] (ldq, W % 256 == 0), K % 64 == 0;
+// part: fp32 workspace of splits * 64 * W floats; trans = 1 writes C^T [W][J] (ldc) instead of C [J][W].
+EM_API int em_wgrad_skinny(const void* P, int64_t ldp, const void* Q, int64_t ldq, int K, int J, int W, float* C,
+                           int64_t ldc, int trans, float alpha, float beta, float* part, int splits, int kstep,
+                           hipStream_t stream) {
+  if (!P || !Q || !C || !part || K <= 0 || (K & 63) || J < 1 || J > 64 || W <= 0 || (W % SK_WT) || splits < 1 ||
+      kstep <= 0 || (kstep & 63) || (int64_t)splits * kstep < K || (int64_t)(splits - 1) * kstep >= K)
+    return EM_ERR_ARG;
+  if ((ldp & 7) || (ldq & 7) || ldp < J || ldq < W || ldc < (trans ? J : W) ||
+      (((uintptr_t)P | (uintptr_t)Q) & 15))
+    return EM_ERR_ARG;
+  if ((int64_t)kstep * ldq * 2 >= (1ll << 31) || (int64_t)kstep * ldp * 2 >= (1ll << 31)) return EM_ERR_ARG;  // 32-bit offsets
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_skinny_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SK_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(wgrad_skinny_kernel, dim3(W / SK_WT, splits), dim3(256), SK_LDS, stream, (const __bf16*)P, ldp,
+                     (const __bf16*)Q, ldq, K, W, kstep, part);
+  EM_CHECK_LAUNCH();
+  const int64_t n = (int64_t)J * W;
+  hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, splits,
+                     J, W, C, ldc, trans, alpha, beta);
   EM_CHECK_LAUNCH();
   return 0;
 }

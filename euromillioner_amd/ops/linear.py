@@ -29,6 +29,8 @@ N.register_signatures({
                               N._c_void_p, N._i64, N._c_void_p]),
     "em_gemm_bf16_splitk": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64,
                                      N._i32, N._i32, N._i32, N._i32, N._f32, N._i32, N._i32, N._i64, N._c_void_p]),
+    "em_wgrad_skinny": (N._i32, [N._c_void_p, N._i64, N._c_void_p, N._i64, N._i32, N._i32, N._i32, N._c_void_p,
+                                 N._i64, N._i32, N._f32, N._f32, N._c_void_p, N._i32, N._i32, N._c_void_p]),
     "em_colsum_ws_floats": (N._i32, [N._i32, N._i32]),
     "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p,
                                 N._c_void_p]),
@@ -175,6 +177,8 @@ def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
     K = x.shape[1]
     if out is None:
         out = empty_aligned(N_, K, torch.float32, dz.device)
+    if split_k is None and _skinny_ok(dz, x, out):
+        return _wgrad_skinny(dz, x, out, alpha, beta)
     tiles = ((N_ + 127) // 128) * ((K + 127) // 128)
     if split_k is None:
         split_k = 1
@@ -198,6 +202,35 @@ def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
         out.mul_(beta).add_(red)
     else:
         out.copy_(red)
+    return out
+
+
+def _skinny_ok(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> bool:
+    """64-wide x (batch >> 64) x 256k-wide weight gradients: the streaming skinny kernel."""
+    M, N_ = dz.shape
+    K = x.shape[1]
+    narrow, wide = (N_, K) if N_ <= 64 else (K, N_)
+    return (narrow <= 64 and wide % 256 == 0 and M % 64 == 0 and M >= 4096 and out.dtype == torch.float32
+            and out.stride(1) == 1 and out.stride(0) % 8 == 0 and is_aligned(dz) and is_aligned(x))
+
+
+def _wgrad_skinny(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor, alpha: float, beta: float) -> torch.Tensor:
+    """``out = alpha * dz^T x (+ beta out)`` via em_wgrad_skinny: P = the 64-wide operand, Q = the wide
+    one; the output is written transposed when dz is the wide side (first layer: [8192, 64])."""
+    M, N_ = dz.shape
+    trans = N_ > 64
+    P, Q = (x, dz) if trans else (dz, x)
+    J, W = P.shape[1], Q.shape[1]
+    splits = max(1, min(256 // (W // 256), M // 64))
+    kstep = ((M + splits - 1) // splits + 63) // 64 * 64
+    while kstep * Q.stride(0) * 2 >= 1 << 31:  # 32-bit buffer offsets inside a K-slice
+        splits *= 2
+        kstep = ((M + splits - 1) // splits + 63) // 64 * 64
+    splits = (M + kstep - 1) // kstep
+    part = torch.empty(splits * 64 * W, dtype=torch.float32, device=dz.device)
+    N.call("em_wgrad_skinny", P.data_ptr(), P.stride(0), Q.data_ptr(), Q.stride(0), M, J, W, out.data_ptr(),
+           out.stride(0), int(trans), float(alpha), float(beta), part.data_ptr(), splits, kstep,
+           N.stream_handle(dz.device))
     return out
 
 

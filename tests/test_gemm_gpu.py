@@ -283,3 +283,25 @@ def test_big_nt_schedule_race_screen(M, N):
         for _ in range(7):
             again = LIN.linear_fwd(x, w, None, "none", torch.float32)
             assert torch.equal(again, first), (M, N, K)
+
+
+@pytest.mark.parametrize("M,J,W,wide_dz", [(8192, 64, 512, False), (8192, 62, 768, False), (4096, 64, 256, True),
+                                           (12288, 62, 512, True)])
+def test_wgrad_skinny_matches_fp32(M, J, W, wide_dz):
+    """The streaming skinny wgrad (64 x W over a big batch; both orientations, 62-wide padded
+    operands, alpha/beta accumulate) vs the fp32 product of the same bf16 operands."""
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(M + J + W)
+    narrow = LIN.aligned(torch.randn(M, J, device="cuda", generator=g))
+    wide = LIN.aligned(torch.randn(M, W, device="cuda", generator=g))
+    dz, x = (wide, narrow) if wide_dz else (narrow, wide)
+    assert LIN._skinny_ok(dz, x, LIN.empty_aligned(dz.shape[1], x.shape[1], torch.float32, dz.device))
+    gw = LIN.linear_wgrad(dz, x)
+    ref = dz.double().t() @ x.double()
+    assert gw.shape == ref.shape
+    assert _rel(gw.double(), ref) < 1e-5, _rel(gw.double(), ref)
+    gw2 = LIN.linear_wgrad(dz, x, out=gw.clone(), alpha=0.5, beta=1.0)
+    assert _rel(gw2.double(), 1.5 * ref) < 1e-5
+    again = LIN.linear_wgrad(dz, x)
+    assert torch.equal(again, gw)  # fixed-order slice reduction: bitwise repeatable
