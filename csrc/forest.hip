@@ -279,44 +279,65 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t*
   const int start = sg[0], count = sg[1];
   const int f = p.feat[(int64_t)t * p.nodes + node];
   if (f < 0 || count < 0) return;
-  __shared__ int lc[4], rc[4];
-  __shared__ int lbase, rbase;
+  // chunks of 4 x blockDim rows: 4 ballots per wave (row k of the thread = c + k*blockDim + tid), one
+  // LDS count exchange and one atomic reservation per side per chunk (instead of per blockDim rows);
+  // the small count arrays are double-buffered so a chunk needs two barriers
+  constexpr int RR = 4;
+  __shared__ int lc[2][RR][4], rc[2][RR][4];
+  __shared__ int lbase[2], rbase[2];
   int32_t* ctr = p.lrc + ((int64_t)t * nodesL + nd) * 2;
   const int32_t* ri = rin + (int64_t)t * p.N + start;
   int32_t* ro = rout + (int64_t)t * p.N + start;
   const int i0 = (int)((int64_t)count * blockIdx.x / B), i1 = (int)((int64_t)count * (blockIdx.x + 1) / B);
-  for (int c = i0; c < i1; c += blockDim.x) {
-    const int i = c + threadIdx.x;
-    const bool live = i < i1;
-    const int32_t r = live ? ri[i] : 0;
-    const bool right = live && xbit(p.X, p.W, r, f);
-    const bool left = live && !right;
-    const uint64_t bl = __ballot(left), br = __ballot(right);
-    const int pl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0));
-    const int pr = __builtin_amdgcn_mbcnt_hi((uint32_t)(br >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)br, 0));
-    if (lane == 0) {
-      lc[wv] = __builtin_popcountll(bl);
-      rc[wv] = __builtin_popcountll(br);
+  int buf = 0;
+  for (int c = i0; c < i1; c += RR * blockDim.x, buf ^= 1) {
+    int32_t r[RR];
+    bool right[RR], left[RR];
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {  // the RR row-index loads, then the RR feature-bit loads, all in flight
+      const int i = c + k * blockDim.x + threadIdx.x;
+      r[k] = i < i1 ? ri[i] : -1;
+    }
+    int pl[RR], pr[RR];
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {
+      right[k] = r[k] >= 0 && xbit(p.X, p.W, r[k], f);
+      left[k] = r[k] >= 0 && !right[k];
+      const uint64_t bl = __ballot(left[k]), br = __ballot(right[k]);
+      pl[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0));
+      pr[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(br >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)br, 0));
+      if (lane == 0) {
+        lc[buf][k][wv] = __builtin_popcountll(bl);
+        rc[buf][k][wv] = __builtin_popcountll(br);
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       int tl = 0, tr = 0;
-      for (int k = 0; k < nwv; ++k) {
-        tl += lc[k];
-        tr += rc[k];
+      for (int k = 0; k < RR; ++k)
+        for (int q = 0; q < nwv; ++q) {
+          tl += lc[buf][k][q];
+          tr += rc[buf][k][q];
+        }
+      lbase[buf] = atomicAdd(&ctr[0], tl);
+      rbase[buf] = atomicAdd(&ctr[1], tr);
+    }
+    __syncthreads();
+    int lo = lbase[buf], roff = rbase[buf];
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {  // offsets in (k, wave, lane) order
+      int l = lo, rr = roff;
+      for (int q = 0; q < wv; ++q) {
+        l += lc[buf][k][q];
+        rr += rc[buf][k][q];
       }
-      lbase = atomicAdd(&ctr[0], tl);
-      rbase = atomicAdd(&ctr[1], tr);
+      if (left[k]) ro[l + pl[k]] = r[k];
+      if (right[k]) ro[count - 1 - (rr + pr[k])] = r[k];
+      for (int q = 0; q < nwv; ++q) {
+        lo += lc[buf][k][q];
+        roff += rc[buf][k][q];
+      }
     }
-    __syncthreads();
-    int lo = lbase, roff = rbase;
-    for (int k = 0; k < wv; ++k) {
-      lo += lc[k];
-      roff += rc[k];
-    }
-    if (left) ro[lo + pl] = r;
-    if (right) ro[count - 1 - (roff + pr)] = r;
-    __syncthreads();
   }
 }
 
