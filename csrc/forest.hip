@@ -52,6 +52,12 @@ __device__ inline int row_weight(int bootstrap, uint64_t seed, int tree, int64_t
   return bootstrap ? poisson1(hash3(seed, 0x100000000ull + (uint64_t)tree, (uint64_t)row)) : 1;
 }
 
+// Row-list entries carry the row's bootstrap weight (1..9, computed once in rf_init_rows) in bits
+// 27..30 when N < 2^27, so the per-level kernels skip the hash + Poisson inverse CDF per row.
+constexpr int RF_WSHIFT = 27;
+constexpr int32_t RF_RMASK = (1 << RF_WSHIFT) - 1;
+__device__ inline bool rf_packed(int64_t N) { return N <= RF_RMASK; }
+
 __device__ inline int xbit(const uint64_t* __restrict__ X, int W, int64_t row, int f) {
   return (int)((X[row * W + (f >> 6)] >> (f & 63)) & 1ull);
 }
@@ -89,7 +95,8 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, int32_t* __res
   const int64_t r0 = p.N * blockIdx.x / B, r1 = p.N * (blockIdx.x + 1) / B;
   for (int64_t c = r0; c < r1; c += RF_NT) {
     const int64_t r = c + threadIdx.x;
-    const bool keep = r < r1 && row_weight(p.bootstrap, p.seed, t + p.t_off, r) > 0;
+    const int w = r < r1 ? row_weight(p.bootstrap, p.seed, t + p.t_off, r) : 0;
+    const bool keep = w > 0;
     const uint64_t bal = __ballot(keep);
     const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
     if (lane == 0) wcnt[wv] = __builtin_popcountll(bal);
@@ -98,7 +105,7 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, int32_t* __res
     __syncthreads();
     int off = base;
     for (int i = 0; i < wv; ++i) off += wcnt[i];
-    if (keep) out[off + pre] = (int32_t)r;
+    if (keep) out[off + pre] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w << RF_WSHIFT)) : (int32_t)r;
     __syncthreads();
   }
 }
@@ -176,9 +183,11 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const int32_t* __re
   const int32_t* rl = rows + (int64_t)t * p.N + start;
   const int i0 = (int)((int64_t)count * blockIdx.x / B), i1 = (int)((int64_t)count * (blockIdx.x + 1) / B);
   uint32_t my_n = 0;
+  const bool packed = rf_packed(p.N);
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int64_t r = rl[i];
-    const uint32_t w = (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
+    const int32_t e = rl[i];
+    const int64_t r = packed ? (e & RF_RMASK) : e;
+    const uint32_t w = packed ? (uint32_t)e >> RF_WSHIFT : (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
     my_n += w;
     const uint64_t y = p.Y[r] & ((1ull << 62) - 1);
     uint64_t yy = y;
@@ -301,7 +310,7 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t*
     int pl[RR], pr[RR];
 #pragma unroll
     for (int k = 0; k < RR; ++k) {
-      right[k] = r[k] >= 0 && xbit(p.X, p.W, r[k], f);
+      right[k] = r[k] >= 0 && xbit(p.X, p.W, r[k] & (rf_packed(p.N) ? RF_RMASK : 0x7FFFFFFF), f);
       left[k] = r[k] >= 0 && !right[k];
       const uint64_t bl = __ballot(left[k]), br = __ballot(right[k]);
       pl[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0));
