@@ -480,7 +480,7 @@ constexpr int V4_BASE = IMG_BYTES + LUT_BYTES;
 constexpr int V4_YLUT = V4_BASE + 4 * V4_PAIR_BYTES;  // 16 x f32x4: target nibble -> 4 {0,1} floats
 constexpr int V4_XLUT = V4_YLUT + 256;  // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V4_LOOP_LDS = V4_XLUT + 128;
-constexpr int V4_RED = 65536;  // epilogue fp32 dW image [16384]
+constexpr int V4_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below this offset
 constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 4096);
 #ifndef V4_STAGGER
 #define V4_STAGGER 0
@@ -893,8 +893,10 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
   if (h == 0) DB2S[pair * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
   if (lane == 0) LOSSS[2 * pair + RHO] = lsum;
   // the same number of barriers in both role instantiations (wave-uniform branch)
-  for (int stage = 0; stage < 4; ++stage) {
-    if (pair == stage) {
+  // two stages: pairs 0/1 store into halves 0/1, then pairs 2/3 add theirs (fixed order, so the
+  // slab is bit-reproducible); the slab writer sums the halves
+  for (int stage = 0; stage < 2; ++stage) {
+    if ((pair >> 1) == stage) {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -905,7 +907,7 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
             const int T = 8 * which + 2 * (2 * RHO + tt) + u;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              f32x4* p = reinterpret_cast<f32x4*>(RED + ((T * 4 + g) * 64 + lane) * 4);
+              f32x4* p = reinterpret_cast<f32x4*>(RED + (pair & 1) * 16384 + ((T * 4 + g) * 64 + lane) * 4);
               f32x4 v = {acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
               if (stage) v += *p;
               *p = v;
@@ -925,12 +927,18 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pair = wave >> 1, rho = wave & 1;
-  {
+  {  // all loads of the weight image in flight before the first LDS store
+    constexpr int N16 = IMG_BYTES / 16, K = (N16 + 511) / 512;
     const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
     u32x4* dst = reinterpret_cast<u32x4*>(smem);
-    for (int i = tid; i < IMG_BYTES / 16; i += 512) dst[i] = src[i];
+    u32x4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (tid + 512 * k < N16) v[k] = src[tid + 512 * k];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (tid + 512 * k < N16) dst[tid + 512 * k] = v[k];
   }
-  fill_lut(smem + IMG_BYTES, tid);
   if (tid < 64) reinterpret_cast<float*>(smem + V4_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
   if (tid < 32) {  // nibble n = tid >> 1, dword tid & 1 holds elements 2(tid&1), 2(tid&1)+1
     const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
@@ -955,7 +963,7 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
   for (int e = tid; e < 16 * 4 * 64; e += 512) {
     const int T = e >> 8, g = (e >> 6) & 3, l = e & 63, hh = l >> 5, rr = l & 31;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + e * 4);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + e * 4) + *reinterpret_cast<const f32x4*>(RED + 16384 + e * 4);
     const int c0 = 32 * ((T & 7) >> 1) + 8 * g + 4 * hh;  // hidden rows c0..c0+3
     const int col = 32 * (T & 1) + rr;
     if (T < 8) {

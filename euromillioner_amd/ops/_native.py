@@ -74,7 +74,7 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.lib_path()
+        path = os.environ.get("EUROM_NATIVE_LIB") or _build.lib_path()  # override: A/B builds
         try:
             if not os.path.exists(path) or os.environ.get("EUROM_FORCE_BUILD") == "1":
                 if os.environ.get("EUROM_AUTOBUILD", "1") != "1":
