@@ -18,7 +18,8 @@ namespace {
 
 constexpr int IN = 64, HID = 128, OUT = 64;
 constexpr int P_W2 = IN * HID, P_B2 = P_W2 + HID * OUT, P_TOTAL = P_B2 + OUT;
-constexpr int IMG_W1T = 0, IMG_W2P = 16384, IMG_W2Q = 32768, IMG_B2 = 49152;
+constexpr int W1T_RS = 144, W2P_RS = 272, W2Q_RS = 144;  // padded image rows (csrc/mlp_fused.hip)
+constexpr int IMG_W1T = 0, IMG_W2P = IMG_W1T + 128 * W1T_RS, IMG_W2Q = IMG_W2P + 64 * W2P_RS, IMG_B2 = IMG_W2Q + 128 * W2Q_RS;
 
 // true for padding slots that must stay exactly zero (W1 row 63, W2 cols 62/63, b2[62/63])
 EM_DEVICE bool mlp_pad_slot(int p) {
@@ -31,20 +32,20 @@ EM_DEVICE void mlp_pack_one(int p, float val, uint8_t* img) {
   const uint16_t b = f2bf_bits(val);
   if (p < P_W2) {  // W1[f][c] -> W1T image row c, feature f
     const int f = p >> 7, c = p & 127;
-    const uint32_t off = IMG_W1T + c * 128 + ((((f >> 3) ^ ((c >> 1) & 7))) << 4) + (f & 7) * 2;
+    const uint32_t off = IMG_W1T + c * W1T_RS + (f >> 3) * 16 + (f & 7) * 2;
     *reinterpret_cast<uint16_t*>(img + off) = b;
   } else if (p < P_B2) {  // W2[c][o]
     const int q = p - P_W2, c = q >> 6, o = q & 63;
     {  // W2P: row o, hid c = 32t + perm(s,h,j)
       const int t = c >> 5, cc = c & 31, s = cc >> 4, a = (cc >> 3) & 1, hh = (cc >> 2) & 1, bb = cc & 3;
       const int j = 4 * a + bb, k16 = (2 * t + s) * 2 + hh;
-      const uint32_t off = IMG_W2P + o * 256 + ((k16 ^ (o & 15)) << 4) + j * 2;
+      const uint32_t off = IMG_W2P + o * W2P_RS + k16 * 16 + j * 2;
       *reinterpret_cast<uint16_t*>(img + off) = b;
     }
     {  // W2Q: row c, out o = 32u + perm(s,h,j)
       const int u = o >> 5, oo = o & 31, s = oo >> 4, a = (oo >> 3) & 1, hh = (oo >> 2) & 1, bb = oo & 3;
       const int j = 4 * a + bb, k8 = (2 * u + s) * 2 + hh;
-      const uint32_t off = IMG_W2Q + c * 128 + ((k8 ^ ((c >> 1) & 7)) << 4) + j * 2;
+      const uint32_t off = IMG_W2Q + c * W2Q_RS + k8 * 16 + j * 2;
       *reinterpret_cast<uint16_t*>(img + off) = b;
     }
   } else {

@@ -39,7 +39,12 @@ constexpr int P_W1 = 0, P_W2 = IN * HID, P_B2 = P_W2 + HID * OUT, P_TOTAL = P_B2
 // gradient slabs are SLAB_STRIDE floats apart (P_TOTAL rounded to an odd multiple of 256 B so the
 // cross-slab reduction in em_adam_slab does not hit the same HBM channel for every slab)
 constexpr int SLAB_STRIDE = 16640;
-constexpr int IMG_W1T = 0, IMG_W2P = 16384, IMG_W2Q = 32768, IMG_B2 = 49152, IMG_BYTES = 49408;
+// weight images with padded rows (144 B / 272 B: 16 consecutive rows start in distinct 16-B bank
+// groups, so the 16-lane phases of ds_read_b128 are conflict-free) instead of an XOR swizzle: a
+// fragment address is then one per-lane base + an immediate, not one VGPR per (row, chunk) pair
+constexpr int W1T_RS = 144, W2P_RS = 272, W2Q_RS = 144;
+constexpr int IMG_W1T = 0, IMG_W2P = IMG_W1T + 128 * W1T_RS, IMG_W2Q = IMG_W2P + 64 * W2P_RS,
+              IMG_B2 = IMG_W2Q + 128 * W2Q_RS, IMG_BYTES = IMG_B2 + 256;  // 54528
 
 constexpr uint64_t MAIN_BITS = (1ull << 50) - 1;
 constexpr uint64_t STAR_BITS = ((1ull << 12) - 1) << 50;
@@ -60,9 +65,9 @@ EM_DEVICE bf16x8 lut_frag(const char* lut, uint64_t m, int q, int h) {
 }
 
 // byte offsets into the LDS weight images (see em_adam_pack for the writer)
-EM_DEVICE uint32_t w1t_off(int row, int k8) { return IMG_W1T + row * 128 + ((k8 ^ ((row >> 1) & 7)) << 4); }
-EM_DEVICE uint32_t w2p_off(int row, int k16) { return IMG_W2P + row * 256 + ((k16 ^ (row & 15)) << 4); }
-EM_DEVICE uint32_t w2q_off(int row, int k8) { return IMG_W2Q + row * 128 + ((k8 ^ ((row >> 1) & 7)) << 4); }
+EM_DEVICE uint32_t w1t_off(int row, int k8) { return IMG_W1T + row * W1T_RS + k8 * 16; }
+EM_DEVICE uint32_t w2p_off(int row, int k16) { return IMG_W2P + row * W2P_RS + k16 * 16; }
+EM_DEVICE uint32_t w2q_off(int row, int k8) { return IMG_W2Q + row * W2Q_RS + k8 * 16; }
 // wave-private [32 samples][64 cols] bf16 image, 128-B rows, chunk ^= row&7
 EM_DEVICE uint32_t img_off(uint32_t base, int row, int col) {
   return base + row * 128 + ((((col >> 3) ^ (row & 7))) << 4) + (col & 7) * 2;
@@ -493,6 +498,7 @@ constexpr int V4_LDS = (V4_LOOP_LDS > V4_RED + 4096 ? V4_LOOP_LDS : V4_RED + 409
 #endif
 constexpr int V4_SPIN_LIMIT = V4_SLEEP ? (1 << 22) : (1 << 24);
 static_assert(V4_LDS <= 163840, "v4 LDS budget");
+static_assert(IMG_BYTES == 54528 && IMG_BYTES % 16 == 0, "image size (ops/fused_mlp.py IMG_BYTES)");
 
 EM_DEVICE void pair_signal(char* smem, uint32_t flag_off, int value) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -520,6 +526,9 @@ EM_DEVICE int v4_cls(int i, int h) {
 // Diagnostic phase timers (build with --define V4_STAMPS=1; tools/fused_phases.py reads them):
 // s_memtime deltas summed per phase per wave, written after the dW slab into spare slab floats.
 // They force an lgkmcnt drain at every mark, so they perturb what they measure (+~10 %).
+#ifndef V4_NODB2
+#define V4_NODB2 0
+#endif
 #ifndef V4_STAMPS
 #define V4_STAMPS 0
 #endif
@@ -766,7 +775,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
       for (int tt = 0; tt < 2; ++tt) mfma_acc_agpr(dW2[tt][RHO], hR[tt][q], bd);
       // db2 of the own output tile on the matrix pipe: ones(32 x samples) · dZ2 (every row of the
       // accumulator is the column sum) instead of 16 VALU adds per tile
-      db2 = mfma32(ones, bd, db2);
+      if (!V4_NODB2) db2 = mfma32(ones, bd, db2);
     }
   }
   ok &= pair_wait(smem, PAFL, sig);

@@ -21,7 +21,7 @@ from . import _native as N
 IN, HID, OUT = 64, 128, 64
 P_W1, P_W2, P_B2 = 0, IN * HID, IN * HID + HID * OUT
 P_TOTAL = P_B2 + OUT
-IMG_BYTES = 49408
+IMG_BYTES = 54528  # == em_mlp_fused_image_bytes() (csrc/mlp_fused.hip, padded weight images)
 SLAB_STRIDE = 16640  # floats between per-workgroup gradient slabs (csrc/mlp_fused.hip)
 LOSS_KINDS = {"softmax": 0, "bce": 1}
 
