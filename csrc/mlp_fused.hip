@@ -526,6 +526,9 @@ EM_DEVICE int v4_cls(int i, int h) {
 // Diagnostic phase timers (build with --define V4_STAMPS=1; tools/fused_phases.py reads them):
 // s_memtime deltas summed per phase per wave, written after the dW slab into spare slab floats.
 // They force an lgkmcnt drain at every mark, so they perturb what they measure (+~10 %).
+#ifndef V4_MIX
+#define V4_MIX 1
+#endif
 #ifndef V4_NODB2
 #define V4_NODB2 0
 #endif
@@ -935,7 +938,9 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pair = wave >> 1, rho = wave & 1;
+  // wave w runs on SIMD w % 4: pairs 2/3 take their roles swapped so every SIMD hosts one role-0 and
+  // one role-1 wave (role 1 owns the star group and issues ~20 % more VALU per tile)
+  const int pair = wave >> 1, rho = (wave & 1) ^ (V4_MIX ? (wave >> 2) : 0);
   {  // all loads of the weight image in flight before the first LDS store
     constexpr int N16 = IMG_BYTES / 16, K = (N16 + 511) / 512;
     const u32x4* src = reinterpret_cast<const u32x4*>(wimg);

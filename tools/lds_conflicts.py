@@ -44,24 +44,37 @@ def lanes():
 
 
 # ---- kernel layout formulas (keep in sync with csrc/mlp_fused.hip) ----
-def w1t_off(row, k8):
-    return row * 128 + ((k8 ^ ((row >> 1) & 7)) << 4)
+def w1t_off(row, k8):  # padded rows (144 B): 16 consecutive rows start in distinct 16-B bank groups
+    return row * 144 + k8 * 16
 
 
 def w2p_off(row, k16):
-    return 16384 + row * 256 + ((k16 ^ (row & 15)) << 4)
+    return 18432 + row * 272 + k16 * 16
 
 
 def w2q_off(row, k8):
-    return 32768 + row * 128 + ((k8 ^ ((row >> 1) & 7)) << 4)
+    return 35840 + row * 144 + k8 * 16
 
 
 def img_off(base, row, col, swz):
     return base + swz(row, col)
 
 
-def swz_v4(row, col):  # [32][64] bf16, 128-B rows, chunk ^= row & 7
+def swz_v4(row, col):  # [32][64] bf16, 128-B rows, chunk ^= row & 7 (the first v4 layout)
     return row * 128 + ((((col >> 3) ^ (row & 7))) << 4) + (col & 7) * 2
+
+
+def v4_fr(r):
+    return ((r ^ (r >> 4)) & 1) | (((r >> 2) & 1) << 1) | (((r >> 1) & 1) << 2)
+
+
+def v4_gr(r):
+    return (r >> 3) & 1
+
+
+def swz_v4g(row, col):  # the kernel's v4_img<true> (H, D2 images)
+    c = ((col >> 3) ^ v4_fr(row)) << 4
+    return row * 128 + c + ((((col >> 2) & 1) ^ v4_gr(row)) << 3) + (col & 3) * 2
 
 
 def report(name, kind, addr, count):
@@ -99,22 +112,25 @@ def model(swz=swz_v4, label="v4"):
             add(report(nm, "read_tr", [base + swz(16 * 0 + 4 * h + q4, 0 + 16 * g1 + 4 * p4)
                                         for _, r, h, q4, p4, g1 in L], n))
         rnd = random.Random(0)
-        # X fragments from the byte LUT: data-dependent (multi-hot masks: mostly-zero bytes broadcast)
+        # X fragments from the 16-entry nibble table (two ds_read_b64 per fragment, 8 per tile):
+        # data-dependent, so averaged over random multi-hot draws
         sample = []
         for _ in range(200):
-            bytes_ = [0] * 64
+            nib = []
             for r in range(32):
                 m = 0
                 for b in rnd.sample(range(62), 7):
                     m |= 1 << b
-                for h in (0, 1):
-                    bytes_[r + 32 * h] = (m >> (8 * h)) & 0xFF
-            sample.append(cycles("read_b128", [49408 + b * 16 for b in bytes_])[0])
-        print(f"  {'X LUT frag (random draws)':34s} read_b128  x4: {sum(sample) / len(sample):5.1f} cycles (min 4)")
-        tot[0] += 4 * sum(sample) / len(sample)
+                nib.append(m)
+            for sh in (0, 4):
+                addr = [155392 + ((nib[lane & 31] >> (8 * (lane >> 5) + sh)) & 15) * 8 for lane in range(64)]
+                sample.append(cycles("read_b64", addr)[0])
+        avg = sum(sample) / len(sample)
+        print(f"  {'X nibble-table frag (random draws)':34s} read_b64   x8: {avg:5.1f} cycles (min 2)")
+        tot[0] += 8 * avg
         tot[1] += 16
     print(f" total per tile (both roles): {tot[0]:.0f} LDS cycles vs conflict-free {tot[1]}")
 
 
 if __name__ == "__main__":
-    model()
+    model(swz_v4g, "v4_img (fr/gr swizzle; X image uses gr = 0)")
