@@ -97,6 +97,10 @@ def main():
     ap.add_argument("--hidden", default=None, help="GEMM-path hidden sizes, e.g. 8192,8192")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks sharing one GPU)")
+    ap.add_argument("--device-data-gb", type=float, default=0.0,
+                    help="HBM-resident dataset: generate this many GiB of draw masks on the GPU "
+                         "(csrc/datagen.hip) instead of --draws-per-gpu on the host; the timed steps "
+                         "are spread over the whole training split (no hipGraph: offsets change per step)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="DP gradient all-reduce of the fused path: xgmi = one-shot peer-memory reduction fused "
                          "into Adam (hipGraph-replayable); rccl = torch.distributed all_reduce; auto = xgmi if the "
@@ -129,11 +133,23 @@ def main():
     from euromillioner_amd.data.synthetic import generate_draws
     from euromillioner_amd.models.mlp import FusedSmallMLP
 
-    n_draws = a.draws_per_gpu
-    nums, _ = generate_draws(n_draws, seed=a.seed + 1000 * rank, planted=a.planted, native=True)
     from euromillioner_amd.ops.fused_mlp import rows_to_masks
 
-    draws = rows_to_masks(torch.from_numpy(nums).to(dev))  # device feature masks (8 B / draw)
+    gen_s = None
+    if a.device_data_gb > 0:
+        from euromillioner_amd.data.device_gen import gb_to_draws, generate_masks
+
+        n_draws = gb_to_draws(a.device_data_gb)
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        draws = generate_masks(n_draws, seed=a.seed + 1000 * rank, planted=a.planted, device=dev)
+        torch.cuda.synchronize()
+        gen_s = time.perf_counter() - tg
+        a.graph = 0  # per-step offsets walk the whole dataset
+    else:
+        n_draws = a.draws_per_gpu
+        nums, _ = generate_draws(n_draws, seed=a.seed + 1000 * rank, planted=a.planted, native=True)
+        draws = rows_to_masks(torch.from_numpy(nums).to(dev))  # device feature masks (8 B / draw)
     n_samples = n_draws - 1
     margin = int(0.7 * n_samples)
     B = a.batch
@@ -141,6 +157,11 @@ def main():
         raise SystemExit("dataset too small for the batch")
 
     n_off = max(1, (margin - B) // B)
+    # device-data runs spread the warmup + timed steps over the whole training split
+    spread = max(1, n_off // max(1, a.steps + a.warmup)) if a.device_data_gb > 0 else 1
+
+    def boff(i):
+        return ((i * spread) % n_off) * B
     sizes = (62, 128, 62)
     if a.model == "mlp-wide":
         from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
@@ -151,13 +172,13 @@ def main():
         model.broadcast_parameters()
 
         def step(i):
-            return model.step(draws, B, offset=(i % n_off) * B)
+            return model.step(draws, B, offset=boff(i))
     elif a.impl == "fused":
         model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group, comm=a.comm)
         model.broadcast_parameters()
 
         def step(i):
-            return model.step(draws, B, offset=(i % n_off) * B)
+            return model.step(draws, B, offset=boff(i))
     else:
         model = _TorchBaseline(dev, a, draws, B, group)
 
@@ -216,7 +237,8 @@ def main():
 
     ev, ev_iid = {}, {}
     if not a.no_eval:
-        ev = model.evaluate(draws, n_samples - margin, offset=margin)
+        n_val = n_samples - margin if a.device_data_gb <= 0 else min(n_samples - margin, 1 << 24)
+        ev = model.evaluate(draws, n_val, offset=margin)
         # the same model on iid draws (no planted structure): must sit at chance
         n_iid = min(1 << 20, n_samples - margin)
         iid_nums, _ = generate_draws(n_iid + 1, seed=a.seed + 777 + 1000 * rank, planted=0.0, native=True)
@@ -243,7 +265,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (seeded Euromillions draws, planted Markov p=%.2f; random-init weights)" % a.planted,
+            "data": ("synthetic (seeded Euromillions draws, planted Markov p=%.2f; random-init weights)" % a.planted
+                     if a.device_data_gb <= 0 else
+                     "synthetic, generated on the GPU: %.1f GiB of HBM-resident draw masks per GPU (%d draws, "
+                     "planted Markov p=%.2f; random-init weights)" % (a.device_data_gb, n_draws, a.planted)),
             "config": {"model": desc,
                        "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": B, "optimizer": "adam", "hipgraph": use_graph,
@@ -253,6 +278,9 @@ def main():
             "val_iid": ev_iid,
             **extra,
         }
+        if gen_s is not None:
+            out["device_datagen"] = {"draws": n_draws, "gib": a.device_data_gb, "seconds": gen_s,
+                                     "gb_per_s": n_draws * 8 / gen_s / 1e9, "steps_spread": spread}
         print(json.dumps(out))
     if hasattr(model, "close"):
         model.close()

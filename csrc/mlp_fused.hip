@@ -1069,7 +1069,12 @@ EM_API int em_mlp_fused_lds_bytes() { return TRAIN_LDS; }
 EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
                               const void* wimg, float* slabs, float* loss_slabs, int nslab, int loss_kind,
                               hipStream_t stream) {
-  if (!draws || !wimg || !slabs || !loss_slabs || nslab <= 0 || B < 0 || B + offset + 1 > (int64_t)INT32_MAX)
+  if (draws && !sidx && offset > 0) {  // sequential samples: 64-bit offsets (HBM-filling datasets) via the base
+    draws += offset;
+    offset = 0;
+  }
+  if (!draws || !wimg || !slabs || !loss_slabs || nslab <= 0 || B < 0 || offset < 0 ||
+      B + offset + 1 > (int64_t)INT32_MAX)
     return EM_ERR_ARG;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1107,7 +1112,12 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
 
 EM_API int em_mlp_fused_forward(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
                                 const void* wimg, float* logits, int nblocks, hipStream_t stream) {
-  if (!draws || !wimg || !logits || nblocks <= 0 || B + offset > (int64_t)INT32_MAX) return EM_ERR_ARG;
+  if (draws && !sidx && offset > 0) {
+    draws += offset;
+    offset = 0;
+  }
+  if (!draws || !wimg || !logits || nblocks <= 0 || B < 0 || offset < 0 || B + offset > (int64_t)INT32_MAX)
+    return EM_ERR_ARG;
   hipLaunchKernelGGL(mlp_fused_forward_kernel, dim3(nblocks), dim3(256), IMG_BYTES + LUT_BYTES, stream, draws, sidx,
                      (int)B, (int)offset,
                      (const uint8_t*)wimg, logits);

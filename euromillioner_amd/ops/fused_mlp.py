@@ -92,9 +92,11 @@ def _check_draws(draws: torch.Tensor, sidx: torch.Tensor | None, B: int, offset:
     if draws.dim() != 1:
         raise ValueError("masks must be a 1-D int64 tensor of feature masks (see rows_to_masks)")
     n = draws.shape[0]
-    if n >= 2**31 - 1:
-        raise ValueError("at most 2^31-2 draws per device")
+    if B >= 2**31 - 1:
+        raise ValueError("at most 2^31-2 samples per step")
     if sidx is not None:
+        if n >= 2**31 - 1:
+            raise ValueError("sample_idx addressing covers at most 2^31-2 draws (use sequential offsets)")
         N.check_cuda(sidx, "sample_idx", torch.int32)
         if sidx.numel() < B:
             raise ValueError("sample_idx shorter than B")

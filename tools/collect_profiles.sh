@@ -24,6 +24,8 @@ run wide_pmc 400 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_
 run bench_headline 300 python3 bench.py --steps 100 --warmup 10
 run bench_torch 300 python3 bench.py --steps 20 --warmup 3 --graph 0 --impl torch --no-eval
 run bench_wide 300 python3 bench.py --model mlp-wide --steps 10 --warmup 3
+run bench_mega_data 300 python3 bench.py --device-data-gb 200 --steps 50 --warmup 5
+run bench_mega_batch 300 python3 bench.py --device-data-gb 200 --batch 268435456 --steps 10 --warmup 2
 run gemm_bench 300 python3 tools/gemm_bench.py
 run rf_bench 300 python3 tools/rf_bench.py
 run gbdt_bench 300 python3 tools/gbdt_bench.py

@@ -48,11 +48,32 @@ def last_json(log: str) -> list[dict]:
     return out
 
 
+def mega_lines() -> list[str]:
+    """HBM-resident dataset runs (bench.py --device-data-gb), read from the committed jsonl lines."""
+    out = []
+    for name, label in (("bench_mega_data", "1M-sample steps streamed over the dataset"),
+                        ("bench_mega_batch", "mega-batch: 256M samples per optimizer step")):
+        path = os.path.join(DST, f"{name}.jsonl")
+        if not os.path.exists(path):
+            continue
+        j = [json.loads(x) for x in open(path) if x.strip()][-1]
+        g = j.get("device_datagen", {})
+        out.append(f"* {label}: **{j['value'] / 1e9:.2f} G samples/s**, {j['ms_per_step']:.3f} ms/step, "
+                   f"val acc {j.get('val', {}).get('acc', float('nan')):.4f}; dataset {g.get('gib', 0):.0f} GiB = "
+                   f"{g.get('draws', 0) / 1e9:.1f} G draws generated on the GPU in {g.get('seconds', 0):.2f} s")
+    if out:
+        out = ["### HBM-resident dataset (`bench.py --device-data-gb 200`, draws generated on the GPU)", ""] + out + [""]
+    return out
+
+
 def main():
     os.makedirs(DST, exist_ok=True)
     for d in ("fused", "wide", "rf", "gbdt"):
         shutil.copy(os.path.join(SRC, d, "run_kernel_stats.csv"), os.path.join(DST, f"kernel_stats_{d}.csv"))
-    for log in ("bench_headline", "bench_torch", "bench_wide", "gemm_bench", "rf_bench", "gbdt_bench"):
+    for log in ("bench_headline", "bench_torch", "bench_wide", "gemm_bench", "rf_bench", "gbdt_bench",
+                "bench_mega_data", "bench_mega_batch"):
+        if not os.path.exists(os.path.join(SRC, f"{log}.log")):
+            continue
         with open(os.path.join(DST, f"{log}.jsonl"), "w") as f:
             for j in last_json(f"{log}.log"):
                 f.write(json.dumps(j) + "\n")
@@ -92,6 +113,7 @@ def main():
         f"| MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES / SIMD-cycles) | {mfma_busy:.2f} | |",
         f"| SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE | {f2.get('SQ_LDS_BANK_CONFLICT', 0) / max(1, f2.get('SQ_LDS_IDX_ACTIVE', 1)):.2f} | |",
         "",
+        *mega_lines(),
         "## Wide MLP 62->8192->8192->62 (64k samples / step)",
         "",
         f"* bench: {wide['value'] / 1e6:.2f} M samples/s, {wide['ms_per_step']:.1f} ms/step, "
