@@ -101,6 +101,9 @@ def main():
                     help="HBM-resident dataset: generate this many GiB of draw masks on the GPU "
                          "(csrc/datagen.hip) instead of --draws-per-gpu on the host; the timed steps "
                          "are spread over the whole training split (no hipGraph: offsets change per step)")
+    ap.add_argument("--accum", type=int, default=1,
+                    help="mlp-wide: micro-batches of --batch per optimizer step (gradient accumulation; "
+                         "the per-GPU batch of the step is batch * accum)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="DP gradient all-reduce of the fused path: xgmi = one-shot peer-memory reduction fused "
                          "into Adam (hipGraph-replayable); rccl = torch.distributed all_reduce; auto = xgmi if the "
@@ -153,15 +156,18 @@ def main():
     n_samples = n_draws - 1
     margin = int(0.7 * n_samples)
     B = a.batch
-    if margin < B:
+    if a.accum < 1 or (a.accum > 1 and a.model != "mlp-wide"):
+        raise SystemExit("--accum applies to --model mlp-wide (the fused kernel takes any batch directly)")
+    BS = B * a.accum  # samples per GPU per optimizer step
+    if margin < BS:
         raise SystemExit("dataset too small for the batch")
 
-    n_off = max(1, (margin - B) // B)
+    n_off = max(1, (margin - BS) // BS)
     # device-data runs spread the warmup + timed steps over the whole training split
     spread = max(1, n_off // max(1, a.steps + a.warmup)) if a.device_data_gb > 0 else 1
 
     def boff(i):
-        return ((i * spread) % n_off) * B
+        return ((i * spread) % n_off) * BS
     sizes = (62, 128, 62)
     if a.model == "mlp-wide":
         from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
@@ -172,7 +178,7 @@ def main():
         model.broadcast_parameters()
 
         def step(i):
-            return model.step(draws, B, offset=boff(i))
+            return model.step(draws, B, offset=boff(i), accum=a.accum)
     elif a.impl == "fused":
         model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group, comm=a.comm)
         model.broadcast_parameters()
@@ -245,13 +251,15 @@ def main():
         iid = rows_to_masks(torch.from_numpy(iid_nums).to(dev))
         ev_iid = model.evaluate(iid, n_iid, offset=0)
 
-    value = B * world / (ms / 1000.0)
+    value = BS * world / (ms / 1000.0)
     desc = "mlp " + "->".join(str(x) for x in sizes) + " relu, " + (
         "grouped softmax-CE" if a.loss == "softmax" else "sigmoid-BCE")
     extra = {}
     if a.model == "mlp-wide":
-        tf = model.flops_per_sample() * B / (ms / 1000.0) / 1e12
+        tf = model.flops_per_sample() * BS / (ms / 1000.0) / 1e12
         extra = {"tflops_per_gpu": tf, "flops_per_sample": model.flops_per_sample()}
+        if a.accum > 1:
+            extra.update({"micro_batch": B, "accum": a.accum})
     if rank == 0:
         out = {
             "metric": "samples/sec training 3-layer MLP (62-in/62-out)",
@@ -270,8 +278,8 @@ def main():
                      "synthetic, generated on the GPU: %.1f GiB of HBM-resident draw masks per GPU (%d draws, "
                      "planted Markov p=%.2f; random-init weights)" % (a.device_data_gb, n_draws, a.planted)),
             "config": {"model": desc,
-                       "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
-                       "per_gpu_batch": B, "optimizer": "adam", "hipgraph": use_graph,
+                       "global_batch": BS * world, "seq_len": 1, "parallelism": f"dp{world}",
+                       "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none")},
             "train_loss_last": loss,
             "val": ev,

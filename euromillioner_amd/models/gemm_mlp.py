@@ -182,9 +182,12 @@ class GemmMLPTrainer:
             h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out, ct=ct)
         return h, inputs
 
-    def _backward(self, dz, inputs, ws, on_layer_done=None):
-        """Last layer first: wgrad + bias grad into the flat gradient buffer, then dgrad (act' fused)."""
+    def _backward(self, dz, inputs, ws, on_layer_done=None, accumulate: bool = False):
+        """Last layer first: wgrad + bias grad into the flat gradient buffer (added to it when
+        ``accumulate``: gradient accumulation over micro-batches), then dgrad (act' fused)."""
         L = len(self.offsets)
+        if self.f32 and accumulate:
+            raise ValueError("gradient accumulation runs on the bf16 path")
         if self.f32:
             for i in reversed(range(L)):
                 gw, gbias = self._views(self.grads, i)
@@ -199,12 +202,13 @@ class GemmMLPTrainer:
         plan = ws["plan"]
         for i in reversed(range(L)):
             gw, gbias = self._views(self.grads, i)
+            beta = 1.0 if accumulate else 0.0
             if plan["wgrad"][i]:
-                LIN.linear_wgrad_nt(ws["dzt"][i], ws["actt"][i], out=gw)
-                LIN.rowsum(ws["dzt"][i], out=gbias)
+                LIN.linear_wgrad_nt(ws["dzt"][i], ws["actt"][i], out=gw, beta=beta)
+                LIN.rowsum(ws["dzt"][i], out=gbias, accumulate=accumulate)
             else:
-                LIN.linear_wgrad(dz, inputs[i], out=gw)
-                LIN.colsum(dz, out=gbias, ws=ws["colsum_ws"])
+                LIN.linear_wgrad(dz, inputs[i], out=gw, beta=beta)
+                LIN.colsum(dz, out=gbias, accumulate=accumulate, ws=ws["colsum_ws"])
             if on_layer_done is not None:
                 on_layer_done(i)
             if i > 0:
@@ -223,15 +227,33 @@ class GemmMLPTrainer:
             self._checked = True
 
     def step(self, masks: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None,
-             global_batch: int | None = None) -> torch.Tensor:
-        """One optimizer step on B local samples; returns the global mean loss (device tensor)."""
-        self._check(masks, B, offset, sidx)
+             global_batch: int | None = None, accum: int = 1) -> torch.Tensor:
+        """One optimizer step on ``accum`` consecutive micro-batches of B local samples (gradient
+        accumulation: the mega-batch B * accum never has to fit as activations); returns the global
+        mean loss (device tensor)."""
+        if accum < 1 or (accum > 1 and sidx is not None):
+            raise ValueError("accum >= 1, and accumulation walks consecutive samples (no sample_idx)")
+        self._check(masks, B * accum, offset, sidx)
         ws = self._ws(B)
-        gb = global_batch if global_batch is not None else B * self.world
-        logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
-        dz, part = (LF if self.f32 else LIN).loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
+        gb = global_batch if global_batch is not None else B * accum * self.world
+        for k in range(accum - 1):  # all but the last micro-batch: local accumulation only
+            off = offset + k * B
+            logits, inputs = self._forward(masks, B, off, None, ws, train=True)
+            dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=off, grad_scale=1.0 / gb,
+                                     dz=ws["dz"][-1], partials=ws["part"])
+            if k == 0:
+                torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
+            else:
+                self.grads[self.P:] += part.sum()
+            self._backward(dz, inputs, ws, accumulate=k > 0)
+        last = offset + (accum - 1) * B
+        logits, inputs = self._forward(masks, B, last, sidx, ws, train=True)
+        dz, part = (LF if self.f32 else LIN).loss_grad(logits, masks, B, self.loss_name, offset=last, sidx=sidx,
                                                        grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
-        torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
+        if accum == 1:
+            torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
+        else:
+            self.grads[self.P:] += part.sum()
         self.grads[self.P:].mul_(1.0 / gb)
         handles = []
         hook = None
@@ -246,7 +268,7 @@ class GemmMLPTrainer:
                 for s0 in range(a, c, self.bucket_elems):
                     handles.append(dist.all_reduce(self.grads[s0:min(c, s0 + self.bucket_elems)],
                                                    op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-        self._backward(dz, inputs, ws, hook)
+        self._backward(dz, inputs, ws, hook, accumulate=accum > 1)
         for h in handles:
             h.wait()
         FM.adam_flat(self.params, self.grads[:self.P], self.m, self.v, self.hp, self.state, 1.0, shadow=self.shadow)

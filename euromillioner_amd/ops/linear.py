@@ -146,13 +146,16 @@ def linear_dgrad_nt(dz: torch.Tensor, wt: torch.Tensor, y_prev: torch.Tensor | N
     return gemm(dz, True, wt, True, out, M, K, N_, dact_src=y_prev, dact=dact, ct=ct)
 
 
-def linear_wgrad_nt(dzt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """wgrad from transposed copies: ``dzt`` [N, M], ``xt`` [K, M] -> fp32 ``dzt @ xt.T`` [N, K]."""
+def linear_wgrad_nt(dzt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None,
+                    beta: float = 0.0) -> torch.Tensor:
+    """wgrad from transposed copies: ``dzt`` [N, M], ``xt`` [K, M] -> fp32 ``dzt @ xt.T (+ beta * out)`` [N, K]."""
     N_, M = dzt.shape
     K = xt.shape[0]
     if out is None:
+        if beta != 0.0:
+            raise ValueError("beta needs an existing out")
         out = empty_aligned(N_, K, torch.float32, dzt.device)
-    return gemm(dzt, True, xt, True, out, N_, K, M)
+    return gemm(dzt, True, xt, True, out, N_, K, M, beta=beta)
 
 
 def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",

@@ -26,6 +26,7 @@ run bench_torch 300 python3 bench.py --steps 20 --warmup 3 --graph 0 --impl torc
 run bench_wide 300 python3 bench.py --model mlp-wide --steps 10 --warmup 3
 run bench_mega_data 300 python3 bench.py --device-data-gb 200 --steps 50 --warmup 5
 run bench_mega_batch 300 python3 bench.py --device-data-gb 200 --batch 268435456 --steps 10 --warmup 2
+run bench_wide_mega 400 python3 bench.py --model mlp-wide --device-data-gb 100 --accum 16 --steps 4 --warmup 1
 run gemm_bench 300 python3 tools/gemm_bench.py
 run rf_bench 300 python3 tools/rf_bench.py
 run gbdt_bench 300 python3 tools/gbdt_bench.py

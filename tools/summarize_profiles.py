@@ -52,13 +52,18 @@ def mega_lines() -> list[str]:
     """HBM-resident dataset runs (bench.py --device-data-gb), read from the committed jsonl lines."""
     out = []
     for name, label in (("bench_mega_data", "1M-sample steps streamed over the dataset"),
-                        ("bench_mega_batch", "mega-batch: 256M samples per optimizer step")):
+                        ("bench_mega_batch", "mega-batch: 256M samples per optimizer step"),
+                        ("bench_wide_mega", "wide MLP 62->8192->8192->62, 1M-sample steps (16 x 64k micro-batches, "
+                                            "gradient accumulation)")):
         path = os.path.join(DST, f"{name}.jsonl")
         if not os.path.exists(path):
             continue
         j = [json.loads(x) for x in open(path) if x.strip()][-1]
         g = j.get("device_datagen", {})
-        out.append(f"* {label}: **{j['value'] / 1e9:.2f} G samples/s**, {j['ms_per_step']:.3f} ms/step, "
+        rate = f"**{j['value'] / 1e9:.2f} G samples/s**" if j["value"] > 1e8 else f"**{j['value'] / 1e6:.2f} M samples/s**"
+        if "tflops_per_gpu" in j:
+            rate += f" ({j['tflops_per_gpu']:.0f} TFLOP/s)"
+        out.append(f"* {label}: {rate}, {j['ms_per_step']:.3f} ms/step, "
                    f"val acc {j.get('val', {}).get('acc', float('nan')):.4f}; dataset {g.get('gib', 0):.0f} GiB = "
                    f"{g.get('draws', 0) / 1e9:.1f} G draws generated on the GPU in {g.get('seconds', 0):.2f} s")
     if out:
@@ -71,7 +76,7 @@ def main():
     for d in ("fused", "wide", "rf", "gbdt"):
         shutil.copy(os.path.join(SRC, d, "run_kernel_stats.csv"), os.path.join(DST, f"kernel_stats_{d}.csv"))
     for log in ("bench_headline", "bench_torch", "bench_wide", "gemm_bench", "rf_bench", "gbdt_bench",
-                "bench_mega_data", "bench_mega_batch"):
+                "bench_mega_data", "bench_mega_batch", "bench_wide_mega"):
         if not os.path.exists(os.path.join(SRC, f"{log}.log")):
             continue
         with open(os.path.join(DST, f"{log}.jsonl"), "w") as f:
