@@ -32,7 +32,7 @@ _FLAGS = {
     "--to-date": "data.to_date", "--html-table-class": "data.html_table_class", "--train-pct": "data.train_pct",
     "--date-format": "data.date_format", "--label-column": "data.label_column", "--n-draws": "data.n_draws",
     "--seed": "data.seed", "--planted": "data.planted", "--lags": "data.lags", "--workdir": "data.workdir",
-    "--header": "data.header", "--fetch-jitter-ms": "data.fetch_jitter_ms",
+    "--header": "data.header", "--fetch-jitter-ms": "data.fetch_jitter_ms", "--device-gb": "data.device_gb",
     "--eta": "gbdt.eta", "--max-depth": "gbdt.max_depth", "--objective": "gbdt.objective",
     "--subsample": "gbdt.subsample", "--nthread": "gbdt.nthread", "--gamma": "gbdt.gamma",
     "--eval-metric": "gbdt.eval_metric", "--nround": "gbdt.nround", "--lambda": "gbdt.reg_lambda",
@@ -40,7 +40,7 @@ _FLAGS = {
     "--trees": "rf.n_trees", "--rf-max-depth": "rf.max_depth", "--min-samples-leaf": "rf.min_samples_leaf",
     "--feature-subset": "rf.feature_subset",
     "--hidden": "mlp.hidden", "--activation": "mlp.activation", "--loss": "mlp.loss", "--lr": "mlp.lr",
-    "--batch": "mlp.batch", "--steps": "mlp.steps", "--epochs": "mlp.epochs", "--dtype": "mlp.dtype",
+    "--batch": "mlp.batch", "--accum": "mlp.accum", "--steps": "mlp.steps", "--epochs": "mlp.epochs", "--dtype": "mlp.dtype",
     "--weight-decay": "mlp.weight_decay", "--eval-every": "mlp.eval_every",
     "--dp": "dist.dp", "--backend": "dist.backend", "--bucket-mb": "dist.bucket_mb", "--timeout": "dist.timeout_s",
     "--fault-at-step": "dist.fault_at_step", "--fault-rank": "dist.fault_rank",

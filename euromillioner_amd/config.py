@@ -36,7 +36,7 @@ REFERENCE_TABLE_CLASS = "table table-bordered table-condensed table-striped text
 
 @dataclasses.dataclass
 class DataConfig:
-    source: str = "synthetic"  # synthetic | csv | html | reference-csv
+    source: str = "synthetic"  # synthetic | csv | html | reference-csv | device (generated on the GPU)
     path: str | None = None
     from_date: str = "1900-01-01"
     to_date: str = "2020-06-14"
@@ -51,6 +51,7 @@ class DataConfig:
     workdir: str | None = None  # where the emn*.csv split files go (None: a temp dir, removed afterwards; D-h)
     header: str = "auto"  # CSV header handling: auto | yes | no (D-b / D-c)
     fetch_jitter_ms: int = 0  # Main.java:53-54 random pre-fetch sleep; accepted for parity, no network here
+    device_gb: float = 0.0  # source=device: GiB of HBM-resident draw masks (8 B each) unless n_draws is set
 
 
 @dataclasses.dataclass
@@ -97,6 +98,7 @@ class MLPConfig:
     eps: float = 1e-8
     weight_decay: float = 0.0
     batch: int = 1 << 20
+    accum: int = 1  # GEMM engine: micro-batches per optimizer step (gradient accumulation; batch % accum == 0)
     steps: int = 200
     epochs: int | None = None
     dtype: str = "bf16"
@@ -235,7 +237,7 @@ def apply_env(cfg: RunConfig, environ=None) -> None:
 CHOICES = {
     "model": ("gbdt", "rf", "mlp", "mlp-wide"),
     "device": ("auto", "cuda", "cpu"),
-    "data.source": ("synthetic", "csv", "html", "reference-csv"),
+    "data.source": ("synthetic", "csv", "html", "reference-csv", "device"),
     "gbdt.objective": ("reg:logistic", "binary:logistic", "reg:squarederror", "multi:softprob", "multi:softmax"),
     "gbdt.eval_metric": ("logloss", "rmse", "error", "mlogloss", "merror"),
     "gbdt.device": ("auto", "cuda", "cpu"),
@@ -254,6 +256,10 @@ def validate(cfg: RunConfig) -> RunConfig:
             obj = getattr(obj, part)
         if obj not in allowed:
             raise ValueError(f"{dotted}={obj!r}: expected one of {', '.join(allowed)}")
+    if cfg.mlp.accum < 1 or cfg.mlp.batch % cfg.mlp.accum:
+        raise ValueError(f"mlp.accum={cfg.mlp.accum}: must be >= 1 and divide mlp.batch={cfg.mlp.batch}")
+    if cfg.data.source == "device" and not cfg.data.n_draws and cfg.data.device_gb <= 0:
+        raise ValueError("data.source=device needs data.n_draws or data.device_gb")
     return cfg
 
 

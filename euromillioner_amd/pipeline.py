@@ -34,6 +34,8 @@ from .data.draws import DrawSet, featurize_raw, multi_hot, positional_split
 
 def load_draws(cfg: RunConfig) -> DrawSet:
     d = cfg.data
+    if d.source == "device":
+        raise ValueError("data.source=device (GPU-generated, HBM-resident draws) feeds MLP training only")
     if d.source == "synthetic":
         ds = DrawSet.synthetic(n=d.n_draws, seed=d.seed, planted=d.planted)
     elif d.source == "csv":

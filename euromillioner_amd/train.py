@@ -138,8 +138,12 @@ class _GemmEngine(_Engine):
                                     betas=tuple(m.betas), eps=m.eps, weight_decay=m.weight_decay, state_dict=sd,
                                     process_group=info.group, bucket_mb=cfg.dist.bucket_mb, dtype=m.dtype)
         self.masks = masks
+        self.accum = m.accum
 
     def step(self, idx, offset, B, global_batch):
+        k = self.accum
+        if k > 1:  # B consecutive samples as k micro-batches (gradient accumulation)
+            return self.model.step(self.masks, B // k, offset=offset, global_batch=global_batch, accum=k)
         return self.model.step(self.masks, B, offset=offset, sidx=idx, global_batch=global_batch)
 
     def evaluate(self, offset, n):
@@ -352,16 +356,29 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
     m = cfg.mlp
     sizes = _mlp_sizes(cfg)
     lags = cfg.data.lags
-    ds = load_draws(cfg)
-    n_samples = len(ds) - lags
+    device_data = cfg.data.source == "device"
+    if device_data:  # HBM-resident draws generated on the GPU (csrc/datagen.hip); no host copy
+        from .data.device_gen import gb_to_draws, generate_masks
+
+        if info.device.type != "cuda" or lags != 1:
+            raise ValueError("data.source=device needs a GPU and lags=1")
+        n_draws = int(cfg.data.n_draws) if cfg.data.n_draws else gb_to_draws(cfg.data.device_gb)
+        dmasks = generate_masks(n_draws, seed=cfg.data.seed, planted=cfg.data.planted, device=info.device)
+        ds = None
+        n_samples = n_draws - lags
+    else:
+        ds = load_draws(cfg)
+        n_samples = len(ds) - lags
     if n_samples < 4:
-        raise ValueError(f"need more draws than lags+3 (have {len(ds)})")
+        raise ValueError(f"need more draws than lags+3 (have {n_samples + lags})")
     margin = positional_split(n_samples, cfg.data.train_pct)
     a, b = D.shard_range(margin, info)
     shard = b - a
     if shard < 1:
         raise ValueError("training split smaller than the number of ranks")
     local_b = max(1, min(shard, math.ceil(m.batch / info.world)))
+    if m.accum > 1:
+        local_b = max(m.accum, local_b // m.accum * m.accum)
     global_b = local_b * info.world
     steps = m.steps if m.epochs is None else int(m.epochs) * math.ceil(shard / local_b)
 
@@ -378,11 +395,16 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
 
         sd = DrawMLP(sizes, activation=m.activation, loss=m.loss, seed=m.seed).state_dict()
     kind = _pick_engine(cfg, info, sizes)
+    if device_data and kind == "torch":
+        raise ValueError("data.source=device feeds the fused/GEMM engines (bf16, lags=1, no parameter averaging)")
+    if m.accum > 1 and kind != "gemm":
+        raise ValueError(f"mlp.accum applies to the GEMM engine (this run uses {kind}); the fused kernel takes "
+                         "any batch in one launch")
     dev = info.device
     if kind in ("fused", "gemm"):
         from .models.mlp import FusedSmallMLP
 
-        masks = FusedSmallMLP.prepare(torch.from_numpy(ds.numbers).to(dev))
+        masks = dmasks if device_data else FusedSmallMLP.prepare(torch.from_numpy(ds.numbers).to(dev))
         engine = _FusedEngine(cfg, info, masks, sd) if kind == "fused" else _GemmEngine(cfg, info, masks, sizes, sd)
         sample_base = 0  # sample i -> masks[i] -> masks[i+1]
     else:
@@ -399,8 +421,12 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
     log.info(f"mlp {'->'.join(map(str, sizes))} engine={engine.name} device={dev} world={info.world} "
              f"train={margin} (shard {shard}) val={n_samples - margin} batch={global_b} steps={steps}")
 
-    use_perm = m.shuffle and local_b < shard
+    # sample-level shuffles need int32 indices and a host permutation of the shard; device datasets
+    # (up to HBM size) and gradient accumulation shuffle whole windows of local_b samples instead
+    window_shuffle = device_data or m.accum > 1
+    use_perm = m.shuffle and local_b < shard and not window_shuffle
     per_epoch = max(1, shard // local_b)
+    wperm, wperm_epoch = None, -1
     perm, perm_epoch = None, -1
     ckpt_path = cfg.ckpt.path
     hist = []
@@ -428,13 +454,20 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
                 perm = torch.from_numpy((a + g.permutation(shard)).astype(np.int32)).to(dev)
                 perm_epoch = epoch
             idx = perm[k * local_b:(k + 1) * local_b]
+        elif window_shuffle:
+            epoch, k = divmod(step, per_epoch)
+            if m.shuffle and epoch != wperm_epoch:
+                wperm = np.random.default_rng([m.seed, info.rank, epoch]).permutation(per_epoch)
+                wperm_epoch = epoch
+            off += int(wperm[k] if m.shuffle else k) * local_b
         loss_t = engine.step(idx, off, local_b, global_b)
         done += 1
         if cfg.dist.check_sync_every and (step + 1) % cfg.dist.check_sync_every == 0:
             check_sync(engine, info)
         last = step == steps - 1
         if (m.eval_every and (step + 1) % m.eval_every == 0) or last:
-            ev = engine.evaluate(margin, n_samples - margin) if n_samples > margin else {}
+            n_val = n_samples - margin if not device_data else min(n_samples - margin, 1 << 24)
+            ev = engine.evaluate(margin, n_val) if n_samples > margin else {}
             loss = float(loss_t.reshape(-1)[0].item())
             hist.append({"step": step + 1, "loss": loss, **{f"val_{k}": v for k, v in ev.items()}})
             log.info(f"step {step + 1}/{steps} loss {loss:.5f} val_acc {ev.get('acc', float('nan')):.4f} "

@@ -88,3 +88,16 @@ def test_cli_rejects_bad_dtype_with_exit_2():
     from euromillioner_amd.cli import main
 
     assert main(["train", "--model", "mlp", "--dtype", "fp16", "--device", "cpu"]) == 2
+
+
+def test_device_source_and_accum_validation():
+    import pytest
+
+    from euromillioner_amd import config as C
+
+    with pytest.raises(ValueError):
+        C.build_config(None, {"data.source": "device"}, environ={})  # needs n_draws or device_gb
+    with pytest.raises(ValueError):
+        C.build_config(None, {"mlp.batch": 1000, "mlp.accum": 3}, environ={})
+    cfg = C.build_config(None, {"data.source": "device", "data.device_gb": 2.5, "mlp.accum": 4}, environ={})
+    assert cfg.data.device_gb == 2.5 and cfg.mlp.accum == 4

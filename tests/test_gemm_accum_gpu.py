@@ -24,3 +24,29 @@ def test_accumulated_step_matches_single_batch(sizes, B, accum):
     a.step(masks, B * accum, offset=100 + B * accum // 2)
     b.step(masks, B, offset=100 + B * accum // 2, accum=accum)
     assert (a.params - b.params).abs().max().item() < 5e-3
+
+
+def test_cli_device_data_with_accumulation():
+    """`euromillioner train --data-source device --accum 2` on the GEMM engine: learns the planted map."""
+    from euromillioner_amd import config as C
+    from euromillioner_amd.train import train
+
+    cfg = C.build_config(None, {"model": "mlp", "device": "cuda", "data.source": "device", "data.n_draws": 200001,
+                                "data.planted": 0.8, "data.seed": 3, "mlp.hidden": (256, 128), "mlp.batch": 4096,
+                                "mlp.accum": 2, "mlp.steps": 150, "mlp.lr": 0.005, "mlp.eval_every": 0,
+                                "log.level": "WARN"}, environ={})
+    res = train(cfg)
+    assert res["engine"] == "gemm"
+    assert res["val"]["acc"] > res["val"]["trivial_acc"] and res["val"]["hits_main"] > 1.0, res["val"]
+
+
+def test_cli_device_data_fused():
+    from euromillioner_amd import config as C
+    from euromillioner_amd.train import train
+
+    cfg = C.build_config(None, {"model": "mlp", "device": "cuda", "data.source": "device", "data.n_draws": 300001,
+                                "data.planted": 0.8, "mlp.batch": 8192, "mlp.steps": 150, "mlp.lr": 0.005,
+                                "mlp.eval_every": 0, "log.level": "WARN"}, environ={})
+    res = train(cfg)
+    assert res["engine"] == "fused"
+    assert res["val"]["acc"] > res["val"]["trivial_acc"] and res["val"]["hits_main"] > 1.0, res["val"]
