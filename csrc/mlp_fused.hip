@@ -938,6 +938,8 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint64_t ts[4] = {};  // V4_STAMPS: 100 MHz wall-clock marks (entry, prologue done, loop done, dW folded)
+  if (V4_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
   // wave w runs on SIMD w % 4: pairs 2/3 take their roles swapped so every SIMD hosts one role-0 and
   // one role-1 wave (role 1 owns the star group and issues ~20 % more VALU per tile)
   const int pair = wave >> 1, rho = (wave & 1) ^ (V4_MIX ? (wave >> 2) : 0);
@@ -960,6 +962,7 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   }
   if (lane < 2) reinterpret_cast<int*>(smem + V4_BASE + pair * V4_PAIR_BYTES + V4_PFL)[lane] = 0;
   __syncthreads();
+  if (V4_STAMPS) ts[1] = __builtin_amdgcn_s_memrealtime();
   // waves 4-7 share SIMDs with waves 0-3 (other pairs): start them half a tile later so the two
   // co-resident waves do not hit their MFMA and VALU phases in lockstep (MI355X_MICROARCH.md,
   // "Two waves per SIMD" item 9), and give the younger half static priority (item 4)
@@ -970,6 +973,7 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
     v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane, slab_spare);
   else
     v4_body<LOSS, 1>(smem, masks, sidx, B, offset, pair, lane, slab_spare);
+  if (V4_STAMPS) ts[2] = __builtin_amdgcn_s_memrealtime();
 
   const float* RED = reinterpret_cast<const float*>(smem);
   const float* DB2S = reinterpret_cast<const float*>(smem + V4_RED);
@@ -986,6 +990,11 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
     } else {
       *reinterpret_cast<f32x4*>(slab + P_W1 + col * HID + c0) = v;
     }
+  }
+  if (V4_STAMPS && tid == 0) {
+    ts[3] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) slab_spare[128 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
   }
   if (tid < 64) slab[P_B2 + tid] = DB2S[tid] + DB2S[64 + tid] + DB2S[128 + tid] + DB2S[192 + tid];
   if (tid == 0) {

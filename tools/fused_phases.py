@@ -37,6 +37,20 @@ def main():
     st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
     if not st.any():
         raise SystemExit("no stamps recorded: build with --define V4_STAMPS=1")
+    raw = m.slabs[:nslab, FM.P_TOTAL + 128:FM.P_TOTAL + 132].contiguous().view(torch.int32).cpu().numpy()
+    t = raw.astype(np.int64) & 0xFFFFFFFF
+    t -= t[:, 0].min()
+    us = t / 100.0  # s_memrealtime ticks at 100 MHz
+    print(f"block wall clock (us, {nslab} blocks): entry spread {us[:, 0].max():.2f}; "
+          f"prologue {np.mean(us[:, 1] - us[:, 0]):.2f}; loop {np.mean(us[:, 2] - us[:, 1]):.2f} "
+          f"(max {np.max(us[:, 2] - us[:, 1]):.2f}); dW fold {np.mean(us[:, 3] - us[:, 2]):.2f}; "
+          f"first entry -> last fold {us[:, 3].max():.2f}")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"kernel (event) {ev0.elapsed_time(ev1) * 1e3:.2f} us")
     for role in (0, 1):
         v = st[:, role::2, :].reshape(-1, 10).mean(0)
         tot = v.sum()
