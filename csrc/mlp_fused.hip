@@ -597,12 +597,16 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 
   // ---- F1 (own hidden half) -> relu -> hT (B of F2) + own H image [32 samples][64 hid] ----
   bf16x8 hT[2][2];
+  // both hidden tiles' chains interleaved: 8 independent-pair MFMAs back to back on the matrix pipe
+  f32x16 a1s[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+      a1s[tt] = mfma32(lds_frag(smem, w1t_off(32 * (2 * RHO + tt) + r, 2 * q + h)), xf[q], a1s[tt]);
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    const int t = 2 * RHO + tt;
-    f32x16 a1 = f32x16{};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a1 = mfma32(lds_frag(smem, w1t_off(32 * t + r, 2 * q + h)), xf[q], a1);
+    const f32x16& a1 = a1s[tt];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       hT[tt][q] = relu_pack(a1, q);
