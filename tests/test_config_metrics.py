@@ -101,3 +101,23 @@ def test_device_source_and_accum_validation():
         C.build_config(None, {"mlp.batch": 1000, "mlp.accum": 3}, environ={})
     cfg = C.build_config(None, {"data.source": "device", "data.device_gb": 2.5, "mlp.accum": 4}, environ={})
     assert cfg.data.device_gb == 2.5 and cfg.mlp.accum == 4
+
+
+def test_profile_dir_writes_a_chrome_trace(tmp_path):
+    """--profile-dir exports a torch.profiler trace of the first profile_steps steps."""
+    import os
+
+    from euromillioner_amd.train import train
+
+    cfg = C.build_config(None, {"model": "mlp", "device": "cpu", "data.n_draws": 400, "data.seed": 1,
+                                "mlp.steps": 4, "mlp.batch": 64, "mlp.eval_every": 0, "log.level": "WARN",
+                                "log.profile_dir": str(tmp_path), "log.profile_steps": 2}, environ={})
+    train(cfg)
+    files = [f for f in os.listdir(tmp_path) if f.endswith(".json")]
+    assert files, os.listdir(tmp_path)
+    assert os.path.getsize(os.path.join(tmp_path, files[0])) > 100
+
+
+def test_fetch_jitter_flag_is_accepted():
+    cfg = C.build_config(None, {"data.fetch_jitter_ms": "250"}, environ={})
+    assert cfg.data.fetch_jitter_ms == 250
