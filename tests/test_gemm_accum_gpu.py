@@ -50,3 +50,24 @@ def test_cli_device_data_fused():
     res = train(cfg)
     assert res["engine"] == "fused"
     assert res["val"]["acc"] > res["val"]["trivial_acc"] and res["val"]["hits_main"] > 1.0, res["val"]
+
+
+@pytest.mark.parametrize("args", [["--device-data-gb", "0.25", "--steps", "3", "--warmup", "1"],
+                                  ["--model", "mlp-wide", "--hidden", "512,512", "--batch", "8192", "--accum", "2",
+                                   "--device-data-gb", "0.25", "--steps", "3", "--warmup", "1"]])
+def test_bench_device_data_modes(args):
+    """bench.py's HBM-resident-data and gradient-accumulation modes print one valid JSON line."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["value"] > 0 and d["steps"] == 3 and "device_datagen" in d
+    if "--accum" in args:
+        assert d["config"]["per_gpu_batch"] == 16384 and d["accum"] == 2
