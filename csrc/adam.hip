@@ -73,9 +73,12 @@ EM_DEVICE void adam_end(int* state, int t) {
   }
 }
 
-// torch.optim.Adam update of parameter p with gradient g (pad slots of the MLP image pinned to 0)
-EM_DEVICE void adam_apply(int p, float g, int tstep, float* __restrict__ params, float* __restrict__ m,
-                          float* __restrict__ v, const float* __restrict__ hp, uint8_t* __restrict__ mlp_img) {
+// torch.optim.Adam update of parameter p with gradient g (pad slots of the MLP image pinned to 0).
+// w0/m0/v0 are params[p]/m[p]/v[p], loaded by the caller (the slab kernel issues those loads
+// before its slab reduction so their latency overlaps it).
+EM_DEVICE void adam_apply_loaded(int p, float g, float w0, float m0, float v0, int tstep, float* __restrict__ params,
+                                 float* __restrict__ m, float* __restrict__ v, const float* __restrict__ hp,
+                                 uint8_t* __restrict__ mlp_img) {
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
   const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
   if (mlp_img && mlp_pad_slot(p)) {
@@ -84,16 +87,21 @@ EM_DEVICE void adam_apply(int p, float g, int tstep, float* __restrict__ params,
     v[p] = 0.f;
     mlp_pack_one(p, 0.f, mlp_img);
   } else {
-    float w = params[p];
+    float w = w0;
     g += wd * w;
-    const float mm = b1 * m[p] + (1.f - b1) * g;
-    const float vv = b2 * v[p] + (1.f - b2) * g * g;
+    const float mm = b1 * m0 + (1.f - b1) * g;
+    const float vv = b2 * v0 + (1.f - b2) * g * g;
     m[p] = mm;
     v[p] = vv;
     w -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
     params[p] = w;
     if (mlp_img) mlp_pack_one(p, w, mlp_img);
   }
+}
+
+EM_DEVICE void adam_apply(int p, float g, int tstep, float* __restrict__ params, float* __restrict__ m,
+                          float* __restrict__ v, const float* __restrict__ hp, uint8_t* __restrict__ mlp_img) {
+  adam_apply_loaded(p, g, params[p], m[p], v[p], tstep, params, m, v, hp, mlp_img);
 }
 
 // 16 threads per parameter (slab-split, all loads issued up front), 64 parameters per 1024-thread block.
@@ -171,6 +179,13 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
   const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int p0 = blockIdx.x * 64 + 4 * q;
   const float* src = slabs + p0;
+  float w0 = 0.f, m0 = 0.f, v0 = 0.f;  // Adam operands, in flight during the slab reduction
+  if (mode != 1 && threadIdx.x < 64) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    w0 = params[p];
+    m0 = m[p];
+    v0 = v[p];
+  }
   f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
   int sl = g;
   for (; sl + 15 * A4_G < nslab; sl += 16 * A4_G) {
@@ -196,7 +211,7 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
     for (int k = 0; k < A4_G; ++k) t += part[k][pq][e];
     const float gsum = t * grad_scale;
     if (mode == 1) grad_io[p] = gsum;
-    else adam_apply(p, gsum, tstep, params, m, v, hp, mlp_img);
+    else adam_apply_loaded(p, gsum, w0, m0, v0, tstep, params, m, v, hp, mlp_img);
   }
   if (mode != 1) adam_end(state, tstep);
 }
