@@ -5,13 +5,22 @@ BASELINE.json metric "samples/sec training 3-layer MLP (62-in/62-out) at 1/2/4/8
 MI355X; val acc", config "3-layer MLP (62->128->62) bf16 on 1xMI355X, 1M-row
 synthetic batch" (DP=N over RCCL for N>1).
 
-* one process per GPU (torchrun), RCCL ("nccl") all-reduce of the flat gradient;
-* weak scaling: every rank trains on its own 1M-row batch per step (global batch
-  = N x 1M), each rank reading its own shard of an HBM-resident synthetic draw
-  sequence (planted Markov structure, seeded);
+* one process per GPU: under torchrun (``WORLD_SIZE`` set) this process is one rank; with
+  ``--gpus N > 1`` and no ``WORLD_SIZE`` it launches N ranks itself
+  (``euromillioner_amd/parallel/launch.py``: subprocesses, no GPU call in the parent, no exec)
+  and exits with the first failing rank's code;
+* DP gradient all-reduce: the xGMI one-shot reduction fused into Adam when the node passes its
+  self-test, else RCCL ("nccl") all-reduce of the flat gradient;
+* weak scaling: every rank trains on its own 1M-row batch per step (global batch = N x 1M);
+* ONE task for every rank: one synthetic draw sequence (one seed, so one planted Markov map)
+  of N x draws-per-gpu draws generated on the GPU; the first 70% is the training split and the
+  last 30% the validation split (positional, as ``Main.java:83-84,103-104``); rank r generates and
+  trains on the r-th contiguous shard of the training split and evaluates the r-th shard of the
+  validation split (metrics summed over ranks);
 * a timed step = fused fwd+loss+bwd launch, [all-reduce], fused Adam launch —
   the full optimizer step, nothing skipped;
-* K steps timed between barrier + synchronize on both sides, MAX over ranks;
+* K steps timed between barrier + synchronize on both sides, MAX over ranks; per-step
+  hipEvent times give the median step and the slowest rank's median;
 * after timing, validation metrics on a held-out positional 30% split
   (outside the timed region).
 """
@@ -77,18 +86,20 @@ class _TorchBaseline:
         return draw_metrics_torch(z, y.float(), self.loss_name)
 
 
-def main():
+def _parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="ranks (one per GPU); without a torchrun env, N > 1 launches N processes")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1 << 20, help="rows per GPU per step (1M)")
-    ap.add_argument("--draws-per-gpu", type=int, default=(1 << 24) + 1)
+    ap.add_argument("--draws-per-gpu", type=int, default=1 << 24,
+                    help="draws of the shared sequence per rank (rounded up to whole 4096-draw segments)")
     ap.add_argument("--loss", default="softmax", choices=["softmax", "bce"])
     ap.add_argument("--lr", type=float, default=3e-3)
     ap.add_argument("--planted", type=float, default=0.9)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--graph", type=int, default=1, help="replay the step from a hipGraph (1 GPU)")
+    ap.add_argument("--graph", type=int, default=1, help="replay the step from hipGraphs (needs a graph-safe step)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="fused = our HIP kernels (headline); torch = plain PyTorch/hipBLASLt eager (comparison)")
@@ -98,9 +109,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks sharing one GPU)")
     ap.add_argument("--device-data-gb", type=float, default=0.0,
-                    help="HBM-resident dataset: generate this many GiB of draw masks on the GPU "
-                         "(csrc/datagen.hip) instead of --draws-per-gpu on the host; the timed steps "
-                         "are spread over the whole training split (no hipGraph: offsets change per step)")
+                    help="HBM-resident dataset: this many GiB of draw masks per GPU (replaces --draws-per-gpu); "
+                         "the timed steps are spread over the whole training shard (no hipGraph: offsets "
+                         "change per step)")
     ap.add_argument("--accum", type=int, default=1,
                     help="mlp-wide: micro-batches of --batch per optimizer step (gradient accumulation; "
                          "the per-GPU batch of the step is batch * accum)")
@@ -108,17 +119,66 @@ def main():
                     help="DP gradient all-reduce of the fused path: xgmi = one-shot peer-memory reduction fused "
                          "into Adam (hipGraph-replayable); rccl = torch.distributed all_reduce; auto = xgmi if the "
                          "node passes its self-test")
-    a = ap.parse_args()
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launched multi-rank job: kill every rank after this many seconds")
+    return ap.parse_args()
+
+
+SEG = 4096  # device generator segment (a rank's shard starts on a segment boundary)
+
+
+class _Shards:
+    """One draw sequence of ``world * n_loc`` draws; positional 70/30 split; rank r's contiguous
+    shard of each split (``parallel.dist.shard_range``)."""
+
+    def __init__(self, n_loc: int, rank: int, world: int):
+        from euromillioner_amd.parallel.dist import DistInfo, shard_range
+
+        self.n_draws = n_loc * world
+        self.n_samples = self.n_draws - 1  # sample t = (draw t -> draw t+1)
+        self.margin = int(0.7 * self.n_samples)
+        info = DistInfo(rank, world)
+        self.train = shard_range(self.margin, info)  # sample range [a, b) of this rank
+        va, vb = shard_range(self.n_samples - self.margin, info)
+        self.val = (self.margin + va, self.margin + vb)
+
+    @staticmethod
+    def materialize(rng, seed, planted, dev):
+        """Masks covering samples [a, b) (draws a .. b) -> (buffer, offset of sample a in it)."""
+        from euromillioner_amd.data.device_gen import generate_masks, region
+
+        a, b = rng
+        first, n, skip = region(a, b + 1, SEG)
+        return generate_masks(n, seed=seed, planted=planted, seg_len=SEG, device=dev, first=first), skip
+
+
+def main():
+    a = _parse()
+    from euromillioner_amd.parallel import launch
+
+    try:
+        world, must_spawn = launch.requested_world(a.gpus)
+    except ValueError as e:
+        raise SystemExit(f"bench.py: {e}")
+    if must_spawn:
+        # this process never touches the GPU: N children, rank 0's stdout is the job's stdout
+        argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(launch.spawn(argv, world, timeout_s=a.launch_timeout, quiet_ranks=True))
+
     if a.model == "mlp-wide":
         if a.batch == 1 << 20:
             a.batch = 1 << 16
-        if a.draws_per_gpu == (1 << 24) + 1:
-            a.draws_per_gpu = (1 << 20) * 3 + 1
+        if a.draws_per_gpu == 1 << 24:
+            a.draws_per_gpu = (1 << 20) * 3
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(torch.cuda.device_count(), 1)  # (identity on a node with >= N GPUs)
+    ndev = max(torch.cuda.device_count(), 1)
+    if local >= ndev:
+        if world > 1 and a.dist_backend == "nccl":
+            raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs (found {ndev}); "
+                             "use --dist-backend gloo to rehearse ranks sharing a GPU")
+        local %= ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
@@ -132,42 +192,37 @@ def main():
         else:
             dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
         group = dist.group.WORLD
+        if dist.get_world_size() != world:
+            raise SystemExit("bench.py: process group size != WORLD_SIZE")
 
-    from euromillioner_amd.data.synthetic import generate_draws
+    from euromillioner_amd.data.device_gen import gb_to_draws
     from euromillioner_amd.models.mlp import FusedSmallMLP
 
-    from euromillioner_amd.ops.fused_mlp import rows_to_masks
-
-    gen_s = None
+    n_loc = gb_to_draws(a.device_data_gb) if a.device_data_gb > 0 else a.draws_per_gpu
+    n_loc = -(-n_loc // SEG) * SEG
+    sh = _Shards(n_loc, rank, world)
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    draws, tr_skip = sh.materialize(sh.train, a.seed, a.planted, dev)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - tg
     if a.device_data_gb > 0:
-        from euromillioner_amd.data.device_gen import gb_to_draws, generate_masks
+        a.graph = 0  # per-step offsets walk the whole training shard
 
-        n_draws = gb_to_draws(a.device_data_gb)
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        draws = generate_masks(n_draws, seed=a.seed + 1000 * rank, planted=a.planted, device=dev)
-        torch.cuda.synchronize()
-        gen_s = time.perf_counter() - tg
-        a.graph = 0  # per-step offsets walk the whole dataset
-    else:
-        n_draws = a.draws_per_gpu
-        nums, _ = generate_draws(n_draws, seed=a.seed + 1000 * rank, planted=a.planted, native=True)
-        draws = rows_to_masks(torch.from_numpy(nums).to(dev))  # device feature masks (8 B / draw)
-    n_samples = n_draws - 1
-    margin = int(0.7 * n_samples)
     B = a.batch
     if a.accum < 1 or (a.accum > 1 and a.model != "mlp-wide"):
         raise SystemExit("--accum applies to --model mlp-wide (the fused kernel takes any batch directly)")
     BS = B * a.accum  # samples per GPU per optimizer step
-    if margin < BS:
+    n_train = sh.train[1] - sh.train[0]
+    if n_train < BS:
         raise SystemExit("dataset too small for the batch")
 
-    n_off = max(1, (margin - BS) // BS)
-    # device-data runs spread the warmup + timed steps over the whole training split
+    n_off = max(1, (n_train - BS) // BS + 1)
+    # device-data runs spread the warmup + timed steps over the whole training shard
     spread = max(1, n_off // max(1, a.steps + a.warmup)) if a.device_data_gb > 0 else 1
 
     def boff(i):
-        return ((i * spread) % n_off) * BS
+        return tr_skip + ((i * spread) % n_off) * BS
     sizes = (62, 128, 62)
     if a.model == "mlp-wide":
         from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
@@ -189,17 +244,16 @@ def main():
         model = _TorchBaseline(dev, a, draws, B, group)
 
         def step(i):
-            return model.step((i % n_off) * B)
+            return model.step(boff(i))
 
     use_graph = bool(a.graph) and (world == 1 or getattr(model, "graph_safe", False))
-    graph = None
     loss_t = None
     for i in range(a.warmup):
         loss_t = step(i)
     torch.cuda.synchronize()
     if use_graph:
-        # offsets baked into graph nodes: capture n_off variants lazily would be heavy; capture a
-        # ring of G graphs with distinct offsets and replay them round-robin.
+        # offsets are baked into graph nodes: capture a ring of G graphs with distinct offsets
+        # and replay them round-robin
         G = min(n_off, 8)
         graphs = []
         s = torch.cuda.Stream()
@@ -212,14 +266,15 @@ def main():
                 graphs.append(g)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        graph = graphs
 
         def run(i):
-            graph[i % len(graph)].replay()
+            graphs[i % len(graphs)].replay()
     else:
         def run(i):
             step(i)
 
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     if world > 1:
         import torch.distributed as dist
 
@@ -227,28 +282,41 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
+        ev0[i].record()
         run(i)
+        ev1[i].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1000.0 / a.steps
+    step_ms = sorted(e0.elapsed_time(e1) for e0, e1 in zip(ev0, ev1))
+    med = step_ms[len(step_ms) // 2] if step_ms else float("nan")
     if hasattr(model, "check_comm"):
         model.check_comm()  # an xGMI peer wait that timed out is an error, not a fast step
+    med_max = med
     if world > 1:
-        t = torch.tensor([ms], device=dev)
+        t = torch.tensor([ms, med], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms = float(t.item())
+        ms, med_max = float(t[0].item()), float(t[1].item())
+    if rank == 0 and (t1 - t0) < 0.05:
+        print(f"bench.py: warning: timed window {1000 * (t1 - t0):.1f} ms < 50 ms; use more --steps for a "
+              "stable number", file=sys.stderr)
     loss = float(loss_t.reshape(-1)[0].item()) if loss_t is not None else float("nan")
 
     ev, ev_iid = {}, {}
     if not a.no_eval:
-        n_val = n_samples - margin if a.device_data_gb <= 0 else min(n_samples - margin, 1 << 24)
-        ev = model.evaluate(draws, n_val, offset=margin)
+        del draws
+        torch.cuda.empty_cache()
+        va, vb = sh.val
+        if a.device_data_gb > 0:  # cap the validation work (the full split can be tens of GiB)
+            vb = min(vb, va + max(1, (1 << 24) // world))
+        vdraws, v_skip = sh.materialize((va, vb), a.seed, a.planted, dev)
+        ev = model.evaluate(vdraws, vb - va, offset=v_skip)
+        del vdraws
         # the same model on iid draws (no planted structure): must sit at chance
-        n_iid = min(1 << 20, n_samples - margin)
-        iid_nums, _ = generate_draws(n_iid + 1, seed=a.seed + 777 + 1000 * rank, planted=0.0, native=True)
-        iid = rows_to_masks(torch.from_numpy(iid_nums).to(dev))
+        n_iid = -(-(1 << 20) // (world * SEG)) * SEG  # per rank
+        iid = _Shards.materialize((rank * n_iid, (rank + 1) * n_iid), a.seed + 777, 0.0, dev)[0]
         ev_iid = model.evaluate(iid, n_iid, offset=0)
 
     value = BS * world / (ms / 1000.0)
@@ -273,23 +341,26 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": ("synthetic (seeded Euromillions draws, planted Markov p=%.2f; random-init weights)" % a.planted
-                     if a.device_data_gb <= 0 else
-                     "synthetic, generated on the GPU: %.1f GiB of HBM-resident draw masks per GPU (%d draws, "
-                     "planted Markov p=%.2f; random-init weights)" % (a.device_data_gb, n_draws, a.planted)),
+            "data": ("synthetic, generated on the GPU: one seeded Euromillions draw sequence of %d draws "
+                     "(%d per GPU%s), planted Markov p=%.2f, shared by all ranks; positional 70/30 split, "
+                     "contiguous shard per rank; random-init weights"
+                     % (sh.n_draws, n_loc, ", %.1f GiB HBM-resident" % a.device_data_gb if a.device_data_gb > 0
+                        else "", a.planted)),
             "config": {"model": desc,
                        "global_batch": BS * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
-                       "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none")},
+                       "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
+                       "dist_backend": a.dist_backend if world > 1 else None},
+            "ms_per_step_median": med,
+            "ms_per_step_max_rank": med_max,
             "train_loss_last": loss,
             "val": ev,
             "val_iid": ev_iid,
+            "datagen": {"draws": n_loc, "seconds": gen_s, "gb_per_s": n_loc * 8 / max(gen_s, 1e-9) / 1e9,
+                        "steps_spread": spread},
             **extra,
         }
-        if gen_s is not None:
-            out["device_datagen"] = {"draws": n_draws, "gib": a.device_data_gb, "seconds": gen_s,
-                                     "gb_per_s": n_draws * 8 / gen_s / 1e9, "steps_spread": spread}
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if hasattr(model, "close"):
         model.close()
     if world > 1:

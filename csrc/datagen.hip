@@ -59,14 +59,15 @@ EM_DEVICE uint64_t gen_one(SplitMix& g, uint64_t prev, bool planted, uint32_t th
 constexpr int GEN_T = 256, GEN_LINE = 16;  // masks per 128-B line
 
 __global__ void __launch_bounds__(GEN_T)
-gen_masks_kernel(uint64_t seed, uint32_t thr, int64_t n, int64_t seg_len, int64_t nseg,
+gen_masks_kernel(uint64_t seed, uint32_t thr, int64_t n, int64_t seg_len, int64_t nseg, int64_t seg0,
                  const int32_t* __restrict__ perm, uint64_t* __restrict__ out) {
   __shared__ uint8_t P[64];
   if (threadIdx.x < 62) P[threadIdx.x] = (uint8_t)perm[threadIdx.x];
   __syncthreads();
   const int64_t seg = (int64_t)blockIdx.x * GEN_T + threadIdx.x;
   if (seg >= nseg) return;
-  SplitMix g{mix64(seed ^ ((uint64_t)(seg + 1) * SEG_SALT))};
+  // global segment index seg0 + seg: a shard of one long sequence starts at draw seg0 * seg_len
+  SplitMix g{mix64(seed ^ ((uint64_t)(seg0 + seg + 1) * SEG_SALT))};
   const int64_t t0 = seg * seg_len, t1 = (t0 + seg_len < n) ? t0 + seg_len : n;
   uint64_t prev = 0;
   bool first = true;
@@ -94,16 +95,23 @@ gen_masks_kernel(uint64_t seed, uint32_t thr, int64_t n, int64_t seg_len, int64_
 
 }  // namespace
 
-// masks[n] (int64, 16-B aligned) <- segmented synthetic draws; seg_len must be a multiple of 16
-EM_API int em_gen_masks(uint64_t seed, uint32_t planted_thr, int64_t n, int64_t seg_len, const int32_t* perm,
-                        uint64_t* out, hipStream_t stream) {
-  if (n <= 0 || seg_len <= 0 || seg_len % GEN_LINE || !perm || !out || ((uintptr_t)out & 15)) return EM_ERR_ARG;
+// masks[n] (int64, 16-B aligned) <- draws [seg0 * seg_len, seg0 * seg_len + n) of the segmented synthetic
+// sequence (seg0 > 0: a rank's shard of one sequence); seg_len must be a multiple of 16
+EM_API int em_gen_masks_at(uint64_t seed, uint32_t planted_thr, int64_t n, int64_t seg_len, int64_t seg0,
+                           const int32_t* perm, uint64_t* out, hipStream_t stream) {
+  if (n <= 0 || seg_len <= 0 || seg_len % GEN_LINE || seg0 < 0 || !perm || !out || ((uintptr_t)out & 15))
+    return EM_ERR_ARG;
   if (planted_thr > (1u << 24)) return EM_ERR_ARG;
   const int64_t nseg = (n + seg_len - 1) / seg_len;
   const int64_t nb = (nseg + GEN_T - 1) / GEN_T;
   if (nb > 0x7FFFFFFF) return EM_ERR_ARG;
   hipLaunchKernelGGL(gen_masks_kernel, dim3((unsigned)nb), dim3(GEN_T), 0, stream, seed, planted_thr, n, seg_len,
-                     nseg, perm, out);
+                     nseg, seg0, perm, out);
   EM_CHECK_LAUNCH();
   return 0;
+}
+
+EM_API int em_gen_masks(uint64_t seed, uint32_t planted_thr, int64_t n, int64_t seg_len, const int32_t* perm,
+                        uint64_t* out, hipStream_t stream) {
+  return em_gen_masks_at(seed, planted_thr, n, seg_len, 0, perm, out, stream);
 }

@@ -114,6 +114,20 @@ def main(argv=None) -> int:
         return 2
     L.setup(cfg.log.level, rank=int(os.environ.get("RANK", "0")) if "RANK" in os.environ else None)
     log = L.get("Main")
+    if a.cmd in ("run", "train"):
+        # --dp N: N ranks on this node.  Under torchrun (WORLD_SIZE set) it must match the launch;
+        # otherwise this process starts the N ranks itself (parallel/launch.py) and waits.
+        from .parallel import launch
+
+        try:
+            world, must_spawn = launch.requested_world(cfg.dist.dp)
+        except ValueError as e:
+            log.error(f"invalid configuration: {e}")
+            return 2
+        if must_spawn:
+            log.info(f"launching {world} ranks (127.0.0.1 rendezvous)")
+            return launch.spawn([sys.executable, "-m", "euromillioner_amd"] + argv, world,
+                                timeout_s=float(os.environ.get("EUROM_LAUNCH_TIMEOUT", "86400")))
     try:
         if a.cmd == "run":
             from .pipeline import run_reference_pipeline

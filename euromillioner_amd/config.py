@@ -109,7 +109,7 @@ class MLPConfig:
 
 @dataclasses.dataclass
 class DistConfig:
-    dp: int = 1
+    dp: int = 1  # ranks on this node: > 1 without a torchrun env -> the CLI launches them (parallel/launch.py)
     backend: str = "auto"  # auto -> nccl (RCCL) on GPU, gloo on CPU
     bucket_mb: float = 25.0
     timeout_s: float = 300.0
@@ -258,6 +258,8 @@ def validate(cfg: RunConfig) -> RunConfig:
             raise ValueError(f"{dotted}={obj!r}: expected one of {', '.join(allowed)}")
     if cfg.mlp.accum < 1 or cfg.mlp.batch % cfg.mlp.accum:
         raise ValueError(f"mlp.accum={cfg.mlp.accum}: must be >= 1 and divide mlp.batch={cfg.mlp.batch}")
+    if cfg.dist.dp < 1 or cfg.dist.dp > 64:
+        raise ValueError(f"dist.dp={cfg.dist.dp}: must be in 1..64 (ranks of one node)")
     if cfg.data.source == "device" and not cfg.data.n_draws and cfg.data.device_gb <= 0:
         raise ValueError("data.source=device needs data.n_draws or data.device_gb")
     return cfg

@@ -47,14 +47,22 @@ def planted_threshold(planted: float) -> int:
     return int(round(planted * (1 << 24)))
 
 
-def generate_masks_py(n: int, seed: int = 0, planted: float = 0.0, seg_len: int = 4096) -> np.ndarray:
-    """Specification: draw masks [n] int64 (slow; for tests and small n)."""
+def _check_first(first: int, seg_len: int) -> int:
+    if first < 0 or first % seg_len:
+        raise ValueError(f"first ({first}) must be a non-negative multiple of seg_len ({seg_len})")
+    return first // seg_len
+
+
+def generate_masks_py(n: int, seed: int = 0, planted: float = 0.0, seg_len: int = 4096, first: int = 0) -> np.ndarray:
+    """Specification: draws [first, first + n) of the sequence as masks [n] int64 (slow; for tests and
+    small n).  ``first`` must be a multiple of ``seg_len`` (a shard starts on a segment boundary)."""
+    seg0 = _check_first(first, seg_len)
     perm = permutations(seed)
     pim, pis = perm[:50], perm[50:]
     thr = planted_threshold(planted)
     out = np.zeros(n, dtype=np.uint64)
     for seg in range((n + seg_len - 1) // seg_len):
-        g = _SplitMix64(_seg_seed(seed, seg))
+        g = _SplitMix64(_seg_seed(seed, seg0 + seg))
 
         def rng_range(k: int) -> int:
             return ((g.next() >> 32) * k) >> 32
@@ -82,8 +90,11 @@ def generate_masks_py(n: int, seed: int = 0, planted: float = 0.0, seg_len: int 
 
 
 def generate_masks(n: int, seed: int = 0, planted: float = 0.0, seg_len: int = 4096,
-                   device: torch.device | str = "cuda", out: torch.Tensor | None = None) -> torch.Tensor:
-    """Draw masks [n] int64 generated on the GPU (``em_gen_masks``), HBM-resident."""
+                   device: torch.device | str = "cuda", out: torch.Tensor | None = None, first: int = 0) -> torch.Tensor:
+    """Draws [first, first + n) of the sequence as masks [n] int64 generated on the GPU
+    (``em_gen_masks_at``), HBM-resident.  Every rank of a data-parallel job passes the same seed
+    (same planted maps = same task) and its own ``first`` (a disjoint shard of one sequence)."""
+    seg0 = _check_first(first, seg_len)
     from ..ops import _native as N
 
     if n <= 0 or seg_len <= 0:
@@ -94,11 +105,20 @@ def generate_masks(n: int, seed: int = 0, planted: float = 0.0, seg_len: int = 4
     elif out.dtype != torch.int64 or out.numel() < n or not out.is_contiguous():
         raise ValueError("out must be a contiguous int64 tensor with >= n elements")
     perm = torch.from_numpy(permutations(seed)).to(dev)
-    N.call("em_gen_masks", seed & M64, planted_threshold(planted), n, seg_len, perm.data_ptr(), out.data_ptr(),
-           N.stream_handle(dev))
+    N.call("em_gen_masks_at", seed & M64, planted_threshold(planted), n, seg_len, seg0, perm.data_ptr(),
+           out.data_ptr(), N.stream_handle(dev))
     return out[:n]
 
 
 def gb_to_draws(gb: float) -> int:
     """Number of 8-byte draw masks in ``gb`` GiB."""
     return int(gb * (1 << 30)) // 8
+
+
+def region(a: int, b: int, seg_len: int = 4096) -> tuple[int, int, int]:
+    """Segment-aligned cover of draws [a, b): (first, n, skip) with first % seg_len == 0 and
+    draws [a, b) == generated[skip : skip + b - a]."""
+    if not 0 <= a <= b:
+        raise ValueError("need 0 <= a <= b")
+    first = (a // seg_len) * seg_len
+    return first, max(b - first, 1), a - first

@@ -54,3 +54,20 @@ def test_segments_are_independent_streams():
 
 def test_gb_to_draws():
     assert DG.gb_to_draws(1) == (1 << 27)
+
+
+def test_shard_at_offset_equals_slice_of_whole_sequence():
+    """A rank's shard generated at ``first`` is bit-identical to that slice of the whole sequence."""
+    whole = DG.generate_masks_py(5 * 256 + 40, seed=4, planted=0.9, seg_len=256)
+    for first, n in ((256, 300), (3 * 256, 2 * 256 + 40), (0, 100)):
+        part = DG.generate_masks_py(n, seed=4, planted=0.9, seg_len=256, first=first)
+        assert (part == whole[first:first + n]).all()
+    import pytest
+
+    with pytest.raises(ValueError):
+        DG.generate_masks_py(10, seed=4, seg_len=256, first=100)
+
+
+def test_region_cover():
+    first, n, skip = DG.region(1000, 3000, seg_len=256)
+    assert first == 768 and skip == 232 and first + skip == 1000 and first + n == 3000

@@ -47,3 +47,11 @@ def test_train_step_at_64bit_offset():
         outs.append((m.slabs[:n].clone(), m.loss_slabs[:n].clone()))
     del big
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("first,n", [(1024, 2500), (4096 * 3, 4096 + 17)])
+def test_kernel_shard_matches_spec(first, n):
+    seg = 1024 if first % 4096 else 4096
+    got = DG.generate_masks(n, seed=11, planted=0.9, seg_len=seg, first=first).cpu().numpy()
+    ref = DG.generate_masks_py(n, seed=11, planted=0.9, seg_len=seg, first=first)
+    assert (got == ref).all()
