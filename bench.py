@@ -19,8 +19,10 @@ synthetic batch" (DP=N over RCCL for N>1).
   validation split (metrics summed over ranks);
 * a timed step = fused fwd+loss+bwd launch, [all-reduce], fused Adam launch —
   the full optimizer step, nothing skipped;
-* K steps timed between barrier + synchronize on both sides, MAX over ranks; per-step
-  hipEvent times give the median step and the slowest rank's median;
+* the steps replay from hipGraphs of ``--graph-steps`` consecutive steps (each node set a full
+  step with its own data offset), so graph-launch gaps are paid once per chunk;
+* K steps timed between barrier + synchronize on both sides, MAX over ranks; hipEvents around
+  each graph replay give the median step and the slowest rank's median;
 * after timing, validation metrics on a held-out positional 30% split
   (outside the timed region).
 """
@@ -100,6 +102,8 @@ def _parse():
     ap.add_argument("--planted", type=float, default=0.9)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="replay the step from hipGraphs (needs a graph-safe step)")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="consecutive training steps captured per hipGraph (each a full fwd+bwd+Adam step)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="fused = our HIP kernels (headline); torch = plain PyTorch/hipBLASLt eager (comparison)")
@@ -248,49 +252,57 @@ def main():
 
     use_graph = bool(a.graph) and (world == 1 or getattr(model, "graph_safe", False))
     loss_t = None
-    for i in range(a.warmup):
+    # warmup: with hipGraphs, one eager step (first-launch setup) and the other W-1 as replays of the
+    # 1-step graph right before the timed loop, so the GPU enters it warm; otherwise W eager steps
+    for i in range(a.warmup if not use_graph else min(a.warmup, 1)):
         loss_t = step(i)
     torch.cuda.synchronize()
     if use_graph:
-        # offsets are baked into graph nodes: capture a ring of G graphs with distinct offsets
-        # and replay them round-robin
-        G = min(n_off, 8)
-        graphs = []
+        # hipGraphs of C consecutive steps (distinct data offsets baked into the nodes): one graph
+        # launch per C steps, so the ~19 us launch gap between graph replays (rocprof kernel trace,
+        # profiles/README.md) is paid once per chunk instead of once per step.  Steps that do not
+        # fill a chunk replay a 1-step graph.
+        C = max(1, min(a.graph_steps, a.steps))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+
+        def capture(n):
+            nonlocal loss_t
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for c in range(n):
+                    loss_t = step(c)
+            return g
         with torch.cuda.stream(s):
-            for gi in range(G):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s):
-                    loss_t = step(gi)
-                graphs.append(g)
+            g_c = capture(C)
+            g_1 = capture(1)
         torch.cuda.current_stream().wait_stream(s)
+        for _ in range(a.warmup - 1):
+            g_1.replay()
         torch.cuda.synchronize()
-
-        def run(i):
-            graphs[i % len(graphs)].replay()
+        plan = [(g_c, C)] * (a.steps // C) + [(g_1, 1)] * (a.steps % C)
+        runs = [(lambda g=g: g.replay(), n) for g, n in plan]
     else:
-        def run(i):
-            step(i)
+        runs = [(lambda i=i: step(i), 1) for i in range(a.steps)]
 
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in runs]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in runs]
     if world > 1:
         import torch.distributed as dist
 
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev0[i].record()
-        run(i)
-        ev1[i].record()
+    for k, (fn, _) in enumerate(runs):
+        ev0[k].record()
+        fn()
+        ev1[k].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1000.0 / a.steps
-    step_ms = sorted(e0.elapsed_time(e1) for e0, e1 in zip(ev0, ev1))
+    step_ms = sorted(e0.elapsed_time(e1) / n for e0, e1, (_, n) in zip(ev0, ev1, runs))
     med = step_ms[len(step_ms) // 2] if step_ms else float("nan")
     if hasattr(model, "check_comm"):
         model.check_comm()  # an xGMI peer wait that timed out is an error, not a fast step
@@ -349,6 +361,7 @@ def main():
             "config": {"model": desc,
                        "global_batch": BS * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
+                       "graph_steps": C if use_graph else 0,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
                        "dist_backend": a.dist_backend if world > 1 else None},
             "ms_per_step_median": med,

@@ -92,6 +92,21 @@ EM_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Combine lanes l and l ^ 32 (the two k-halves that share an MFMA 32x32 accumulator column) with one
+// v_permlane32_swap (VALU) instead of a ds_bpermute LDS round trip.  With vdst = src = v the swap
+// leaves r[0] = v[l & 31] and r[1] = v[(l & 31) + 32] in every lane, so both halves compute the same
+// expression in the same operand order: bitwise-identical results.
+EM_DEVICE float xhalf_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+EM_DEVICE float xhalf_max(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
 EM_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -680,8 +680,8 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
       mx_m = (c == 0) ? fmaxf(mx_m, z[i]) : mx_m;
       if (RHO == 1) mx_s = (c == 1) ? fmaxf(mx_s, z[i]) : mx_s;
     }
-    mx_m = fmaxf(mx_m, __shfl_xor(mx_m, 32));
-    if (RHO == 1) mx_s = fmaxf(mx_s, __shfl_xor(mx_s, 32));
+    mx_m = xhalf_max(mx_m);
+    if (RHO == 1) mx_s = xhalf_max(mx_s);
     const float nmL = -mx_m * L2E, nsL = -mx_s * L2E;
     float s_m = 0.f, s_s = 0.f, zt_m = 0.f, zt_s = 0.f;
 #pragma unroll
@@ -698,8 +698,8 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
         zt_s = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z[i], zt_s);
       }
     }
-    s_m += __shfl_xor(s_m, 32);
-    if (RHO == 1) s_s += __shfl_xor(s_s, 32);
+    s_m = xhalf_sum(s_m);
+    if (RHO == 1) s_s = xhalf_sum(s_s);
     // exchange (2): online-softmax merge of the main-group statistics
     if (h == 0) *reinterpret_cast<float2*>(smem + PB + V4_PST + RHO * 256 + r * 8) = float2{mx_m, s_m};
     st.mark(4);
@@ -847,7 +847,7 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 // the AGPR-pinned dW accumulators never cross a role branch (a merge point would force copies).
 template <int LOSS, int RHO>
 EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                       int offset, int pair, int lane, float* slab_spare) {
+                       int offset, int pair, int lane, float* slab_spare, uint64_t nin, uint64_t ntg) {
   const int r = lane & 31, h = lane >> 5;
   const char* lut = smem + IMG_BYTES;
   const uint32_t PB = V4_BASE + pair * V4_PAIR_BYTES;
@@ -879,9 +879,7 @@ EM_DEVICE void v4_body(char* smem, const uint64_t* __restrict__ masks, const int
     }
   };
   V4Stamps st;
-  const int first = blockIdx.x * 4 + pair;
-  uint64_t nin, ntg;
-  fetch(first, nin, ntg);
+  const int first = blockIdx.x * 4 + pair;  // its masks (nin, ntg) were fetched before the prologue
   st.start();
   for (int tile = first; tile < ntiles; tile += npairs) {
     const int s = tile * 32 + r;
@@ -947,6 +945,16 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   // wave w runs on SIMD w % 4: pairs 2/3 take their roles swapped so every SIMD hosts one role-0 and
   // one role-1 wave (role 1 owns the star group and issues ~20 % more VALU per tile)
   const int pair = wave >> 1, rho = (wave & 1) ^ (V4_MIX ? (wave >> 2) : 0);
+  // the first tile's feature masks: loads issued before the prologue so their HBM latency overlaps it
+  uint64_t nin = 0, ntg = 0;
+  {
+    const int s0 = (blockIdx.x * 4 + pair) * 32 + (lane & 31);
+    if (s0 < B) {
+      const int idx = sidx ? sidx[s0] : (offset + s0);
+      nin = masks[idx];
+      ntg = masks[idx + 1];
+    }
+  }
   {  // all loads of the weight image in flight before the first LDS store
     constexpr int N16 = IMG_BYTES / 16, K = (N16 + 511) / 512;
     const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
@@ -974,26 +982,35 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   if (V4_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
   if (rho == 0)
-    v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane, slab_spare);
+    v4_body<LOSS, 0>(smem, masks, sidx, B, offset, pair, lane, slab_spare, nin, ntg);
   else
-    v4_body<LOSS, 1>(smem, masks, sidx, B, offset, pair, lane, slab_spare);
+    v4_body<LOSS, 1>(smem, masks, sidx, B, offset, pair, lane, slab_spare, nin, ntg);
   if (V4_STAMPS) ts[2] = __builtin_amdgcn_s_memrealtime();
 
   const float* RED = reinterpret_cast<const float*>(smem);
   const float* DB2S = reinterpret_cast<const float*>(smem + V4_RED);
   const float* LOSSS = reinterpret_cast<const float*>(smem + V4_RED + 1024);
   float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
-  for (int e = tid; e < 16 * 4 * 64; e += 512) {
-    const int T = e >> 8, g = (e >> 6) & 3, l = e & 63, hh = l >> 5, rr = l & 31;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + e * 4) + *reinterpret_cast<const f32x4*>(RED + 16384 + e * 4);
-    const int c0 = 32 * ((T & 7) >> 1) + 8 * g + 4 * hh;  // hidden rows c0..c0+3
-    const int col = 32 * (T & 1) + rr;
-    if (T < 8) {
+  // The slab is written in parameter order with 16-B write-through (sc1) stores: the bytes head for
+  // memory while later workgroups are still in their loops, instead of sitting dirty in the XCD's L2
+  // until the kernel boundary writes them back in front of the Adam launch (MI355X_MICROARCH.md,
+  // "publish-large" and the "boundary" row: +B / 6 TB/s for B dirty bytes).
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(slab, 0, SLAB_STRIDE * 4, 0x00020000);
+  for (int e = tid; e < 2 * 2048; e += 512) {
+    f32x4 v;
+    if (e < 2048) {  // W1[f][c..c+3] = dW1T tile T = 8 + 2 (c >> 5) + (f >> 5): one 16-B read per half
+      const int f = e >> 5, c = (e & 31) * 4;
+      const int T = 8 + 2 * (c >> 5) + (f >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (f & 31);
+      const int at = ((T * 4 + g) * 64 + l) * 4;
+      v = *reinterpret_cast<const f32x4*>(RED + at) + *reinterpret_cast<const f32x4*>(RED + 16384 + at);
+    } else {  // W2[c][o..o+3]: 4 lanes of dW2 tile T = 2 (c >> 5) + (o >> 5), register k = c & 3
+      const int q = e - 2048, c = q >> 4, o = (q & 15) * 4;
+      const int T = 2 * (c >> 5) + (o >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (o & 31);
+      const int at = ((T * 4 + g) * 64 + l) * 4 + (c & 3);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) slab[P_W2 + (c0 + k) * OUT + col] = v[k];
-    } else {
-      *reinterpret_cast<f32x4*>(slab + P_W1 + col * HID + c0) = v;
+      for (int k = 0; k < 4; ++k) v[k] = RED[at + 4 * k] + RED[16384 + at + 4 * k];
     }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, e * 16, 0, 16 /* sc1 */);
   }
   if (V4_STAMPS && tid == 0) {
     ts[3] = __builtin_amdgcn_s_memrealtime();
