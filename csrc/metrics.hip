@@ -155,6 +155,31 @@ __global__ void onehot_kernel(const uint64_t* __restrict__ masks, const int32_t*
   }
 }
 
+// K14 with a lag window (data.lags > 1): row s = [onehot(masks[i]) | onehot(masks[i+1]) | ... |
+// onehot(masks[i+lags-1])] with i = sidx ? sidx[s] : offset + s, each block 64 wide (62 live + 2 pad),
+// row stride 64 * lags.  The matching target is masks[i + lags] (the trainer passes masks + lags - 1 to
+// the loss/metric kernels, whose target is their masks[i + 1]).  This is the multi-hot lag window of
+// data/draws.lag_features, built on the device from 8-byte masks.
+template <typename T>
+__global__ void onehot_lags_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int64_t B,
+                                   int64_t offset, int lags, T* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (sample, block, 8-feature chunk)
+  const int64_t per = (int64_t)lags * 8;
+  if (e >= B * per) return;
+  const int64_t s = e / per;
+  const int r = (int)(e - s * per), k = r >> 3, c = r & 7;
+  const int64_t idx = (sidx ? (int64_t)sidx[s] : offset + s) + k;
+  const uint32_t b = (uint32_t)((masks[idx] & (MAIN_BITS | STAR_BITS)) >> (8 * c)) & 0xFFu;
+  T* o = out + s * 64 * lags + 64 * k + 8 * c;
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<bf16x8*>(o) = bits_to_bf16x8(b);
+  } else {
+    f32x4* q = reinterpret_cast<f32x4*>(o);
+    q[0] = f32x4{(float)(b & 1u), (float)((b >> 1) & 1u), (float)((b >> 2) & 1u), (float)((b >> 3) & 1u)};
+    q[1] = f32x4{(float)((b >> 4) & 1u), (float)((b >> 5) & 1u), (float)((b >> 6) & 1u), (float)((b >> 7) & 1u)};
+  }
+}
+
 // K10: loss + dL/dlogits for the GEMM-path MLPs.  One wavefront per sample, lane j = output j
 // (62 live lanes; 62/63 are padding and get dz = 0).  dz is written bf16 (the next GEMM's
 // operand) already scaled by grad_scale (1/global_batch); per-block loss sums -> partials.
@@ -265,6 +290,23 @@ EM_API int em_loss_grad_f32(const float* logits, int ld, const uint64_t* masks, 
   if (B == 0) return 0;
   hipLaunchKernelGGL(loss_grad_kernel<float>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks,
                      sidx, B, offset, loss_kind, grad_scale, dz, ldz, partials);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// lag-window multi-hot [B][64 * lags] (bf16 if fp32 == 0, else fp32)
+EM_API int em_onehot_lags(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset, int lags, int fp32,
+                          void* out, hipStream_t stream) {
+  if (!draws || !out || B < 0 || lags < 1 || lags > 64) return EM_ERR_ARG;
+  if (B == 0) return 0;
+  const int64_t n = B * lags * 8;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  if (fp32)
+    hipLaunchKernelGGL(onehot_lags_kernel<float>, dim3(nb), dim3(256), 0, stream, draws, sidx, B, offset, lags,
+                       (float*)out);
+  else
+    hipLaunchKernelGGL(onehot_lags_kernel<__bf16>, dim3(nb), dim3(256), 0, stream, draws, sidx, B, offset, lags,
+                       (__bf16*)out);
   EM_CHECK_LAUNCH();
   return 0;
 }

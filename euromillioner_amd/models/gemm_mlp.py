@@ -24,6 +24,11 @@ one extra slot at the end carries the step loss through the same all-reduce.
 
 ``dtype="fp32"`` (``--dtype fp32``) runs the same step in fp32 end to end on the exact-fp32 MFMA
 GEMM (``csrc/gemm_f32.hip``): fp32 activations and dL/dZ, no bf16 shadow.
+
+``lags=k`` (``--lags k``) takes the lag window of ``data/draws.lag_features``: the input
+of sample i is the multi-hot of draws i .. i+k-1 (built on the device, K14 ``onehot_lags``; each 62-wide
+block padded to 64), the target is draw i+k.  Layer 0 is then ``W [N_pad, 64k]``; the logical
+``[N, 62k]`` weight maps block j's columns 62j..62j+61 to 64j..64j+61.
 """
 from __future__ import annotations
 
@@ -44,9 +49,11 @@ def _pad(n: int) -> int:
 class GemmMLPTrainer:
     def __init__(self, sizes=(62, 8192, 8192, 62), device="cuda", activation: str = "relu", loss: str = "softmax",
                  lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
-                 state_dict: dict | None = None, process_group=None, bucket_mb: float = 25.0, dtype: str = "bf16"):
-        if sizes[0] != 62 or sizes[-1] != 62:
-            raise ValueError("draw MLPs are 62-in / 62-out")
+                 state_dict: dict | None = None, process_group=None, bucket_mb: float = 25.0, dtype: str = "bf16",
+                 lags: int = 1):
+        if lags < 1 or sizes[0] != 62 * lags or sizes[-1] != 62:
+            raise ValueError(f"draw MLPs are (62 * lags)-in / 62-out (lags={lags}, sizes={tuple(sizes)})")
+        self.lags = int(lags)
         if activation not in ("relu", "tanh", "sigmoid"):
             raise ValueError("activation must be relu|tanh|sigmoid")
         if activation == "sigmoid" and any(h % 8 for h in sizes[1:-1]):
@@ -62,7 +69,7 @@ class GemmMLPTrainer:
             raise ValueError("GemmMLPTrainer runs on the GPU (use DrawMLP on the CPU)")
         N.lib()
         self.sizes = tuple(int(s) for s in sizes)
-        self.padded = (64,) + tuple(_pad(h) for h in self.sizes[1:-1]) + (64,)
+        self.padded = (64 * self.lags,) + tuple(_pad(h) for h in self.sizes[1:-1]) + (64,)
         self.activation, self.loss_name, self.group = activation, loss, process_group
         self.bucket_elems = max(1 << 16, int(bucket_mb * (1 << 20) // 4))
         self.offsets = []
@@ -123,7 +130,7 @@ class GemmMLPTrainer:
         if ws is None and self.f32:
             dev, P = self.device, self.padded
             f = torch.float32
-            ws = {"x": torch.empty(B, 64, dtype=f, device=dev),
+            ws = {"x": torch.empty(B, 64 * self.lags, dtype=f, device=dev),
                   "act": [torch.empty(B, n, dtype=f, device=dev) for n in P[1:-1]],
                   "dz": [torch.empty(B, n, dtype=f, device=dev) for n in P[1:]],
                   "logits": torch.empty(B, 64, dtype=f, device=dev),
@@ -135,7 +142,7 @@ class GemmMLPTrainer:
             plan = self._plan(B)
             L = len(self.offsets)
             P = self.padded
-            ws = {"x": torch.empty(B, 64, dtype=torch.bfloat16, device=dev),
+            ws = {"x": torch.empty(B, 64 * self.lags, dtype=torch.bfloat16, device=dev),
                   "act": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in P[1:-1]],
                   "dz": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in P[1:]],
                   "logits": torch.empty(B, 64, dtype=torch.float32, device=dev),
@@ -157,9 +164,16 @@ class GemmMLPTrainer:
     def prepare(draws) -> torch.Tensor:
         return FusedSmallMLP.prepare(draws)
 
+    def _tmasks(self, masks: torch.Tensor) -> torch.Tensor:
+        """Masks as the loss/metric kernels see them: their target masks[i + 1] is draw i + lags."""
+        return masks[self.lags - 1:] if self.lags > 1 else masks
+
     def _forward(self, masks, B, offset, sidx, ws, train: bool = False):
         if self.f32:
-            h = LF.onehot(masks, B, offset=offset, which=0, sidx=sidx, out=ws["x"])
+            if self.lags > 1:
+                h = FM.onehot_lags(masks, B, self.lags, offset=offset, sidx=sidx, out=ws["x"], dtype=torch.float32)
+            else:
+                h = LF.onehot(masks, B, offset=offset, which=0, sidx=sidx, out=ws["x"])
             inputs = []
             L = len(self.offsets)
             for i in range(L):
@@ -169,7 +183,10 @@ class GemmMLPTrainer:
                 h = LF.linear_fwd(h, w, bf, "none" if last else self.activation,
                                   out=ws["logits"] if last else ws["act"][i])
             return h, inputs
-        x = FM.onehot(masks, B, offset=offset, which=0, bias=False, sidx=sidx, out=ws["x"])
+        if self.lags > 1:
+            x = FM.onehot_lags(masks, B, self.lags, offset=offset, sidx=sidx, out=ws["x"])
+        else:
+            x = FM.onehot(masks, B, offset=offset, which=0, bias=False, sidx=sidx, out=ws["x"])
         h, inputs = x, []
         L = len(self.offsets)
         for i in range(L):
@@ -223,7 +240,7 @@ class GemmMLPTrainer:
 
     def _check(self, masks, B, offset, sidx):
         if not self._checked:
-            FM._check_draws(masks, sidx, B, offset)
+            FM._check_draws(self._tmasks(masks), sidx, B, offset)
             self._checked = True
 
     def step(self, masks: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None,
@@ -239,7 +256,7 @@ class GemmMLPTrainer:
         for k in range(accum - 1):  # all but the last micro-batch: local accumulation only
             off = offset + k * B
             logits, inputs = self._forward(masks, B, off, None, ws, train=True)
-            dz, part = LIN.loss_grad(logits, masks, B, self.loss_name, offset=off, grad_scale=1.0 / gb,
+            dz, part = LIN.loss_grad(logits, self._tmasks(masks), B, self.loss_name, offset=off, grad_scale=1.0 / gb,
                                      dz=ws["dz"][-1], partials=ws["part"])
             if k == 0:
                 torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
@@ -248,7 +265,8 @@ class GemmMLPTrainer:
             self._backward(dz, inputs, ws, accumulate=k > 0)
         last = offset + (accum - 1) * B
         logits, inputs = self._forward(masks, B, last, sidx, ws, train=True)
-        dz, part = (LF if self.f32 else LIN).loss_grad(logits, masks, B, self.loss_name, offset=last, sidx=sidx,
+        dz, part = (LF if self.f32 else LIN).loss_grad(logits, self._tmasks(masks), B, self.loss_name, offset=last,
+                                                       sidx=sidx,
                                                        grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
         if accum == 1:
             torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
@@ -278,15 +296,11 @@ class GemmMLPTrainer:
         """(loss, {name: grad}) for tests: same kernels, no all-reduce, no update."""
         ws = self._ws(B)
         logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
-        dz, part = (LF if self.f32 else LIN).loss_grad(logits, masks, B, self.loss_name, offset=offset, sidx=sidx,
+        dz, part = (LF if self.f32 else LIN).loss_grad(logits, self._tmasks(masks), B, self.loss_name, offset=offset,
+                                                       sidx=sidx,
                                                        grad_scale=1.0 / B, dz=ws["dz"][-1], partials=ws["part"])
         self._backward(dz, inputs, ws)
-        out = {}
-        for i in range(len(self.offsets)):
-            gw, gbias = self._views(self.grads, i)
-            k, n = self.sizes[i], self.sizes[i + 1]
-            out[f"layers.{i}.weight"] = gw[:n, :k].clone()
-            out[f"layers.{i}.bias"] = gbias[:n].clone()
+        out = {k: v.clone() for k, v in self._logical(self.grads, flat_layer0=True).items()}
         return float(part.double().sum().item()) / B, out
 
     def logits(self, masks, B, offset=0, sidx=None) -> torch.Tensor:
@@ -301,7 +315,8 @@ class GemmMLPTrainer:
             o = offset + done if sidx is None else 0
             si = None if sidx is None else sidx[done:done + b]
             lg = self.logits(masks, b, o, si)
-            tot += FM.draw_metrics(lg, masks, b, loss=self.loss_name, offset=o, sidx=si).double().sum(0).cpu().numpy()
+            tot += FM.draw_metrics(lg, self._tmasks(masks), b, loss=self.loss_name, offset=o,
+                                   sidx=si).double().sum(0).cpu().numpy()
             done += b
         if self.group is not None:
             import torch.distributed as dist
@@ -315,44 +330,69 @@ class GemmMLPTrainer:
         return out
 
     # ------------------------------------------------------------------ state
-    def _logical(self, flat: torch.Tensor) -> dict[str, torch.Tensor]:
+    def _logical(self, flat: torch.Tensor, flat_layer0: bool = False) -> dict[str, torch.Tensor]:
+        """Views of the logical weights.  Layer 0's weight is the view [N, lags, 62] of its padded
+        [N_pad, 64 * lags] block (``flat_layer0``: a [N, 62 * lags] copy instead)."""
         out = {}
         for i in range(len(self.offsets)):
             w, b = self._views(flat, i)
             k, n = self.sizes[i], self.sizes[i + 1]
-            out[f"layers.{i}.weight"] = w[:n, :k]
+            if i == 0:
+                w3 = w.view(w.shape[0], self.lags, 64)[:n, :, :62]
+                out["layers.0.weight"] = w3.reshape(n, k) if flat_layer0 else w3
+            else:
+                out[f"layers.{i}.weight"] = w[:n, :k]
             out[f"layers.{i}.bias"] = b[:n]
         return out
 
+    def _to_logical(self, name: str, v: torch.Tensor) -> torch.Tensor:
+        return v.reshape(v.shape[0], -1) if name == "layers.0.weight" else v
+
+    def _load_logical(self, flat: torch.Tensor, named: dict) -> None:
+        for k, v in self._logical(flat).items():
+            src = named[k].to(self.device, torch.float32)
+            v.copy_(src.view(v.shape) if k == "layers.0.weight" else src)
+
     def state_dict(self) -> dict[str, torch.Tensor]:
-        return {k: v.detach().clone().cpu() for k, v in self._logical(self.params).items()}
+        return {k: self._to_logical(k, v.detach()).clone().cpu() for k, v in self._logical(self.params).items()}
 
     def load_state_dict(self, sd: dict) -> None:
         self.params.zero_()
-        for k, v in self._logical(self.params).items():
-            v.copy_(sd[k].to(self.device, torch.float32))
+        self._load_logical(self.params, sd)
         if self.shadow is not None:
             self.shadow.copy_(self.params)
 
     def optimizer_state(self) -> dict:
-        return {"m": {k: v.clone().cpu() for k, v in self._logical(self.m).items()},
-                "v": {k: v.clone().cpu() for k, v in self._logical(self.v).items()},
+        return {"m": {k: self._to_logical(k, v).clone().cpu() for k, v in self._logical(self.m).items()},
+                "v": {k: self._to_logical(k, v).clone().cpu() for k, v in self._logical(self.v).items()},
                 "step": int(self.state[0].item()), "hp": self.hp.cpu().tolist()}
 
     def load_optimizer_state(self, st: dict) -> None:
         self.m.zero_()
         self.v.zero_()
         for name, buf in (("m", self.m), ("v", self.v)):
-            for k, v in self._logical(buf).items():
-                v.copy_(st[name][k].to(self.device, torch.float32))
+            self._load_logical(buf, st[name])
         self.state[0] = int(st.get("step", 0))
         self.state[1] = 0
 
-    def broadcast_parameters(self, src: int = 0) -> None:
-        if self.group is None:
+    def broadcast_parameters(self, src: int = 0, group=None) -> None:
+        group = group if group is not None else self.group
+        if group is None:
             return
         import torch.distributed as dist
 
-        dist.broadcast(self.params, src=src, group=self.group)
+        dist.broadcast(self.params, src=src, group=group)
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)
+
+    def average_parameters(self, group) -> None:
+        """Spark ``ParameterAveragingTrainingMaster`` parity (``--avg-frequency``): the mean of the
+        flat parameters and Adam moments over ``group`` (three flat all-reduces, no per-tensor calls)."""
+        import torch.distributed as dist
+
+        w = dist.get_world_size(group)
+        for buf in (self.params, self.m, self.v):
+            dist.all_reduce(buf, group=group)
+            buf.mul_(1.0 / w)
         if self.shadow is not None:
             self.shadow.copy_(self.params)

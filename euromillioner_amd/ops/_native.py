@@ -46,6 +46,7 @@ _SIGS = {
                             _c_void_p]),
     "em_draw_metrics": (_i32, [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p]),
     "em_onehot_encode": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p]),
+    "em_onehot_lags": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p]),
     "em_rows_to_masks": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "em_gen_masks": (_i32, [ctypes.c_uint64, ctypes.c_uint32, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
     "em_gen_masks_at": (_i32, [ctypes.c_uint64, ctypes.c_uint32, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),

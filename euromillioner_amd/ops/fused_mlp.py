@@ -195,6 +195,25 @@ def draw_metrics(logits: torch.Tensor, draws: torch.Tensor, B: int, loss: str = 
     return part
 
 
+def onehot_lags(draws: torch.Tensor, B: int, lags: int, offset: int = 0, sidx: torch.Tensor | None = None,
+                out: torch.Tensor | None = None, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """K14 lag window: [B, 64 * lags] rows [onehot(draw i) | ... | onehot(draw i + lags - 1)] (each block
+    62 live + 2 zero columns), i = sidx[s] or offset + s; the target of sample i is draw i + lags."""
+    if lags < 1:
+        raise ValueError("lags >= 1")
+    if dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("bf16 or fp32 output")
+    _check_draws(draws[lags - 1:] if lags > 1 else draws, sidx, B, offset, need_next=False)
+    if out is None:
+        out = torch.empty(B, 64 * lags, dtype=dtype, device=draws.device)
+    N.check_cuda(out, "out", dtype)
+    if out.shape[0] < B or out.shape[1] != 64 * lags:
+        raise ValueError(f"out must be [>= B, {64 * lags}]")
+    N.call("em_onehot_lags", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset, lags,
+           1 if dtype == torch.float32 else 0, out.data_ptr(), N.stream_handle(draws.device))
+    return out
+
+
 def onehot(draws: torch.Tensor, B: int, offset: int = 0, which: int = 0, bias: bool = False,
            sidx: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """K14: multi-hot bf16 [B, 64] of draws[idx + which] (which=1 -> targets)."""

@@ -134,17 +134,34 @@ class _GemmEngine(_Engine):
         from .models.gemm_mlp import GemmMLPTrainer
 
         m = cfg.mlp
+        self.info = info
+        # --avg-frequency k (Spark ParameterAveraging parity): local steps, flat parameter + moment
+        # averaging every k steps; otherwise synchronous gradient all-reduce inside the step
+        self.avg_k = int(cfg.dist.avg_frequency or 0)
         self.model = GemmMLPTrainer(sizes, info.device, activation=m.activation, loss=m.loss, lr=m.lr,
                                     betas=tuple(m.betas), eps=m.eps, weight_decay=m.weight_decay, state_dict=sd,
-                                    process_group=info.group, bucket_mb=cfg.dist.bucket_mb, dtype=m.dtype)
+                                    process_group=None if self.avg_k > 0 else info.group,
+                                    bucket_mb=cfg.dist.bucket_mb, dtype=m.dtype, lags=cfg.data.lags)
         self.masks = masks
         self.accum = m.accum
+        self.n_local = 0
 
     def step(self, idx, offset, B, global_batch):
         k = self.accum
+        gb = B if self.avg_k > 0 else global_batch  # local steps average over the local batch
         if k > 1:  # B consecutive samples as k micro-batches (gradient accumulation)
-            return self.model.step(self.masks, B // k, offset=offset, global_batch=global_batch, accum=k)
-        return self.model.step(self.masks, B, offset=offset, sidx=idx, global_batch=global_batch)
+            out = self.model.step(self.masks, B // k, offset=offset, global_batch=gb, accum=k)
+        else:
+            out = self.model.step(self.masks, B, offset=offset, sidx=idx, global_batch=gb)
+        if self.avg_k > 0:
+            self.n_local += 1
+            if self.n_local % self.avg_k == 0:
+                self.model.average_parameters(self.info.group)
+            if self.info.is_dist:
+                out = out.clone()
+                torch.distributed.all_reduce(out)
+                out /= self.info.world
+        return out
 
     def evaluate(self, offset, n):
         return _sharded_eval(self.model, self.masks, offset, n)
@@ -159,15 +176,21 @@ class _GemmEngine(_Engine):
         self.model.load_optimizer_state(st)
 
     def broadcast(self):
-        self.model.broadcast_parameters()
+        self.model.broadcast_parameters(group=self.info.group)
 
     def flat_params(self):
         return self.model.params
 
+    def average_parameters(self):
+        if self.info.is_dist:
+            self.model.average_parameters(self.info.group)
+
 
 class _TorchEngine(_Engine):
-    """DrawMLP (HIP autograd GEMMs on the GPU, PyTorch on the CPU) + torch.optim.Adam +
-    bucketed gradient all-reduce overlapped with backward (GradBucketer)."""
+    """CPU plumbing engine (BASELINE.json config 1): DrawMLP in PyTorch + torch.optim.Adam + bucketed
+    gradient all-reduce overlapped with backward (GradBucketer).  Every GPU run takes the fused or
+    the GEMM engine (HIP kernels end to end, fused Adam), lag windows and parameter averaging
+    included."""
 
     name = "torch"
 
@@ -336,11 +359,12 @@ def _mlp_sizes(cfg: RunConfig) -> tuple:
 
 
 def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
-    if info.device.type != "cuda" or cfg.data.lags != 1 or cfg.dist.avg_frequency:
-        return "torch"  # (parameter averaging runs on the DrawMLP engine)
-    if sizes == (62, 128, 62) and cfg.mlp.activation == "relu" and cfg.mlp.dtype == "bf16":
+    if info.device.type != "cuda":
+        return "torch"  # CPU plumbing path
+    if (sizes == (62, 128, 62) and cfg.mlp.activation == "relu" and cfg.mlp.dtype == "bf16"
+            and not cfg.dist.avg_frequency):
         return "fused"  # the single-launch kernel is bf16; --dtype fp32 takes the fp32 MFMA GEMM engine
-    return "gemm"
+    return "gemm"  # any stack, lag windows, fp32, parameter averaging
 
 
 def train_mlp(cfg: RunConfig) -> dict:
@@ -360,8 +384,8 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
     if device_data:  # HBM-resident draws generated on the GPU (csrc/datagen.hip); no host copy
         from .data.device_gen import gb_to_draws, generate_masks
 
-        if info.device.type != "cuda" or lags != 1:
-            raise ValueError("data.source=device needs a GPU and lags=1")
+        if info.device.type != "cuda":
+            raise ValueError("data.source=device needs a GPU")
         n_draws = int(cfg.data.n_draws) if cfg.data.n_draws else gb_to_draws(cfg.data.device_gb)
         dmasks = generate_masks(n_draws, seed=cfg.data.seed, planted=cfg.data.planted, device=info.device)
         ds = None
@@ -396,7 +420,7 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
         sd = DrawMLP(sizes, activation=m.activation, loss=m.loss, seed=m.seed).state_dict()
     kind = _pick_engine(cfg, info, sizes)
     if device_data and kind == "torch":
-        raise ValueError("data.source=device feeds the fused/GEMM engines (bf16, lags=1, no parameter averaging)")
+        raise ValueError("data.source=device feeds the GPU engines")
     if m.accum > 1 and kind != "gemm":
         raise ValueError(f"mlp.accum applies to the GEMM engine (this run uses {kind}); the fused kernel takes "
                          "any batch in one launch")

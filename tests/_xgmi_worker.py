@@ -1,7 +1,8 @@
 """One rank of the xGMI communicator GPU test (tests/test_xgmi_gpu.py).
 
-Ranks share whatever GPUs are visible (all on cuda:0 on a 1-GPU box: IPC between processes
-on one device exercises the same flag/slot protocol as peer devices over xGMI).  A gloo
+Rank r runs on cuda:(r % device_count): distinct GPUs (real xGMI peers) on a node with >= world
+GPUs, all on cuda:0 on a 1-GPU box (IPC between processes on one device exercises the same
+flag/slot protocol).  With EUROM_XGMI=0 it checks the RCCL/host fallback instead.  A gloo
 group carries the handle exchange and the reference results.  Prints one JSON line.
 """
 import json
@@ -15,12 +16,38 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def fallback(rank, world, dev):
+    """EUROM_XGMI=0: the communicator declines collectively and comm="auto" runs the host all-reduce."""
+    from euromillioner_amd.data.device_gen import generate_masks
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.parallel.xgmi import XgmiComm
+
+    out = {"rank": rank, "create": XgmiComm.create(dist.group.WORLD, dev, 1024) is None}
+    m = FusedSmallMLP(dev, loss="softmax", lr=3e-3, seed=0, process_group=dist.group.WORLD, comm="auto")
+    m.broadcast_parameters()
+    out["comm"] = m.comm
+    B = 4096
+    draws = generate_masks(world * B + 16, seed=5, planted=0.8, device=dev)
+    losses = [float(m.step(draws, B, offset=rank * B).item()) for _ in range(3)]
+    torch.cuda.synchronize()
+    out["finite"] = all(x == x and x > 0 for x in losses)
+    allp = [torch.empty_like(m.params.cpu()) for _ in range(world)]
+    dist.all_gather(allp, m.params.cpu())
+    out["params_bit_identical"] = all(torch.equal(allp[0], a) for a in allp)
+    m.close()
+    print("XGMI_RESULT " + json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", rank % ndev)
+    dev = torch.device("cuda", rank % ndev)  # distinct devices whenever the node has >= world GPUs
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
+    if os.environ.get("EUROM_XGMI", "1") == "0":
+        return fallback(rank, world, dev)
     from euromillioner_amd.data.synthetic import generate_draws
     from euromillioner_amd.models.mlp import FusedSmallMLP
     from euromillioner_amd.parallel.xgmi import XgmiComm, XgmiError

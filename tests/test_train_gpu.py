@@ -14,7 +14,7 @@ def _cfg(**over):
     return C.build_config(None, base, environ={})
 
 
-@pytest.mark.parametrize("hidden,lags,engine", [((128,), 1, "fused"), ((256, 128), 1, "gemm"), ((128,), 2, "torch")])
+@pytest.mark.parametrize("hidden,lags,engine", [((128,), 1, "fused"), ((256, 128), 1, "gemm"), ((128,), 2, "gemm")])
 def test_engines_learn(hidden, lags, engine):
     from euromillioner_amd.train import train
 
@@ -90,3 +90,11 @@ def test_dp_code_path_on_one_rank_matches_local(engine):
         dist.destroy_process_group()
     assert torch.isfinite(loss).all()
     assert torch.allclose(dp.params, local.params, atol=1e-6, rtol=0), float((dp.params - local.params).abs().max())
+
+
+def test_parameter_averaging_runs_on_the_gemm_engine():
+    from euromillioner_amd.train import train
+
+    res = train(_cfg(**{"mlp.steps": 60, "mlp.batch": 1024, "mlp.lr": 0.005, "dist.avg_frequency": 4}))
+    assert res["engine"] == "gemm"
+    assert res["val"]["acc"] > res["val"]["trivial_acc"], res["val"]
