@@ -155,7 +155,7 @@ class _GemmEngine(_Engine):
             out = self.model.step(self.masks, B, offset=offset, sidx=idx, global_batch=gb)
         if self.avg_k > 0:
             self.n_local += 1
-            if self.n_local % self.avg_k == 0:
+            if self.n_local % self.avg_k == 0 and self.info.is_dist:
                 self.model.average_parameters(self.info.group)
             if self.info.is_dist:
                 out = out.clone()
