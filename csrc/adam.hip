@@ -240,9 +240,21 @@ __global__ void mlp_pack_kernel(const float* __restrict__ params, uint8_t* __res
   mlp_pack_one(p, mlp_pad_slot(p) ? 0.f : params[p], img);
 }
 
-// plain multi-tensor-style Adam over a flat buffer (generic path: K6 for any model)
+// plain multi-tensor-style Adam over a flat buffer (generic path: K6 for any model).  G = float, or
+// __bf16 for gradients that were all-reduced in bf16 (GemmMLPTrainer comm_dtype="bf16"): they are
+// widened here and the moments / master weights stay fp32.
+template <typename G>
+EM_DEVICE f32x4 load_grad4(const G* g) {
+  if constexpr (sizeof(G) == 4) {
+    return *reinterpret_cast<const f32x4*>(g);
+  } else {
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(g);
+    return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+  }
+}
+template <typename G>
 __global__ void __launch_bounds__(256)
-adam_flat_kernel(float* __restrict__ params, const float* __restrict__ grad, float* __restrict__ m,
+adam_flat_kernel(float* __restrict__ params, const G* __restrict__ grad, float* __restrict__ m,
                  float* __restrict__ v, int64_t n, const float* __restrict__ hp, int* __restrict__ state,
                  float grad_scale, __bf16* __restrict__ shadow) {
   const int tstep = adam_begin(state);
@@ -251,7 +263,7 @@ adam_flat_kernel(float* __restrict__ params, const float* __restrict__ grad, flo
   for (int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += (int64_t)gridDim.x * blockDim.x * 4) {
     if (i4 + 4 <= n) {
       f32x4 w = *reinterpret_cast<const f32x4*>(params + i4);
-      f32x4 g = *reinterpret_cast<const f32x4*>(grad + i4);
+      f32x4 g = load_grad4<G>(grad + i4);
       f32x4 mm = *reinterpret_cast<const f32x4*>(m + i4);
       f32x4 vv = *reinterpret_cast<const f32x4*>(v + i4);
 #pragma unroll
@@ -272,7 +284,7 @@ adam_flat_kernel(float* __restrict__ params, const float* __restrict__ grad, flo
     } else {
       for (int64_t i = i4; i < n; ++i) {
         float w = params[i];
-        const float gg = grad[i] * grad_scale + wd * w;
+        const float gg = (float)grad[i] * grad_scale + wd * w;
         const float mm = b1 * m[i] + (1.f - b1) * gg;
         const float vv = b2 * v[i] + (1.f - b2) * gg * gg;
         m[i] = mm;
@@ -340,8 +352,50 @@ EM_API int em_adam_flat(float* params, const float* grad, float* m, float* v, in
   int64_t nb = (n / 4 + 255) / 256;
   if (nb > 4096) nb = 4096;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)nb), dim3(256), 0, stream, params, grad, m, v, n, hp, state,
-                     grad_scale, (__bf16*)shadow_bf16);
+  hipLaunchKernelGGL(adam_flat_kernel<float>, dim3((unsigned)nb), dim3(256), 0, stream, params, grad, m, v, n, hp,
+                     state, grad_scale, (__bf16*)shadow_bf16);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same update from a bf16 gradient (all-reduced in bf16); grad must be 8-B aligned
+EM_API int em_adam_flat_bf16g(float* params, const void* grad_bf16, float* m, float* v, int64_t n, const float* hp,
+                              int* state, float grad_scale, void* shadow_bf16, hipStream_t stream) {
+  if (!params || !grad_bf16 || !m || !v || !hp || !state || n < 0 || ((uintptr_t)grad_bf16 & 7)) return EM_ERR_ARG;
+  if (n == 0) return 0;
+  int64_t nb = (n / 4 + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(adam_flat_kernel<__bf16>, dim3((unsigned)nb), dim3(256), 0, stream, params,
+                     (const __bf16*)grad_bf16, m, v, n, hp, state, grad_scale, (__bf16*)shadow_bf16);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+namespace {
+__global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ dst,
+                                                            int64_t n) {
+  for (int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i4 < n; i4 += (int64_t)gridDim.x * 256 * 4) {
+    if (i4 + 4 <= n) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(src + i4);
+      bf16x4 b;
+      b[0] = (__bf16)x[0]; b[1] = (__bf16)x[1]; b[2] = (__bf16)x[2]; b[3] = (__bf16)x[3];
+      *reinterpret_cast<bf16x4*>(dst + i4) = b;
+    } else {
+      for (int64_t i = i4; i < n; ++i) dst[i] = (__bf16)src[i];
+    }
+  }
+}
+}  // namespace
+
+// fp32 -> bf16 (round to nearest even) of a gradient bucket before a bf16 all-reduce
+EM_API int em_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
+  if (!src || !dst || n < 0 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 7)) return EM_ERR_ARG;
+  if (n == 0) return 0;
+  int64_t nb = (n / 4 + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((unsigned)nb), dim3(256), 0, stream, src, (__bf16*)dst, n);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -12,9 +12,13 @@ Per step (all on the current HIP stream, no host sync):
 2. forward GEMMs with fused bias+act (bf16 activations), fp32 logits;
 3. K10 fused loss + dL/dlogits (bf16, pre-scaled by 1 / global batch);
 4. backward, last layer first: wgrad (fp32, written in place into the flat gradient
-   buffer) + bias colsum, then dgrad with act' fused; as soon as a layer's gradients
-   exist their all-reduce is launched (``async_op``: RCCL's stream overlaps the
-   remaining backward GEMMs; chunks of ``bucket_mb``);
+   buffer) + bias colsum, then dgrad with act' fused.  Data parallel: a hidden layer's
+   256-tile weight gradient is computed in row panels of about ``bucket_mb`` each, and each
+   panel's all-reduce is launched as soon as the panel is written (``async_op``: RCCL's stream
+   runs it under the next panels and the layer's dgrad GEMM), so the 8192x8192 layer's
+   268 MB of fp32 gradient (~99 % of the bytes) is not held back to the end of its wgrad;
+   ``comm_dtype="bf16"`` all-reduces bf16 copies of the buckets (half the xGMI bytes) and Adam
+   widens them back to fp32;
 5. one fused Adam over the flat fp32 master weights that also refreshes the bf16
    shadow the GEMMs read (no per-step weight casts).
 
@@ -50,7 +54,7 @@ class GemmMLPTrainer:
     def __init__(self, sizes=(62, 8192, 8192, 62), device="cuda", activation: str = "relu", loss: str = "softmax",
                  lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
                  state_dict: dict | None = None, process_group=None, bucket_mb: float = 25.0, dtype: str = "bf16",
-                 lags: int = 1):
+                 lags: int = 1, comm_dtype: str = "fp32"):
         if lags < 1 or sizes[0] != 62 * lags or sizes[-1] != 62:
             raise ValueError(f"draw MLPs are (62 * lags)-in / 62-out (lags={lags}, sizes={tuple(sizes)})")
         self.lags = int(lags)
@@ -62,8 +66,11 @@ class GemmMLPTrainer:
             raise ValueError(f"loss must be one of {list(FM.LOSS_KINDS)}")
         if dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be bf16 or fp32")
+        if comm_dtype not in ("fp32", "bf16"):
+            raise ValueError("comm_dtype must be fp32 or bf16")
         self.dtype = dtype
         self.f32 = dtype == "fp32"
+        self.comm_dtype = comm_dtype
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("GemmMLPTrainer runs on the GPU (use DrawMLP on the CPU)")
@@ -85,6 +92,9 @@ class GemmMLPTrainer:
         self.v = torch.zeros(self.P, dtype=torch.float32, device=dev)
         # bf16 copy of the weights the bf16 GEMMs read (refreshed by the fused Adam); fp32 reads params
         self.shadow = None if self.f32 else torch.zeros(self.P, dtype=torch.bfloat16, device=dev)
+        # bf16 wire format of the gradient (comm_dtype="bf16", data parallel only)
+        self.grads_bf16 = (torch.zeros(self.P, dtype=torch.bfloat16, device=dev)
+                           if comm_dtype == "bf16" and process_group is not None else None)
         self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
         self.state = torch.zeros(2, dtype=torch.int32, device=dev)
         if state_dict is None:
@@ -92,6 +102,8 @@ class GemmMLPTrainer:
         self.load_state_dict(state_dict)
         self._ws_cache: dict[int, dict] = {}
         self._checked = False
+        self.panel_ncu: int | None = None  # (tests: pretend a smaller GPU to get several wgrad panels)
+        self.last_buckets: list[tuple[int, int]] = []
 
     # ------------------------------------------------------------------ layout
     def _views(self, flat: torch.Tensor, i: int):
@@ -199,9 +211,19 @@ class GemmMLPTrainer:
             h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out, ct=ct)
         return h, inputs
 
-    def _backward(self, dz, inputs, ws, on_layer_done=None, accumulate: bool = False):
+    def wgrad_panels(self, i: int) -> list[tuple[int, int]]:
+        """Row panels of layer i's weight gradient, each all-reduced as soon as it is written
+        (``parallel.buckets.plan_panels``: whole waves of 256x256 tiles, >= ``bucket_mb``)."""
+        from ..parallel.buckets import plan_panels
+
+        ncu = self.panel_ncu or N.cu_count(self.device)
+        return plan_panels(self.padded[i + 1], self.padded[i], self.bucket_elems, ncu, LIN.BIG_M, LIN.BIG_N)
+
+    def _backward(self, dz, inputs, ws, on_ready=None, accumulate: bool = False):
         """Last layer first: wgrad + bias grad into the flat gradient buffer (added to it when
-        ``accumulate``: gradient accumulation over micro-batches), then dgrad (act' fused)."""
+        ``accumulate``: gradient accumulation over micro-batches), then dgrad (act' fused).
+        ``on_ready(a, c)`` is called as soon as flat gradient range [a, c) is final: per row panel
+        of a 256-tile wgrad, per whole weight otherwise, then per bias."""
         L = len(self.offsets)
         if self.f32 and accumulate:
             raise ValueError("gradient accumulation runs on the bf16 path")
@@ -210,8 +232,8 @@ class GemmMLPTrainer:
                 gw, gbias = self._views(self.grads, i)
                 LF.linear_wgrad(dz, inputs[i], out=gw, parts_cache=ws["parts"])
                 torch.sum(dz, dim=0, out=gbias)
-                if on_layer_done is not None:
-                    on_layer_done(i)
+                if on_ready is not None:
+                    on_ready(self.offsets[i][0], self.offsets[i][2])
                 if i > 0:
                     w, _ = self._views(self.params, i)
                     dz = LF.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
@@ -220,14 +242,22 @@ class GemmMLPTrainer:
         for i in reversed(range(L)):
             gw, gbias = self._views(self.grads, i)
             beta = 1.0 if accumulate else 0.0
+            a, b_off, c = self.offsets[i]
+            K = self.padded[i]
             if plan["wgrad"][i]:
-                LIN.linear_wgrad_nt(ws["dzt"][i], ws["actt"][i], out=gw, beta=beta)
+                panels = self.wgrad_panels(i) if on_ready is not None else [(0, gw.shape[0])]
+                for r0, r1 in panels:  # each panel's all-reduce starts while the next panels run
+                    LIN.linear_wgrad_nt(ws["dzt"][i][r0:r1], ws["actt"][i], out=gw[r0:r1], beta=beta)
+                    if on_ready is not None:
+                        on_ready(a + r0 * K, a + r1 * K)
                 LIN.rowsum(ws["dzt"][i], out=gbias, accumulate=accumulate)
             else:
                 LIN.linear_wgrad(dz, inputs[i], out=gw, beta=beta)
+                if on_ready is not None:
+                    on_ready(a, b_off)
                 LIN.colsum(dz, out=gbias, accumulate=accumulate, ws=ws["colsum_ws"])
-            if on_layer_done is not None:
-                on_layer_done(i)
+            if on_ready is not None:
+                on_ready(b_off, c)
             if i > 0:
                 w, _ = self._views(self.shadow, i)
                 if plan["dgrad"][i]:
@@ -273,23 +303,22 @@ class GemmMLPTrainer:
         else:
             self.grads[self.P:] += part.sum()
         self.grads[self.P:].mul_(1.0 / gb)
-        handles = []
-        hook = None
+        red = None
         if self.group is not None:
             import torch.distributed as dist
 
-            L = len(self.offsets)
+            from ..parallel.buckets import RangeAllReducer
 
-            def hook(i):  # C1: launch this layer's bucket(s) while the remaining backward runs
-                a = self.offsets[i][0]
-                c = self.offsets[i][2] if i < L - 1 else self.P + 1  # the last layer also carries the loss slot
-                for s0 in range(a, c, self.bucket_elems):
-                    handles.append(dist.all_reduce(self.grads[s0:min(c, s0 + self.bucket_elems)],
-                                                   op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-        self._backward(dz, inputs, ws, hook, accumulate=accum > 1)
-        for h in handles:
-            h.wait()
-        FM.adam_flat(self.params, self.grads[:self.P], self.m, self.v, self.hp, self.state, 1.0, shadow=self.shadow)
+            red = RangeAllReducer(self.grads, self.bucket_elems, self.group, wire=self.grads_bf16, cast=FM.cast_bf16)
+            # the loss slot travels in fp32 on its own (tiny), before the backward starts
+            red.handles.append(dist.all_reduce(self.grads[self.P:], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+        self._backward(dz, inputs, ws, red.ready if red is not None else None, accumulate=accum > 1)
+        if red is not None:
+            red.wait()
+            self.last_buckets = red.launched
+        g = self.grads_bf16 if self.grads_bf16 is not None else self.grads[:self.P]
+        FM.adam_flat(self.params, g, self.m, self.v, self.hp, self.state, 1.0, shadow=self.shadow)
         return self.grads[self.P:]
 
     def grads_only(self, masks, B, offset=0, sidx=None):

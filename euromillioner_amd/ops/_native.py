@@ -44,6 +44,9 @@ _SIGS = {
                             _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p]),
     "em_adam_flat": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _f32, _c_void_p,
                             _c_void_p]),
+    "em_adam_flat_bf16g": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _f32,
+                                  _c_void_p, _c_void_p]),
+    "em_cast_f32_bf16": (_i32, [_c_void_p, _c_void_p, _i64, _c_void_p]),
     "em_draw_metrics": (_i32, [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p]),
     "em_onehot_encode": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p]),
     "em_onehot_lags": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p]),

@@ -168,12 +168,31 @@ def adam_xgmi(xgmi: int, params: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
            loss_out.data_ptr() if loss_out is not None else None, N.stream_handle(params.device))
 
 
+def cast_bf16(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """fp32 -> bf16 (round to nearest even), one HIP launch (gradient buckets before a bf16 all-reduce)."""
+    N.check_cuda(src, "src", torch.float32)
+    N.check_cuda(dst, "dst", torch.bfloat16)
+    if dst.numel() < src.numel():
+        raise ValueError("dst too small")
+    N.call("em_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), N.stream_handle(src.device))
+    return dst
+
+
 def adam_flat(params: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor,
               state: torch.Tensor, grad_scale: float = 1.0, shadow: torch.Tensor | None = None) -> None:
-    for t, nm in ((params, "params"), (grad, "grad"), (m, "m"), (v, "v")):
+    """K6 over a flat fp32 buffer; ``grad`` fp32, or bf16 (a gradient all-reduced in bf16, widened in
+    the kernel: moments and master weights stay fp32)."""
+    for t, nm in ((params, "params"), (m, "m"), (v, "v")):
         N.check_cuda(t, nm, torch.float32)
     if shadow is not None:
         N.check_cuda(shadow, "shadow", torch.bfloat16)
+    if grad.dtype == torch.bfloat16:
+        N.check_cuda(grad, "grad", torch.bfloat16)
+        N.call("em_adam_flat_bf16g", params.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), params.numel(),
+               hp.data_ptr(), state.data_ptr(), float(grad_scale),
+               shadow.data_ptr() if shadow is not None else None, N.stream_handle(params.device))
+        return
+    N.check_cuda(grad, "grad", torch.float32)
     N.call("em_adam_flat", params.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), params.numel(),
            hp.data_ptr(), state.data_ptr(), float(grad_scale), shadow.data_ptr() if shadow is not None else None,
            N.stream_handle(params.device))

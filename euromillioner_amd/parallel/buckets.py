@@ -98,3 +98,46 @@ class GradBucketer:
     def remove(self) -> None:
         for h in self._hooks:
             h.remove()
+
+
+def plan_panels(rows: int, K: int, bucket_elems: int, ncu: int, tile_m: int = 256, tile_n: int = 256
+                ) -> list[tuple[int, int]]:
+    """Row panels [r0, r1) of a [rows, K] weight gradient produced by a 256x256-tile GEMM, each
+    all-reduced as soon as it is written.  A panel is a whole number of full waves of tiles (one tile
+    per CU: a 768-row panel of an 8192^2 gradient would run 96 tiles on 256 CUs) and at least
+    ``bucket_elems`` elements: 8192 x 8192 on 256 CUs gives four 2048-row (64 MB fp32) panels."""
+    tiles_per_row = max(1, K // tile_n)
+    wave_rows = tile_m * max(1, -(-ncu // tiles_per_row))
+    want = max(wave_rows, bucket_elems // max(K, 1))
+    per = -(-want // wave_rows) * wave_rows
+    return [(r, min(rows, r + per)) for r in range(0, rows, per)]
+
+
+class RangeAllReducer:
+    """Async SUM all-reduce of ranges of one flat gradient as they become final (C1 for the GEMM
+    trainer): :meth:`ready` launches ``[a, c)`` in buckets of at most ``bucket_elems``; with ``wire``
+    (a bf16 twin of the flat buffer) and ``cast`` (fp32 -> bf16 into it) the buckets travel in bf16.
+    :meth:`wait` completes every launched bucket.  Buckets go out in the order ranges become ready,
+    which is the same on every rank (the backward schedule is deterministic)."""
+
+    def __init__(self, flat: torch.Tensor, bucket_elems: int, group=None, wire: torch.Tensor | None = None,
+                 cast=None):
+        self.flat, self.bucket_elems, self.group = flat, max(1, int(bucket_elems)), group
+        self.wire, self.cast = wire, cast
+        self.handles: list = []
+        self.launched: list[tuple[int, int]] = []
+
+    def ready(self, a: int, c: int) -> None:
+        for s0 in range(a, c, self.bucket_elems):
+            s1 = min(c, s0 + self.bucket_elems)
+            if self.wire is not None:
+                buf = self.cast(self.flat[s0:s1], self.wire[s0:s1])
+            else:
+                buf = self.flat[s0:s1]
+            self.handles.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self.launched.append((s0, s1))
+
+    def wait(self) -> None:
+        for h in self.handles:
+            h.wait()
+        self.handles = []

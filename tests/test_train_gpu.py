@@ -98,3 +98,39 @@ def test_parameter_averaging_runs_on_the_gemm_engine():
     res = train(_cfg(**{"mlp.steps": 60, "mlp.batch": 1024, "mlp.lr": 0.005, "dist.avg_frequency": 4}))
     assert res["engine"] == "gemm"
     assert res["val"]["acc"] > res["val"]["trivial_acc"], res["val"]
+
+
+def test_gemm_dp_panels_and_bf16_wire_on_one_rank():
+    """The GEMM trainer's panelled wgrad all-reduce (several panels per hidden layer) equals the local
+    step bit for bit on a 1-rank RCCL group; the bf16 wire stays within bf16 rounding of it."""
+    import torch
+
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds = DrawSet.synthetic(n=9000, seed=6, planted=0.7, calendar=False)
+    masks = FusedSmallMLP.prepare(torch.from_numpy(ds.numbers).cuda())
+    sizes, B = (62, 512, 512, 62), 1024
+
+    def run(g, wire="fp32"):
+        tr = GemmMLPTrainer(sizes, "cuda", seed=2, lr=3e-3, process_group=g, bucket_mb=0.05, comm_dtype=wire)
+        tr.panel_ncu = 2  # 512-row layers -> two 256-row wgrad panels
+        for k in range(3):
+            tr.step(masks, B, offset=1500 * k)
+        torch.cuda.synchronize()
+        return tr
+
+    local = run(None)
+    dist = _nccl_world1()
+    try:
+        dp = run(dist.group.WORLD)
+        assert dp._plan(B)["wgrad"][1] and len(dp.wgrad_panels(1)) == 2
+        a, c = dp.offsets[1][0], dp.offsets[1][1]
+        assert sum(1 for s0, _ in dp.last_buckets if a <= s0 < c) >= 2
+        bf = run(dist.group.WORLD, "bf16")
+    finally:
+        dist.destroy_process_group()
+    assert torch.equal(dp.params, local.params), float((dp.params - local.params).abs().max())
+    d = (bf.params - local.params).abs().max().item()
+    assert 0 < d < 2e-3, d  # bf16 gradient rounding through Adam's normalisation, 3 steps
