@@ -68,6 +68,6 @@ def test_bench_device_data_modes(args):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
-    assert d["value"] > 0 and d["steps"] == 3 and "device_datagen" in d
+    assert d["value"] > 0 and d["steps"] == 3 and d["datagen"]["draws"] > 0 and d["n_gpus"] == 1
     if "--accum" in args:
         assert d["config"]["per_gpu_batch"] == 16384 and d["accum"] == 2

@@ -132,5 +132,7 @@ def test_gemm_dp_panels_and_bf16_wire_on_one_rank():
     finally:
         dist.destroy_process_group()
     assert torch.equal(dp.params, local.params), float((dp.params - local.params).abs().max())
-    d = (bf.params - local.params).abs().max().item()
-    assert 0 < d < 2e-3, d  # bf16 gradient rounding through Adam's normalisation, 3 steps
+    p0 = GemmMLPTrainer(sizes, "cuda", seed=2).params
+    du_local, du_bf = local.params - p0, bf.params - p0
+    rel = ((du_bf - du_local).norm() / du_local.norm()).item()
+    assert 0 < rel < 0.05, rel  # bf16 gradient rounding through Adam's normalisation, 3 steps
