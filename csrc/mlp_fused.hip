@@ -572,10 +572,11 @@ EM_DEVICE bf16x8 v4_tr_frag(const char* smem, uint32_t base, int colbase, int q,
 }
 // X fragments from a 16-entry nibble table (4 bf16 {0,1} per entry, 128 B): two ds_read_b64 per
 // fragment; distinct entries never share a bank, unlike a 256-entry byte table
+template <int LUT = V4_XLUT>
 EM_DEVICE bf16x8 v4_xfrag(const char* smem, uint32_t w, int q) {
   const int sh = 16 * (q & 1);
-  const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + V4_XLUT + (__builtin_amdgcn_ubfe(w, sh, 4) << 3));
-  const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + V4_XLUT + (__builtin_amdgcn_ubfe(w, sh + 4, 4) << 3));
+  const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + LUT + (__builtin_amdgcn_ubfe(w, sh, 4) << 3));
+  const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + LUT + (__builtin_amdgcn_ubfe(w, sh + 4, 4) << 3));
   return __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
 }
 
@@ -1025,6 +1026,442 @@ mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   }
 }
 
+// ============================================================================================
+// v5: round-synchronous workgroup -- per-wave forward/backward chains, cross-wave dW GEMMs.
+//
+// v4's hidden-split pairs exchange H, the softmax statistics and dZ2 through LDS three times per
+// tile; phase stamps showed each wave waiting on its partner ~28 % of the time, and the AGPR-resident
+// full dW (128 AGPRs per wave) caps the CU at two waves per SIMD with no room to pipeline.  v5 moves
+// the dW accumulation out of the per-tile chain:
+//   phase A   each of the 8 waves runs ONE 32-sample tile through F1 -> relu -> F2 -> loss -> B1 ->
+//             mask entirely on its own (48 MFMAs, no exchange), leaving its H image [32 x 128] and
+//             its dZ2 image [32 x 64] in LDS and dZ1ᵀ (samples on the lanes) in registers;
+//   barrier   then the workgroup computes dW2 = Hᵀ·dZ2 over all 8 tiles (K = 256 samples): wave w
+//   phase B1  owns hidden block w >> 1 and K-half w & 1, both output blocks (16 MFMAs; db2 rides on
+//             4 waves as a ones·dZ2 MFMA);
+//   dump      the dZ1 image overwrites the H image, the X image overwrites dZ2;
+//   phase B2  dW1ᵀ = dZ1ᵀ·X the same way (16 MFMAs).
+// Each wave keeps only a quarter of a dW partial (64 registers + 16 for db2), the per-tile work has no
+// waits, and phase B is a dense MFMA stream.  The two K-halves are summed in a fixed order in the
+// epilogue (bit-reproducible slabs).  LDS: weights 54.5 KB + 8 tiles x 12 KB = 150 KB.
+//
+// Status (measured, 1x MI355X, same box): correct (tests/test_fused_mlp_gpu.py under EM_FUSED_V5=1)
+// but 135 us/step vs v4's 127 us.  Phase stamps: phase A takes ~7.2 k cycles per 32-sample tile -- one
+// wave's serial F1 -> F2 -> loss -> B1 chain is latency-bound, and with every wave of a group in the
+// same phase the co-resident waves of a SIMD cannot hide each other's stalls; ~25 % of its VALU is LDS
+// address arithmetic for the XOR-swizzled images.  v4 stays the default; v5 is opt-in (EM_FUSED_V5=1)
+// for further work (shorter chains per wave, fewer swizzled addresses).
+constexpr int V5_XLUT = IMG_BYTES;        // 16 x 8 B: input nibble -> 4 bf16 {0,1}
+constexpr int V5_YLUT = V5_XLUT + 128;    // 16 x f32x4: target nibble -> 4 {0,1} floats
+constexpr int V5_TILES = V5_YLUT + 256;   // 8 x [H image / dZ1 frags 8 KB | dZ2 image / X image 4 KB]
+constexpr int V5_TILE_BYTES = 12288;
+constexpr int V5_FLAGS = V5_TILES + 8 * V5_TILE_BYTES;  // [2 groups][4 waves] sync counters
+#ifndef V5_STAGGER
+#define V5_STAGGER 1
+#endif
+constexpr int V5_LOOP_LDS = V5_FLAGS + 32;
+constexpr int V5_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below, DB2S [8][32] + LOSSS [8] above
+constexpr int V5_LDS = (V5_LOOP_LDS > V5_RED + 2048 ? V5_LOOP_LDS : V5_RED + 2048);
+static_assert(V5_LDS <= 163840 && V5_TILES % 16 == 0, "v5 LDS budget");
+
+// class of output o = 32 u + oo0(i) + 4h: 0 main, 1 star, 2 pad
+EM_DEVICE int v5_cls(int u, int i, int h) {
+  const int o = 32 * u + oo0(i) + 4 * h;
+  return o < 50 ? 0 : (o < 62 ? 1 : 2);
+}
+
+template <int LOSS>
+__global__ void __launch_bounds__(512, 1)
+mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
+                          const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                          float* __restrict__ loss_slabs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
+  const int ntiles = (B + 31) / 32;
+  const int per_round = gridDim.x * 8;
+  auto fetch = [&](int tile, uint64_t& mi, uint64_t& mt) {
+    const int s = tile * 32 + r;
+    mi = 0;
+    mt = 0;
+    if (tile < ntiles && s < B) {
+      const int idx = sidx ? sidx[s] : (offset + s);
+      mi = masks[idx];
+      mt = masks[idx + 1];
+    }
+  };
+  uint64_t nin, ntg;  // the first round's masks: in flight during the prologue
+  fetch(blockIdx.x * 8 + wave, nin, ntg);
+  {
+    constexpr int N16 = IMG_BYTES / 16, K = (N16 + 511) / 512;
+    const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
+    u32x4* dst = reinterpret_cast<u32x4*>(smem);
+    u32x4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (tid + 512 * k < N16) v[k] = src[tid + 512 * k];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (tid + 512 * k < N16) dst[tid + 512 * k] = v[k];
+  }
+  if (tid < 64) reinterpret_cast<float*>(smem + V5_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
+  if (tid < 32) {
+    const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
+    reinterpret_cast<uint32_t*>(smem + V5_XLUT)[tid] =
+        (((n >> b) & 1u) ? 0x3F80u : 0u) | (((n >> (b + 1)) & 1u) ? 0x3F800000u : 0u);
+  }
+  if (tid < 8) reinterpret_cast<int*>(smem + V5_FLAGS)[tid] = 0;
+  __syncthreads();
+
+  const uint32_t HB = V5_TILES + wave * V5_TILE_BYTES, DB = HB + 8192;  // this wave's tile regions
+  // two independent groups of 4 waves (wave w and w + 4 share a SIMD): group kh owns the tiles of
+  // waves 4kh .. 4kh+3 and the K-half kh of every dW partial; wave TB = w & 3 of the group owns hidden
+  // block TB.  The groups synchronise only internally (LDS counters), so one group's phase A (a
+  // latency-bound chain) runs beside the other group's phase B (a dense MFMA stream) on every SIMD.
+  const int TB = wave & 3, kh = wave >> 2;
+  int gsig = 0;
+  bool ok = true;
+  const uint32_t GFL = V5_FLAGS + kh * 16;
+  auto group_sync = [&]() {  // the 4 waves of this group: release own LDS writes, acquire the others'
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    int* own = static_cast<int*>(__builtin_assume_aligned(smem + GFL + TB * 4, 4));
+    __hip_atomic_store(own, ++gsig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int spins = 0;
+    for (;;) {
+      const int* f = static_cast<const int*>(__builtin_assume_aligned(smem + GFL, 16));
+      const int m0 = __hip_atomic_load(f + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int m1 = __hip_atomic_load(f + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int m2 = __hip_atomic_load(f + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int m3 = __hip_atomic_load(f + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (min(min(m0, m1), min(m2, m3)) >= gsig) break;
+      if (++spins > V4_SPIN_LIMIT) {  // a broken protocol poisons the loss instead of hanging the GPU
+        ok = false;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  f32x16 dW2p[2], dW1p[2];  // partials (80 registers with db2a): [out block] / [feature block] of hidden block TB
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    dW2p[u] = f32x16{};
+    dW1p[u] = f32x16{};
+  }
+  f32x16 db2a = f32x16{};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  float loss_acc = 0.f;
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  V4Stamps st;  // V4_STAMPS builds: A, wait 1, B1, wait 2, dump, wait 3, B2, wait 4 (tools/fused_phases.py)
+  if (V5_STAGGER && kh == 1 && blockIdx.x * 8 < ntiles) {
+    // start group 1 once group 0 has finished its first phase A, so the two groups run opposite
+    // phases (chain beside stream) instead of in lockstep; group 0 never waits for group 1
+    int spins = 0;
+    const int* f = static_cast<const int*>(__builtin_assume_aligned(smem + V5_FLAGS, 16));
+    while (min(min(__hip_atomic_load(f + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                   __hip_atomic_load(f + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)),
+               min(__hip_atomic_load(f + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                   __hip_atomic_load(f + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) < 1) {
+      if (++spins > V4_SPIN_LIMIT) {
+        ok = false;
+        break;
+      }
+    }
+  }
+  st.start();
+
+  for (int base = blockIdx.x * 8; base < ntiles; base += per_round) {
+    const int tile = base + wave;
+    const bool valid = tile * 32 + r < B;
+    const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
+    const uint64_t tmask = valid ? ntg : 0ull;
+    fetch(tile + per_round, nin, ntg);
+
+    // ================= phase A: this wave's tile, start to dZ1 =================
+    const uint32_t wlo = (uint32_t)imask >> (8 * h), whi = (uint32_t)(imask >> 32) >> (8 * h);
+    bf16x8 xf[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xf[q] = v4_xfrag<V5_XLUT>(smem, q < 2 ? wlo : whi, q);
+    // F1: Z1ᵀ = W1ᵀ·Xᵀ, two hidden tiles' chains interleaved -> relu -> Hᵀ fragments + H image
+    bf16x8 hT[4][2];
+#pragma unroll
+    for (int tp = 0; tp < 2; ++tp) {
+      f32x16 a1s[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+          a1s[tt] = mfma32(lds_frag(smem, w1t_off(32 * (2 * tp + tt) + r, 2 * q + h)), xf[q], a1s[tt]);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * tp + tt;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          hT[t][q] = relu_pack(a1s[tt], q);
+          const u32x4 d = __builtin_bit_cast(u32x4, hT[t][q]);
+          *reinterpret_cast<u32x2*>(smem + HB + r * 256 + ((((4 * t + 2 * q) ^ (r & 15))) << 4) + h * 8) =
+              u32x2{d[0], d[1]};
+          *reinterpret_cast<u32x2*>(smem + HB + r * 256 + ((((4 * t + 2 * q + 1) ^ (r & 15))) << 4) + h * 8) =
+              u32x2{d[2], d[3]};
+        }
+      }
+    }
+    // F2: Z2ᵀ = W2ᵀ·Hᵀ + b2, both output tiles' chains interleaved
+    f32x16 z2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
+        z2[u][4 * g + 0] = b[0]; z2[u][4 * g + 1] = b[1]; z2[u][4 * g + 2] = b[2]; z2[u][4 * g + 3] = b[3];
+      }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          z2[u] = mfma32(lds_frag(smem, w2p_off(32 * u + r, (2 * t + q) * 2 + h)), hT[t][q], z2[u]);
+
+    // loss + dZ2 over the lane's 32 outputs (its sample r; lanes r and r + 32 share the sample).
+    // Targets as {0,1} floats, one output tile at a time: register group g of tile u holds outputs
+    // 32u + 8g + 4h .. +3 = one nibble of the target mask -> one ds_read_b128 of a 16-entry table
+    auto targets = [&](int u, float (&yb)[16]) {
+      const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + V5_YLUT + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+        yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
+      }
+    };
+    float dz[2][16];
+    if (LOSS == 0) {
+      // grouped softmax (main 50 / stars 12): exp2 with the max folded into one fma, v_rcp, and no
+      // validity select -- an invalid sample has an all-zero target mask, so nm = ns = 0 zero it
+      const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
+      const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);
+      const int ns = __builtin_popcount(thi & 0x3FFC0000u);
+      const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
+      const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
+      float mx_m = -3.0e38f, mx_s = -3.0e38f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = v5_cls(u, i, h);
+          mx_m = (c == 0) ? fmaxf(mx_m, z2[u][i]) : mx_m;
+          mx_s = (c == 1) ? fmaxf(mx_s, z2[u][i]) : mx_s;
+        }
+      mx_m = xhalf_max(mx_m);
+      mx_s = xhalf_max(mx_s);
+      const float nmL = -mx_m * L2E, nsL = -mx_s * L2E;
+      float s_m = 0.f, s_s = 0.f, zt_m = 0.f, zt_s = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float yb[16];
+        targets(u, yb);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = v5_cls(u, i, h);
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z2[u][i], L2E, c == 1 ? nsL : nmL));
+          const float ee = (c == 2) ? 0.f : e;
+          s_m += (c == 0) ? ee : 0.f;
+          s_s += (c == 1) ? ee : 0.f;
+          zt_m = __builtin_fmaf((c == 0) ? yb[i] : 0.f, z2[u][i], zt_m);
+          zt_s = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z2[u][i], zt_s);
+          dz[u][i] = ee;
+        }
+      }
+      s_m = xhalf_sum(s_m);
+      s_s = xhalf_sum(s_s);
+      const float f_m = nm ? __builtin_amdgcn_rcpf(s_m) : 0.f, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float yb[16];
+        targets(u, yb);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = v5_cls(u, i, h);
+          dz[u][i] = (c == 2) ? 0.f : __builtin_fmaf(dz[u][i], c == 0 ? f_m : f_s, -yb[i] * (c == 0 ? inv_m : inv_s));
+        }
+      }
+      float l = -(zt_m * inv_m + zt_s * inv_s);
+      if (h == 0)
+        l += (nm ? mx_m + __builtin_amdgcn_logf(s_m) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
+      loss_acc += l;
+    } else {
+      float l = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float yb[16];
+        targets(u, yb);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = v5_cls(u, i, h);
+          const float v = z2[u][i], y = yb[i];
+          const float en = __builtin_amdgcn_exp2f(-fabsf(v) * L2E);  // stable sigmoid / softplus
+          const float rp = __builtin_amdgcn_rcpf(1.f + en);
+          const float pr = v >= 0.f ? rp : en * rp;
+          const float sp = fmaxf(v, 0.f) + __builtin_amdgcn_logf(1.f + en) * LN2;
+          const bool okc = valid && c != 2;
+          dz[u][i] = okc ? (pr - y) : 0.f;
+          l += okc ? (sp - y * v) : 0.f;
+        }
+      }
+      loss_acc += l;
+    }
+    bf16x8 dzf[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        dzf[u][q] = pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2], dz[u][8 * q + 3], dz[u][8 * q + 4],
+                          dz[u][8 * q + 5], dz[u][8 * q + 6], dz[u][8 * q + 7]);
+    // dZ2 image [32 samples][64 outs] (phase B1's B operand)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 f = __builtin_bit_cast(u32x4, dzf[u][g >> 1]);
+        *reinterpret_cast<u32x2*>(smem + DB + r * 128 + ((((4 * u + g) ^ (r & 7))) << 4) + h * 8) =
+            u32x2{f[2 * (g & 1)], f[2 * (g & 1) + 1]};
+      }
+    // B1: dHᵀ = W2·dZ2ᵀ with the samples on the lanes (the W2Q fragments as the A operand, dZ2ᵀ
+    // straight from its accumulator as B), so dHᵀ has hT's layout and dZ1ᵀ = dHᵀ * (H > 0) needs no
+    // LDS round trip
+    bf16x8 dz1[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x16 aD = f32x16{};
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          aD = mfma32(lds_frag(smem, w2q_off(32 * t + r, (2 * u + q) * 2 + h)), dzf[u][q], aD);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dz1[t][q] = mask_by(hT[t][q], aD, q);
+    }
+    st.mark(0);
+    group_sync();  // (1) the group's H and dZ2 images are in LDS
+    st.mark(1);
+    // Phase B and the dump address LDS through lane values the compiler may not hoist out of the
+    // loop: hoisted, their ~30 loop-invariant addresses spill (256-VGPR budget); recomputed here they
+    // cost a few VALU while the matrix pipe is the bottleneck.
+    int lb = lane;
+    asm volatile("" : "+v"(lb));
+    const int rb = lb & 31, hb_ = lb >> 5, q4b = (lb & 15) >> 2, p4b = lb & 3, g1b = (lb >> 4) & 1;
+
+    // ================= phase B1: dW2 partial = Hᵀ·dZ2 over this K-half's 4 tiles =================
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t hb = V5_TILES + (4 * kh + j) * V5_TILE_BYTES, db = hb + 8192;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const bf16x8 a = tr_frag<1>(smem, hb, 32 * TB, q, hb_, q4b, p4b, g1b);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bf16x8 bd = tr_frag<0>(smem, db, 32 * u, q, hb_, q4b, p4b, g1b);
+          dW2p[u] = mfma32(a, bd, dW2p[u]);
+          if (TB == u) db2a = mfma32(ones, bd, db2a);  // waves 0-3: db2 of out block TB, this K-half
+        }
+      }
+    }
+    st.mark(2);
+    group_sync();  // (2) the group's H and dZ2 images are consumed
+    st.mark(3);
+
+    // dump: the dZ1 image [32 samples][128 hid] over the H image (same layout: phase B2 reads it
+    // transposed like B1 reads H), the X image [32 samples][64 feat] over the dZ2 image
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const u32x4 d = __builtin_bit_cast(u32x4, dz1[t][q]);
+        *reinterpret_cast<u32x2*>(smem + HB + rb * 256 + ((((4 * t + 2 * q) ^ (rb & 15))) << 4) + hb_ * 8) =
+            u32x2{d[0], d[1]};
+        *reinterpret_cast<u32x2*>(smem + HB + rb * 256 + ((((4 * t + 2 * q + 1) ^ (rb & 15))) << 4) + hb_ * 8) =
+            u32x2{d[2], d[3]};
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<bf16x8*>(smem + DB + rb * 128 + ((((2 * q + hb_) ^ (rb & 7))) << 4)) =
+          v4_xfrag<V5_XLUT>(smem, q < 2 ? wlo : whi, q);
+    st.mark(4);
+    group_sync();  // (3)
+    st.mark(5);
+
+    // ================= phase B2: dW1ᵀ partial = dZ1ᵀ·X over this K-half's 4 tiles =================
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t hb = V5_TILES + (4 * kh + j) * V5_TILE_BYTES, xb = hb + 8192;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const bf16x8 a = tr_frag<1>(smem, hb, 32 * TB, q, hb_, q4b, p4b, g1b);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) dW1p[u] = mfma32(a, tr_frag<0>(smem, xb, 32 * u, q, hb_, q4b, p4b, g1b), dW1p[u]);
+      }
+    }
+    st.mark(6);
+    group_sync();  // (4) the next round rewrites the group's tile regions
+    st.mark(7);
+  }
+  // ================= epilogue: the two K-halves -> one slab, fixed order =================
+  float lsum = wave_sum(loss_acc);
+  if (!ok) lsum = __builtin_nanf("");
+  __syncthreads();  // both groups are out of their loops: the tile regions are free
+  float* RED = reinterpret_cast<float*>(smem);  // [kh][16 tiles][4 g][64 lanes][4]: 0..7 dW2, 8..15 dW1ᵀ
+  float* DB2S = reinterpret_cast<float*>(smem + V5_RED);  // [4 waves][32]
+  float* LOSSS = DB2S + 8 * 32;                           // [8]
+#pragma unroll
+  for (int which = 0; which < 2; ++which)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f32x16& acc = which ? dW1p[u] : dW2p[u];
+      const int T = 8 * which + 2 * TB + u;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(RED + kh * 16384 + ((T * 4 + g) * 64 + lane) * 4) =
+            f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+    }
+  if (TB < 2 && h == 0) DB2S[wave * 32 + r] = db2a[0];  // accumulator column r = output 32 TB + r
+  if (lane == 0) LOSSS[wave] = lsum;
+  __syncthreads();
+  float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(slab, 0, SLAB_STRIDE * 4, 0x00020000);
+  for (int e = tid; e < 2 * 2048; e += 512) {
+    f32x4 v;
+    if (e < 2048) {
+      const int f = e >> 5, c = (e & 31) * 4;
+      const int T = 8 + 2 * (c >> 5) + (f >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (f & 31);
+      const int at = ((T * 4 + g) * 64 + l) * 4;
+      v = *reinterpret_cast<const f32x4*>(RED + at) + *reinterpret_cast<const f32x4*>(RED + 16384 + at);
+    } else {
+      const int q = e - 2048, c = q >> 4, o = (q & 15) * 4;
+      const int T = 2 * (c >> 5) + (o >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (o & 31);
+      const int at = ((T * 4 + g) * 64 + l) * 4 + (c & 3);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = RED[at + 4 * k] + RED[16384 + at + 4 * k];
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, e * 16, 0, 16 /* sc1 */);
+  }
+  if (tid < 64) {  // b2: out block u = tid >> 5 from waves u (K-half 0) and 4 + u (K-half 1)
+    const int u = tid >> 5, o = tid & 31;
+    slab[P_B2 + tid] = DB2S[u * 32 + o] + DB2S[(4 + u) * 32 + o];
+  }
+  if (tid == 0) {
+    float l = 0.f;
+    for (int w = 0; w < 8; ++w) l += LOSSS[w];
+    loss_slabs[blockIdx.x] = l;
+  }
+  if (V4_STAMPS && lane < 10) {  // phase cycles of this wave -> spare slab floats (after the slab)
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) v = (lane == j) ? st.acc[j] : v;
+    slab[P_TOTAL + wave * 16 + lane] = (float)v;
+  }
+}
+
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
 __global__ void __launch_bounds__(256)
 mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
@@ -1114,16 +1551,29 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
                               TRAIN_LDS);
     attr_set = true;
   }
-  static int use_v3 = -1;
+  static int use_v3 = -1, use_v5 = 0;
   if (use_v3 < 0) {
     const char* e = std::getenv("EM_FUSED_V3");
     use_v3 = (e && e[0] == '1') ? 1 : 0;
+    const char* e5 = std::getenv("EM_FUSED_V5");
+    use_v5 = (e5 && e5[0] == '1') ? 1 : 0;
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_v4_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               V4_LDS);
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_v4_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               V4_LDS);
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v5_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V5_LDS);
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v5_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V5_LDS);
   }
-  if (!use_v3) {
+  if (use_v5 && !use_v3) {
+    if (loss_kind == 0)
+      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<0>, dim3(nslab), dim3(512), V5_LDS, stream, draws, sidx, (int)B,
+                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+    else
+      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<1>, dim3(nslab), dim3(512), V5_LDS, stream, draws, sidx, (int)B,
+                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+  } else if (!use_v3) {
     if (loss_kind == 0)
       hipLaunchKernelGGL(mlp_fused_train_v4_kernel<0>, dim3(nslab), dim3(512), V4_LDS, stream, draws, sidx, (int)B,
                          (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);

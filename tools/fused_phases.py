@@ -17,6 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = ["F1+relu+Himg", "F2 own", "wait H", "F2 partner+Ximg", "loss part1", "wait stats", "dz+pack+D2",
           "wait dz", "B1+mask", "dW+db2"]
+if os.environ.get("EM_FUSED_V5") == "1":  # v5 round phases (csrc/mlp_fused.hip, mlp_fused_train_v5_kernel)
+    PHASES = ["A (own tile)", "wait 1", "B1 dW2", "wait 2", "dump", "wait 3", "B2 dW1", "wait 4", "-", "-"]
 
 
 def main():
@@ -38,6 +40,8 @@ def main():
     if not st.any():
         raise SystemExit("no stamps recorded: build with --define V4_STAMPS=1")
     raw = m.slabs[:nslab, FM.P_TOTAL + 128:FM.P_TOTAL + 132].contiguous().view(torch.int32).cpu().numpy()
+    if not raw.any():
+        raw = np.zeros((nslab, 4), np.int32)
     t = raw.astype(np.int64) & 0xFFFFFFFF
     t -= t[:, 0].min()
     us = t / 100.0  # s_memrealtime ticks at 100 MHz
