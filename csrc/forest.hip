@@ -20,6 +20,8 @@
 //   rf_partition   stable-free ballot partition of the node's row list into its children.
 // Trees are complete binary arrays: node i has children 2i+1 (x_f = 0) and 2i+2 (x_f = 1).
 #include <cstdint>
+#include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -62,6 +64,21 @@ __device__ inline int xbit(const uint64_t* __restrict__ X, int W, int64_t row, i
   return (int)((X[row * W + (f >> 6)] >> (f & 63)) & 1ull);
 }
 
+// Row lists come in two forms.  Index form (int32, any W): the row id, with the bootstrap weight in
+// bits 27..30 when N < 2^27; every level gathers X[r] and Y[r] at random.  Record form (W == 1,
+// N < 2^27): the row's data itself, 16 B = {x | w_hi << 62, y | w_lo << 62} (x, y: 62 feature / output
+// bits, w: 4-bit bootstrap weight), so each level streams its nodes' rows contiguously and the
+// partition moves records instead of indices (MI355X: the deep levels were bound by the 8-B random
+// gathers -- 4.4 ms of a 4.5 ms level at 64 nodes per tree -- not by the histogram arithmetic).
+constexpr uint64_t RF_M62 = (1ull << 62) - 1;
+struct RfRec {
+  uint64_t x, y;
+};
+EM_DEVICE RfRec rf_make_rec(uint64_t x, uint64_t y, uint32_t w) {
+  return RfRec{(x & RF_M62) | ((uint64_t)(w >> 2) << 62), (y & RF_M62) | ((uint64_t)(w & 3u) << 62)};
+}
+EM_DEVICE uint32_t rf_rec_w(const RfRec& r) { return (uint32_t)((r.x >> 62) << 2 | (r.y >> 62)); }
+
 struct RfParams {
   const uint64_t* X;
   const uint64_t* Y;
@@ -86,12 +103,14 @@ __host__ __device__ inline int rec_words(int k) { return 68 + ((k + 3) & ~3) + 6
 // Root row lists: rows with non-zero bootstrap weight, compacted per tree by (blocks x tree)
 // workgroups; each 256-row chunk reserves its output range with one atomic (row order inside a list
 // is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
-__global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, int32_t* __restrict__ rows) {
+template <bool REC>
+__global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restrict__ rows_v) {
   const int t = blockIdx.y, B = gridDim.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ int wcnt[4];
   __shared__ int base;
-  int32_t* out = rows + (int64_t)t * p.N;
+  int32_t* out = static_cast<int32_t*>(rows_v) + (int64_t)t * p.N;
+  RfRec* outr = static_cast<RfRec*>(rows_v) + (int64_t)t * p.N;
   const int64_t r0 = p.N * blockIdx.x / B, r1 = p.N * (blockIdx.x + 1) / B;
   for (int64_t c = r0; c < r1; c += RF_NT) {
     const int64_t r = c + threadIdx.x;
@@ -105,7 +124,10 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, int32_t* __res
     __syncthreads();
     int off = base;
     for (int i = 0; i < wv; ++i) off += wcnt[i];
-    if (keep) out[off + pre] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w << RF_WSHIFT)) : (int32_t)r;
+    if (keep) {
+      if constexpr (REC) outr[off + pre] = rf_make_rec(p.X[r], p.Y[r], (uint32_t)w);
+      else out[off + pre] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w << RF_WSHIFT)) : (int32_t)r;
+    }
     __syncthreads();
   }
 }
@@ -148,13 +170,67 @@ __global__ void rf_level_prep(RfParams p, int level) {
   }
 }
 
+// Level work lists.  Deep levels are very unbalanced (a one-hot split sends ~90 % of a node's rows to
+// the x = 0 child, so at level 6 one node of each tree holds about half of its rows), and sizing the
+// blocks per node from the AVERAGE node left one workgroup grinding through a 200k-row node while the
+// rest of the GPU idled.  rf_worklist gives every (tree, node) of the level ceil(count / RF_CHUNK)
+// blocks (exclusive prefix in wl[]); the level kernels run a 1-D grid and map block g to its
+// (tree, node, slice) by binary search.
+constexpr int RF_CHUNK = 8192;
+struct RfWork {
+  int t, nd, j, nb;
+};
+EM_DEVICE bool rf_work(const int32_t* __restrict__ wl, int nitems, int nodesL, RfWork& w) {
+  const int g = blockIdx.x;
+  if (g >= wl[nitems]) return false;
+  int lo = 0, hi = nitems;  // last i with wl[i] <= g (then g < wl[i + 1])
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (wl[mid] <= g) lo = mid;
+    else hi = mid;
+  }
+  w = RfWork{lo / nodesL, lo % nodesL, g - wl[lo], wl[lo + 1] - wl[lo]};
+  return true;
+}
+
+__global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32_t* __restrict__ wl) {
+  const int nodesL = 1 << level, first = nodesL - 1, n = p.T * nodesL;
+  __shared__ int part[1024];
+  const int per = (n + 1023) / 1024, a = threadIdx.x * per, b = min(n, a + per);
+  auto blocks = [&](int i) {
+    const int t = i / nodesL, nd = i - t * nodesL;
+    const int cnt = p.seg[((int64_t)t * p.nodes + first + nd) * 2 + 1];
+    return cnt < 0 ? 0 : max(1, (cnt + RF_CHUNK - 1) / RF_CHUNK);
+  };
+  int sum = 0;
+  for (int i = a; i < b; ++i) sum += blocks(i);
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = part[threadIdx.x] - sum;
+  for (int i = a; i < b; ++i) {
+    wl[i] = run;
+    run += blocks(i);
+  }
+  if (threadIdx.x == 1023) wl[n] = part[1023];
+}
+
 // K8: (blocks x nodes x trees) workgroups; block b of a node sums its slice of the node's row list
 // into LDS (integer atomics on set bits only: y bits for S, candidate x bits for cnt/hist), then
 // merges into the node record (plain stores when one block owns the node, else global atomics).
-__global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const int32_t* __restrict__ rows, int level) {
+template <bool REC>
+__global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restrict__ rows_v, int level,
+                                                 const int32_t* __restrict__ wl) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int nodesL = 1 << level, first = nodesL - 1;
-  const int t = blockIdx.z, nd = blockIdx.y, B = gridDim.x;
+  RfWork wk;
+  if (!rf_work(wl, p.T * nodesL, nodesL, wk)) return;
+  const int t = wk.t, nd = wk.nd, B = wk.nb;
   const int node = first + nd;
   const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
   const int start = sg[0], count = sg[1];
@@ -180,16 +256,27 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const int32_t* __re
     }
   }
   __syncthreads();
-  const int32_t* rl = rows + (int64_t)t * p.N + start;
-  const int i0 = (int)((int64_t)count * blockIdx.x / B), i1 = (int)((int64_t)count * (blockIdx.x + 1) / B);
+  const int32_t* rl = static_cast<const int32_t*>(rows_v) + (int64_t)t * p.N + start;
+  const RfRec* rr = static_cast<const RfRec*>(rows_v) + (int64_t)t * p.N + start;
+  const int i0 = (int)((int64_t)count * wk.j / B), i1 = (int)((int64_t)count * (wk.j + 1) / B);
   uint32_t my_n = 0;
   const bool packed = rf_packed(p.N);
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int32_t e = rl[i];
-    const int64_t r = packed ? (e & RF_RMASK) : e;
-    const uint32_t w = packed ? (uint32_t)e >> RF_WSHIFT : (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
+    int64_t r = 0;
+    uint32_t w;
+    uint64_t y, xr = 0;
+    if constexpr (REC) {
+      const RfRec e = rr[i];
+      w = rf_rec_w(e);
+      y = e.y & RF_M62;
+      xr = e.x & RF_M62;
+    } else {
+      const int32_t e = rl[i];
+      r = packed ? (e & RF_RMASK) : e;
+      w = packed ? (uint32_t)e >> RF_WSHIFT : (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
+      y = p.Y[r] & RF_M62;
+    }
     my_n += w;
-    const uint64_t y = p.Y[r] & ((1ull << 62) - 1);
     uint64_t yy = y;
     while (yy) {
       atomicAdd(&S[__builtin_ctzll(yy)], w);
@@ -197,7 +284,7 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const int32_t* __re
     }
     if (!split) continue;
     for (int wd = 0; wd < p.W; ++wd) {
-      uint64_t xx = p.X[r * p.W + wd] & cmask[wd];
+      uint64_t xx = (REC ? xr : p.X[r * p.W + wd]) & cmask[wd];
       while (xx) {
         const int sl = slot[wd * 64 + __builtin_ctzll(xx)];
         xx &= xx - 1;
@@ -220,6 +307,126 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const int32_t* __re
   } else {
     for (int i = threadIdx.x; i < used; i += blockDim.x)
       if (lds[i]) atomicAdd(&dst[i], lds[i]);
+  }
+}
+
+// K8 on the matrix cores (binary features, W == 1, k <= 15 candidates): the node histogram is one
+// small GEMM over the node's rows, hist = (w * Xc)ᵀ · Y, with
+//   A [16 x rows]  row c < k: w_r * x_{cand c}(r); row 15: w_r (so D[15][j] = S[j], D[15][62] = n);
+//                  rows k..14: 0
+//   B [rows x 64]  y_j(r) for j < 62; column 62: 1 (so D[c][62] = cnt[c]); column 63: 0
+// on v_mfma_f32_16x16x32_bf16 (K = 32 rows per instruction, 4 output tiles).  Every operand is an
+// integer <= 15 (exact in bf16) and every per-wave sum stays < 2^24 (exact in fp32), so the record is
+// still exact integers and the trees stay bit-identical to the atomic kernel and the numpy oracle.
+// Instead of ~14 LDS atomics per row on 62 + 8x62 contended bins it costs ~3 VALU + 1/8 MFMA per row;
+// each wave keeps its 16 x 64 partial in 16 registers and folds it into the block record once.
+// Measured on the record-form row lists it is ~10 % slower than the atomic kernel (operand bits are
+// gathered one VALU op per row and column), so it is opt-in: EM_RF_MFMA=1.
+// Row data (y | w low bits, x | w high bits) are staged through a wave-private 1 KB LDS slice.
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+EM_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(RF_NT) rf_hist_mfma(RfParams p, const RfRec* __restrict__ rows, int level,
+                                                      const int32_t* __restrict__ wl) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int nodesL = 1 << level, first = nodesL - 1;
+  RfWork wk;
+  if (!rf_work(wl, p.T * nodesL, nodesL, wk)) return;
+  const int t = wk.t, nd = wk.nd, B = wk.nb;
+  const int node = first + nd;
+  const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
+  const int start = sg[0], count = sg[1];
+  if (count < 0) return;
+  const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
+  const bool split = level < p.max_depth;
+  const int kk = split ? (k < p.F ? k : p.F) : 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  // LDS: [rec] record | [256] byte -> 8 bf16 {0,1} table (4 KB) | per wave 64 rows x 16 B
+  uint32_t* recd = lds;
+  const uint32_t LUT = (uint32_t)(((rec + 3) & ~3) * 4);
+  const uint32_t ROWS = LUT + 4096 + (uint32_t)wv * 1024;
+  char* smem = reinterpret_cast<char*>(lds);
+  for (int i = threadIdx.x; i < rec; i += blockDim.x) recd[i] = 0u;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x)
+    *reinterpret_cast<bf16x8*>(smem + LUT + i * 16) = bits_to_bf16x8((uint32_t)i);
+  // this lane's A row: candidate slot m = lane & 15 (15 = the all-w row), its feature bit
+  const int m = lane & 15, g = lane >> 4;
+  int fbit = -1;  // -1: zero row
+  if (m < kk) fbit = p.cand[((int64_t)t * nodesL + nd) * k + m];
+  const bool wrow = m == 15;
+  __syncthreads();
+
+  const RfRec* rl = rows + (int64_t)t * p.N + start;
+  const int i0 = (int)((int64_t)count * wk.j / B), i1 = (int)((int64_t)count * (wk.j + 1) / B);
+  f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
+  for (int c0 = i0 + wv * 64; c0 < i1; c0 += nwv * 64) {
+    // stage 64 rows: lane = row
+    {  // the node's records are contiguous: one 16-B load per lane (zero record = weight 0 past the end)
+      const int i = c0 + lane;
+      const RfRec e = i < i1 ? rl[i] : RfRec{0, 0};
+      *reinterpret_cast<u32x4*>(smem + ROWS + lane * 16) =
+          u32x4{(uint32_t)e.y, (uint32_t)(e.y >> 32), (uint32_t)e.x, (uint32_t)(e.x >> 32)};
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      // this lane's 8 rows: 32 half + 8 g + j
+      uint32_t ylo[8], yhi[8], xw[8];
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(smem + ROWS + (32 * half + 8 * g + j) * 16);
+        ylo[j] = v[0];
+        yhi[j] = v[1] & 0x3FFFFFFFu;
+        const uint32_t w = (v[1] >> 30) | ((v[3] >> 30) << 2);
+        const uint32_t xb = fbit < 0 ? 0u : ((fbit < 32 ? v[2] >> fbit : v[3] >> (fbit - 32)) & 1u);
+        a[j] = (float)(wrow ? w : xb * w);
+        xw[j] = w;
+      }
+      const bf16x8 af = pack8(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        const int n = 16 * tn + m;  // output column of this lane in tile tn
+        uint32_t byte = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          uint32_t bit;
+          if (tn < 2) bit = (ylo[j] >> n) & 1u;
+          else bit = n == 62 ? (xw[j] != 0u ? 1u : 0u) : (n == 63 ? 0u : (yhi[j] >> (n - 32)) & 1u);
+          byte |= bit << j;
+        }
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(smem + LUT + byte * 16);
+        acc[tn] = mfma16(af, bfr, acc[tn]);
+      }
+    }
+    wave_lds_sync();  // the staging slice is rewritten by the next chunk
+  }
+  // fold: D[row 4g + i][col 16 tn + m] -> record (integer LDS atomics: exact, order-free)
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 4 * g + i, col = 16 * tn + m;
+      const uint32_t v = (uint32_t)acc[tn][i];
+      if (v == 0u) continue;
+      if (row == 15) {
+        if (col < 62) atomicAdd(&recd[col], v);   // S[j]
+        else if (col == 62) atomicAdd(&recd[64], v);  // n
+      } else if (row < kk) {
+        if (col < 62) atomicAdd(&recd[68 + kp + row * 64 + col], v);  // hist[c][j]
+        else if (col == 62) atomicAdd(&recd[68 + row], v);            // cnt[c]
+      }
+    }
+  __syncthreads();
+  uint32_t* dst = p.acc + ((int64_t)t * nodesL + nd) * rec;
+  const int used = split ? rec : 68;
+  if (B == 1) {
+    for (int i = threadIdx.x; i < used; i += blockDim.x) dst[i] = recd[i];
+  } else {
+    for (int i = threadIdx.x; i < used; i += blockDim.x)
+      if (recd[i]) atomicAdd(&dst[i], recd[i]);
   }
 }
 
@@ -279,10 +486,17 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
 // K10: children row lists, (blocks x nodes x trees) workgroups: left rows (x_f = 0) fill the parent
 // segment from its start, right rows from its end; every 256-row chunk reserves its ranges with one
 // atomic per side on the node's counters (lrc), which rf_level_prep turns into the child segments.
-__global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t* __restrict__ rin,
-                                                      int32_t* __restrict__ rout, int level) {
+template <bool REC>
+__global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __restrict__ rin_v,
+                                                      void* __restrict__ rout_v, int level,
+                                                      const int32_t* __restrict__ wl) {
+  using E = typename std::conditional<REC, RfRec, int32_t>::type;
+  const E* rin = static_cast<const E*>(rin_v);
+  E* rout = static_cast<E*>(rout_v);
   const int nodesL = 1 << level, first = nodesL - 1;
-  const int t = blockIdx.z, nd = blockIdx.y, B = gridDim.x, node = first + nd;
+  RfWork wk;
+  if (!rf_work(wl, p.T * nodesL, nodesL, wk)) return;
+  const int t = wk.t, nd = wk.nd, B = wk.nb, node = first + nd;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
   const int start = sg[0], count = sg[1];
@@ -295,23 +509,25 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const int32_t*
   __shared__ int lc[2][RR][4], rc[2][RR][4];
   __shared__ int lbase[2], rbase[2];
   int32_t* ctr = p.lrc + ((int64_t)t * nodesL + nd) * 2;
-  const int32_t* ri = rin + (int64_t)t * p.N + start;
-  int32_t* ro = rout + (int64_t)t * p.N + start;
-  const int i0 = (int)((int64_t)count * blockIdx.x / B), i1 = (int)((int64_t)count * (blockIdx.x + 1) / B);
+  const E* ri = rin + (int64_t)t * p.N + start;
+  E* ro = rout + (int64_t)t * p.N + start;
+  const int i0 = (int)((int64_t)count * wk.j / B), i1 = (int)((int64_t)count * (wk.j + 1) / B);
   int buf = 0;
   for (int c = i0; c < i1; c += RR * blockDim.x, buf ^= 1) {
-    int32_t r[RR];
-    bool right[RR], left[RR];
+    E r[RR];
+    bool right[RR], left[RR], have[RR];
 #pragma unroll
-    for (int k = 0; k < RR; ++k) {  // the RR row-index loads, then the RR feature-bit loads, all in flight
+    for (int k = 0; k < RR; ++k) {  // the RR row loads, then the RR feature-bit loads, all in flight
       const int i = c + k * blockDim.x + threadIdx.x;
-      r[k] = i < i1 ? ri[i] : -1;
+      have[k] = i < i1;
+      if (have[k]) r[k] = ri[i];
     }
     int pl[RR], pr[RR];
 #pragma unroll
     for (int k = 0; k < RR; ++k) {
-      right[k] = r[k] >= 0 && xbit(p.X, p.W, r[k] & (rf_packed(p.N) ? RF_RMASK : 0x7FFFFFFF), f);
-      left[k] = r[k] >= 0 && !right[k];
+      if constexpr (REC) right[k] = have[k] && ((r[k].x >> f) & 1ull);
+      else right[k] = have[k] && xbit(p.X, p.W, r[k] & (rf_packed(p.N) ? RF_RMASK : 0x7FFFFFFF), f);
+      left[k] = have[k] && !right[k];
       const uint64_t bl = __ballot(left[k]), br = __ballot(right[k]);
       pl[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0));
       pr[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(br >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)br, 0));
@@ -395,6 +611,10 @@ __global__ void __launch_bounds__(256) rf_predict(const uint64_t* __restrict__ X
 
 EM_API int em_rf_nodes(int max_depth) { return (1 << (max_depth + 1)) - 1; }
 
+// bytes per row of the rows_a / rows_b scratch em_rf_fit expects: 16 (record form: one feature word with
+// bits 62/63 free for the weight) or 4 (index form)
+EM_API int em_rf_row_bytes(int W, int F, int64_t N) { return (W == 1 && F <= 62 && N <= (int64_t)RF_RMASK) ? 16 : 4; }
+
 // per-level launch shape: blocks per node from the average node size (>= 4096 rows per block)
 static void rf_shape(int64_t N, int level, int& B, int& nt) {
   const int64_t avg = N / (1ll << level);
@@ -411,10 +631,10 @@ EM_API int64_t em_rf_acc_words(int T, int max_depth, int k_feat) {
 // Native level-wise driver: all T trees advance one level per (prep, hist, split, partition) round.
 // scratch: cand int16 [T][2^D][k], acc uint32 [em_rf_acc_words], lrc int32 [T][2^D][2]
 EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int F, int T, int max_depth, int k_feat,
-                     int min_leaf, int bootstrap, uint64_t seed, int t_off, int32_t* rows_a, int32_t* rows_b,
+                     int min_leaf, int bootstrap, uint64_t seed, int t_off, void* rows_a, void* rows_b,
                      int32_t* seg, int16_t* feat, float* value, double* gain, float* cover, int16_t* cand,
-                     uint32_t* acc, int32_t* lrc, hipStream_t stream) {
-  if (!X || !Y || !rows_a || !rows_b || !seg || !feat || !value || !gain || !cover || !cand || !acc || !lrc)
+                     uint32_t* acc, int32_t* lrc, int32_t* wl, hipStream_t stream) {
+  if (!X || !Y || !rows_a || !rows_b || !seg || !feat || !value || !gain || !cover || !cand || !acc || !lrc || !wl)
     return EM_ERR_ARG;
   if (W < 1 || F < 1 || F > RF_MAXF || F > 64 * W || T < 1 || max_depth < 0 || max_depth > 14 || k_feat < 1 ||
       k_feat > RF_MAXF || min_leaf < 1 || N < 1 || N >= (1ll << 31))
@@ -424,21 +644,41 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const size_t lds = (size_t)rec * 4;
   if (lds > 160 * 1024 - 8192) return EM_ERR_ARG;
   static bool attr = false;
+  static int mfma_env = -1;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)rf_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
+    (void)hipFuncSetAttribute((const void*)rf_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 8192);
+    (void)hipFuncSetAttribute((const void*)rf_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 8192);
+    (void)hipFuncSetAttribute((const void*)rf_hist_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 8192);
+    // opt-in: on the record-form row lists the LDS-atomic histogram measured faster (fit 6.2 vs
+    // 7.0 ms, 700k rows x 100 trees, depth 8): the matrix-core form spends its time building
+    // operands bit by bit, not in the MFMAs
+    const char* e = std::getenv("EM_RF_MFMA");
+    mfma_env = (e && e[0] == '1') ? 1 : 0;
     attr = true;
   }
+  // record-form row lists for one-word features (rows_a/rows_b hold 16 B per row: em_rf_row_bytes);
+  // the matrix-core histogram on them for <= 15 candidates (bootstrap weight < 10: every operand is an
+  // exact bf16 integer)
+  const bool rec_rows = em_rf_row_bytes(W, F, N) == 16;
+  const bool use_mfma = rec_rows && mfma_env && k_feat <= 15;
+  const size_t lds_mfma = (size_t)(((rec + 3) & ~3) * 4) + 4096 + 4 * 1024;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
              cover, cand, acc, lrc};
   (void)hipMemsetAsync(lrc, 0, (size_t)T * 2 * sizeof(int32_t), stream);
   {
     int B, nt;
     rf_shape(N, 0, B, nt);
-    hipLaunchKernelGGL(rf_init_rows, dim3(B, T), dim3(RF_NT), 0, stream, p, rows_a);
+    if (rec_rows)
+      hipLaunchKernelGGL(rf_init_rows<true>, dim3(B, T), dim3(RF_NT), 0, stream, p, (void*)rows_a);
+    else
+      hipLaunchKernelGGL(rf_init_rows<false>, dim3(B, T), dim3(RF_NT), 0, stream, p, (void*)rows_a);
   }
   EM_CHECK_LAUNCH();
-  int32_t* rin = rows_a;
-  int32_t* rout = rows_b;
+  void* rin = rows_a;
+  void* rout = rows_b;
   const int64_t kept = bootstrap ? (N * 632) / 1000 : N;  // expected rows per tree (Poisson(1): 1 - 1/e)
   for (int level = 0; level <= max_depth; ++level) {
     const int nodesL = 1 << level;
@@ -446,15 +686,30 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     rf_shape(kept, level, B, nt);
     const int64_t tn = (int64_t)T * nodesL;
     hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level);
-    if (B > 1) (void)hipMemsetAsync(acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
-    hipLaunchKernelGGL(rf_hist, dim3(B, nodesL, T), dim3(nt), lds, stream, p, rin, level);
+    hipLaunchKernelGGL(rf_worklist, dim3(1), dim3(1024), 0, stream, p, level, wl);
+    // grid: an upper bound of the work list (the kernels exit past wl[tn])
+    const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;  // kept rows per tree <= N
+    const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
+    (void)B;
+    (void)hipMemsetAsync(acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
+    if (use_mfma)
+      hipLaunchKernelGGL(rf_hist_mfma, dim3(G), dim3(nt), lds_mfma, stream, p, (const RfRec*)rin, level, (const int32_t*)wl);
+    else if (rec_rows)
+      hipLaunchKernelGGL(rf_hist<true>, dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
+    else
+      hipLaunchKernelGGL(rf_hist<false>, dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
     hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level);
     EM_CHECK_LAUNCH();
     if (level == max_depth) break;
     (void)hipMemsetAsync(lrc, 0, (size_t)tn * 2 * sizeof(int32_t), stream);
-    hipLaunchKernelGGL(rf_partition, dim3(B, nodesL, T), dim3(nt), 0, stream, p, rin, rout, level);
+    if (rec_rows)
+      hipLaunchKernelGGL(rf_partition<true>, dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
+                         (const int32_t*)wl);
+    else
+      hipLaunchKernelGGL(rf_partition<false>, dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
+                         (const int32_t*)wl);
     EM_CHECK_LAUNCH();
-    int32_t* tmp = rin;
+    void* tmp = rin;
     rin = rout;
     rout = tmp;
   }

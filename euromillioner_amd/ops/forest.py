@@ -12,10 +12,12 @@ from . import _native as N
 
 N.register_signatures({
     "em_rf_nodes": (N._i32, [N._i32]),
+    "em_rf_row_bytes": (N._i32, [N._i32, N._i32, N._i64]),
     "em_rf_acc_words": (N._i64, [N._i32, N._i32, N._i32]),
     "em_rf_fit": (N._i32, [N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32, N._i32, N._i32, N._i32, N._i32, N._i32,
                            N.ctypes.c_uint64, N._i32, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p,
-                           N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p]),
+                           N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p,
+                           N._c_void_p]),
     "em_rf_predict": (N._i32, [N._c_void_p, N._i32, N._i64, N._c_void_p, N._c_void_p, N._i32, N._i32, N._i32,
                                N._c_void_p, N._i32, N._c_void_p]),
 })
@@ -38,8 +40,10 @@ def fit(X: np.ndarray | torch.Tensor, Y: np.ndarray | torch.Tensor, F: int, t_of
     if n >= 2**31 - 1 or n < 1:
         raise ValueError("rows must be in [1, 2^31-2]")
     nodes = (1 << (max_depth + 1)) - 1
-    rows_a = torch.empty(T, n, dtype=torch.int32, device=dev)
-    rows_b = torch.empty(T, n, dtype=torch.int32, device=dev)
+    # per-tree row lists: 16-B records (x, y, weight) for one-word features, else int32 row ids
+    rw = N.query("em_rf_row_bytes", W, F, n) // 4
+    rows_a = torch.empty(T, n, rw, dtype=torch.int32, device=dev)
+    rows_b = torch.empty(T, n, rw, dtype=torch.int32, device=dev)
     seg = torch.empty(T, nodes, 2, dtype=torch.int32, device=dev)
     feat = torch.full((T, nodes), -2, dtype=torch.int16, device=dev)
     value = torch.zeros(T, nodes, 64, dtype=torch.float32, device=dev)
@@ -52,11 +56,12 @@ def fit(X: np.ndarray | torch.Tensor, Y: np.ndarray | torch.Tensor, F: int, t_of
     cand = torch.empty(T, 1 << max_depth, k, dtype=torch.int16, device=dev)
     acc = torch.empty(acc_words, dtype=torch.int32, device=dev)
     lrc = torch.empty(T, 1 << max_depth, 2, dtype=torch.int32, device=dev)
+    wl = torch.empty(T * (1 << max_depth) + 1, dtype=torch.int32, device=dev)  # per-level work list
     N.call("em_rf_fit", Xd.data_ptr(), W, Yd.data_ptr(), n, F, T, max_depth, k, min_leaf, int(bootstrap),
            int(seed) & 0xFFFFFFFFFFFFFFFF, int(t_off), rows_a.data_ptr(), rows_b.data_ptr(), seg.data_ptr(),
            feat.data_ptr(), value.data_ptr(), gain.data_ptr(), cover.data_ptr(), cand.data_ptr(), acc.data_ptr(),
-           lrc.data_ptr(), N.stream_handle(dev))
-    del rows_a, rows_b, cand, acc, lrc
+           lrc.data_ptr(), wl.data_ptr(), N.stream_handle(dev))
+    del rows_a, rows_b, cand, acc, lrc, wl
     if return_device:
         return feat, value, gain, cover
     return feat.cpu().numpy(), value.cpu().numpy(), gain.cpu().numpy(), cover.cpu().numpy()

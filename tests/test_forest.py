@@ -90,7 +90,11 @@ def test_tree_ids_make_shards_compose(draws):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("depth,subset,boot,lags", [(5, "sqrt", True, 1), (3, "all", False, 1), (6, "0.3", True, 2)])
+# one feature word: record-form row lists (sqrt / log2 / all); two words (lags 2): index form.  Every
+# histogram kernel must reproduce the oracle exactly (test_hip_forest_mfma_histogram_matches_oracle
+# runs the matrix-core one)
+@pytest.mark.parametrize("depth,subset,boot,lags", [(5, "sqrt", True, 1), (3, "all", False, 1), (6, "0.3", True, 2),
+                                                   (7, "log2", False, 1), (8, "sqrt", True, 1)])
 def test_hip_forest_matches_oracle(depth, subset, boot, lags):
     ds = DrawSet.synthetic(n=3000, seed=2, planted=0.7, calendar=False)
     X, Y, F = draw_features(ds.numbers, lags)
@@ -150,3 +154,29 @@ def test_hip_forest_predict_matches_torch_traversal(depth):
         acc += value[t][nd]
     ref = acc / feat.shape[0]
     assert torch.allclose(p[:, :62], ref[:, :62], atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_hip_forest_mfma_histogram_matches_oracle():
+    """EM_RF_MFMA=1 (the matrix-core histogram, rf_hist_mfma) in a fresh process: trees equal the oracle's."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import numpy as np\n"
+        "from euromillioner_amd.data.draws import DrawSet\n"
+        "from euromillioner_amd.models.forest import RandomForest, draw_features\n"
+        "ds = DrawSet.synthetic(n=3000, seed=2, planted=0.7, calendar=False)\n"
+        "X, Y, F = draw_features(ds.numbers, 1)\n"
+        "for depth, subset, boot in ((5, 'sqrt', True), (7, 'log2', False)):\n"
+        "    g = RandomForest(n_trees=10, max_depth=depth, feature_subset=subset, bootstrap=boot, seed=11, device='cuda')\n"
+        "    g.fit(X, Y, F)\n"
+        "    c = RandomForest(n_trees=10, max_depth=depth, feature_subset=subset, bootstrap=boot, seed=11, device='cpu')\n"
+        "    c.fit(X, Y, F)\n"
+        "    assert np.array_equal(g.feat, c.feat) and np.array_equal(g.gain, c.gain)\n"
+        "print('MFMA_RF_OK')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, EM_RF_MFMA="1", PYTHONPATH=root),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "MFMA_RF_OK" in r.stdout, r.stderr[-2000:]
