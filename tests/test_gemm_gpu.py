@@ -305,3 +305,30 @@ def test_wgrad_skinny_matches_fp32(M, J, W, wide_dz):
     assert _rel(gw2.double(), 1.5 * ref) < 1e-5
     again = LIN.linear_wgrad(dz, x)
     assert torch.equal(again, gw)  # fixed-order slice reduction: bitwise repeatable
+
+
+def test_gemm_trainer_odd_wide_layers_take_the_tile_path(data):
+    """Hidden 1000 pads to 1024 (relu, bf16): the 256-tile GEMMs run every layer, the pad units stay
+    exactly zero through a step, and the gradients still match the fp32 DrawMLP."""
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+    from euromillioner_amd.models.mlp import DrawMLP
+
+    ds, masks = data
+    sizes, B, off = (62, 1000, 1000, 62), 1024, 7
+    tr = GemmMLPTrainer(sizes, seed=4, lr=1e-3)
+    assert tr.padded == (64, 1024, 1024, 64)
+    plan = tr._plan(B)
+    assert plan["wgrad"][1] and plan["dgrad"][1] and plan["dgrad"][2]
+    ref = DrawMLP(sizes, seed=4)
+    X = torch.from_numpy(multi_hot(ds.numbers[off:off + B])).float()
+    Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).float()
+    l = ref.loss(ref(X), Y)
+    l.backward()
+    lk, gk = tr.grads_only(masks, B, offset=off)
+    assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
+    for n, p in ref.named_parameters():
+        assert _rel(gk[n].cpu(), p.grad) < 5e-2, n
+    tr.step(masks, B, offset=off)
+    torch.cuda.synchronize()
+    w1, _ = tr._views(tr.params, 1)  # [1024, 1024]: rows/cols 1000.. are padding
+    assert float(w1[1000:].abs().max()) == 0.0 and float(w1[:, 1000:].abs().max()) == 0.0
