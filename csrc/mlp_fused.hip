@@ -535,6 +535,9 @@ EM_DEVICE int v4_cls(int i, int h) {
 #ifndef V4_STAMPS
 #define V4_STAMPS 0
 #endif
+#ifndef V4_F1_HOIST
+#define V4_F1_HOIST 1
+#endif
 struct V4Stamps {
   uint64_t last = 0;
   uint64_t acc[10] = {};
@@ -598,13 +601,23 @@ EM_DEVICE void v4_tile(char* smem, const char* lut, uint32_t PB, int pairw, int 
 
   // ---- F1 (own hidden half) -> relu -> hT (B of F2) + own H image [32 samples][64 hid] ----
   bf16x8 hT[2][2];
-  // both hidden tiles' chains interleaved: 8 independent-pair MFMAs back to back on the matrix pipe
+  // every W1ᵀ fragment read issued before the first MFMA (V4_F1_HOIST), so the chain pays one LDS
+  // latency instead of one per MFMA pair; then both hidden tiles' chains interleaved
+  bf16x8 w1f[2][4];
+  if (V4_F1_HOIST) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) w1f[tt][q] = lds_frag(smem, w1t_off(32 * (2 * RHO + tt) + r, 2 * q + h));
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain (the scheduler interleaves them)
+  }
   f32x16 a1s[2] = {f32x16{}, f32x16{}};
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
-      a1s[tt] = mfma32(lds_frag(smem, w1t_off(32 * (2 * RHO + tt) + r, 2 * q + h)), xf[q], a1s[tt]);
+      a1s[tt] = mfma32(V4_F1_HOIST ? w1f[tt][q] : lds_frag(smem, w1t_off(32 * (2 * RHO + tt) + r, 2 * q + h)), xf[q],
+                       a1s[tt]);
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const f32x16& a1 = a1s[tt];

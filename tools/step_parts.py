@@ -42,10 +42,11 @@ def main():
     from euromillioner_amd.models.mlp import FusedSmallMLP
     from euromillioner_amd.ops import fused_mlp as FM
 
-    draws = generate_masks((1 << 23) + 16, seed=1, planted=0.9)
+    draws = generate_masks((1 << 24) + 16, seed=1, planted=0.9)
     m = FusedSmallMLP("cuda", lr=1e-3)
     out = []
-    for B in (1 << 20, 1 << 21, 1 << 22):
+    sizes = [int(x) for x in os.environ.get("STEP_PARTS_B", "%d,%d,%d" % (1 << 20, 1 << 21, 1 << 22)).split(",")]
+    for B in sizes:
         nslab = FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
         lscale = 1.0 / B
 
