@@ -705,7 +705,15 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
   }
 }
 
-template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+// BAL = 1 spreads the fragment reads evenly over the four load segments of a K-tile (at most 8
+// ds_read_b128 per wave instead of 12, 8, 4, 0): phase 3's segment reads the NEXT K-tile's A(qm 0)
+// half into fa[0] (free during phase 3, which runs on fa[1] x B(qn 1)), so phase 0 reads only
+// B(qn 0).  In phase 0 the loading group's 12 reads + the LDS-DMA unit filled the LDS array for the
+// whole 256-cycle MFMA slot of the other group.  Hazards, with the unchanged staging schedule:
+// A0 / A2 of K-tile kt+1 are issued in slots 8kt-2 / 8kt-1 (-10 / -9 relative to 8(kt+1)), so they are
+// readable from 8kt+5 / 8kt+6 -- exactly the slots in which G0 / G1 read phase 3 of kt; their last read
+// now sits 3 slots earlier than before, so the WAR distance to the restage only grows.
+template <int OUT_BF16, int FN, int DACT, int HAS_CT, int BAL>
 __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                     void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
@@ -763,12 +771,16 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
           for (int ks = 0; ks < 2; ++ks)
             fb[jj][ks] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + (q >> 1) * 32 + 16 * jj + r16, 4 * ks + c4));
       }
-      if (q < 2) {
+      const bool rd_a = BAL ? (q == 1 || (q == 0 && kt == 0) || (q == 3 && kt + 1 < ktiles)) : q < 2;
+      if (rd_a) {
+        const int qa = q & 1;  // q == 3 reads qm 0 of the next K-tile
+        const char* lsrc = (BAL && q == 3) ? smem + ((kt + 1) & 1) * 2 * G_TILE : la;
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            fa[q][ii][ks] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + q * 64 + 16 * ii + r16, 4 * ks + c4));
+            fa[qa ^ (q == 3)][ii][ks] =
+                *reinterpret_cast<const bf16x8*>(lsrc + g_off(wm * 128 + (qa ^ (q == 3)) * 64 + 16 * ii + r16, 4 * ks + c4));
       }
     }
     if (pp_stage_slot(pa, pb, smem, slot, ktiles, wi)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -825,10 +837,15 @@ int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf
   static bool attr = false;
   static const bool pp = !getenv_flag_off("EM_GEMM_PP");
   static const bool m16 = !getenv_flag_off("EM_GEMM_MFMA16");
-  auto kern = pp ? (m16 ? gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT> : gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>)
+  static const bool bal = !getenv_flag_off("EM_GEMM_BAL");
+  auto kern = pp ? (m16 ? (bal ? gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 1>
+                               : gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 0>)
+                        : gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>)
                  : gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT>,
+    (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 0>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     (void)hipFuncSetAttribute((const void*)gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);

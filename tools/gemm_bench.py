@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--hidden", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cases", default="", help="comma-separated case names (default: all)")
+    ap.add_argument("--no-lib", action="store_true", help="skip the library (torch/hipBLASLt) timing")
     a = ap.parse_args()
     from euromillioner_amd.ops import linear as LIN
 
@@ -74,9 +76,12 @@ def main():
         ("square_8192", 2.0 * 8192 ** 3, lambda: LIN.linear_fwd(x[:8192], w, None, "none", out=y[:8192]),
          lambda: torch.nn.functional.linear(x[:8192], w)),
     ]
+    want = set(a.cases.split(",")) if a.cases else None
     for name, flop, ours, lib in cases:
+        if want is not None and name not in want:
+            continue
         t_o = timeit(ours, a.iters)
-        t_l = timeit(lib, a.iters)
+        t_l = timeit(lib, a.iters) if not a.no_lib else float("nan")
         print(json.dumps({"case": name, "B": B, "H": H, "ours_ms": round(t_o, 4), "lib_ms": round(t_l, 4),
                           "ours_tflops": round(flop / t_o / 1e9, 1), "lib_tflops": round(flop / t_l / 1e9, 1)}),
               flush=True)
