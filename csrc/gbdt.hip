@@ -104,11 +104,18 @@ __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restr
 constexpr int HIST_MAX_CHUNK = 1024;        // rows staged in LDS per piece
 constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // doubles of per-chunk partials (1 GiB) per level
 constexpr int HIST_LDS_BUDGET = 36 * 1024;  // per-block histogram copies (+ 10 B/row staging)
+constexpr int HIST_STAGE_LDS = 24 * 1024;   // per-block row staging (node, g, h, bins) when bins are staged
 
+// STAGE = 1 (opt-in, see plan_hist): the piece's bin rows are staged in LDS too, with wide
+// coalesced loads by the whole block, so the per-row chain runs on LDS only.  It does not pay: the
+// 8 byte loads in flight per wave of the STAGE = 0 form are not what bounds a large level, the
+// serial per-thread LDS update chain is.  Either way, per 8 rows every input is read before the 8
+// cell updates.  Rows go to copies exactly as in STAGE = 0 for the same piece size.
+template <int STAGE>
 __global__ void __launch_bounds__(256)
 gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
-          int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC) {
+          int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int c = blockIdx.x, t = blockIdx.y;
@@ -120,49 +127,84 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   const int per = NTn * ldsC * 2;
   for (int i = threadIdx.x; i < P * per; i += blockDim.x) hist[i] = 0.0;  // (ordered by the loop's first barrier)
   float* sg = reinterpret_cast<float*>(smem + (size_t)P * per * sizeof(double));
-  float* sh = sg + HIST_MAX_CHUNK;
-  int16_t* sn = reinterpret_cast<int16_t*>(sh + HIST_MAX_CHUNK);
+  float* sh = sg + piece;
+  int16_t* sn = reinterpret_cast<int16_t*>(sh + piece);
+  uint32_t* sbw = reinterpret_cast<uint32_t*>(sn + ((piece + 1) & ~1));  // staged bin words (STAGE)
   const int64_t base = (int64_t)t * n;
   const int nth = f1 - f0;
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
   const int f = f0 + (p < P ? fl : 0);
   double* my = hist + (size_t)(p < P ? p : 0) * per + (foff[f] - c0) * 2;
-  // the block's rows [c*chunk, +chunk) in staged pieces of <= HIST_MAX_CHUNK rows: per piece the
-  // rows' (node, g, h) go to LDS once (shared by every feature thread), then thread (p, fl) adds
+  // the block's rows [c*chunk, +chunk) in staged pieces of <= piece rows: per piece the rows'
+  // (node, g, h) (and bins) go to LDS once, shared by every feature thread, then thread (p, fl) adds
   // the p-th contiguous part of the piece to its copy in row order
   const int rb = c * chunk, re = min(n, rb + chunk);
-  for (int r0 = rb; r0 < re; r0 += HIST_MAX_CHUNK) {
-    const int r1 = min(re, r0 + HIST_MAX_CHUNK);
+  const int64_t nbytes = (int64_t)n * F;
+  for (int r0 = rb; r0 < re; r0 += piece) {
+    const int r1 = min(re, r0 + piece);
     __syncthreads();  // the previous piece's staging is consumed
     for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
       sg[r - r0] = g[base + r];
       sh[r - r0] = h[base + r];
       sn[r - r0] = (int16_t)(node[base + r] - first - n0);  // tile-relative node (outside -> skipped)
     }
+    int boff = 0;  // byte offset of row r0 inside the staged words
+    if (STAGE) {
+      const int64_t b0 = (int64_t)r0 * F, w0 = b0 >> 2;
+      boff = (int)(b0 & 3);
+      const int nw = (int)((((int64_t)r1 * F + 3) >> 2) - w0);
+      const bool tail = (w0 + nw) * 4 > nbytes;  // the array's last word, partly past its end
+      const int nwl = nw - (tail ? 1 : 0);        // words loaded whole
+      // range-checked buffer loads of the piece's words
+      const int64_t left = nbytes - w0 * 4;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(bins + w0 * 4), 0, (int)(left < 0x7FFFFFF0 ? left : 0x7FFFFFF0), 0x00020000);
+      int i = threadIdx.x;
+      for (; i + 3 * (int)blockDim.x < nwl; i += 4 * blockDim.x) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (i + u * blockDim.x) * 4, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sbw[i + u * blockDim.x] = v[u];
+      }
+      for (; i < nwl; i += blockDim.x) sbw[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, i * 4, 0, 0);
+      // a buffer load of a word that runs past the array end returns 0 in full: that word bytewise
+      if (threadIdx.x == 0 && tail) {
+        uint32_t v = 0;
+        for (int64_t q = (w0 + nw - 1) * 4; q < nbytes; ++q) v |= (uint32_t)bins[q] << (8 * (q & 3));
+        sbw[nw - 1] = v;
+      }
+    }
     __syncthreads();
     if (p < P) {
       const int len = r1 - r0, sub = (len + P - 1) / P;
       const int a0 = min(len, p * sub), a1 = min(len, a0 + sub);
+      const uint8_t* colL = reinterpret_cast<const uint8_t*>(sbw) + boff + f;  // STAGE: row r at colL[(r - r0) * F]
       const uint8_t* col = bins + (int64_t)r0 * F + f;
       int r = a0;
-      // 8 bin loads in flight, then the 8 updates in row order (sums bitwise = the plain loop)
+      // 8 rows' inputs first, then their 8 updates in row order (sums bitwise = the plain loop)
       for (; r + 8 <= a1; r += 8) {
-        int b[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) b[u] = col[(int64_t)(r + u) * F];
+        int b[8], nd[8];
+        float gv[8], hv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int nd = sn[r + u];
-          if ((unsigned)nd >= (unsigned)NTn) continue;
-          double* e = my + (nd * ldsC + b[u]) * 2;
-          e[0] += (double)sg[r + u];
-          e[1] += (double)sh[r + u];
+          b[u] = STAGE ? colL[(r + u) * F] : col[(int64_t)(r + u) * F];
+          nd[u] = sn[r + u];
+          gv[u] = sg[r + u];
+          hv[u] = sh[r + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if ((unsigned)nd[u] >= (unsigned)NTn) continue;
+          double* e = my + (nd[u] * ldsC + b[u]) * 2;
+          e[0] += (double)gv[u];
+          e[1] += (double)hv[u];
         }
       }
       for (; r < a1; ++r) {
         const int nd = sn[r];
         if ((unsigned)nd >= (unsigned)NTn) continue;
-        double* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
+        double* e = my + (nd * ldsC + (STAGE ? colL[r * F] : col[(int64_t)r * F])) * 2;
         e[0] += (double)sg[r];
         e[1] += (double)sh[r];
       }
@@ -483,7 +525,7 @@ inline int grid_for(int64_t total, int bs = 256) {
 // ------------------------------------------------------------------ host-side histogram plan
 namespace {
 struct HistPlan {
-  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads;
+  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece, stage;
   size_t lds;
 };
 
@@ -522,7 +564,16 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
         chunk = chunk < 64 ? 64 : chunk;
         pl.chunk = (int)chunk;
         pl.nchunks = (int)((n + chunk - 1) / chunk);
-        pl.lds = (size_t)P * NTn * maxC * 16 + (size_t)HIST_MAX_CHUNK * 10;
+        // pieces: rows staged per pass; with bins staged (F + 10 B/row) they fill <= HIST_STAGE_LDS
+        // (opt-in, EM_GBDT_HIST_STAGE=1: measured slower, 1316 vs 1170 us per level at 183k rows x 62
+        // tasks, equal at the reference's 928 rows -- the per-row LDS update chain, not the byte loads,
+        // bounds this kernel)
+        static const bool stage_on = getenv("EM_GBDT_HIST_STAGE") && getenv("EM_GBDT_HIST_STAGE")[0] == '1';
+        int piece = (int)(HIST_STAGE_LDS / (F + 10)) & ~15;
+        pl.stage = stage_on && piece >= 64;
+        pl.piece = pl.stage ? (piece < HIST_MAX_CHUNK ? piece : HIST_MAX_CHUNK) : HIST_MAX_CHUNK;
+        pl.lds = (size_t)P * NTn * maxC * 16 + (size_t)pl.piece * 10 + 4 +
+                 (pl.stage ? (((size_t)pl.piece * F + 8) & ~(size_t)3) + 4 : 0);
         return true;
       }
       if (FT == 1) break;
@@ -549,12 +600,17 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
   const int C = foff_h[F];
   const int64_t S = (int64_t)T * (1 << level) * C * 2;
   if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
-  hipLaunchKernelGGL(gbdt_hist, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g, h,
-                     node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC);
+  if (pl.stage)
+    hipLaunchKernelGGL(gbdt_hist<1>, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g,
+                       h, node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
+  else
+    hipLaunchKernelGGL(gbdt_hist<0>, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g,
+                       h, node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
   const bool split_folds = !fold && pl.nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
   if (pl.nchunks > 1 && !split_folds)
     hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
   *nchunks_out = split_folds ? pl.nchunks : 1;
+  EM_CHECK_LAUNCH();
   return 0;
 }
 

@@ -24,6 +24,9 @@ def main():
     cfg = C.RunConfig()
     cases = [("reference_calendar", None, 500, True), ("synthetic_262k", 262145, 50, False)]
     only = sys.argv[1] if len(sys.argv) > 1 else None
+    hip_only = only == "hip"  # every case, HIP engine only
+    if hip_only:
+        only = None
     for name, n, rounds, with_numpy in cases:
         if only and only not in name:
             continue
@@ -31,7 +34,7 @@ def main():
         X, Y, _ = gbdt_dataset(ds, cfg)
         m = int(0.7 * len(X))
         res = {"case": name, "rows": m, "features": X.shape[1], "tasks": Y.shape[1], "rounds": rounds}
-        for be in (["hip", "numpy"] if with_numpy and not only else ["hip"]):
+        for be in (["hip", "numpy"] if with_numpy and not only and not hip_only else ["hip"]):
             if be == "hip":  # exclude one-time GPU context / code-object load from the timing
                 GBDT.from_params(cfg.gbdt_params(), nround=2, backend=be).fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
             g = GBDT.from_params(cfg.gbdt_params(), nround=rounds, backend=be)
