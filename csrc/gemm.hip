@@ -232,9 +232,15 @@ EM_DEVICE uint32_t g_off(int row, int chunk) { return row * 128 + ((chunk ^ ((ro
 // (XCD-contiguous) block id -> output tile, grouped GM tile-rows at a time: the ~32 blocks an XCD
 // runs at once form a GM x (32/GM) super-tile, so each A panel slice is shared by 32/GM blocks and
 // each B panel slice by GM blocks in that XCD's L2 (GM = 8: ~12 GB of panel traffic per 65536 x 8192
-// x 8192 GEMM instead of ~33 GB with whole tile-rows, whose 32 distinct B panels miss L2)
+// x 8192 GEMM instead of ~33 GB with whole tile-rows, whose 32 distinct B panels miss L2).
+// GM: tile-rows per group.  Measured (tools/gpurun_gemm_gm.sh, TF/s at GM = 1 / 2 / 4 / 8): without a
+// C^T output 4 is best (65536x8192x8192 forward 1353 / 1384 / 1413 / 1366, NT dgrad 1270 / 1311 /
+// 1341 / 1324); with C^T 8 is (forward+C^T 1256 / 1287 / 1314 / 1329).  EM_GEMM_GM overrides both.
+__constant__ int g_gm_c = 0;
+
+template <int HAS_CT>
 EM_DEVICE void g_tile(int bid, int tiles_m, int tiles_n, int& m0, int& n0) {
-  constexpr int GM = 8;
+  const int GM = g_gm_c > 0 ? g_gm_c : (HAS_CT ? 8 : 4);
   const int per = GM * tiles_n;
   const int grp = bid / per, first = grp * GM;
   const int gm = tiles_m - first < GM ? tiles_m - first : GM;
@@ -395,7 +401,7 @@ gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   const int nwg = (M / G_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
   int m0, n0;
-  g_tile(bid, M / G_BM, tiles_n, m0, n0);
+  g_tile<HAS_CT>(bid, M / G_BM, tiles_n, m0, n0);
   const int ktiles = K / G_BK;
 
   f32x16 acc[4][2];
@@ -514,7 +520,7 @@ gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   const int nwg = (M / G_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
   int m0, n0;
-  g_tile(bid, M / G_BM, tiles_n, m0, n0);
+  g_tile<HAS_CT>(bid, M / G_BM, tiles_n, m0, n0);
   const int ktiles = K / G_BK;
   const int nph = 4 * ktiles;
 
@@ -726,7 +732,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   const int nwg = (M / G_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
   int m0, n0;
-  g_tile(bid, M / G_BM, tiles_n, m0, n0);
+  g_tile<HAS_CT>(bid, M / G_BM, tiles_n, m0, n0);
   const int ktiles = K / G_BK;
   const int nph = 4 * ktiles;
 
@@ -843,6 +849,11 @@ int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf
                         : gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>)
                  : gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
   if (!attr) {
+    static const char* gm_env = getenv("EM_GEMM_GM");
+    if (gm_env) {
+      const int gm = atoi(gm_env);
+      if (gm >= 1 && gm <= 64) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gm_c), &gm, sizeof(int));
+    }
     (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 1>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 0>,

@@ -167,6 +167,10 @@ def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None 
         out = empty_aligned(M, K, torch.bfloat16, dz.device)
     if dact in ("none", "identity"):
         y_prev = None
+    if big_ok(M, K, N_) and is_aligned(dz):
+        # 256-tile shapes: transpose the (weight-sized) w once and take the NT path
+        # (65536 x 8192 x 8192: 1250 TF/s vs 648 for the any-layout kernel, tools/gemm_bench.py)
+        return gemm(dz, True, transpose(w), True, out, M, K, N_, dact_src=y_prev, dact=dact)
     return gemm(dz, True, w, False, out, M, K, N_, dact_src=y_prev, dact=dact)
 
 
@@ -182,6 +186,10 @@ def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
         out = empty_aligned(N_, K, torch.float32, dz.device)
     if split_k is None and _skinny_ok(dz, x, out):
         return _wgrad_skinny(dz, x, out, alpha, beta)
+    if split_k is None and alpha == 1.0 and big_ok(N_, K, M) and out.dtype == torch.float32:
+        # 256-tile shapes: both operands transposed to K-major (two LDS-tiled copies, ~7 % of the
+        # GEMM at 65536 x 8192 x 8192) and the NT path (~1.2 PF/s vs 330 TF/s any-layout)
+        return gemm(transpose(dz), True, transpose(x), True, out, N_, K, M, beta=beta)
     tiles = ((N_ + 127) // 128) * ((K + 127) // 128)
     if split_k is None:
         split_k = 1

@@ -37,9 +37,9 @@ def test_forward_nt(M, N, K, act):
     assert _rel(yb, ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 200, 70), (64, 8192, 64), (2048, 136, 1000)])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 70), (64, 8192, 64), (2048, 136, 1000), (512, 512, 768)])
 @pytest.mark.parametrize("dact", ["none", "relu", "sigmoid", "tanh"])
-def test_dgrad_nn(M, N, K, dact):
+def test_dgrad_nn(M, N, K, dact):  # (512, 512, 768): 256-tile shape, routed through w^T and the NT path
     from euromillioner_amd.ops import linear as LIN
 
     g = torch.Generator(device="cuda").manual_seed(3 + M + N)
@@ -60,8 +60,8 @@ def test_dgrad_nn(M, N, K, dact):
     assert _rel(out, ref) < 1e-2, _rel(out, ref)
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 62, 64), (4096, 200, 136), (77, 9, 13)])
-def test_wgrad_tn_and_accumulate(M, N, K):
+@pytest.mark.parametrize("M,N,K", [(1000, 62, 64), (4096, 200, 136), (77, 9, 13), (1024, 256, 512)])
+def test_wgrad_tn_and_accumulate(M, N, K):  # (1024, 256, 512): alpha = 1 runs dz^T, x^T and the NT path
     from euromillioner_amd.ops import linear as LIN
 
     g = torch.Generator(device="cuda").manual_seed(M + K)
