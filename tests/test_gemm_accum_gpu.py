@@ -71,3 +71,23 @@ def test_bench_device_data_modes(args):
     assert d["value"] > 0 and d["steps"] == 3 and d["datagen"]["draws"] > 0 and d["n_gpus"] == 1
     if "--accum" in args:
         assert d["config"]["per_gpu_batch"] == 16384 and d["accum"] == 2
+
+
+def test_bench_two_ranks_share_one_task():
+    """bench.py --gpus 2 (gloo, both ranks on this GPU) launches its own ranks, reports n_gpus 2, and --
+    every rank training a shard of ONE planted sequence -- the averaged model beats the trivial
+    all-zero predictor on validation (per-rank tasks averaged below it: ADVICE round 1)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = ["--gpus", "2", "--dist-backend", "gloo", "--steps", "40", "--warmup", "2", "--batch", "65536",
+            "--draws-per-gpu", str(1 << 21)]
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=600, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2", d["config"]
+    assert d["val"]["acc"] > d["val"]["trivial_acc"] + 0.01, d["val"]
