@@ -119,6 +119,9 @@ def _parse():
     ap.add_argument("--accum", type=int, default=1,
                     help="mlp-wide: micro-batches of --batch per optimizer step (gradient accumulation; "
                          "the per-GPU batch of the step is batch * accum)")
+    ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="mlp-wide: gradient all-reduce wire dtype (bf16 halves the bytes; Adam state stays fp32)")
+    ap.add_argument("--bucket-mb", type=float, default=25.0, help="mlp-wide: gradient bucket size")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="DP gradient all-reduce of the fused path: xgmi = one-shot peer-memory reduction fused "
                          "into Adam (hipGraph-replayable); rccl = torch.distributed all_reduce; auto = xgmi if the "
@@ -233,7 +236,8 @@ def main():
 
         hidden = tuple(int(h) for h in (a.hidden or "8192,8192").split(","))
         sizes = (62,) + hidden + (62,)
-        model = GemmMLPTrainer(sizes, dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group)
+        model = GemmMLPTrainer(sizes, dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group,
+                               bucket_mb=a.bucket_mb, comm_dtype=a.comm_dtype)
         model.broadcast_parameters()
 
         def step(i):
@@ -363,6 +367,7 @@ def main():
                        "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
                        "graph_steps": C if use_graph else 0,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
+                       **({"comm_dtype": a.comm_dtype, "bucket_mb": a.bucket_mb} if a.model == "mlp-wide" else {}),
                        "dist_backend": a.dist_backend if world > 1 else None},
             "ms_per_step_median": med,
             "ms_per_step_max_rank": med_max,

@@ -43,6 +43,7 @@ _FLAGS = {
     "--batch": "mlp.batch", "--accum": "mlp.accum", "--steps": "mlp.steps", "--epochs": "mlp.epochs", "--dtype": "mlp.dtype",
     "--weight-decay": "mlp.weight_decay", "--eval-every": "mlp.eval_every",
     "--dp": "dist.dp", "--backend": "dist.backend", "--bucket-mb": "dist.bucket_mb", "--timeout": "dist.timeout_s",
+    "--comm-dtype": "dist.comm_dtype",
     "--fault-at-step": "dist.fault_at_step", "--fault-rank": "dist.fault_rank",
     "--check-sync-every": "dist.check_sync_every", "--avg-frequency": "dist.avg_frequency",
     "--profile-dir": "log.profile_dir", "--profile-steps": "log.profile_steps",

@@ -112,6 +112,7 @@ class DistConfig:
     dp: int = 1  # ranks on this node: > 1 without a torchrun env -> the CLI launches them (parallel/launch.py)
     backend: str = "auto"  # auto -> nccl (RCCL) on GPU, gloo on CPU
     bucket_mb: float = 25.0
+    comm_dtype: str = "fp32"  # GEMM engine gradient wire: fp32, or bf16 (half the all-reduce bytes)
     timeout_s: float = 300.0
     fault_at_step: int | None = None  # test-only fault injection
     fault_rank: int | None = None
@@ -258,6 +259,8 @@ def validate(cfg: RunConfig) -> RunConfig:
             raise ValueError(f"{dotted}={obj!r}: expected one of {', '.join(allowed)}")
     if cfg.mlp.accum < 1 or cfg.mlp.batch % cfg.mlp.accum:
         raise ValueError(f"mlp.accum={cfg.mlp.accum}: must be >= 1 and divide mlp.batch={cfg.mlp.batch}")
+    if cfg.dist.comm_dtype not in ("fp32", "bf16"):
+        raise ValueError(f"dist.comm_dtype={cfg.dist.comm_dtype!r}: must be fp32 or bf16")
     if cfg.dist.dp < 1 or cfg.dist.dp > 64:
         raise ValueError(f"dist.dp={cfg.dist.dp}: must be in 1..64 (ranks of one node)")
     if cfg.data.source == "device" and not cfg.data.n_draws and cfg.data.device_gb <= 0:

@@ -141,7 +141,8 @@ class _GemmEngine(_Engine):
         self.model = GemmMLPTrainer(sizes, info.device, activation=m.activation, loss=m.loss, lr=m.lr,
                                     betas=tuple(m.betas), eps=m.eps, weight_decay=m.weight_decay, state_dict=sd,
                                     process_group=None if self.avg_k > 0 else info.group,
-                                    bucket_mb=cfg.dist.bucket_mb, dtype=m.dtype, lags=cfg.data.lags)
+                                    bucket_mb=cfg.dist.bucket_mb, dtype=m.dtype, lags=cfg.data.lags,
+                                    comm_dtype=cfg.dist.comm_dtype)
         self.masks = masks
         self.accum = m.accum
         self.n_local = 0

@@ -121,3 +121,18 @@ def test_pipeline_cleans_temp_workdir(capsys):
     out = capsys.readouterr().out
     js = [l for l in out.splitlines() if l.startswith("{")]
     assert js and _json.loads(js[-1])["workdir"] is None
+
+
+def test_comm_dtype_flag_reaches_config_and_is_validated():
+    import pytest
+
+    from euromillioner_amd import cli
+    from euromillioner_amd import config as C
+
+    p = cli.build_parser()
+    a = p.parse_args(["train", "--model", "mlp-wide", "--comm-dtype", "bf16", "--bucket-mb", "8"])
+    cfg = cli._cfg_from_args(a)
+    assert cfg.dist.comm_dtype == "bf16" and cfg.dist.bucket_mb == 8.0
+    cfg.dist.comm_dtype = "fp16"
+    with pytest.raises(ValueError, match="comm_dtype"):
+        C.validate(cfg)
