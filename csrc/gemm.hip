@@ -1276,7 +1276,8 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
     attr = true;
   }
   const bool big = splits == 1 && a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
-                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL");
+                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL") &&
+                   (c_bf16 || (act == ACT_NONE && !mask));  // fp32 + act / act' epilogues: any-layout kernel
   if (big) {
     const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
                               ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
