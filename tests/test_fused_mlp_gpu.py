@@ -151,3 +151,31 @@ def test_fused_sample_index_path(data):
     l3, g3 = m.grads(draws, 2000, sidx=perm)
     assert abs(l3 - l2) < 1e-4
     assert torch.allclose(g3, g2, atol=1e-5, rtol=1e-3)
+
+
+def test_fused_grads_property_random_batches():
+    """Random batch sizes (1 .. 70k: single partial tile up to several tiles per pair) and offsets,
+    both losses, against the fp32 reference of the same bf16-rounded weights."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+    from euromillioner_amd.ops.fused_mlp import rows_to_masks
+
+    ds = DrawSet.synthetic(n=80000, seed=13, planted=0.6, calendar=False)
+    draws = rows_to_masks(torch.from_numpy(ds.numbers).cuda())
+    models = {loss: FusedSmallMLP(loss=loss, seed=7) for loss in ("softmax", "bce")}
+
+    @settings(max_examples=16, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @given(st.integers(1, 70000), st.integers(0, 5000), st.sampled_from(["softmax", "bce"]))
+    def check(B, offset, loss):
+        m = models[loss]
+        lk, gk = m.grads(draws, B, offset=offset)
+        lr_, gr, _ = _ref_grads(m.state_dict(), ds.numbers, offset, B, loss)
+        gflat = FM.flatten(gr, device="cuda")
+        assert abs(lk - lr_) <= 2e-3 * max(1.0, abs(lr_)), (B, offset, loss, lk, lr_)
+        err = float((gk - gflat).norm() / gflat.norm())
+        assert err < 2e-2, (B, offset, loss, err)
+
+    check()
