@@ -21,6 +21,10 @@ synthetic batch" (DP=N over RCCL for N>1).
   the full optimizer step, nothing skipped;
 * the steps replay from hipGraphs of ``--graph-steps`` consecutive steps (each node set a full
   step with its own data offset), so graph-launch gaps are paid once per chunk;
+* warmup: the W steps, then more untimed steps until ``--warmup-ms`` (250 ms) of wall time has
+  passed, because the GPU ramps its clock over the first ~100 ms of load (at 20 timed steps the
+  window would otherwise measure the ramp: 137 vs 117 us per step); the JSON reports the extra
+  steps as ``warmup_extra_steps``;
 * K steps timed between barrier + synchronize on both sides, MAX over ranks; hipEvents around
   each graph replay give the median step and the slowest rank's median;
 * after timing, validation metrics on a held-out positional 30% split
@@ -104,6 +108,10 @@ def _parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the step from hipGraphs (needs a graph-safe step)")
     ap.add_argument("--graph-steps", type=int, default=10,
                     help="consecutive training steps captured per hipGraph (each a full fwd+bwd+Adam step)")
+    ap.add_argument("--warmup-ms", type=float, default=250.0,
+                    help="after the W warmup steps, keep replaying untimed warmup steps until this much wall "
+                         "time has passed (the chip ramps its clock over the first ~100 ms of load; a training "
+                         "run spends its life at the steady clock).  0 = exactly W warmup steps")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="fused = our HIP kernels (headline); torch = plain PyTorch/hipBLASLt eager (comparison)")
@@ -256,11 +264,32 @@ def main():
 
     use_graph = bool(a.graph) and (world == 1 or getattr(model, "graph_safe", False))
     loss_t = None
+    tw = time.perf_counter()
     # warmup: with hipGraphs, one eager step (first-launch setup) and the other W-1 as replays of the
     # 1-step graph right before the timed loop, so the GPU enters it warm; otherwise W eager steps
     for i in range(a.warmup if not use_graph else min(a.warmup, 1)):
         loss_t = step(i)
     torch.cuda.synchronize()
+    extra_warm = 0
+
+    def clock_warmup(fn, n_per_call):
+        """Untimed extra warmup steps until --warmup-ms of wall time has passed since warmup began
+        (reported as warmup_extra_steps); every rank runs the same count (rank 0's) so DP ranks stay
+        in lockstep."""
+        nonlocal extra_warm
+        calls = 0
+        while True:
+            go = (time.perf_counter() - tw) * 1000.0 < a.warmup_ms
+            if world > 1:  # rank 0 decides, so every rank runs the same steps (each one a collective)
+                t = torch.tensor([1 if go else 0], device=dev)
+                dist.broadcast(t, 0)
+                go = bool(t.item())
+            if not go:
+                break
+            fn()
+            calls += 1
+            torch.cuda.synchronize()
+        extra_warm = calls * n_per_call
     if use_graph:
         # hipGraphs of C consecutive steps (distinct data offsets baked into the nodes): one graph
         # launch per C steps, so the ~19 us launch gap between graph replays (rocprof kernel trace,
@@ -284,9 +313,12 @@ def main():
         for _ in range(a.warmup - 1):
             g_1.replay()
         torch.cuda.synchronize()
+        clock_warmup(g_c.replay, C)
         plan = [(g_c, C)] * (a.steps // C) + [(g_1, 1)] * (a.steps % C)
         runs = [(lambda g=g: g.replay(), n) for g, n in plan]
     else:
+        wi = iter(range(a.warmup, 1 << 62))
+        clock_warmup(lambda: step(next(wi)), 1)
         runs = [(lambda i=i: step(i), 1) for i in range(a.steps)]
 
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in runs]
@@ -352,6 +384,8 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_extra_steps": extra_warm,
+            "warmup_min_ms": a.warmup_ms,
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "weak",

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Per-block wall-clock timeline of the fused v4 train kernel inside a 10-launch hipGraph (steady clock).
+Needs a V4_STAMPS=1 build.  Prints, per batch size, the spread of block entry, prologue, loop and fold
+times of the LAST launch of the graph, plus the per-role phase split."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+PHASES = ["F1+relu+Himg", "F2 own", "wait H", "F2 partner+Ximg", "loss part1", "wait stats", "dz+pack+D2",
+          "wait dz", "B1+mask", "dW+db2"]
+
+
+def main():
+    from euromillioner_amd.data.device_gen import generate_masks
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    draws = generate_masks((1 << 23) + 16, seed=1, planted=0.9)
+    m = FusedSmallMLP("cuda", lr=1e-3)
+    for B in [int(x) for x in os.environ.get("TL_B", "262144,1048576,2097152,4194304").split(",")]:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            nslab = FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(10):
+                    FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(30):
+            g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        per = e0.elapsed_time(e1) * 1e3 / 10
+        raw = m.slabs[:nslab, FM.P_TOTAL + 128:FM.P_TOTAL + 132].contiguous().view(torch.int32).cpu().numpy()
+        t = raw.astype(np.int64) & 0xFFFFFFFF
+        t -= t[:, 0].min()
+        us = t / 100.0
+        loop = us[:, 2] - us[:, 1]
+        q = lambda a: "min %.1f med %.1f max %.1f" % (a.min(), np.median(a), a.max())
+        print(f"B={B}: {per:.1f} us/launch (graph); entry spread {us[:, 0].max():.2f}; prologue {q(us[:, 1] - us[:, 0])};"
+              f" loop {q(loop)}; fold {q(us[:, 3] - us[:, 2])}; first entry -> last fold {us[:, 3].max():.1f}", flush=True)
+        xcd = np.arange(nslab) % 8
+        print("   loop median per blockIdx%8:", " ".join("%.1f" % np.median(loop[xcd == k]) for k in range(8)))
+        st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
+        for role in (0, 1):
+            v = st[:, role::2, :].reshape(-1, 10).mean(0)
+            tot = v.sum()
+            print(f"   role {role}: {tot / 1e3:.1f} k cycles/wave; " +
+                  ", ".join(f"{n} {x / tot * 100:.0f}%" for n, x in zip(PHASES, v)))
+
+
+if __name__ == "__main__":
+    main()
