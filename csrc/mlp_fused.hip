@@ -1083,6 +1083,99 @@ EM_DEVICE int v5_cls(int u, int i, int h) {
   return o < 50 ? 0 : (o < 62 ? 1 : 2);
 }
 
+// Loss + dZ2 of a whole 32-sample tile in ONE wave (both 32-output tiles; v5 and v6): the lane's
+// 32 logits z2[u][i] (output 32u + oo0(i) + 4h of sample r; lanes r and r + 32 share the sample).
+// Targets as {0,1} floats, one output tile at a time: register group g of tile u holds outputs
+// 32u + 8g + 4h .. +3 = one nibble of the target mask -> one ds_read_b128 of a 16-entry table (YL).
+template <int LOSS, int YL>
+EM_DEVICE void full_tile_loss(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, bool valid, int h,
+                              float (&dz)[2][16], float& loss_acc) {
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  auto targets = [&](int u, float (&yb)[16]) {
+    const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
+    }
+  };
+  if (LOSS == 0) {
+    // grouped softmax (main 50 / stars 12): exp2 with the max folded into one fma, v_rcp, and no
+    // validity select -- an invalid sample has an all-zero target mask, so nm = ns = 0 zero it
+    const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
+    const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);
+    const int ns = __builtin_popcount(thi & 0x3FFC0000u);
+    const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
+    const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
+    float mx_m = -3.0e38f, mx_s = -3.0e38f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = v5_cls(u, i, h);
+        mx_m = (c == 0) ? fmaxf(mx_m, z2[u][i]) : mx_m;
+        mx_s = (c == 1) ? fmaxf(mx_s, z2[u][i]) : mx_s;
+      }
+    mx_m = xhalf_max(mx_m);
+    mx_s = xhalf_max(mx_s);
+    const float nmL = -mx_m * L2E, nsL = -mx_s * L2E;
+    float s_m = 0.f, s_s = 0.f, zt_m = 0.f, zt_s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float yb[16];
+      targets(u, yb);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = v5_cls(u, i, h);
+        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z2[u][i], L2E, c == 1 ? nsL : nmL));
+        const float ee = (c == 2) ? 0.f : e;
+        s_m += (c == 0) ? ee : 0.f;
+        s_s += (c == 1) ? ee : 0.f;
+        zt_m = __builtin_fmaf((c == 0) ? yb[i] : 0.f, z2[u][i], zt_m);
+        zt_s = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z2[u][i], zt_s);
+        dz[u][i] = ee;
+      }
+    }
+    s_m = xhalf_sum(s_m);
+    s_s = xhalf_sum(s_s);
+    const float f_m = nm ? __builtin_amdgcn_rcpf(s_m) : 0.f, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float yb[16];
+      targets(u, yb);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = v5_cls(u, i, h);
+        dz[u][i] = (c == 2) ? 0.f : __builtin_fmaf(dz[u][i], c == 0 ? f_m : f_s, -yb[i] * (c == 0 ? inv_m : inv_s));
+      }
+    }
+    float l = -(zt_m * inv_m + zt_s * inv_s);
+    if (h == 0)
+      l += (nm ? mx_m + __builtin_amdgcn_logf(s_m) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
+    loss_acc += l;
+  } else {
+    float l = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float yb[16];
+      targets(u, yb);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = v5_cls(u, i, h);
+        const float v = z2[u][i], y = yb[i];
+        const float en = __builtin_amdgcn_exp2f(-fabsf(v) * L2E);  // stable sigmoid / softplus
+        const float rp = __builtin_amdgcn_rcpf(1.f + en);
+        const float pr = v >= 0.f ? rp : en * rp;
+        const float sp = fmaxf(v, 0.f) + __builtin_amdgcn_logf(1.f + en) * LN2;
+        const bool okc = valid && c != 2;
+        dz[u][i] = okc ? (pr - y) : 0.f;
+        l += okc ? (sp - y * v) : 0.f;
+      }
+    }
+    loss_acc += l;
+  }
+}
+
 template <int LOSS>
 __global__ void __launch_bounds__(512, 1)
 mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
@@ -1237,93 +1330,8 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
         for (int u = 0; u < 2; ++u)
           z2[u] = mfma32(lds_frag(smem, w2p_off(32 * u + r, (2 * t + q) * 2 + h)), hT[t][q], z2[u]);
 
-    // loss + dZ2 over the lane's 32 outputs (its sample r; lanes r and r + 32 share the sample).
-    // Targets as {0,1} floats, one output tile at a time: register group g of tile u holds outputs
-    // 32u + 8g + 4h .. +3 = one nibble of the target mask -> one ds_read_b128 of a 16-entry table
-    auto targets = [&](int u, float (&yb)[16]) {
-      const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + V5_YLUT + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
-        yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
-      }
-    };
     float dz[2][16];
-    if (LOSS == 0) {
-      // grouped softmax (main 50 / stars 12): exp2 with the max folded into one fma, v_rcp, and no
-      // validity select -- an invalid sample has an all-zero target mask, so nm = ns = 0 zero it
-      const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
-      const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);
-      const int ns = __builtin_popcount(thi & 0x3FFC0000u);
-      const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
-      const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
-      float mx_m = -3.0e38f, mx_s = -3.0e38f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int c = v5_cls(u, i, h);
-          mx_m = (c == 0) ? fmaxf(mx_m, z2[u][i]) : mx_m;
-          mx_s = (c == 1) ? fmaxf(mx_s, z2[u][i]) : mx_s;
-        }
-      mx_m = xhalf_max(mx_m);
-      mx_s = xhalf_max(mx_s);
-      const float nmL = -mx_m * L2E, nsL = -mx_s * L2E;
-      float s_m = 0.f, s_s = 0.f, zt_m = 0.f, zt_s = 0.f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float yb[16];
-        targets(u, yb);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int c = v5_cls(u, i, h);
-          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z2[u][i], L2E, c == 1 ? nsL : nmL));
-          const float ee = (c == 2) ? 0.f : e;
-          s_m += (c == 0) ? ee : 0.f;
-          s_s += (c == 1) ? ee : 0.f;
-          zt_m = __builtin_fmaf((c == 0) ? yb[i] : 0.f, z2[u][i], zt_m);
-          zt_s = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z2[u][i], zt_s);
-          dz[u][i] = ee;
-        }
-      }
-      s_m = xhalf_sum(s_m);
-      s_s = xhalf_sum(s_s);
-      const float f_m = nm ? __builtin_amdgcn_rcpf(s_m) : 0.f, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float yb[16];
-        targets(u, yb);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int c = v5_cls(u, i, h);
-          dz[u][i] = (c == 2) ? 0.f : __builtin_fmaf(dz[u][i], c == 0 ? f_m : f_s, -yb[i] * (c == 0 ? inv_m : inv_s));
-        }
-      }
-      float l = -(zt_m * inv_m + zt_s * inv_s);
-      if (h == 0)
-        l += (nm ? mx_m + __builtin_amdgcn_logf(s_m) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
-      loss_acc += l;
-    } else {
-      float l = 0.f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float yb[16];
-        targets(u, yb);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int c = v5_cls(u, i, h);
-          const float v = z2[u][i], y = yb[i];
-          const float en = __builtin_amdgcn_exp2f(-fabsf(v) * L2E);  // stable sigmoid / softplus
-          const float rp = __builtin_amdgcn_rcpf(1.f + en);
-          const float pr = v >= 0.f ? rp : en * rp;
-          const float sp = fmaxf(v, 0.f) + __builtin_amdgcn_logf(1.f + en) * LN2;
-          const bool okc = valid && c != 2;
-          dz[u][i] = okc ? (pr - y) : 0.f;
-          l += okc ? (sp - y * v) : 0.f;
-        }
-      }
-      loss_acc += l;
-    }
+    full_tile_loss<LOSS, V5_YLUT>(smem, z2, tmask, valid, h, dz, loss_acc);
     bf16x8 dzf[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -1475,6 +1483,519 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   }
 }
 
+// ============================================================================================
+// v6: producer/consumer units -- forward waves feed backward waves through a 3-slot LDS ring.
+//
+// v4's hidden-split pairs meet three times per 32-sample tile (H halves, softmax statistics, dZ2
+// halves); V4_STAMPS phase timers show each wave spending ~27 % of the tile waiting on its partner,
+// and a meeting costs its LDS round trips even when both arrive together.  v6 splits the work by
+// STAGE instead of by hidden unit:
+//   * a unit = 4 waves working on one tile stream: two forward waves F0/F1 (even / odd tiles of the
+//     unit) and two backward waves B0/B1 (hidden halves of every tile of the unit);
+//   * F runs a whole tile alone -- X -> F1 (16 MFMAs) -> relu -> F2 (16) -> full grouped softmax over
+//     all 64 outputs (no statistics exchange) -> dZ2 -- and leaves the H, dZ2 and X images of the
+//     tile in a ring slot (16 KB), then raises the slot's FULL counter;
+//   * B_rho waits for FULL, runs B1 for its hidden half (dZ2 A fragments read back from the dZ2
+//     image: the same 8-byte granules F wrote), the relu mask from the H image, then dW2 / dW1T
+//     into its AGPR-resident half of dW (v4's accumulator set) and db2 of output tile rho; it raises
+//     its DONE counter once its last read of the slot has returned;
+//   * F waits for a slot only when the ring is full (3 slots: F writes tile k while B works on k-1,
+//     k-2), so in steady state nobody waits: the only coupling is a one-way hand-off.
+// Both units share the CU so that every SIMD hosts one forward and one backward wave (wave w runs
+// on SIMD w % 4): the VALU-heavy loss of one beside the MFMA-heavy dW chain of the other.  Counters
+// are monotonic (no ABA) and every wait is bounded: a broken protocol poisons the loss with NaN.
+#ifndef V6_AGPR
+#define V6_AGPR 0  // 1: B's dW accumulators pinned in AGPRs (128 V + 128 A); 0: VGPR-form (256 VGPRs for both roles)
+#endif
+#ifndef V6_WREG
+#define V6_WREG 1  // forward waves keep their 32 weight fragments in registers (needs V6_AGPR 0)
+#endif
+#ifndef V6_BPRE
+#define V6_BPRE 1  // backward waves issue every LDS read of a tile at once and release the slot before computing
+#endif
+#ifndef V6_XMASK
+#define V6_XMASK 0  // 1: a slot carries the tile's 32 input masks (256 B) instead of the 4 KB X image
+#endif
+// slot: H0 4K | H1 4K | D2 4K | X image 4K (V6_XMASK 0) or input masks 256 B (V6_XMASK 1: 4 slots fit)
+constexpr int V6_SLOT = V6_XMASK ? 12544 : 16384, V6_NSLOT = V6_XMASK ? 4 : 3;
+constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
+constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
+constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
+constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[3] | done0[3] | done1[3]
+constexpr int V6_RING = V6_FLAGS + 128;  // [2 units][3 slots][16 KB]
+constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_NSLOT * V6_SLOT;
+constexpr int V6_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below, DB2S [2][64] + LOSSS [8] above
+constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 2048);
+static_assert(V6_LDS <= 163840 && V6_RING % 16 == 0, "v6 LDS budget");
+constexpr int V6_SPIN_LIMIT = 1 << 20;  // ~50 ms of polling: a legitimate wait is microseconds
+
+// wait until the LDS counter at off reaches target (skipped once a wait has failed: the launch then
+// drains quickly and reports NaN)
+EM_DEVICE void v6_wait(const char* smem, uint32_t off, int target, bool& ok) {
+  if (!ok) return;
+  int spins = 0;
+  while (__hip_atomic_load(reinterpret_cast<const int*>(smem + off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+         target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > V6_SPIN_LIMIT) {
+      ok = false;
+      return;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
+  const int ntiles = (B + 31) / 32;
+  return U < ntiles ? (ntiles - U + nunits - 1) / nunits : 0;
+}
+
+// Grouped softmax-CE of a whole tile in ONE wave (v6 forward), with the max / sum / target-dot
+// reductions split into independent partial chains (full_tile_loss runs each as one serial chain of
+// 32 dependent ops).
+template <int YL>
+EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
+                          float& loss_acc) {
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  auto targets = [&](int u, float (&yb)[16]) {
+    const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
+    }
+  };
+  const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
+  const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
+  const int ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
+  const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
+  const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
+  float mm[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f}, ms[2] = {-3.0e38f, -3.0e38f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v5_cls(u, i, h);
+      mm[i & 3] = (c == 0) ? fmaxf(mm[i & 3], z2[u][i]) : mm[i & 3];
+      ms[i & 1] = (c == 1) ? fmaxf(ms[i & 1], z2[u][i]) : ms[i & 1];
+    }
+  const float mx_m = xhalf_max(fmaxf(fmaxf(mm[0], mm[1]), fmaxf(mm[2], mm[3])));
+  const float mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
+  const float nmL = -mx_m * L2E, nsL = -mx_s * L2E;
+  float sm[4] = {0.f, 0.f, 0.f, 0.f}, ss[2] = {0.f, 0.f}, tm[4] = {0.f, 0.f, 0.f, 0.f}, ts[2] = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float yb[16];
+    targets(u, yb);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v5_cls(u, i, h);
+      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z2[u][i], L2E, c == 1 ? nsL : nmL));
+      const float ee = (c == 2) ? 0.f : e;
+      sm[i & 3] += (c == 0) ? ee : 0.f;
+      ss[i & 1] += (c == 1) ? ee : 0.f;
+      tm[i & 3] = __builtin_fmaf((c == 0) ? yb[i] : 0.f, z2[u][i], tm[i & 3]);
+      ts[i & 1] = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z2[u][i], ts[i & 1]);
+      dz[u][i] = ee;
+    }
+  }
+  const float s_m = xhalf_sum((sm[0] + sm[1]) + (sm[2] + sm[3])), s_s = xhalf_sum(ss[0] + ss[1]);
+  const float f_m = nm ? __builtin_amdgcn_rcpf(s_m) : 0.f, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float yb[16];  // re-read (8 LDS loads) rather than held across the sums: keeps the forward wave spill-free
+    targets(u, yb);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = v5_cls(u, i, h);
+      dz[u][i] = (c == 2) ? 0.f : __builtin_fmaf(dz[u][i], c == 0 ? f_m : f_s, -yb[i] * (c == 0 ? inv_m : inv_s));
+    }
+  }
+  float l = -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
+  if (h == 0)
+    l += (nm ? mx_m + __builtin_amdgcn_logf(s_m) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
+  loss_acc += l;
+}
+
+// forward wave f (0/1) of unit `unit`: tiles k = f, f + 2, ... of the unit's stream
+template <int LOSS>
+EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                          int offset, int unit, int f, int lane, float& loss_acc, bool& ok, V4Stamps& st) {
+  const int r = lane & 31, h = lane >> 5;
+  const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
+  const int K = v6_ntiles_of_unit(B, U, nunits);
+  const uint32_t RB = V6_RING + unit * V6_NSLOT * V6_SLOT, FL = V6_FLAGS + unit * 64;
+  auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {
+    const int s = (U + k * nunits) * 32 + r;
+    mi = 0;
+    mt = 0;
+    if (k < K && s < B) {
+      const int idx = sidx ? sidx[s] : (offset + s);
+      mi = masks[idx];
+      mt = masks[idx + 1];
+    }
+  };
+  uint64_t nin, ntg;
+  fetch(f, nin, ntg);
+  // the forward wave's weight fragments (W1ᵀ 4 x 4, W2ᵀ 2 x 8: 128 VGPRs) stay in registers for the
+  // whole launch: no LDS read stands between the tile's operands and its 32 MFMAs
+  bf16x8 w1r[4][4], w2r[2][8];
+  if (V6_WREG) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w1r[t][q] = lds_frag(smem, w1t_off(32 * t + r, 2 * q + h));
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) w2r[u][kk] = lds_frag(smem, w2p_off(32 * u + r, kk * 2 + h));
+  }
+  st.start();
+  for (int k = f; k < K; k += 2) {
+    const bool valid = (U + k * nunits) * 32 + r < B;
+    const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
+    const uint64_t tmask = valid ? ntg : 0ull;
+    fetch(k + 2, nin, ntg);
+    const int slot = k % V6_NSLOT;
+    const uint32_t SB = RB + slot * V6_SLOT;
+    if (k >= V6_NSLOT) {  // the slot's previous tile (k - 3) must be consumed by both backward waves
+      v6_wait(smem, FL + (V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
+      v6_wait(smem, FL + (2 * V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
+    }
+    st.mark(0);
+
+    // X fragments (B of F1) + X image [32 samples][64 feat] for dW1T
+    const uint32_t wlo = (uint32_t)imask >> (8 * h), whi = (uint32_t)(imask >> 32) >> (8 * h);
+    bf16x8 xf[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xf[q] = v4_xfrag<V6_XLUT>(smem, q < 2 ? wlo : whi, q);
+    if (V6_XMASK) {
+      if (h == 0) *reinterpret_cast<uint64_t*>(smem + SB + V6_SX + 8 * r) = imask;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(smem + v4_img<false>(SB + V6_SX, r, 16 * q + 8 * h)) = xf[q];
+    }
+
+    // F1: Z1ᵀ = W1ᵀ·Xᵀ (two hidden tiles' chains interleaved) -> relu -> Hᵀ fragments + H images
+    bf16x8 hT[4][2];
+    constexpr int F1P = V6_WREG ? 1 : 2;  // hidden tiles per F1 chain group (1 with register weights: VGPR budget)
+#pragma unroll
+    for (int tp = 0; tp < 4 / F1P; ++tp) {
+      f32x16 a1s[F1P];
+#pragma unroll
+      for (int tt = 0; tt < F1P; ++tt) a1s[tt] = f32x16{};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int tt = 0; tt < F1P; ++tt)
+          a1s[tt] = mfma32(V6_WREG ? w1r[F1P * tp + tt][q] : lds_frag(smem, w1t_off(32 * (F1P * tp + tt) + r, 2 * q + h)),
+                           xf[q], a1s[tt]);
+#pragma unroll
+      for (int tt = 0; tt < F1P; ++tt) {
+        const int t = F1P * tp + tt;
+        const uint32_t HB = SB + V6_SH + (t >> 1) * 4096;  // H sub-image of hidden half t >> 1
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          hT[t][q] = relu_pack(a1s[tt], q);
+          const u32x4 d = __builtin_bit_cast(u32x4, hT[t][q]);
+          *reinterpret_cast<u32x2*>(smem + v4_img<true>(HB, r, 32 * (t & 1) + 16 * q + 4 * h)) = u32x2{d[0], d[1]};
+          *reinterpret_cast<u32x2*>(smem + v4_img<true>(HB, r, 32 * (t & 1) + 16 * q + 8 + 4 * h)) = u32x2{d[2], d[3]};
+        }
+      }
+    }
+
+    st.mark(1);
+    // F2: Z2ᵀ = W2ᵀ·Hᵀ + b2, both output tiles' chains interleaved
+    f32x16 z2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
+        z2[u][4 * g + 0] = b[0]; z2[u][4 * g + 1] = b[1]; z2[u][4 * g + 2] = b[2]; z2[u][4 * g + 3] = b[3];
+      }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          z2[u] = mfma32(V6_WREG ? w2r[u][2 * t + q] : lds_frag(smem, w2p_off(32 * u + r, (2 * t + q) * 2 + h)),
+                         hT[t][q], z2[u]);
+    st.mark(2);
+
+    float dz[2][16];
+    if (LOSS == 0)
+      v6_softmax<V6_YLUT>(smem, z2, tmask, h, dz, loss_acc);
+    else
+      full_tile_loss<LOSS, V6_YLUT>(smem, z2, tmask, valid, h, dz, loss_acc);
+    st.mark(3);
+
+    // dZ2 image [32 samples][64 outs]: 8-byte granules of 4 consecutive outputs (B reads the same
+    // granules back as its B1 A fragments and through transposing reads for dW2 / db2)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const u32x4 fq = __builtin_bit_cast(
+            u32x4, pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2], dz[u][8 * q + 3], dz[u][8 * q + 4],
+                         dz[u][8 * q + 5], dz[u][8 * q + 6], dz[u][8 * q + 7]));
+        *reinterpret_cast<u32x2*>(smem + v4_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 4 * h)) = u32x2{fq[0], fq[1]};
+        *reinterpret_cast<u32x2*>(smem + v4_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
+            u32x2{fq[2], fq[3]};
+      }
+    pair_signal(smem, FL + slot * 4, k + 1);  // FULL
+    st.mark(4);
+  }
+}
+
+// backward wave of hidden half RHO: every tile of the unit's stream.  V6_BPRE: every LDS read of the
+// tile (dZ2 A fragments, H / dZ2 / X transposes, W2ᵀ fragments: ~96 VGPRs) is issued at once right
+// after FULL, the slot is released as soon as they have landed, and the 26 MFMAs then run from
+// registers (B1, then dW2 + db2 while B1's results drain, the relu mask, dW1ᵀ).
+template <int RHO>
+EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[2][2], f32x16 (&dW1T)[2][2],
+                           f32x16& db2, bool& ok, V4Stamps& st) {
+  const int r = lane & 31, h = lane >> 5;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
+  const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
+  const int K = v6_ntiles_of_unit(B, U, nunits);
+  const uint32_t RB = V6_RING + unit * V6_NSLOT * V6_SLOT, FL = V6_FLAGS + unit * 64;
+  const uint32_t MYDONE = FL + ((1 + RHO) * V6_NSLOT) * 4;
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  auto acc_mfma = [&](f32x16& d, bf16x8 x, bf16x8 y) {
+    if (V6_AGPR) mfma_acc_agpr(d, x, y);
+    else d = mfma32(x, y, d);
+  };
+  st.start();
+  for (int k = 0; k < K; ++k) {
+    const int slot = k % V6_NSLOT;
+    const uint32_t SB = RB + slot * V6_SLOT, D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
+    v6_wait(smem, FL + slot * 4, k + 1, ok);
+    st.mark(5);
+
+    // dZ2 as B1's A operand (samples x outputs): F's own 8-byte granules, k-step (u, q)
+    bf16x8 dzA[2][2], hR[2][2], bd[2][2], bx[2][2], w2q[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + v4_img<true>(D2, r, 32 * u + 16 * q + 4 * h));
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + v4_img<true>(D2, r, 32 * u + 16 * q + 8 + 4 * h));
+        dzA[u][q] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) hR[tt][q] = v4_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) bd[u][q] = v4_tr_frag<true>(smem, D2, 32 * u, q, h, q4, p4, g1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (V6_XMASK) {
+          // X[sample perm(q,h,j)][feature 32u + r] from the tile's masks: the 8 samples of the k-step are
+          // two runs of 4 (16q + 4h + 0..3, 16q + 8 + 4h + 0..3), read as 4 broadcast 16-B loads
+          const u32x4* MK = reinterpret_cast<const u32x4*>(smem + SB + V6_SX);
+          const u32x4 mA = MK[8 * q + 2 * h], mB = MK[8 * q + 2 * h + 1], mC = MK[8 * q + 4 + 2 * h],
+                      mD = MK[8 * q + 4 + 2 * h + 1];
+          const uint32_t w[8] = {mA[u], mA[2 + u], mB[u], mB[2 + u], mC[u], mC[2 + u], mD[u], mD[2 + u]};
+          u32x4 d;
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+            d[p] = ((uint32_t)__builtin_amdgcn_sbfe(w[2 * p], r, 1) & 0x3F80u) |
+                   ((uint32_t)__builtin_amdgcn_sbfe(w[2 * p + 1], r, 1) & 0x3F800000u);
+          bx[u][q] = __builtin_bit_cast(bf16x8, d);
+        } else {
+          bx[u][q] = v4_tr_frag<false>(smem, SB + V6_SX, 32 * u, q, h, q4, p4, g1);
+        }
+      }
+    if (V6_BPRE) pair_signal(smem, MYDONE + slot * 4, k + 1);  // DONE: the release waits for every read above
+    st.mark(6);
+
+    // B1: dH = dZ2·W2ᵀ for the own hidden half
+    f32x16 aD[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) aD[tt] = mfma32(dzA[kk >> 1][kk & 1], w2q[tt][kk], aD[tt]);
+    // dW2[own hid][out] += Hᵀ·dZ2 ; db2[out tile RHO] += ones·dZ2 (independent of B1: fills the pipe)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) acc_mfma(dW2[tt][u], hR[tt][q], bd[u][q]);
+        if (u == RHO) db2 = mfma32(ones, bd[u][q], db2);
+      }
+    st.mark(7);
+    // dZ1 = dH * (H > 0), then dW1ᵀ[own hid][feat] += dZ1ᵀ·X
+    bf16x8 dz1[2][2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dz1[tt][q] = mask_by(hR[tt][q], aD[tt], q);
+    if (!V6_BPRE) pair_signal(smem, MYDONE + slot * 4, k + 1);
+    st.mark(8);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) acc_mfma(dW1T[tt][u], dz1[tt][q], bx[u][q]);
+    st.mark(9);
+  }
+}
+
+// one role's loop + its share of the epilogue (the same two barriers in every role instantiation)
+template <int LOSS, int ROLE>  // ROLE 0/1 = forward f, 2/3 = backward rho
+EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                       int offset, int unit, int wave, int lane, float* slab_spare) {
+  const int r = lane & 31, h = lane >> 5;
+  bool ok = true;
+  V4Stamps st;
+  float* RED = reinterpret_cast<float*>(smem);  // [unit][16 tiles][4 g][64 lanes][4]: 0..7 dW2, 8..15 dW1T
+  float* DB2S = reinterpret_cast<float*>(smem + V6_RED);          // [2 units][64]
+  float* LOSSS = reinterpret_cast<float*>(smem + V6_RED + 512);   // [8]
+  auto dump = [&]() {
+    if (V4_STAMPS && lane < 10) {  // phase cycles of this wave -> spare slab floats
+      uint64_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) v = (lane == k) ? st.acc[k] : v;
+      slab_spare[wave * 16 + lane] = (float)v;
+    }
+  };
+  if (ROLE < 2) {
+    float loss_acc = 0.f;
+    v6_forward<LOSS>(smem, masks, sidx, B, offset, unit, ROLE, lane, loss_acc, ok, st);
+    float lsum = wave_sum(loss_acc);
+    if (!ok) lsum = __builtin_nanf("");
+    dump();
+    __syncthreads();  // every wave is out of the loop: the loop's LDS is free
+    if (lane == 0) LOSSS[wave] = lsum;
+    __syncthreads();
+  } else {
+    constexpr int RHO = ROLE - 2;
+    f32x16 dW2[2][2], dW1T[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        dW2[t][u] = f32x16{};
+        dW1T[t][u] = f32x16{};
+      }
+    f32x16 db2 = f32x16{};
+    v6_backward<RHO>(smem, B, unit, lane, dW2, dW1T, db2, ok, st);
+    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // asm MFMA (AGPR D) -> v_accvgpr_read hazard
+    dump();
+    __syncthreads();
+    if (h == 0) DB2S[unit * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
+    if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int which = 0; which < 2; ++which) {
+          const f32x16& acc = which ? dW1T[tt][u] : dW2[tt][u];
+          const int T = 8 * which + 2 * (2 * RHO + tt) + u;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<f32x4*>(RED + unit * 16384 + ((T * 4 + g) * 64 + lane) * 4) =
+                f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+        }
+    __syncthreads();
+  }
+}
+
+template <int LOSS>
+__global__ void __launch_bounds__(512, 1)
+mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
+                          const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                          float* __restrict__ loss_slabs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  {  // all loads of the weight image in flight before the first LDS store
+    constexpr int N16 = IMG_BYTES / 16, KK = (N16 + 511) / 512;
+    const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
+    u32x4* dst = reinterpret_cast<u32x4*>(smem);
+    u32x4 v[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+      if (tid + 512 * k < N16) v[k] = src[tid + 512 * k];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+      if (tid + 512 * k < N16) dst[tid + 512 * k] = v[k];
+  }
+  if (tid < 64) reinterpret_cast<float*>(smem + V6_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
+  if (tid < 32) {
+    const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
+    reinterpret_cast<uint32_t*>(smem + V6_XLUT)[tid] =
+        (((n >> b) & 1u) ? 0x3F80u : 0u) | (((n >> (b + 1)) & 1u) ? 0x3F800000u : 0u);
+  }
+  if (tid < 32) reinterpret_cast<int*>(smem + V6_FLAGS)[tid] = 0;
+  __syncthreads();
+  // wave w runs on SIMD w % 4.  unit 0 = waves 0-3 (F0 F1 B0 B1), unit 1 = waves 4-7 (B0 B1 F0 F1):
+  // every SIMD hosts one forward and one backward wave
+  uint64_t ts[4] = {};  // V4_STAMPS: 100 MHz wall-clock marks (entry, prologue done, loop done, dW folded)
+  if (V4_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
+  const int unit = wave >> 2, wl = wave & 3;
+  const int role = unit == 0 ? wl : (wl ^ 2);  // 0/1 forward f, 2/3 backward rho
+  float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
+  if (V4_STAMPS) ts[1] = __builtin_amdgcn_s_memrealtime();
+  if (role == 0)
+    v6_body<LOSS, 0>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+  else if (role == 1)
+    v6_body<LOSS, 1>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+  else if (role == 2)
+    v6_body<LOSS, 2>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+  else
+    v6_body<LOSS, 3>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+  if (V4_STAMPS) ts[2] = __builtin_amdgcn_s_memrealtime();
+
+  const float* RED = reinterpret_cast<const float*>(smem);
+  const float* DB2S = reinterpret_cast<const float*>(smem + V6_RED);
+  const float* LOSSS = reinterpret_cast<const float*>(smem + V6_RED + 512);
+  float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
+  // parameter-order slab with 16-B write-through (sc1) stores (see the v4 epilogue)
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(slab, 0, SLAB_STRIDE * 4, 0x00020000);
+  for (int e = tid; e < 2 * 2048; e += 512) {
+    f32x4 v;
+    if (e < 2048) {
+      const int f = e >> 5, c = (e & 31) * 4;
+      const int T = 8 + 2 * (c >> 5) + (f >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (f & 31);
+      const int at = ((T * 4 + g) * 64 + l) * 4;
+      v = *reinterpret_cast<const f32x4*>(RED + at) + *reinterpret_cast<const f32x4*>(RED + 16384 + at);
+    } else {
+      const int q = e - 2048, c = q >> 4, o = (q & 15) * 4;
+      const int T = 2 * (c >> 5) + (o >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (o & 31);
+      const int at = ((T * 4 + g) * 64 + l) * 4 + (c & 3);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = RED[at + 4 * k] + RED[16384 + at + 4 * k];
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, e * 16, 0, 16 /* sc1 */);
+  }
+  if (V4_STAMPS && tid == 0) {
+    ts[3] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) slab_spare[128 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
+  }
+  if (tid < 64) slab[P_B2 + tid] = DB2S[tid] + DB2S[64 + tid];
+  if (tid == 0) {
+    float l = 0.f;
+    for (int w = 0; w < 8; ++w) l += LOSSS[w];
+    loss_slabs[blockIdx.x] = l;
+  }
+}
+
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
 __global__ void __launch_bounds__(256)
 mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
@@ -1564,8 +2085,14 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
                               TRAIN_LDS);
     attr_set = true;
   }
-  static int use_v3 = -1, use_v5 = 0;
+  static int use_v3 = -1, use_v5 = 0, use_v6 = 0;
   if (use_v3 < 0) {
+    const char* e6 = std::getenv("EM_FUSED_V6");
+    use_v6 = (e6 && e6[0] == '1') ? 1 : 0;
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V6_LDS);
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V6_LDS);
     const char* e = std::getenv("EM_FUSED_V3");
     use_v3 = (e && e[0] == '1') ? 1 : 0;
     const char* e5 = std::getenv("EM_FUSED_V5");
@@ -1579,7 +2106,14 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_v5_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               V5_LDS);
   }
-  if (use_v5 && !use_v3) {
+  if (use_v6 && !use_v3) {
+    if (loss_kind == 0)
+      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, (int)B,
+                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+    else
+      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, (int)B,
+                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+  } else if (use_v5 && !use_v3) {
     if (loss_kind == 0)
       hipLaunchKernelGGL(mlp_fused_train_v5_kernel<0>, dim3(nslab), dim3(512), V5_LDS, stream, draws, sidx, (int)B,
                          (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);

@@ -54,6 +54,15 @@ def main():
         xcd = np.arange(nslab) % 8
         print("   loop median per blockIdx%8:", " ".join("%.1f" % np.median(loop[xcd == k]) for k in range(8)))
         st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
+        if os.environ.get("EM_FUSED_V6") == "1":
+            names = ["F wait slot", "F X+F1+H", "F F2", "F loss", "F D2+signal",
+                     "B wait full", "B reads+B1+mask", "B dW2+db2+bx", "B signal", "B dW1T"]
+            for nm, ws in (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5])):
+                v = st[:, ws, :].reshape(-1, 10).mean(0)
+                tot = v.sum()
+                print(f"   {nm}: {tot / 1e3:.1f} k cycles/wave; " +
+                      ", ".join(f"{n} {x / 1e3:.1f}k" for n, x in zip(names, v) if x > 0))
+            continue
         for role in (0, 1):
             v = st[:, role::2, :].reshape(-1, 10).mean(0)
             tot = v.sum()
