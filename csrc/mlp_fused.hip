@@ -29,6 +29,7 @@
 //     whole launch; one wave per SIMD.  The 4 waves are summed through LDS at
 //     the end and each workgroup writes ONE fp32 slab (deterministic; no atomics).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -1513,17 +1514,37 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
 #ifndef V6_BPRE
 #define V6_BPRE 1  // backward waves issue every LDS read of a tile at once and release the slot before computing
 #endif
+#ifndef V6_FPRIO
+#define V6_FPRIO 1  // 1: forward waves run at s_setprio 1 (they bound the pipeline; backward waves have slack)
+#endif
+#ifndef V6_UNROLL
+#define V6_UNROLL 0  // 1: forward loop unrolled over the 3 ring slots (measured: more live addresses, spills)
+#endif
+#ifndef V6_DB2DOT
+#define V6_DB2DOT 0  // 1 (measured slower): db2 column sums on v_dot2_f32_bf16 (8 VALU per tile) instead of 2 ones·dZ2 MFMAs
+#endif
 #ifndef V6_XMASK
 #define V6_XMASK 0  // 1: a slot carries the tile's 32 input masks (256 B) instead of the 4 KB X image
 #endif
+#ifndef V6_RECYCLE
+#define V6_RECYCLE 1  // 1: the W1ᵀ / W2ᵀ(P) images (dead once the forward waves hold their weights in
+                      // registers) become each unit's 4th ring slot
+#endif
 // slot: H0 4K | H1 4K | D2 4K | X image 4K (V6_XMASK 0) or input masks 256 B (V6_XMASK 1: 4 slots fit)
-constexpr int V6_SLOT = V6_XMASK ? 12544 : 16384, V6_NSLOT = V6_XMASK ? 4 : 3;
+constexpr int V6_SLOT = V6_XMASK ? 12544 : 16384;
+constexpr int V6_RSLOTS = V6_XMASK ? 4 : 3;  // slots per unit in the ring area (+1 recycled image slot)
+constexpr int V6_NSLOT = V6_RSLOTS + ((V6_RECYCLE && V6_WREG) ? 1 : 0);
+static_assert(!V6_RECYCLE || V6_XMASK || 2 * V6_SLOT <= IMG_W2Q, "recycled slots must fit below the W2Q image");
 constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
 constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[3] | done0[3] | done1[3]
 constexpr int V6_RING = V6_FLAGS + 128;  // [2 units][3 slots][16 KB]
-constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_NSLOT * V6_SLOT;
+constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_RSLOTS * V6_SLOT;
+// byte offset of ring slot `slot` of unit `unit`
+EM_DEVICE uint32_t v6_slot(int unit, int slot) {
+  return slot < V6_RSLOTS ? V6_RING + (unit * V6_RSLOTS + slot) * V6_SLOT : unit * V6_SLOT;
+}
 constexpr int V6_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below, DB2S [2][64] + LOSSS [8] above
 constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 2048);
 static_assert(V6_LDS <= 163840 && V6_RING % 16 == 0, "v6 LDS budget");
@@ -1617,14 +1638,14 @@ EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmas
   loss_acc += l;
 }
 
-// forward wave f (0/1) of unit `unit`: tiles k = f, f + 2, ... of the unit's stream
-template <int LOSS>
+// forward wave F (0/1) of unit `unit`: tiles k = F, F + 2, ... of the unit's stream
+template <int LOSS, int F>
 EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                          int offset, int unit, int f, int lane, float& loss_acc, bool& ok, V4Stamps& st) {
+                          int offset, int unit, int lane, float& loss_acc, bool& ok, V4Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
   const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
   const int K = v6_ntiles_of_unit(B, U, nunits);
-  const uint32_t RB = V6_RING + unit * V6_NSLOT * V6_SLOT, FL = V6_FLAGS + unit * 64;
+  const uint32_t FL = V6_FLAGS + unit * 64;
   auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {
     const int s = (U + k * nunits) * 32 + r;
     mi = 0;
@@ -1636,7 +1657,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     }
   };
   uint64_t nin, ntg;
-  fetch(f, nin, ntg);
+  fetch(F, nin, ntg);
   // the forward wave's weight fragments (W1ᵀ 4 x 4, W2ᵀ 2 x 8: 128 VGPRs) stay in registers for the
   // whole launch: no LDS read stands between the tile's operands and its 32 MFMAs
   bf16x8 w1r[4][4], w2r[2][8];
@@ -1650,14 +1671,15 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) w2r[u][kk] = lds_frag(smem, w2p_off(32 * u + r, kk * 2 + h));
   }
+  if (V6_NSLOT > V6_RSLOTS) __syncthreads();  // every forward wave holds its weights: the images are free
   st.start();
-  for (int k = f; k < K; k += 2) {
+  auto ftile = [&](int k, auto slot_c) {  // slot_c: the ring slot, compile-time in the unrolled loop
+    const int slot = slot_c;
     const bool valid = (U + k * nunits) * 32 + r < B;
     const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
     const uint64_t tmask = valid ? ntg : 0ull;
     fetch(k + 2, nin, ntg);
-    const int slot = k % V6_NSLOT;
-    const uint32_t SB = RB + slot * V6_SLOT;
+    const uint32_t SB = v6_slot(unit, slot);
     if (k >= V6_NSLOT) {  // the slot's previous tile (k - 3) must be consumed by both backward waves
       v6_wait(smem, FL + (V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
       v6_wait(smem, FL + (2 * V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
@@ -1746,6 +1768,20 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
       }
     pair_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
+  };
+  if (V6_UNROLL && V6_NSLOT == 3) {
+    // tiles k = f + 2m visit slots f, f + 2, f + 1 (mod 3): unrolled so every slot base is a constant
+    // folded into the LDS instructions' offsets instead of a per-address add per tile
+    constexpr int S0 = F % 3, S1 = (F + 2) % 3, S2 = (F + 1) % 3;
+    for (int k = F; k < K; k += 6) {
+      ftile(k, std::integral_constant<int, S0>{});
+      if (k + 2 >= K) break;
+      ftile(k + 2, std::integral_constant<int, S1>{});
+      if (k + 4 >= K) break;
+      ftile(k + 4, std::integral_constant<int, S2>{});
+    }
+  } else {
+    for (int k = F; k < K; k += 2) ftile(k, k % V6_NSLOT);
   }
 }
 
@@ -1760,17 +1796,18 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
   const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
   const int K = v6_ntiles_of_unit(B, U, nunits);
-  const uint32_t RB = V6_RING + unit * V6_NSLOT * V6_SLOT, FL = V6_FLAGS + unit * 64;
+  const uint32_t FL = V6_FLAGS + unit * 64;
   const uint32_t MYDONE = FL + ((1 + RHO) * V6_NSLOT) * 4;
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   auto acc_mfma = [&](f32x16& d, bf16x8 x, bf16x8 y) {
     if (V6_AGPR) mfma_acc_agpr(d, x, y);
     else d = mfma32(x, y, d);
   };
+  if (V6_NSLOT > V6_RSLOTS) __syncthreads();  // matches the forward waves' barrier (recycled images)
   st.start();
   for (int k = 0; k < K; ++k) {
     const int slot = k % V6_NSLOT;
-    const uint32_t SB = RB + slot * V6_SLOT, D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
+    const uint32_t SB = v6_slot(unit, slot), D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
     v6_wait(smem, FL + slot * 4, k + 1, ok);
     st.mark(5);
 
@@ -1833,7 +1870,18 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
       for (int q = 0; q < 2; ++q) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) acc_mfma(dW2[tt][u], hR[tt][q], bd[u][q]);
-        if (u == RHO) db2 = mfma32(ones, bd[u][q], db2);
+        if (u == RHO) {
+          if (V6_DB2DOT) {  // lane (r, h): 8 samples of output 32 RHO + r; the h halves are summed at the end
+            // (memcpy casts: a bit_cast of an ext_vector element in an unrolled loop reads element 0, see as_s16x2)
+            bf16x2_t b2v[4];
+            __builtin_memcpy(b2v, &bd[u][q], 16);
+            const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) db2[0] = __builtin_amdgcn_fdot2_f32_bf16(b2v[e], one2, db2[0], false);
+          } else {
+            db2 = mfma32(ones, bd[u][q], db2);
+          }
+        }
       }
     st.mark(7);
     // dZ1 = dH * (H > 0), then dW1ᵀ[own hid][feat] += dZ1ᵀ·X
@@ -1874,7 +1922,8 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   };
   if (ROLE < 2) {
     float loss_acc = 0.f;
-    v6_forward<LOSS>(smem, masks, sidx, B, offset, unit, ROLE, lane, loss_acc, ok, st);
+    if (V6_FPRIO) __builtin_amdgcn_s_setprio(1);
+    v6_forward<LOSS, ROLE>(smem, masks, sidx, B, offset, unit, lane, loss_acc, ok, st);
     float lsum = wave_sum(loss_acc);
     if (!ok) lsum = __builtin_nanf("");
     dump();
@@ -1896,6 +1945,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // asm MFMA (AGPR D) -> v_accvgpr_read hazard
     dump();
     __syncthreads();
+    if (V6_DB2DOT) db2[0] = xhalf_sum(db2[0]);           // the two sample halves of output 32 RHO + r
     if (h == 0) DB2S[unit * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
 #pragma unroll

@@ -1,4 +1,5 @@
-# v6 producer/consumer fused kernel: GPU tests under EM_FUSED_V6=1, then same-box bench A/B v4 vs v6
+# v6 producer/consumer fused kernel: GPU tests under EM_FUSED_V6=1, then same-box bench A/B:
+# base (lib/ab/base.so) vs the in-tree build, both v6
 set -o pipefail
 mkdir -p gpurun_out/v6
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -10,9 +11,6 @@ one() {  # tag env...
   python -c "import json;a=json.load(open('gpurun_out/v6/$tag.json'));print(f'$tag {a[\"value\"]/1e9:.3f} G/s med {a[\"ms_per_step_median\"]*1e3:.2f} us acc {a[\"val\"][\"acc\"]:.4f}')"
 }
 for i in 1 2; do
-  one v4_$i EM_FUSED_V6=0 || exit 4
-  one v6_$i EM_FUSED_V6=1 || exit 5
+  one base_$i EM_FUSED_V6=1 EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/base.so || exit 4
+  one new_$i EM_FUSED_V6=1 || exit 5
 done
-python -m euromillioner_amd._build --define V4_STAMPS=1 > gpurun_out/v6/build_st.log 2>&1 || exit 2
-EM_FUSED_V6=1 TL_B=1048576 timeout -k 10 120 python tools/dev/stamps_timeline.py > gpurun_out/v6/timeline.txt 2>&1 || { cat gpurun_out/v6/timeline.txt; exit 3; }
-cat gpurun_out/v6/timeline.txt
