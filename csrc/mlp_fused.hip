@@ -2116,6 +2116,33 @@ EM_API int em_mlp_fused_slab_stride() { return SLAB_STRIDE; }
 EM_API int em_mlp_fused_image_bytes() { return IMG_BYTES; }
 EM_API int em_mlp_fused_lds_bytes() { return TRAIN_LDS; }
 
+// Which train kernel em_mlp_fused_train launches: 6 (default: producer/consumer units), 4 (hidden-split
+// pairs), 5 (round-synchronous, experimental) or 3 (one wave per SIMD).  The first call reads
+// EM_FUSED_KERNEL (or the older EM_FUSED_V3 / EM_FUSED_V5 / EM_FUSED_V6 flags); em_mlp_fused_select_kernel
+// overrides it at run time (tests cover every version in one process).
+static int g_fused_kernel = -1;
+static int fused_kernel_version() {
+  if (g_fused_kernel < 0) {
+    int v = 6;
+    const char* e = std::getenv("EM_FUSED_KERNEL");
+    const char* e3 = std::getenv("EM_FUSED_V3");
+    const char* e5 = std::getenv("EM_FUSED_V5");
+    const char* e6 = std::getenv("EM_FUSED_V6");
+    if (e6 && e6[0] == '0') v = 4;
+    if (e5 && e5[0] == '1') v = 5;
+    if (e3 && e3[0] == '1') v = 3;
+    if (e && (e[0] == '3' || e[0] == '4' || e[0] == '5' || e[0] == '6') && e[1] == 0) v = e[0] - '0';
+    g_fused_kernel = v;
+  }
+  return g_fused_kernel;
+}
+EM_API int em_mlp_fused_select_kernel(int version) {  // returns the previous version; -1 = back to the env default
+  const int prev = fused_kernel_version();
+  if (version == -1 || version == 3 || version == 4 || version == 5 || version == 6) g_fused_kernel = version;
+  else return EM_ERR_ARG;
+  return prev;
+}
+
 // masks: [ndraws] uint64 feature masks; sample s = (masks[i], masks[i+1]) with i = sidx ? sidx[s] : offset+s
 EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
                               const void* wimg, float* slabs, float* loss_slabs, int nslab, int loss_kind,
@@ -2135,18 +2162,8 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
                               TRAIN_LDS);
     attr_set = true;
   }
-  static int use_v3 = -1, use_v5 = 0, use_v6 = 0;
-  if (use_v3 < 0) {
-    const char* e6 = std::getenv("EM_FUSED_V6");
-    use_v6 = (e6 && e6[0] == '1') ? 1 : 0;
-    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              V6_LDS);
-    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              V6_LDS);
-    const char* e = std::getenv("EM_FUSED_V3");
-    use_v3 = (e && e[0] == '1') ? 1 : 0;
-    const char* e5 = std::getenv("EM_FUSED_V5");
-    use_v5 = (e5 && e5[0] == '1') ? 1 : 0;
+  static bool attrs = false;
+  if (!attrs) {
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_v4_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               V4_LDS);
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_v4_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2155,34 +2172,36 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
                               V5_LDS);
     (void)hipFuncSetAttribute((const void*)mlp_fused_train_v5_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               V5_LDS);
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V6_LDS);
+    (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              V6_LDS);
+    attrs = true;
   }
-  if (use_v6 && !use_v3) {
+  const int ver = fused_kernel_version();
+  const dim3 grid(nslab);
+  const int Bi = (int)B, oi = (int)offset;
+  const uint8_t* w = (const uint8_t*)wimg;
+  if (ver == 6) {
     if (loss_kind == 0)
-      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, (int)B,
-                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, grid, dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
     else
-      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, (int)B,
-                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
-  } else if (use_v5 && !use_v3) {
+      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, grid, dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+  } else if (ver == 5) {
     if (loss_kind == 0)
-      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<0>, dim3(nslab), dim3(512), V5_LDS, stream, draws, sidx, (int)B,
-                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<0>, grid, dim3(512), V5_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
     else
-      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<1>, dim3(nslab), dim3(512), V5_LDS, stream, draws, sidx, (int)B,
-                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
-  } else if (!use_v3) {
+      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<1>, grid, dim3(512), V5_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+  } else if (ver == 4) {
     if (loss_kind == 0)
-      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<0>, dim3(nslab), dim3(512), V4_LDS, stream, draws, sidx, (int)B,
-                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<0>, grid, dim3(512), V4_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
     else
-      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<1>, dim3(nslab), dim3(512), V4_LDS, stream, draws, sidx, (int)B,
-                         (int)offset, (const uint8_t*)wimg, slabs, loss_slabs);
-  } else if (loss_kind == 0)
-    hipLaunchKernelGGL(mlp_fused_train_kernel<0>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, (int)B, (int)offset,
-                       (const uint8_t*)wimg, slabs, loss_slabs);
-  else
-    hipLaunchKernelGGL(mlp_fused_train_kernel<1>, dim3(nslab), dim3(256), TRAIN_LDS, stream, draws, sidx, (int)B, (int)offset,
-                       (const uint8_t*)wimg, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<1>, grid, dim3(512), V4_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+  } else if (loss_kind == 0) {
+    hipLaunchKernelGGL(mlp_fused_train_kernel<0>, grid, dim3(256), TRAIN_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+  } else {
+    hipLaunchKernelGGL(mlp_fused_train_kernel<1>, grid, dim3(256), TRAIN_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+  }
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -108,6 +108,17 @@ def _check_draws(draws: torch.Tensor, sidx: torch.Tensor | None, B: int, offset:
         raise ValueError(f"samples [{offset}, {offset + B}) + next draw exceed {n} draws")
 
 
+KERNELS = (3, 4, 5, 6)  # csrc/mlp_fused.hip train kernels; 6 = producer/consumer units (default)
+
+
+def select_kernel(version: int) -> int:
+    """Choose the train kernel (3, 4, 5 or 6; -1 = the EM_FUSED_KERNEL env default, 6 if unset) for
+    later launches in this process.  Returns the previous version."""
+    if version != -1 and version not in KERNELS:
+        raise ValueError(f"fused train kernel must be one of {KERNELS} or -1, got {version}")
+    return int(N.query("em_mlp_fused_select_kernel", int(version)))
+
+
 def train_partials(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.Tensor, loss_slabs: torch.Tensor,
                    loss: str = "softmax", offset: int = 0, sidx: torch.Tensor | None = None,
                    check: bool = True) -> int:

@@ -24,6 +24,16 @@ def _ref_grads(sd, ds_numbers, offset, B, loss, bf16=True):
     return l.item(), {"l1.weight": W1.grad, "l1.bias": b1.grad, "l2.weight": W2.grad, "l2.bias": b2.grad}, z.detach()
 
 
+@pytest.fixture(params=[6, 4], ids=["v6", "v4"])
+def kernel(request):
+    """Run the test on the producer/consumer kernel (v6, default) and the hidden-split pairs (v4)."""
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    prev = FM.select_kernel(request.param)
+    yield request.param
+    FM.select_kernel(prev)
+
+
 @pytest.fixture(scope="module")
 def data():
     from euromillioner_amd.ops.fused_mlp import rows_to_masks
@@ -34,7 +44,7 @@ def data():
 
 @pytest.mark.parametrize("loss", ["softmax", "bce"])
 @pytest.mark.parametrize("B,offset", [(4096, 0), (1000, 7), (37, 100)])
-def test_fused_grads_match_reference(data, loss, B, offset):
+def test_fused_grads_match_reference(data, loss, B, offset, kernel):
     from euromillioner_amd.models.mlp import FusedSmallMLP
     from euromillioner_amd.ops import fused_mlp as FM
 
@@ -124,7 +134,7 @@ def test_onehot_kernel(data):
     assert torch.equal(oh, torch.from_numpy(ref))
 
 
-def test_fused_deterministic(data):
+def test_fused_deterministic(data, kernel):
     from euromillioner_amd.models.mlp import FusedSmallMLP
 
     ds, draws = data
@@ -137,7 +147,7 @@ def test_fused_deterministic(data):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_fused_sample_index_path(data):
+def test_fused_sample_index_path(data, kernel):
     from euromillioner_amd.models.mlp import FusedSmallMLP
 
     ds, draws = data
@@ -153,7 +163,7 @@ def test_fused_sample_index_path(data):
     assert torch.allclose(g3, g2, atol=1e-5, rtol=1e-3)
 
 
-def test_fused_grads_property_random_batches():
+def test_fused_grads_property_random_batches(kernel):
     """Random batch sizes (1 .. 70k: single partial tile up to several tiles per pair) and offsets,
     both losses, against the fp32 reference of the same bf16-rounded weights."""
     from hypothesis import HealthCheck, given, settings
@@ -179,3 +189,12 @@ def test_fused_grads_property_random_batches():
         assert err < 2e-2, (B, offset, loss, err)
 
     check()
+
+
+def test_select_kernel_rejects_unknown():
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    with pytest.raises(ValueError):
+        FM.select_kernel(7)
+    prev = FM.select_kernel(4)
+    assert FM.select_kernel(prev) == 4
