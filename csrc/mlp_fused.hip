@@ -1571,9 +1571,12 @@ EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
   return U < ntiles ? (ntiles - U + nunits - 1) / nunits : 0;
 }
 
-// Grouped softmax-CE of a whole tile in ONE wave (v6 forward), with the max / sum / target-dot
-// reductions split into independent partial chains (full_tile_loss runs each as one serial chain of
-// 32 dependent ops).
+// Grouped softmax-CE of a whole tile in ONE wave (v6 forward).  The class of the lane's element i of
+// output tile u (main / star / pad) is a compile-time constant except for 4 elements of tile 1 whose
+// class depends on the lane half h (outputs 48-51 and 58-63 straddle the group edges), so every
+// statically classified element emits only its own group's ops: a select-form "x ? v : 0" fed into
+// an fma or add would have to be kept (IEEE: fma(0, inf, a) is NaN) and costs a VALU op per element
+// per group.  Max / sum / target-dot reductions run as independent partial chains.
 template <int YL>
 EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
                           float& loss_acc) {
@@ -1586,6 +1589,7 @@ EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmas
       yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
     }
   };
+  const bool h0 = h == 0;
   const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
   const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
   const int ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
@@ -1596,9 +1600,17 @@ EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmas
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = v5_cls(u, i, h);
-      mm[i & 3] = (c == 0) ? fmaxf(mm[i & 3], z2[u][i]) : mm[i & 3];
-      ms[i & 1] = (c == 1) ? fmaxf(ms[i & 1], z2[u][i]) : ms[i & 1];
+      const int c0 = v5_cls(u, i, 0), c1 = v5_cls(u, i, 1);
+      const float v = z2[u][i];
+      if (c0 == c1) {
+        if (c0 == 0) mm[i & 3] = fmaxf(mm[i & 3], v);
+        if (c0 == 1) ms[i & 1] = fmaxf(ms[i & 1], v);
+      } else if (c0 == 0) {  // main (h = 0) / star (h = 1)
+        mm[i & 3] = h0 ? fmaxf(mm[i & 3], v) : mm[i & 3];
+        ms[i & 1] = h0 ? ms[i & 1] : fmaxf(ms[i & 1], v);
+      } else {  // star (h = 0) / pad (h = 1)
+        ms[i & 1] = h0 ? fmaxf(ms[i & 1], v) : ms[i & 1];
+      }
     }
   const float mx_m = xhalf_max(fmaxf(fmaxf(mm[0], mm[1]), fmaxf(mm[2], mm[3])));
   const float mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
@@ -1610,26 +1622,53 @@ EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmas
     targets(u, yb);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = v5_cls(u, i, h);
-      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z2[u][i], L2E, c == 1 ? nsL : nmL));
-      const float ee = (c == 2) ? 0.f : e;
-      sm[i & 3] += (c == 0) ? ee : 0.f;
-      ss[i & 1] += (c == 1) ? ee : 0.f;
-      tm[i & 3] = __builtin_fmaf((c == 0) ? yb[i] : 0.f, z2[u][i], tm[i & 3]);
-      ts[i & 1] = __builtin_fmaf((c == 1) ? yb[i] : 0.f, z2[u][i], ts[i & 1]);
-      dz[u][i] = ee;
+      const int c0 = v5_cls(u, i, 0), c1 = v5_cls(u, i, 1);
+      const float v = z2[u][i];
+      float e = 0.f;
+      if (c0 == c1) {
+        if (c0 == 0) {
+          e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nmL));
+          sm[i & 3] += e;
+          tm[i & 3] = __builtin_fmaf(yb[i], v, tm[i & 3]);
+        } else if (c0 == 1) {
+          e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL));
+          ss[i & 1] += e;
+          ts[i & 1] = __builtin_fmaf(yb[i], v, ts[i & 1]);
+        }
+      } else if (c0 == 0) {  // main (h = 0) / star (h = 1)
+        e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, h0 ? nmL : nsL));
+        const float ty = yb[i] * v;
+        sm[i & 3] = h0 ? sm[i & 3] + e : sm[i & 3];
+        ss[i & 1] = h0 ? ss[i & 1] : ss[i & 1] + e;
+        tm[i & 3] = h0 ? tm[i & 3] + ty : tm[i & 3];
+        ts[i & 1] = h0 ? ts[i & 1] : ts[i & 1] + ty;
+      } else {  // star (h = 0) / pad (h = 1)
+        e = h0 ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL)) : 0.f;
+        ss[i & 1] += e;
+        ts[i & 1] = h0 ? __builtin_fmaf(yb[i], v, ts[i & 1]) : ts[i & 1];
+      }
+      dz[u][i] = e;
     }
   }
   const float s_m = xhalf_sum((sm[0] + sm[1]) + (sm[2] + sm[3])), s_s = xhalf_sum(ss[0] + ss[1]);
   const float f_m = nm ? __builtin_amdgcn_rcpf(s_m) : 0.f, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
+  const float ni_m = -inv_m, ni_s = -inv_s;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     float yb[16];  // re-read (8 LDS loads) rather than held across the sums: keeps the forward wave spill-free
     targets(u, yb);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = v5_cls(u, i, h);
-      dz[u][i] = (c == 2) ? 0.f : __builtin_fmaf(dz[u][i], c == 0 ? f_m : f_s, -yb[i] * (c == 0 ? inv_m : inv_s));
+      const int c0 = v5_cls(u, i, 0), c1 = v5_cls(u, i, 1);
+      if (c0 == c1) {
+        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], f_m, yb[i] * ni_m);
+        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
+        if (c0 == 2) dz[u][i] = 0.f;
+      } else if (c0 == 0) {
+        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? f_m : f_s, yb[i] * (h0 ? ni_m : ni_s));
+      } else {  // the pad lanes' e is 0 and their target bit (outputs 62/63) is 0
+        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
+      }
     }
   }
   float l = -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
@@ -1769,10 +1808,16 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     pair_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
   };
-  if (V6_UNROLL && V6_NSLOT == 3) {
-    // tiles k = f + 2m visit slots f, f + 2, f + 1 (mod 3): unrolled so every slot base is a constant
-    // folded into the LDS instructions' offsets instead of a per-address add per tile
-    constexpr int S0 = F % 3, S1 = (F + 2) % 3, S2 = (F + 1) % 3;
+  if (V6_UNROLL && V6_NSLOT == 4) {
+    // tiles k = F + 2m alternate between slots F and F + 2: unrolled so both slot bases are constants
+    // folded into the LDS instructions' offsets instead of one address add per access per tile
+    for (int k = F; k < K; k += 4) {
+      ftile(k, std::integral_constant<int, F>{});
+      if (k + 2 >= K) break;
+      ftile(k + 2, std::integral_constant<int, F + 2>{});
+    }
+  } else if (V6_UNROLL && V6_NSLOT == 3) {
+    constexpr int S0 = F % 3, S1 = (F + 2) % 3, S2 = (F + 1) % 3;  // tiles k = F + 2m visit these slots
     for (int k = F; k < K; k += 6) {
       ftile(k, std::integral_constant<int, S0>{});
       if (k + 2 >= K) break;

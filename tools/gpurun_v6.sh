@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/v6
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-EM_FUSED_V6=1 timeout -k 10 300 python -u -m pytest tests/test_fused_mlp_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/v6/t_fused.log 2>&1 || { tail -40 gpurun_out/v6/t_fused.log; exit 3; }
+timeout -k 10 300 python -u -m pytest tests/test_fused_mlp_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/v6/t_fused.log 2>&1 || { tail -40 gpurun_out/v6/t_fused.log; exit 3; }
 tail -2 gpurun_out/v6/t_fused.log
 one() {  # tag env...
   local tag=$1; shift
