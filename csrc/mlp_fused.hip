@@ -1517,6 +1517,12 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
 #ifndef V6_FPRIO
 #define V6_FPRIO 1  // 1: forward waves run at s_setprio 1 (they bound the pipeline; backward waves have slack)
 #endif
+#ifndef V6_SPLIT
+#define V6_SPLIT 1  // 1: per-output-tile softmax statistics merged online (tile 0's loss beside tile 1's F2)
+#endif
+#ifndef V6_ILV
+#define V6_ILV 1  // 1: sched_barrier fences keep tile 0's softmax steps between tile 1's F2 MFMAs
+#endif
 #ifndef V6_UNROLL
 #define V6_UNROLL 0  // 1: forward loop unrolled over the 3 ring slots (measured: more live addresses, spills)
 #endif
@@ -1677,6 +1683,140 @@ EM_DEVICE void v6_softmax(const char* smem, const f32x16 (&z2)[2], uint64_t tmas
   loss_acc += l;
 }
 
+// v6_softmax with the main-group statistics split per output tile and merged online (flash-softmax
+// style): tile 0's max / exp / sums need only Z2 tile 0, so they can run on the VALU while tile 1's
+// F2 chain is still in the matrix pipe.  dZ2 of tile u carries its tile's rescale a_u = exp(m_u - M).
+template <int YL, typename Hook>
+EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
+                                float& loss_acc, Hook&& hook) {
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  auto targets = [&](int u, float (&yb)[16]) {
+    const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
+    }
+  };
+  const bool h0 = h == 0;
+  const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
+  const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
+  const int ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
+  const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
+  const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
+  float tm[4] = {0.f, 0.f, 0.f, 0.f}, ts[2] = {0.f, 0.f};
+  // ---- tile 0: outputs 0..31, all main.  step(j), j = 0..7, is issued between tile 1's F2 MFMAs by
+  // the caller (hook): in-order issue lets the VALU run only between MFMAs in program order ----
+  float m0 = 0.f, s0 = 0.f, nL = 0.f;
+  float mm0[4], sm[4] = {0.f, 0.f, 0.f, 0.f}, yb0[16];
+  auto step = [&](int j) {
+    if (j == 0) {
+      mm0[0] = z2[0][0]; mm0[1] = z2[0][1]; mm0[2] = z2[0][2]; mm0[3] = z2[0][3];
+#pragma unroll
+      for (int i = 4; i < 16; ++i) mm0[i & 3] = fmaxf(mm0[i & 3], z2[0][i]);
+      targets(0, yb0);
+    } else if (j == 1) {
+      m0 = xhalf_max(fmaxf(fmaxf(mm0[0], mm0[1]), fmaxf(mm0[2], mm0[3])));
+      nL = -m0 * L2E;
+    } else if (j < 6) {
+#pragma unroll
+      for (int i = 4 * (j - 2); i < 4 * (j - 1); ++i) {
+        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(z2[0][i], L2E, nL));
+        sm[i & 3] += e;
+        tm[i & 3] = __builtin_fmaf(yb0[i], z2[0][i], tm[i & 3]);
+        dz[0][i] = e;
+      }
+    } else if (j == 6) {
+      s0 = xhalf_sum((sm[0] + sm[1]) + (sm[2] + sm[3]));
+    }
+  };
+  hook(step);
+  // ---- tile 1: outputs 32..63 (main 32..49, star 50..61, pad 62/63) ----
+  float mm[2] = {-3.0e38f, -3.0e38f}, ms[2] = {-3.0e38f, -3.0e38f};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c0 = v5_cls(1, i, 0), c1 = v5_cls(1, i, 1);
+    const float v = z2[1][i];
+    if (c0 == c1) {
+      if (c0 == 0) mm[i & 1] = fmaxf(mm[i & 1], v);
+      if (c0 == 1) ms[i & 1] = fmaxf(ms[i & 1], v);
+    } else if (c0 == 0) {  // main (h = 0) / star (h = 1)
+      mm[i & 1] = h0 ? fmaxf(mm[i & 1], v) : mm[i & 1];
+      ms[i & 1] = h0 ? ms[i & 1] : fmaxf(ms[i & 1], v);
+    } else {  // star (h = 0) / pad (h = 1)
+      ms[i & 1] = h0 ? fmaxf(ms[i & 1], v) : ms[i & 1];
+    }
+  }
+  const float m1 = xhalf_max(fmaxf(mm[0], mm[1]));
+  const float mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
+  const float nmL = -m1 * L2E, nsL = -mx_s * L2E;
+  float s1p[2] = {0.f, 0.f}, ss[2] = {0.f, 0.f};
+  {
+    float yb[16];
+    targets(1, yb);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c0 = v5_cls(1, i, 0), c1 = v5_cls(1, i, 1);
+      const float v = z2[1][i];
+      float e = 0.f;
+      if (c0 == c1) {
+        if (c0 == 0) {
+          e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nmL));
+          s1p[i & 1] += e;
+          tm[i & 3] = __builtin_fmaf(yb[i], v, tm[i & 3]);
+        } else if (c0 == 1) {
+          e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL));
+          ss[i & 1] += e;
+          ts[i & 1] = __builtin_fmaf(yb[i], v, ts[i & 1]);
+        }
+      } else if (c0 == 0) {
+        e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, h0 ? nmL : nsL));
+        const float ty = yb[i] * v;
+        s1p[i & 1] = h0 ? s1p[i & 1] + e : s1p[i & 1];
+        ss[i & 1] = h0 ? ss[i & 1] : ss[i & 1] + e;
+        tm[i & 3] = h0 ? tm[i & 3] + ty : tm[i & 3];
+        ts[i & 1] = h0 ? ts[i & 1] : ts[i & 1] + ty;
+      } else {
+        e = h0 ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL)) : 0.f;
+        ss[i & 1] += e;
+        ts[i & 1] = h0 ? __builtin_fmaf(yb[i], v, ts[i & 1]) : ts[i & 1];
+      }
+      dz[1][i] = e;
+    }
+  }
+  const float s1 = xhalf_sum(s1p[0] + s1p[1]), s_s = xhalf_sum(ss[0] + ss[1]);
+  // ---- online merge of the main group: M = max(m0, m1), S = a0 s0 + a1 s1 ----
+  const float M = fmaxf(m0, m1);
+  const float a0 = __builtin_amdgcn_exp2f((m0 - M) * L2E), a1 = __builtin_amdgcn_exp2f((m1 - M) * L2E);
+  const float S = __builtin_fmaf(a0, s0, a1 * s1);
+  const float rS = nm ? __builtin_amdgcn_rcpf(S) : 0.f;
+  const float f0 = a0 * rS, f1 = a1 * rS, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
+  const float ni_m = -inv_m, ni_s = -inv_s;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float yb[16];  // re-read (8 LDS loads) rather than held across the sums: keeps the forward wave spill-free
+    targets(u, yb);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c0 = v5_cls(u, i, 0), c1 = v5_cls(u, i, 1);
+      const float fm = u == 0 ? f0 : f1;
+      if (c0 == c1) {
+        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, yb[i] * ni_m);
+        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
+        if (c0 == 2) dz[u][i] = 0.f;
+      } else if (c0 == 0) {
+        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? fm : f_s, yb[i] * (h0 ? ni_m : ni_s));
+      } else {  // the pad lanes' e is 0 and their target bit (outputs 62/63) is 0
+        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
+      }
+    }
+  }
+  float l = -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
+  if (h == 0)
+    l += (nm ? M + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
+  loss_acc += l;
+}
+
 // forward wave F (0/1) of unit `unit`: tiles k = F, F + 2, ... of the unit's stream
 template <int LOSS, int F>
 EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
@@ -1775,18 +1915,39 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
         const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
         z2[u][4 * g + 0] = b[0]; z2[u][4 * g + 1] = b[1]; z2[u][4 * g + 2] = b[2]; z2[u][4 * g + 3] = b[3];
       }
+    auto f2mfma = [&](int u, int kk) {
+      z2[u] = mfma32(V6_WREG ? w2r[u][kk] : lds_frag(smem, w2p_off(32 * u + r, kk * 2 + h)), hT[kk >> 1][kk & 1], z2[u]);
+    };
+    // tile 0's chain first; tile 1's chain is issued by the softmax hook, one MFMA per step of tile 0's
+    // statistics (V6_ILV: sched_barrier fences pin that order)
+    auto hook = [&](auto&& step) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int j = 0; j < 8; ++j) {
+        f2mfma(1, j);
+        if (V6_ILV) __builtin_amdgcn_sched_barrier(0);
+        step(j);
+        if (V6_ILV) __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if (V6_SPLIT && LOSS == 0) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int kk = 0; kk < 8; ++kk) f2mfma(0, kk);
+    } else {
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-          z2[u] = mfma32(V6_WREG ? w2r[u][2 * t + q] : lds_frag(smem, w2p_off(32 * u + r, (2 * t + q) * 2 + h)),
-                         hT[t][q], z2[u]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            z2[u] = mfma32(V6_WREG ? w2r[u][2 * t + q] : lds_frag(smem, w2p_off(32 * u + r, (2 * t + q) * 2 + h)),
+                           hT[t][q], z2[u]);
+    }
     st.mark(2);
 
     float dz[2][16];
-    if (LOSS == 0)
+    if (LOSS == 0 && V6_SPLIT)
+      v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, loss_acc, hook);
+    else if (LOSS == 0)
       v6_softmax<V6_YLUT>(smem, z2, tmask, h, dz, loss_acc);
     else
       full_tile_loss<LOSS, V6_YLUT>(smem, z2, tmask, valid, h, dz, loss_acc);
