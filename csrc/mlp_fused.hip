@@ -1523,6 +1523,12 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
 #ifndef V6_ILV
 #define V6_ILV 1  // 1: sched_barrier fences keep tile 0's softmax steps between tile 1's F2 MFMAs
 #endif
+#ifndef V6_YB1
+#define V6_YB1 1  // 1: the forward softmax reads the target LUT once per tile (8 KB of LDS reads fewer per tile)
+#endif
+#ifndef V6_DYN
+#define V6_DYN 0  // 1 (measured -0.6%): forward waves claim the unit's tiles from an LDS counter instead of strictly alternating
+#endif
 #ifndef V6_UNROLL
 #define V6_UNROLL 0  // 1: forward loop unrolled over the 3 ring slots (measured: more live addresses, spills)
 #endif
@@ -1544,9 +1550,10 @@ static_assert(!V6_RECYCLE || V6_XMASK || 2 * V6_SLOT <= IMG_W2Q, "recycled slots
 constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
-constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[3] | done0[3] | done1[3]
+constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[N] | done0[N] | done1[N] | next (V6_DYN)
 constexpr int V6_RING = V6_FLAGS + 128;  // [2 units][3 slots][16 KB]
-constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_RSLOTS * V6_SLOT;
+constexpr int V6_LOSSR = V6_RING + 2 * V6_RSLOTS * V6_SLOT;  // V6_DYN: [2 units][slot][64 lanes] per-tile loss
+constexpr int V6_LOOP_LDS = V6_LOSSR + 2 * V6_NSLOT * 256;
 // byte offset of ring slot `slot` of unit `unit`
 EM_DEVICE uint32_t v6_slot(int unit, int slot) {
   return slot < V6_RSLOTS ? V6_RING + (unit * V6_RSLOTS + slot) * V6_SLOT : unit * V6_SLOT;
@@ -1751,9 +1758,10 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   const float mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
   const float nmL = -m1 * L2E, nsL = -mx_s * L2E;
   float s1p[2] = {0.f, 0.f}, ss[2] = {0.f, 0.f};
+  float yb1[16];
+  targets(1, yb1);
   {
-    float yb[16];
-    targets(1, yb);
+    float (&yb)[16] = yb1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c0 = v5_cls(1, i, 0), c1 = v5_cls(1, i, 1);
@@ -1794,8 +1802,9 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   const float ni_m = -inv_m, ni_s = -inv_s;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float yb[16];  // re-read (8 LDS loads) rather than held across the sums: keeps the forward wave spill-free
-    targets(u, yb);
+    float yr[16];  // V6_YB1: the targets read once per tile (held in registers); else re-read here
+    if (!V6_YB1) targets(u, yr);
+    const float (&yb)[16] = V6_YB1 ? (u == 0 ? yb0 : yb1) : yr;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c0 = v5_cls(u, i, 0), c1 = v5_cls(u, i, 1);
@@ -1835,8 +1844,8 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
       mt = masks[idx + 1];
     }
   };
-  uint64_t nin, ntg;
-  fetch(F, nin, ntg);
+  uint64_t nin = 0, ntg = 0;
+  if (!V6_DYN) fetch(F, nin, ntg);
   // the forward wave's weight fragments (W1ᵀ 4 x 4, W2ᵀ 2 x 8: 128 VGPRs) stay in registers for the
   // whole launch: no LDS read stands between the tile's operands and its 32 MFMAs
   bf16x8 w1r[4][4], w2r[2][8];
@@ -1852,12 +1861,12 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
   }
   if (V6_NSLOT > V6_RSLOTS) __syncthreads();  // every forward wave holds its weights: the images are free
   st.start();
-  auto ftile = [&](int k, auto slot_c) {  // slot_c: the ring slot, compile-time in the unrolled loop
+  auto ftile = [&](int k, auto slot_c, int knext) {  // slot_c: the ring slot (compile-time when unrolled)
     const int slot = slot_c;
     const bool valid = (U + k * nunits) * 32 + r < B;
     const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
     const uint64_t tmask = valid ? ntg : 0ull;
-    fetch(k + 2, nin, ntg);
+    fetch(knext, nin, ntg);
     const uint32_t SB = v6_slot(unit, slot);
     if (k >= V6_NSLOT) {  // the slot's previous tile (k - 3) must be consumed by both backward waves
       v6_wait(smem, FL + (V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
@@ -1945,12 +1954,17 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     st.mark(2);
 
     float dz[2][16];
+    float lt = 0.f;  // this lane's loss terms of the tile
     if (LOSS == 0 && V6_SPLIT)
-      v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, loss_acc, hook);
+      v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, lt, hook);
     else if (LOSS == 0)
-      v6_softmax<V6_YLUT>(smem, z2, tmask, h, dz, loss_acc);
+      v6_softmax<V6_YLUT>(smem, z2, tmask, h, dz, lt);
     else
-      full_tile_loss<LOSS, V6_YLUT>(smem, z2, tmask, valid, h, dz, loss_acc);
+      full_tile_loss<LOSS, V6_YLUT>(smem, z2, tmask, valid, h, dz, lt);
+    // V6_DYN: the tile's loss rides in the ring and B0 sums it in tile order (which forward wave ran a tile
+    // varies from run to run; the reported loss must not)
+    if (V6_DYN) reinterpret_cast<float*>(smem + V6_LOSSR)[(unit * V6_NSLOT + slot) * 64 + lane] = lt;
+    else loss_acc += lt;
     st.mark(3);
 
     // dZ2 image [32 samples][64 outs]: 8-byte granules of 4 consecutive outputs (B reads the same
@@ -1969,25 +1983,39 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     pair_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
   };
-  if (V6_UNROLL && V6_NSLOT == 4) {
+  if (V6_DYN) {
+    int* next = reinterpret_cast<int*>(smem + FL + 3 * V6_NSLOT * 4);
+    auto claim = [&]() {
+      int v = 0;
+      if (lane == 0) v = __hip_atomic_fetch_add(next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+    int kc = claim();
+    fetch(kc, nin, ntg);
+    while (kc < K) {
+      const int kn = claim();
+      ftile(kc, kc % V6_NSLOT, kn);
+      kc = kn;
+    }
+  } else if (V6_UNROLL && V6_NSLOT == 4) {
     // tiles k = F + 2m alternate between slots F and F + 2: unrolled so both slot bases are constants
     // folded into the LDS instructions' offsets instead of one address add per access per tile
     for (int k = F; k < K; k += 4) {
-      ftile(k, std::integral_constant<int, F>{});
+      ftile(k, std::integral_constant<int, F>{}, k + 2);
       if (k + 2 >= K) break;
-      ftile(k + 2, std::integral_constant<int, F + 2>{});
+      ftile(k + 2, std::integral_constant<int, F + 2>{}, k + 4);
     }
   } else if (V6_UNROLL && V6_NSLOT == 3) {
     constexpr int S0 = F % 3, S1 = (F + 2) % 3, S2 = (F + 1) % 3;  // tiles k = F + 2m visit these slots
     for (int k = F; k < K; k += 6) {
-      ftile(k, std::integral_constant<int, S0>{});
+      ftile(k, std::integral_constant<int, S0>{}, k + 2);
       if (k + 2 >= K) break;
-      ftile(k + 2, std::integral_constant<int, S1>{});
+      ftile(k + 2, std::integral_constant<int, S1>{}, k + 4);
       if (k + 4 >= K) break;
-      ftile(k + 4, std::integral_constant<int, S2>{});
+      ftile(k + 4, std::integral_constant<int, S2>{}, k + 6);
     }
   } else {
-    for (int k = F; k < K; k += 2) ftile(k, k % V6_NSLOT);
+    for (int k = F; k < K; k += 2) ftile(k, k % V6_NSLOT, k + 2);
   }
 }
 
@@ -1997,7 +2025,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 // registers (B1, then dW2 + db2 while B1's results drain, the relu mask, dW1ᵀ).
 template <int RHO>
 EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[2][2], f32x16 (&dW1T)[2][2],
-                           f32x16& db2, bool& ok, V4Stamps& st) {
+                           f32x16& db2, float& loss_acc, bool& ok, V4Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
   const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
@@ -2018,6 +2046,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
     st.mark(5);
 
     // dZ2 as B1's A operand (samples x outputs): F's own 8-byte granules, k-step (u, q)
+    if (V6_DYN && RHO == 0) loss_acc += reinterpret_cast<const float*>(smem + V6_LOSSR)[(unit * V6_NSLOT + slot) * 64 + lane];
     bf16x8 dzA[2][2], hR[2][2], bd[2][2], bx[2][2], w2q[2][4];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -2147,13 +2176,15 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
         dW1T[t][u] = f32x16{};
       }
     f32x16 db2 = f32x16{};
-    v6_backward<RHO>(smem, B, unit, lane, dW2, dW1T, db2, ok, st);
+    float loss_acc = 0.f;
+    v6_backward<RHO>(smem, B, unit, lane, dW2, dW1T, db2, loss_acc, ok, st);
+    const float lsum = wave_sum(loss_acc);
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");  // asm MFMA (AGPR D) -> v_accvgpr_read hazard
     dump();
     __syncthreads();
     if (V6_DB2DOT) db2[0] = xhalf_sum(db2[0]);           // the two sample halves of output 32 RHO + r
     if (h == 0) DB2S[unit * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
-    if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
+    if (lane == 0) LOSSS[wave] = ok ? lsum : __builtin_nanf("");
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll

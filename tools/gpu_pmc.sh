@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-ARGS="--steps 6 --warmup 2 --graph 0 --no-eval"
+ARGS="--steps 6 --warmup 2 --graph 0 --no-eval --warmup-ms 0"
 i=0
 for set in "$@"; do
   i=$((i+1))
