@@ -170,7 +170,11 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
                   const float* __restrict__ hp, int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img,
                   const float* __restrict__ loss_slabs, float* __restrict__ loss_out, float loss_scale,
                   int* __restrict__ xg_hdr, float* __restrict__ xg_data, int xg_cap) {
-  const int tstep = (mode != 1) ? adam_begin(state) : 0;
+  // the step counter: only wave 0 (the 64 Adam lanes) needs it.  A plain load suffices -- the previous
+  // step's kernel boundary published it, and this launch writes it only after every block's ticket --
+  // whereas 1024 waves issuing an agent-scope atomic load of one word serialise on one L2 channel.
+  int tstep = 0;
+  if (mode != 1 && threadIdx.x < 64) tstep = state[0] + 1;
   if (xg_hdr) {
     grad_io = xg_produce_slot(xg_hdr, xg_data, xg_cap);
     loss_out = grad_io + P;

@@ -2137,6 +2137,15 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
   }
 }
 
+// f32x4 slot of accumulator group g of tile T, lane (L, h) in the epilogue's fold image.  The dW1ᵀ tiles
+// XOR the lane slot with the slab writer's lane bits (hidden tile parity, g, h): the writer's 16-lane
+// groups read 16 distinct (T, g, h) at one L, which without the swizzle all land on one 16-B bank group
+// (a 16-way conflict per read, ~2 us of the epilogue); the B waves' 8-lane store groups stay conflict-free.
+EM_DEVICE int v6_red_slot(int T, int g, int L, int h) {
+  const int sw = T >= 8 ? ((((T - 8) >> 1) & 1) << 3) | (g << 1) | h : 0;
+  return (T * 4 + g) * 64 + h * 32 + (L ^ sw);
+}
+
 // one role's loop + its share of the epilogue (the same two barriers in every role instantiation)
 template <int LOSS, int ROLE>  // ROLE 0/1 = forward f, 2/3 = backward rho
 EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
@@ -2195,7 +2204,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
           const int T = 8 * which + 2 * (2 * RHO + tt) + u;
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<f32x4*>(RED + unit * 16384 + ((T * 4 + g) * 64 + lane) * 4) =
+            *reinterpret_cast<f32x4*>(RED + unit * 16384 + v6_red_slot(T, g, r, h) * 4) =
                 f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
         }
     __syncthreads();
@@ -2254,21 +2263,22 @@ mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
   // parameter-order slab with 16-B write-through (sc1) stores (see the v4 epilogue)
   const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(slab, 0, SLAB_STRIDE * 4, 0x00020000);
-  for (int e = tid; e < 2 * 2048; e += 512) {
-    f32x4 v;
-    if (e < 2048) {
-      const int f = e >> 5, c = (e & 31) * 4;
-      const int T = 8 + 2 * (c >> 5) + (f >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (f & 31);
-      const int at = ((T * 4 + g) * 64 + l) * 4;
-      v = *reinterpret_cast<const f32x4*>(RED + at) + *reinterpret_cast<const f32x4*>(RED + 16384 + at);
-    } else {
-      const int q = e - 2048, c = q >> 4, o = (q & 15) * 4;
-      const int T = 2 * (c >> 5) + (o >> 5), g = (c & 31) >> 3, l = ((c >> 2) & 1) * 32 + (o & 31);
-      const int at = ((T * 4 + g) * 64 + l) * 4 + (c & 3);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = RED[at + 4 * k] + RED[16384 + at + 4 * k];
-    }
+  for (int e = tid; e < 2048; e += 512) {  // W1[f][c..c+3]: one 16-B store per f32x4 of a dW1ᵀ tile
+    const int f = e >> 5, c = (e & 31) * 4;
+    const int T = 8 + 2 * (c >> 5) + (f >> 5), g = (c & 31) >> 3;
+    const int at = v6_red_slot(T, g, f & 31, (c >> 2) & 1) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + at) + *reinterpret_cast<const f32x4*>(RED + 16384 + at);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, e * 16, 0, 16 /* sc1 */);
+  }
+  for (int q = tid; q < 2048; q += 512) {  // dW2 tiles read in slot order; W2[c + k][o] as 4 coalesced scalars
+    const int T = q >> 8, g = (q >> 6) & 3, L = q & 31, hh = (q >> 5) & 1;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + q * 4) + *reinterpret_cast<const f32x4*>(RED + 16384 + q * 4);
+    const int c = 32 * (T >> 1) + 8 * g + 4 * hh, o = 32 * (T & 1) + L;
+    uint32_t vb[4];  // memcpy, not a bit_cast of v[k]: see as_s16x2
+    __builtin_memcpy(vb, &v, 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      __builtin_amdgcn_raw_buffer_store_b32(vb[k], srd, (P_W2 + (c + k) * OUT + o) * 4, 0, 16 /* sc1 */);
   }
   if (V4_STAMPS && tid == 0) {
     ts[3] = __builtin_amdgcn_s_memrealtime();

@@ -63,9 +63,10 @@ def main():
         r["boundary_us"] = r["step_us"] - r["train_us"] - r["adam_us"]
         print(json.dumps(r), flush=True)
         out.append(r)
-    b0, b1 = out[0], out[-1]
-    slope = (b1["train_us"] - b0["train_us"]) / ((b1["B"] - b0["B"]) / (1 << 20))
-    print(json.dumps({"train_us_per_M": slope, "train_fixed_us": b0["train_us"] - slope}))
+    if len(out) > 1:
+        b0, b1 = out[0], out[-1]
+        slope = (b1["train_us"] - b0["train_us"]) / ((b1["B"] - b0["B"]) / (1 << 20))
+        print(json.dumps({"train_us_per_M": slope, "train_fixed_us": b0["train_us"] - slope}))
 
 
 if __name__ == "__main__":
