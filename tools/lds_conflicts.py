@@ -132,5 +132,33 @@ def model(swz=swz_v4, label="v4"):
     print(f" total per tile (both roles): {tot[0]:.0f} LDS cycles vs conflict-free {tot[1]}")
 
 
+def v6_red_slot(T, g, L, h):  # csrc/mlp_fused.hip v6_red_slot (epilogue fold image, f32x4 slots)
+    sw = ((((T - 8) >> 1) & 1) << 3) | (g << 1) | h if T >= 8 else 0
+    return (T * 4 + g) * 64 + h * 32 + (L ^ sw)
+
+
+def v6_epilogue(slot=v6_red_slot):
+    """(modelled, conflict-free) LDS cycles of the v6 epilogue: the backward waves' f32x4 fold stores
+    and the slab writer's reads (W1 part: 16-lane groups at one feature, 16 (T, g, h) each)."""
+    tot = [0, 0]
+    for T in range(16):
+        for g in range(4):
+            c, m = cycles("write_b128", [slot(T, g, lane & 31, lane >> 5) * 16 for lane in range(64)])
+            tot[0] += c
+            tot[1] += m
+    for wave in range(2048 // 64):
+        addr = []
+        for lane in range(64):
+            e = wave * 64 + lane
+            f, c4 = e >> 5, (e & 31) * 4
+            addr.append(slot(8 + 2 * (c4 >> 5) + (f >> 5), (c4 & 31) >> 3, f & 31, (c4 >> 2) & 1) * 16)
+        c, m = cycles("read_b128", addr)
+        tot[0] += c
+        tot[1] += m
+    return tuple(tot)
+
+
 if __name__ == "__main__":
     model(swz_v4g, "v4_img (fr/gr swizzle; X image uses gr = 0)")
+    print("v6 epilogue (fold stores + slab-writer reads): %d LDS cycles vs conflict-free %d" % v6_epilogue())
+    print("  without the fold swizzle: %d vs %d" % v6_epilogue(lambda T, g, L, h: (T * 4 + g) * 64 + h * 32 + L))
