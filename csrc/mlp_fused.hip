@@ -1535,6 +1535,12 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
 #ifndef V6_XPRE
 #define V6_XPRE 0  // 1 (measured -3.7%): the forward wave builds its next tile's X fragments at the end of the current tile
 #endif
+#ifndef V6_SEG
+#define V6_SEG 0  // 1: forward waves share SIMDs with forward waves, backward with backward
+#endif
+#ifndef V6_NOFENCE
+#define V6_NOFENCE 0  // 1: ring counters raised with a compiler barrier only (LDS executes a wave's ops in order)
+#endif
 #ifndef V6_UNROLL
 #define V6_UNROLL 0  // 1: forward loop unrolled over the 3 ring slots (measured: more live addresses, spills)
 #endif
@@ -1568,6 +1574,19 @@ constexpr int V6_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below
 constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 2048);
 static_assert(V6_LDS <= 163840 && V6_RING % 16 == 0, "v6 LDS budget");
 constexpr int V6_SPIN_LIMIT = 1 << 20;  // ~50 ms of polling: a legitimate wait is microseconds
+
+// raise a ring counter.  V6_NOFENCE: the LDS pipeline executes one wave's operations in issue order,
+// so a flag store issued after the wave's data writes (or reads) lands after them and no
+// s_waitcnt lgkmcnt(0) is needed; the asm memory clobbers keep the compiler from moving LDS ops across it
+EM_DEVICE void v6_signal(char* smem, uint32_t off, int value) {
+  if (V6_NOFENCE) {
+    asm volatile("" ::: "memory");
+    __hip_atomic_store(reinterpret_cast<int*>(smem + off), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+  } else {
+    pair_signal(smem, off, value);
+  }
+}
 
 // wait until the LDS counter at off reaches target (skipped once a wait has failed: the launch then
 // drains quickly and reports NaN)
@@ -2000,7 +2019,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
         *reinterpret_cast<u32x2*>(smem + v4_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
             u32x2{fq[2], fq[3]};
       }
-    pair_signal(smem, FL + slot * 4, k + 1);  // FULL
+    v6_signal(smem, FL + slot * 4, k + 1);  // FULL
     if (V6_XPRE) xbuild(knext);  // the next tile's X fragments (its masks were fetched a tile ago)
     st.mark(4);
   };
@@ -2119,7 +2138,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(0);
     }
-    if (V6_BPRE) pair_signal(smem, MYDONE + slot * 4, k + 1);  // DONE: the release waits for every read above
+    if (V6_BPRE) v6_signal(smem, MYDONE + slot * 4, k + 1);  // DONE: the release waits for every read above
     st.mark(6);
 
     // B1: dH = dZ2·W2ᵀ for the own hidden half
@@ -2155,7 +2174,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int q = 0; q < 2; ++q) dz1[tt][q] = mask_by(hR[tt][q], aD[tt], q);
-    if (!V6_BPRE) pair_signal(smem, MYDONE + slot * 4, k + 1);
+    if (!V6_BPRE) v6_signal(smem, MYDONE + slot * 4, k + 1);
     st.mark(8);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -2274,7 +2293,9 @@ mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   uint64_t ts[4] = {};  // V4_STAMPS: 100 MHz wall-clock marks (entry, prologue done, loop done, dW folded)
   if (V4_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
   const int unit = wave >> 2, wl = wave & 3;
-  const int role = unit == 0 ? wl : (wl ^ 2);  // 0/1 forward f, 2/3 backward rho
+  // V6_SEG: both units use the same map, so SIMDs 0/1 host two forward waves and SIMDs 2/3 two backward
+  // waves (forward chains never share a matrix pipe with backward dW streams)
+  const int role = (unit == 0 || V6_SEG) ? wl : (wl ^ 2);  // 0/1 forward f, 2/3 backward rho
   float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
   if (V4_STAMPS) ts[1] = __builtin_amdgcn_s_memrealtime();
   if (role == 0)
