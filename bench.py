@@ -106,8 +106,9 @@ def _parse():
     ap.add_argument("--planted", type=float, default=0.9)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="replay the step from hipGraphs (needs a graph-safe step)")
-    ap.add_argument("--graph-steps", type=int, default=10,
-                    help="consecutive training steps captured per hipGraph (each a full fwd+bwd+Adam step)")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="consecutive training steps captured per hipGraph (each a full fwd+bwd+Adam step); "
+                         "0 = all timed steps up to 50 in one graph (one launch latency per chunk)")
     ap.add_argument("--warmup-ms", type=float, default=250.0,
                     help="after the W warmup steps, keep replaying untimed warmup steps until this much wall "
                          "time has passed (the chip ramps its clock over the first ~100 ms of load; a training "
@@ -295,7 +296,7 @@ def main():
         # launch per C steps, so the ~19 us launch gap between graph replays (rocprof kernel trace,
         # profiles/README.md) is paid once per chunk instead of once per step.  Steps that do not
         # fill a chunk replay a 1-step graph.
-        C = max(1, min(a.graph_steps, a.steps))
+        C = max(1, min(a.graph_steps if a.graph_steps > 0 else 50, a.steps))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
 

@@ -1541,6 +1541,9 @@ mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
 #ifndef V6_NOFENCE
 #define V6_NOFENCE 0  // 1: ring counters raised with a compiler barrier only (LDS executes a wave's ops in order)
 #endif
+#ifndef V6_F1P
+#define V6_F1P 1  // hidden tiles whose F1 accumulator chains are interleaved (1 or 2)
+#endif
 #ifndef V6_UNROLL
 #define V6_UNROLL 0  // 1: forward loop unrolled over the 3 ring slots (measured: more live addresses, spills)
 #endif
@@ -1927,7 +1930,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 
     // F1: Z1ᵀ = W1ᵀ·Xᵀ (two hidden tiles' chains interleaved) -> relu -> Hᵀ fragments + H images
     bf16x8 hT[4][2];
-    constexpr int F1P = V6_WREG ? 1 : 2;  // hidden tiles per F1 chain group (1 with register weights: VGPR budget)
+    constexpr int F1P = V6_F1P;  // hidden tiles per F1 chain group (interleaved accumulator chains)
 #pragma unroll
     for (int tp = 0; tp < 4 / F1P; ++tp) {
       f32x16 a1s[F1P];
