@@ -16,6 +16,6 @@ done
 python - <<'PY'
 import json
 for f in ['bench20_1','bench20_2','bench1000','dp2','dp4']:
-    d=json.load(open(f'gpurun_out/h/{f}.json'))
+    d=json.loads([l for l in open(f"gpurun_out/h/{f}.json") if l.startswith("{")][-1])
     print(f, round(d['value']/1e9,3), 'G/s', round(d['ms_per_step']*1e3,2), 'us/step', 'acc', d.get('val',{}).get('acc'), d['config'].get('grad_allreduce'))
 PY
