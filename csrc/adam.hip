@@ -73,6 +73,18 @@ EM_DEVICE void adam_end(int* state, int t) {
   }
 }
 
+// 1 - beta^t through the native v_log_f32 / v_exp_f32 (about 1 ulp each): powf's edge-case handling
+// was ~0.35 us of dependent latency per launch, on the critical path behind the step-counter load.
+EM_DEVICE float bias_correction(float beta, int t) {
+  return 1.f - __builtin_amdgcn_exp2f((float)t * __builtin_amdgcn_logf(beta));
+}
+
+// Step-counter modes (the `mode` argument's bit 2, EM_ADAM_PRE): without it every launch reads
+// state[0] + 1 and the last block to draw a ticket publishes it (adam_end); with it the producer
+// of this step's gradients already advanced state[0] (mlp_fused.hip advance_step), so the counter
+// is read as is and no ticket is drawn.
+constexpr int EM_ADAM_PRE = 4;
+
 // torch.optim.Adam update of parameter p with gradient g (pad slots of the MLP image pinned to 0).
 // w0/m0/v0 are params[p]/m[p]/v[p], loaded by the caller (the slab kernel issues those loads
 // before its slab reduction so their latency overlaps it).
@@ -80,7 +92,7 @@ EM_DEVICE void adam_apply_loaded(int p, float g, float w0, float m0, float v0, i
                                  float* __restrict__ m, float* __restrict__ v, const float* __restrict__ hp,
                                  uint8_t* __restrict__ mlp_img) {
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
-  const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
+  const float bc1 = bias_correction(b1, tstep), bc2 = bias_correction(b2, tstep);
   if (mlp_img && mlp_pad_slot(p)) {
     params[p] = 0.f;
     m[p] = 0.f;
@@ -113,8 +125,8 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
                  float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io, const float* __restrict__ hp,
                  int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img, const float* __restrict__ loss_slabs,
                  float* __restrict__ loss_out, float loss_scale, int* __restrict__ xg_hdr, float* __restrict__ xg_data,
-                 int xg_cap) {
-  const int tstep = (mode != 1) ? adam_begin(state) : 0;
+                 int xg_cap, int pre) {
+  const int tstep = (mode == 1) ? 0 : pre ? state[0] : adam_begin(state);
   if (xg_hdr) {  // mode 1 producer for the xGMI all-reduce: [grad | loss] into this rank's next slot
     grad_io = xg_produce_slot(xg_hdr, xg_data, xg_cap);
     loss_out = grad_io + P;
@@ -156,7 +168,7 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
     return;
   }
   if (ty == 0 && p < P) adam_apply(p, g, tstep, params, m, v, hp, mlp_img);
-  adam_end(state, tstep);
+  if (!pre) adam_end(state, tstep);
 }
 
 // Vectorised slab reduction (P % 64 == 0, stride % 4 == 0): 256 threads per 64 parameters, thread
@@ -169,12 +181,12 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
                   float* __restrict__ params, float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io,
                   const float* __restrict__ hp, int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img,
                   const float* __restrict__ loss_slabs, float* __restrict__ loss_out, float loss_scale,
-                  int* __restrict__ xg_hdr, float* __restrict__ xg_data, int xg_cap) {
+                  int* __restrict__ xg_hdr, float* __restrict__ xg_data, int xg_cap, int pre) {
   // the step counter: only wave 0 (the 64 Adam lanes) needs it.  A plain load suffices -- the previous
-  // step's kernel boundary published it, and this launch writes it only after every block's ticket --
-  // whereas 1024 waves issuing an agent-scope atomic load of one word serialise on one L2 channel.
+  // kernel boundary published it, and this launch writes it (ticket mode) only after every block's
+  // ticket -- whereas 1024 waves issuing an agent-scope atomic load of one word serialise on one L2 channel.
   int tstep = 0;
-  if (mode != 1 && threadIdx.x < 64) tstep = state[0] + 1;
+  if (mode != 1 && threadIdx.x < 64) tstep = state[0] + (pre ? 0 : 1);
   if (xg_hdr) {
     grad_io = xg_produce_slot(xg_hdr, xg_data, xg_cap);
     loss_out = grad_io + P;
@@ -217,7 +229,7 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
     if (mode == 1) grad_io[p] = gsum;
     else adam_apply_loaded(p, gsum, w0, m0, v0, tstep, params, m, v, hp, mlp_img);
   }
-  if (mode != 1) adam_end(state, tstep);
+  if (mode != 1 && !pre) adam_end(state, tstep);
 }
 
 // xGMI consumer (xgmi.h): g = sum over ranks of slot[s&1][p] (rank order), then the same Adam
@@ -226,16 +238,16 @@ constexpr int AX_B = 256;
 __global__ void __launch_bounds__(AX_B)
 adam_xgmi_kernel(XgmiDesc d, int P, float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
                  const float* __restrict__ hp, int* __restrict__ state, uint8_t* __restrict__ mlp_img,
-                 float* __restrict__ loss_out) {
+                 float* __restrict__ loss_out, int pre) {
   const int s = xg_next_seq(d.my_hdr);
-  const int tstep = adam_begin(state);
+  const int tstep = pre ? state[0] : adam_begin(state);
   if (xg_publish_and_wait(d, s)) {
     const int p = blockIdx.x * AX_B + threadIdx.x;
     if (p < P) adam_apply(p, xg_sum(d, s, p), tstep, params, m, v, hp, mlp_img);
     else if (p == P && loss_out) loss_out[0] = xg_sum(d, s, P);
   }
   xg_finish(d, s);
-  adam_end(state, tstep);
+  if (!pre) adam_end(state, tstep);
 }
 
 __global__ void mlp_pack_kernel(const float* __restrict__ params, uint8_t* __restrict__ img) {
@@ -263,7 +275,7 @@ adam_flat_kernel(float* __restrict__ params, const G* __restrict__ grad, float* 
                  float grad_scale, __bf16* __restrict__ shadow) {
   const int tstep = adam_begin(state);
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
-  const float bc1 = 1.f - powf(b1, (float)tstep), bc2 = 1.f - powf(b2, (float)tstep);
+  const float bc1 = bias_correction(b1, tstep), bc2 = bias_correction(b2, tstep);
   for (int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += (int64_t)gridDim.x * blockDim.x * 4) {
     if (i4 + 4 <= n) {
       f32x4 w = *reinterpret_cast<const f32x4*>(params + i4);
@@ -308,6 +320,9 @@ EM_API int em_adam_slab(const float* slabs, int nslab, int P, int stride, float 
                         float* grad_io, const float* hp, int* state, int mode, void* mlp_img, const float* loss_slabs,
                         float* loss_out, float loss_scale, void* xgmi, hipStream_t stream) {
   XgmiComm* xc = static_cast<XgmiComm*>(xgmi);
+  const int pre = (mode & EM_ADAM_PRE) ? 1 : 0;
+  mode &= ~EM_ADAM_PRE;
+  if (mode < 0 || mode > 2) return EM_ERR_ARG;
   if (xc && (mode != 1 || xc->desc.cap < P + 1)) return EM_ERR_ARG;
   if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0 || stride < P)) || (mode != 0 && !grad_io && !xc)) return EM_ERR_ARG;
   if (mode != 1 && (!params || !m || !v || !hp || !state)) return EM_ERR_ARG;
@@ -316,28 +331,29 @@ EM_API int em_adam_slab(const float* slabs, int nslab, int P, int stride, float 
   if (mode != 2 && P % 64 == 0 && stride % 4 == 0 && ((uintptr_t)slabs & 15) == 0) {
     hipLaunchKernelGGL(adam_slab4_kernel, dim3(P / 64), dim3(A4_T), 0, stream, slabs, nslab, P, stride, grad_scale,
                        params, m, v, grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale,
-                       xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0);
+                       xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0, pre);
     EM_CHECK_LAUNCH();
     return 0;
   }
   hipLaunchKernelGGL(adam_slab_kernel, dim3(nb), dim3(AS_P * AS_G), 0, stream, slabs, nslab, P, stride, grad_scale, params, m, v,
                      grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale,
-                     xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0);
+                     xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0, pre);
   EM_CHECK_LAUNCH();
   return 0;
 }
 
 // Adam step whose gradient is the xGMI all-reduce of every rank's slot (see xgmi.h);
-// loss_out (optional) receives the reduced element P.
+// loss_out (optional) receives the reduced element P; pre = the step counter was already advanced
+// by this step's train kernel (EM_ADAM_PRE).
 EM_API int em_adam_xgmi(void* xgmi, int P, float* params, float* m, float* v, const float* hp, int* state, void* mlp_img,
-                        float* loss_out, hipStream_t stream) {
+                        float* loss_out, int pre, hipStream_t stream) {
   XgmiComm* xc = static_cast<XgmiComm*>(xgmi);
   if (!xc || !xc->connected || P <= 0 || xc->desc.cap < P + 1 || !params || !m || !v || !hp || !state) return EM_ERR_ARG;
   if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
   const int nb = (P + 1 + AX_B - 1) / AX_B;
   if (nb > 256) return EM_ERR_ARG;  // consumer grid must stay co-resident (blocks spin on peer flags)
   hipLaunchKernelGGL(adam_xgmi_kernel, dim3(nb), dim3(AX_B), 0, stream, xc->desc, P, params, m, v, hp, state,
-                     (uint8_t*)mlp_img, loss_out);
+                     (uint8_t*)mlp_img, loss_out, pre ? 1 : 0);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -239,11 +239,20 @@ EM_DEVICE void mfma_acc_agpr(f32x16& d, bf16x8 a, bf16x8 b) {
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
 }
 
+// The optimizer's step counter (Adam bias correction, csrc/adam.hip) is advanced here, by one
+// thread, when the caller passes it: stream order puts this launch strictly between two Adam
+// launches, so Adam can read the counter with a plain load instead of drawing a grid-wide ticket
+// (252 same-address device-scope atomics = 2.8 us per step, tools/dev/adam_probe.py).
+EM_DEVICE void advance_step(int* step) {
+  if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] = step[0] + 1;
+}
+
 template <int LOSS>
 __global__ void __launch_bounds__(256, 1)
 mlp_fused_train_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                        int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
-                       float* __restrict__ loss_slabs) {
+                       float* __restrict__ loss_slabs, int* __restrict__ step) {
+  advance_step(step);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -951,7 +960,8 @@ template <int LOSS>
 __global__ void __launch_bounds__(512, 1)
 mlp_fused_train_v4_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
                           const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
-                          float* __restrict__ loss_slabs) {
+                          float* __restrict__ loss_slabs, int* __restrict__ step) {
+  advance_step(step);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1181,7 +1191,8 @@ template <int LOSS>
 __global__ void __launch_bounds__(512, 1)
 mlp_fused_train_v5_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
                           const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
-                          float* __restrict__ loss_slabs) {
+                          float* __restrict__ loss_slabs, int* __restrict__ step) {
+  advance_step(step);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2267,7 +2278,8 @@ template <int LOSS>
 __global__ void __launch_bounds__(512, 1)
 mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
                           const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
-                          float* __restrict__ loss_slabs) {
+                          float* __restrict__ loss_slabs, int* __restrict__ step) {
+  advance_step(step);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2447,7 +2459,7 @@ EM_API int em_mlp_fused_select_kernel(int version) {  // returns the previous ve
 // masks: [ndraws] uint64 feature masks; sample s = (masks[i], masks[i+1]) with i = sidx ? sidx[s] : offset+s
 EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset,
                               const void* wimg, float* slabs, float* loss_slabs, int nslab, int loss_kind,
-                              hipStream_t stream) {
+                              int* step, hipStream_t stream) {
   if (draws && !sidx && offset > 0) {  // sequential samples: 64-bit offsets (HBM-filling datasets) via the base
     draws += offset;
     offset = 0;
@@ -2485,23 +2497,23 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
   const uint8_t* w = (const uint8_t*)wimg;
   if (ver == 6) {
     if (loss_kind == 0)
-      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, grid, dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, grid, dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
     else
-      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, grid, dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, grid, dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
   } else if (ver == 5) {
     if (loss_kind == 0)
-      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<0>, grid, dim3(512), V5_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<0>, grid, dim3(512), V5_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
     else
-      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<1>, grid, dim3(512), V5_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v5_kernel<1>, grid, dim3(512), V5_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
   } else if (ver == 4) {
     if (loss_kind == 0)
-      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<0>, grid, dim3(512), V4_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<0>, grid, dim3(512), V4_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
     else
-      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<1>, grid, dim3(512), V4_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+      hipLaunchKernelGGL(mlp_fused_train_v4_kernel<1>, grid, dim3(512), V4_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
   } else if (loss_kind == 0) {
-    hipLaunchKernelGGL(mlp_fused_train_kernel<0>, grid, dim3(256), TRAIN_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+    hipLaunchKernelGGL(mlp_fused_train_kernel<0>, grid, dim3(256), TRAIN_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
   } else {
-    hipLaunchKernelGGL(mlp_fused_train_kernel<1>, grid, dim3(256), TRAIN_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs);
+    hipLaunchKernelGGL(mlp_fused_train_kernel<1>, grid, dim3(256), TRAIN_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
   }
   EM_CHECK_LAUNCH();
   return 0;

@@ -161,8 +161,10 @@ class FusedSmallMLP:
         """One optimizer step over B local samples (``draws`` = feature masks from :meth:`prepare`);
         returns the (global) mean loss as a device tensor."""
         FM = self.FM
+        # the train kernel advances the Adam step counter (one store), so no Adam launch below draws a
+        # grid-wide ticket for it (pre=True)
         nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
-                                  offset=offset, sidx=sidx, check=not self._checked)
+                                  offset=offset, sidx=sidx, check=not self._checked, step=self.state)
         self._checked = True
         gb = global_batch if global_batch is not None else B * self.world
         scale = 1.0 / max(gb, 1)
@@ -171,13 +173,13 @@ class FusedSmallMLP:
         lscale = 1.0 / max(gb, 1) / (62.0 if self.loss_name == "bce" else 1.0)
         if self.group is None:
             FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=0,
-                         img=self.img, loss_slabs=self.loss_slabs, loss_out=self.loss_out, loss_scale=lscale)
+                         img=self.img, loss_slabs=self.loss_slabs, loss_out=self.loss_out, loss_scale=lscale, pre=True)
             return self.loss_out
         if self.xgmi is not None:  # producer -> own xGMI slot; consumer = all-reduce + Adam, no host sync
             FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=1,
                          loss_slabs=self.loss_slabs, loss_scale=lscale, xgmi=self.xgmi.handle)
             FM.adam_xgmi(self.xgmi.handle, self.params, self.m, self.v, self.hp, self.state, img=self.img,
-                         loss_out=self.loss_out)
+                         loss_out=self.loss_out, pre=True)
             return self.loss_out
         import torch.distributed as dist
 
@@ -186,7 +188,7 @@ class FusedSmallMLP:
                      grad_io=self.grad_io, loss_slabs=self.loss_slabs, loss_out=loss_view, loss_scale=lscale)
         dist.all_reduce(self.grad_io, op=dist.ReduceOp.SUM, group=self.group)
         FM.adam_slab(None, 0, 1.0, self.params, self.m, self.v, self.hp, self.state, mode=2, grad_io=self.grad_io,
-                     img=self.img)
+                     img=self.img, pre=True)
         return loss_view
 
     @property

@@ -36,7 +36,8 @@ _SIGS = {
     "em_mlp_fused_param_count": (_i32, []),
     "em_mlp_fused_image_bytes": (_i32, []),
     "em_mlp_fused_lds_bytes": (_i32, []),
-    "em_mlp_fused_train": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p]),
+    "em_mlp_fused_train": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p,
+                                   _c_void_p]),
     "em_mlp_fused_select_kernel": (_i32, [_i32]),
     "em_mlp_fused_forward": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i32, _c_void_p]),
     "em_mlp_fused_pack": (_i32, [_c_void_p, _c_void_p, _c_void_p]),

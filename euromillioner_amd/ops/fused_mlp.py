@@ -119,10 +119,15 @@ def select_kernel(version: int) -> int:
     return int(N.query("em_mlp_fused_select_kernel", int(version)))
 
 
+ADAM_PRE = 4  # em_adam_slab mode bit: step counter already advanced by the train kernel (csrc/adam.hip)
+
+
 def train_partials(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.Tensor, loss_slabs: torch.Tensor,
                    loss: str = "softmax", offset: int = 0, sidx: torch.Tensor | None = None,
-                   check: bool = True) -> int:
-    """Launch K7: per-workgroup gradient slabs for B samples.  Returns the grid size used."""
+                   check: bool = True, step: torch.Tensor | None = None) -> int:
+    """Launch K7: per-workgroup gradient slabs for B samples.  Returns the grid size used.
+    ``step`` (the optimizer's int32 state) is advanced by one in the same launch; the Adam launch
+    that consumes these slabs must then pass ``pre=True``."""
     if check:
         _check_draws(draws, sidx, B, offset)
         N.check_cuda(img, "img", torch.uint8)
@@ -134,7 +139,7 @@ def train_partials(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.
     nslab = max(1, min(slabs.shape[0], groups))
     N.call("em_mlp_fused_train", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
            img.data_ptr(), slabs.data_ptr(), loss_slabs.data_ptr(), nslab, LOSS_KINDS[loss],
-           N.stream_handle(draws.device))
+           step.data_ptr() if step is not None else None, N.stream_handle(draws.device))
     return nslab
 
 
@@ -155,28 +160,32 @@ def forward_logits(draws: torch.Tensor, B: int, img: torch.Tensor, out: torch.Te
 def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params: torch.Tensor, m: torch.Tensor,
               v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor, mode: int = 0, grad_io: torch.Tensor | None = None,
               img: torch.Tensor | None = None, loss_slabs: torch.Tensor | None = None,
-              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0, xgmi: int | None = None) -> None:
+              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0, xgmi: int | None = None,
+              pre: bool = False) -> None:
     """mode 0: slab reduce + Adam; mode 1: slab reduce -> grad_io (or, with ``xgmi``, this rank's
-    next xGMI slot); mode 2: Adam from grad_io."""
+    next xGMI slot); mode 2: Adam from grad_io.  ``pre``: the step counter ``state[0]`` was already
+    advanced for this step (train_partials(step=state)), so no grid-wide ticket is drawn."""
     P = params.numel()
     stride = slabs.shape[1] if slabs is not None else P
     N.call("em_adam_slab", slabs.data_ptr() if slabs is not None else None, int(nslab), int(P), int(stride),
            float(grad_scale),
            params.data_ptr(), m.data_ptr(), v.data_ptr(), grad_io.data_ptr() if grad_io is not None else None,
-           hp.data_ptr(), state.data_ptr(), int(mode), img.data_ptr() if img is not None else None,
+           hp.data_ptr(), state.data_ptr(), int(mode) | (ADAM_PRE if pre else 0),
+           img.data_ptr() if img is not None else None,
            loss_slabs.data_ptr() if loss_slabs is not None else None,
            loss_out.data_ptr() if loss_out is not None else None, float(loss_scale), xgmi,
            N.stream_handle(params.device))
 
 
 def adam_xgmi(xgmi: int, params: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor,
-              state: torch.Tensor, img: torch.Tensor | None = None, loss_out: torch.Tensor | None = None) -> None:
+              state: torch.Tensor, img: torch.Tensor | None = None, loss_out: torch.Tensor | None = None,
+              pre: bool = False) -> None:
     """Adam step on the xGMI all-reduce (rank-order sum) of every rank's staged [grad | loss]."""
     from ..parallel import xgmi as _xg  # noqa: F401  (registers the em_xgmi_* signatures)
 
     N.call("em_adam_xgmi", xgmi, params.numel(), params.data_ptr(), m.data_ptr(), v.data_ptr(), hp.data_ptr(),
            state.data_ptr(), img.data_ptr() if img is not None else None,
-           loss_out.data_ptr() if loss_out is not None else None, N.stream_handle(params.device))
+           loss_out.data_ptr() if loss_out is not None else None, int(pre), N.stream_handle(params.device))
 
 
 def cast_bf16(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:

@@ -40,7 +40,7 @@ N.register_signatures({
     "em_xgmi_destroy": (ctypes.c_int, [_v]),
     "em_xgmi_stage": (ctypes.c_int, [_v, _v, ctypes.c_int, _v]),
     "em_xgmi_reduce": (ctypes.c_int, [_v, _v, ctypes.c_int, ctypes.c_float, _v]),
-    "em_adam_xgmi": (ctypes.c_int, [_v, ctypes.c_int, _v, _v, _v, _v, _v, _v, _v, _v]),
+    "em_adam_xgmi": (ctypes.c_int, [_v, ctypes.c_int, _v, _v, _v, _v, _v, _v, _v, ctypes.c_int, _v]),
 })
 
 MAX_WORLD = 8  # one node (XG_MAXW in xgmi.h)

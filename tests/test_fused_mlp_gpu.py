@@ -100,6 +100,27 @@ def test_fused_adam_matches_torch(data):
     assert torch.allclose(m.params, p_ref.detach(), atol=1e-6, rtol=1e-5)
 
 
+def test_step_counter_advanced_by_train_kernel(data, kernel):
+    """FusedSmallMLP.step: the train kernel advances the Adam step counter and Adam reads it without
+    a ticket (pre mode).  Must equal the ticket path (gradient via mode 1, Adam via mode 2) bit for bit."""
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    _, draws = data
+    a = FusedSmallMLP(loss="softmax", seed=4, lr=3e-3)
+    b = FusedSmallMLP(loss="softmax", seed=4, lr=3e-3)
+    B = 2048
+    for it in range(4):
+        a.step(draws, B, offset=37 * it)
+        b.grads(draws, B, offset=37 * it)  # no counter advance
+        FM.adam_slab(None, 0, 1.0, b.params, b.m, b.v, b.hp, b.state, mode=2, grad_io=b.grad_io, img=b.img)
+    torch.cuda.synchronize()
+    assert int(a.state[0]) == 4 and int(b.state[0]) == 4
+    assert int(a.state[1]) == 0 and int(b.state[1]) == 0
+    assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+    assert torch.equal(a.img, b.img)
+
+
 def test_fused_training_learns_planted_structure():
     from euromillioner_amd.models.mlp import FusedSmallMLP
 

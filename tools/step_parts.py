@@ -50,12 +50,12 @@ def main():
         nslab = FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
         lscale = 1.0 / B
 
-        def train():
-            FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
+        def train():  # as FusedSmallMLP.step runs it: the train kernel advances the Adam step counter
+            FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax", step=m.state)
 
         def adam():
             FM.adam_slab(m.slabs, nslab, 1.0 / B, m.params, m.m, m.v, m.hp, m.state, mode=0, img=m.img,
-                         loss_slabs=m.loss_slabs, loss_out=m.loss_out, loss_scale=lscale)
+                         loss_slabs=m.loss_slabs, loss_out=m.loss_out, loss_scale=lscale, pre=True)
 
         def step():
             m.step(draws, B, offset=0)
