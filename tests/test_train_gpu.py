@@ -92,6 +92,49 @@ def test_dp_code_path_on_one_rank_matches_local(engine):
     assert torch.allclose(dp.params, local.params, atol=1e-6, rtol=0), float((dp.params - local.params).abs().max())
 
 
+def test_rccl_step_replays_from_a_hipgraph():
+    """The fused model's RCCL fallback (slab reduce -> RCCL all-reduce -> Adam) is graph-safe: steps
+    captured in one hipGraph and replayed equal the same steps run eagerly on a local model."""
+    import torch
+
+    from euromillioner_amd.data.draws import DrawSet
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds = DrawSet.synthetic(n=9000, seed=5, planted=0.7, calendar=False)
+    masks = FusedSmallMLP.prepare(torch.from_numpy(ds.numbers).cuda())
+    dist = _nccl_world1()
+    try:
+        dp = FusedSmallMLP("cuda", seed=1, lr=3e-3, process_group=dist.group.WORLD, comm="rccl")
+        assert dp.comm == "rccl" and dp.graph_safe
+        dp.broadcast_parameters()
+        dp.step(masks, 2048, offset=0)  # first step eager (argument checks)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for k in range(1, 3):
+                    loss = dp.step(masks, 2048, offset=1000 * k)
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()  # steps 1, 2
+        torch.cuda.synchronize()
+        mid = dp.params.clone()
+        g.replay()  # steps 1, 2 again (same offsets) on the updated parameters
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert torch.isfinite(loss).all()
+    ref = FusedSmallMLP("cuda", seed=1, lr=3e-3)
+    for k in (0, 1, 2):
+        ref.step(masks, 2048, offset=1000 * k)
+    assert torch.allclose(mid, ref.params, atol=1e-6, rtol=0), float((mid - ref.params).abs().max())
+    for k in (1, 2):
+        ref.step(masks, 2048, offset=1000 * k)
+    assert torch.allclose(dp.params, ref.params, atol=1e-6, rtol=0), float((dp.params - ref.params).abs().max())
+    assert not torch.equal(mid, dp.params)
+
+
 def test_parameter_averaging_runs_on_the_gemm_engine():
     from euromillioner_amd.train import train
 
