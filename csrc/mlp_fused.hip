@@ -1618,6 +1618,18 @@ EM_DEVICE void v6_wait(const char* smem, uint32_t off, int target, bool& ok) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// stream index U of a unit (tiles U, U + nunits, ...).  V6_TMAP 1: blocks are numbered XCD-major
+// (block b runs on XCD b % 8), so the 32 blocks of one XCD own 64 consecutive streams and each XCD
+// reads one contiguous 16 KB run of masks per round instead of 512-B pieces 4 KB apart
+#ifndef V6_TMAP
+#define V6_TMAP 0
+#endif
+EM_DEVICE int v6_unit_id(int unit) {
+  int b = blockIdx.x;
+  if (V6_TMAP && (gridDim.x & 7) == 0) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);
+  return b * 2 + unit;
+}
+
 EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
   const int ntiles = (B + 31) / 32;
   return U < ntiles ? (ntiles - U + nunits - 1) / nunits : 0;
@@ -1870,7 +1882,7 @@ template <int LOSS, int F>
 EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                           int offset, int unit, int lane, float& loss_acc, bool& ok, V4Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
-  const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
+  const int nunits = gridDim.x * 2, U = v6_unit_id(unit);
   const int K = v6_ntiles_of_unit(B, U, nunits);
   const uint32_t FL = V6_FLAGS + unit * 64;
   auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {
@@ -2086,7 +2098,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[
                            f32x16& db2, float& loss_acc, bool& ok, V4Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
-  const int nunits = gridDim.x * 2, U = blockIdx.x * 2 + unit;
+  const int nunits = gridDim.x * 2, U = v6_unit_id(unit);
   const int K = v6_ntiles_of_unit(B, U, nunits);
   const uint32_t FL = V6_FLAGS + unit * 64;
   const uint32_t MYDONE = FL + ((1 + RHO) * V6_NSLOT) * 4;
