@@ -59,7 +59,9 @@ def mega_lines() -> list[str]:
         if not os.path.exists(path):
             continue
         j = [json.loads(x) for x in open(path) if x.strip()][-1]
-        g = j.get("device_datagen", {})
+        g = dict(j.get("device_datagen") or j.get("datagen") or {})
+        if "gib" not in g and g.get("draws"):
+            g["gib"] = g["draws"] * 8 / 2 ** 30
         rate = f"**{j['value'] / 1e9:.2f} G samples/s**" if j["value"] > 1e8 else f"**{j['value'] / 1e6:.2f} M samples/s**"
         if "tflops_per_gpu" in j:
             rate += f" ({j['tflops_per_gpu']:.0f} TFLOP/s)"
@@ -84,7 +86,7 @@ def main():
                 f.write(json.dumps(j) + "\n")
     f1 = pmc("fused_pmc", "mlp_fused_train")
     f2 = pmc("fused_pmc2", "mlp_fused_train")
-    w = pmc("wide_pmc", "gemm256_pp16_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_pp_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_nt_kernel<1, 1, 0, 0>")
+    w = pmc("wide_pmc", "gemm256_pp16_kernel<1, 1, 0, 0") or pmc("wide_pmc", "gemm256_pp_kernel<1, 1, 0, 0>") or pmc("wide_pmc", "gemm256_nt_kernel<1, 1, 0, 0>")
     wcyc = w.get("GRBM_GUI_ACTIVE", 0) / 8.0
     w_busy = w.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(1.0, 1024 * wcyc) if wcyc else float("nan")
     head = last_json("bench_headline.log")[-1]
@@ -110,8 +112,8 @@ def main():
         "",
         "| counter | value | reading |",
         "|---|---|---|",
-        f"| SQ_WAVES | {waves:.0f} | 8 waves (4 hidden-split pairs) x 256 CUs |",
-        f"| SQ_INSTS_MFMA / wave | {f1.get('SQ_INSTS_MFMA', 0) / waves:.0f} | 40 per 32-sample tile per wave |",
+        f"| SQ_WAVES | {waves:.0f} | 8 waves (2 units: 2 forward + 2 backward waves) x 256 CUs |",
+        f"| SQ_INSTS_MFMA / wave | {f1.get('SQ_INSTS_MFMA', 0) / waves:.0f} | 32 per tile per forward wave, 26 per tile per backward wave |",
         f"| SQ_INSTS_VALU / wave | {f1.get('SQ_INSTS_VALU', 0) / waves:.0f} | |",
         f"| SQ_WAIT_ANY / SQ_WAVE_CYCLES | {f1.get('SQ_WAIT_ANY', 0) / max(1, f1.get('SQ_WAVE_CYCLES', 1)):.2f} | latency-bound share |",
         f"| SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES | {f1.get('SQ_ACTIVE_INST_VALU', 0) / max(1, f1.get('SQ_WAVE_CYCLES', 1)):.2f} | |",
