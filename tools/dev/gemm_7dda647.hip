@@ -237,12 +237,6 @@ EM_DEVICE uint32_t g_off(int row, int chunk) { return row * 128 + ((chunk ^ ((ro
 // C^T output 4 is best (65536x8192x8192 forward 1353 / 1384 / 1413 / 1366, NT dgrad 1270 / 1311 /
 // 1341 / 1324); with C^T 8 is (forward+C^T 1256 / 1287 / 1314 / 1329).  EM_GEMM_GM overrides both.
 __constant__ int g_gm_c = 0;
-__constant__ int g_lead_c = 0;  // pp16 staging lead (0 or 2 slots) of G_LEAD=-1 builds; EM_GEMM_LEAD sets it
-// The lead is a compile-time constant: read at run time from g_lead_c (G_LEAD -1, the EM_GEMM_LEAD A/B
-// mode) it cost ~15 % of the kernel (fwd 1375 -> 1180 TF/s on one box, profiles/gemm_box_variance.md)
-#ifndef G_LEAD
-#define G_LEAD 0
-#endif
 
 template <int HAS_CT>
 EM_DEVICE void g_tile(int bid, int tiles_m, int tiles_n, int& m0, int& n0) {
@@ -717,28 +711,6 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
   }
 }
 
-// Diagnostic segment timers for the pp16 kernel (diagnostic build only: --define G_STAMPS=1; read
-// with em_gemm_stamps / tools/gemm_stamps.py).  Per wave, s_memtime deltas summed over the main loop:
-// [0] load segment: fragment reads + LDS-DMA issue (the stamp's lgkmcnt(0) also drains the reads)
-// [1] load segment: counted vmcnt wait  [2] load segment: closing barrier
-// [3] MFMA segment: lgkmcnt wait  [4] MFMA issue  [5] MFMA segment: closing barrier
-// [6] prologue (kernel start -> loop)  [7] epilogue (loop end -> kernel end)
-#ifndef G_STAMPS
-#define G_STAMPS 0
-#endif
-constexpr int G_STAMP_BLOCKS = 4096;
-#if G_STAMPS
-__device__ uint64_t g_gstamps[G_STAMP_BLOCKS * 8 * 8];
-#define G_MARK(t)                                                                 \
-  do {                                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                            \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");   \
-    __builtin_amdgcn_sched_barrier(0);                                            \
-  } while (0)
-#else
-#define G_MARK(t) (void)0
-#endif
-
 // BAL = 1 spreads the fragment reads evenly over the four load segments of a K-tile (at most 8
 // ds_read_b128 per wave instead of 12, 8, 4, 0): phase 3's segment reads the NEXT K-tile's A(qm 0)
 // half into fa[0] (free during phase 3, which runs on fa[1] x B(qn 1)), so phase 0 reads only
@@ -754,12 +726,6 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
                     const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
                     float beta) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint64_t st_acc[8] = {}, st_t0 = 0, st_a = 0, st_b = 0;
-  (void)st_acc;
-  (void)st_t0;
-  (void)st_a;
-  (void)st_b;
-  G_MARK(st_t0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_n = N / G_BN;
@@ -782,35 +748,14 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
   g_stage(pa, 0, smem, wave_s);
   g_stage(pb, 0, smem + G_TILE, wave_s);
-  // LEAD (g_lead_c = 2): every unit is issued 2 slots earlier than its scheduled slot and waited
-  // with vmcnt(8) instead of vmcnt(6), so it has 8 slots instead of 6 to land while the slot in
-  // which it becomes readable is unchanged (RAW as above); a restage comes 2 slots closer to the
-  // last read of the unit it overwrites, which still leaves >= 2 slots (B lo: restaged exactly 2
-  // slots after its last read).  The prologue then also issues the units of slots -1 (G0) and 0 (G1).
-  const bool lead = G_LEAD < 0 ? g_lead_c != 0 : G_LEAD != 0;
   if (g1) {
     const bool a = pp_stage_slot(pa, pb, smem, -4, ktiles, wi);
     const bool b = pp_stage_slot(pa, pb, smem, -2, ktiles, wi);
-    if (lead) {
-      const bool c = pp_stage_slot(pa, pb, smem, 0, ktiles, wi);
-      if (a && b && c) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (a && b) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    const bool a = pp_stage_slot(pa, pb, smem, -3, ktiles, wi);
-    if (lead) {
-      const bool b = pp_stage_slot(pa, pb, smem, -1, ktiles, wi);
-      if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (a) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (pp_stage_slot(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
 
@@ -844,38 +789,12 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
                 *reinterpret_cast<const bf16x8*>(lsrc + g_off(wm * 128 + (qa ^ (q == 3)) * 64 + 16 * ii + r16, 4 * ks + c4));
       }
     }
-    const bool staged = pp_stage_slot(pa, pb, smem, lead ? slot + 2 : slot, ktiles, wi);
-    if (G_STAMPS) {
-      uint64_t t;
-      G_MARK(t);
-      st_acc[0] += t - st_a;
-      st_a = t;
-    }
-    if (!staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (lead) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    if (G_STAMPS) {
-      uint64_t t;
-      G_MARK(t);
-      st_acc[1] += t - st_a;
-      st_a = t;
-    }
+    if (pp_stage_slot(pa, pb, smem, slot, ktiles, wi)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (G_STAMPS) {
-      uint64_t t;
-      G_MARK(t);
-      st_acc[2] += t - st_a;
-      st_a = t;
-    }
   };
   auto mfma_seg = [&](int q) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (G_STAMPS) {
-      uint64_t t;
-      G_MARK(t);
-      st_acc[3] += t - st_a;
-      st_a = t;
-    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -887,24 +806,8 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
           c = mfma16(fa[q & 1][ii][ks], fb[jj][ks], c);
         }
     __builtin_amdgcn_s_setprio(0);
-    if (G_STAMPS) {
-      uint64_t t;
-      G_MARK(t);
-      st_acc[4] += t - st_a;
-      st_a = t;
-    }
     __builtin_amdgcn_s_barrier();
-    if (G_STAMPS) {
-      uint64_t t;
-      G_MARK(t);
-      st_acc[5] += t - st_a;
-      st_a = t;
-    }
   };
-  if (G_STAMPS) {
-    G_MARK(st_a);
-    st_acc[6] = st_a - st_t0;
-  }
 
   if (!g1) {
     load_seg(0, -1);
@@ -929,19 +832,8 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (G_STAMPS) G_MARK(st_b);
   g_epilogue16<OUT_BF16, FN, DACT, HAS_CT, 4>(acc, 0, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, C, ldc, CT,
                                               ldct, bias, mask, ldm, alpha, beta);
-#if G_STAMPS
-  {
-    uint64_t t;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    G_MARK(t);
-    st_acc[7] = t - st_b;
-    if (lane == 0 && blockIdx.x < G_STAMP_BLOCKS)
-      for (int k = 0; k < 8; ++k) g_gstamps[((size_t)blockIdx.x * 8 + wave) * 8 + k] = st_acc[k];
-  }
-#endif
 }
 
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
@@ -961,11 +853,6 @@ int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf
     if (gm_env) {
       const int gm = atoi(gm_env);
       if (gm >= 1 && gm <= 64) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gm_c), &gm, sizeof(int));
-    }
-    static const char* lead_env = getenv("EM_GEMM_LEAD");
-    if (lead_env) {
-      const int ld = atoi(lead_env) ? 1 : 0;
-      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lead_c), &ld, sizeof(int));
     }
     (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 1>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
@@ -1281,8 +1168,7 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
     attr = true;
   }
   const bool big = splits == 1 && a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
-                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL") &&
-                   (c_bf16 || (act == ACT_NONE && !mask));  // fp32 + act / act' epilogues: any-layout kernel
+                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL");
   if (big) {
     const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
                               ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
@@ -1373,19 +1259,4 @@ EM_API int em_wgrad_skinny(const void* P, int64_t ldp, const void* Q, int64_t ld
                      J, W, C, ldc, trans, alpha, beta);
   EM_CHECK_LAUNCH();
   return 0;
-}
-
-// Segment timers of the last pp16 launches (diagnostic build, G_STAMPS=1): u64 [G_STAMP_BLOCKS][8 waves][8]
-EM_API int em_gemm_stamps(void* host_out, int64_t bytes) {
-#if G_STAMPS
-  const int64_t have = (int64_t)sizeof(uint64_t) * G_STAMP_BLOCKS * 8 * 8;
-  if (!host_out || bytes <= 0) return EM_ERR_ARG;
-  const hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_gstamps), bytes < have ? bytes : have, 0,
-                                           hipMemcpyDeviceToHost);
-  return e == hipSuccess ? 0 : (int)e;
-#else
-  (void)host_out;
-  (void)bytes;
-  return EM_ERR_ARG;  // not a G_STAMPS build
-#endif
 }

@@ -1,4 +1,4 @@
-# pp16 staging lead A/B: race screen + numerics with EM_GEMM_LEAD=1, then alternating bench rounds
+# pp16 staging lead A/B (needs a --define G_LEAD=-1 build): race screen + numerics with EM_GEMM_LEAD=1, then alternating bench rounds
 set -o pipefail
 mkdir -p gpurun_out/glead
 export TMPDIR=/tmp
