@@ -223,7 +223,10 @@ __global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32
 // K8: (blocks x nodes x trees) workgroups; block b of a node sums its slice of the node's row list
 // into LDS (integer atomics on set bits only: y bits for S, candidate x bits for cnt/hist), then
 // merges into the node record (plain stores when one block owns the node, else global atomics).
-template <bool REC>
+// DERIVE (levels >= 1): the node totals S / n are not accumulated here -- rf_child_totals already
+// wrote them from the parent's record (right child = the parent's histogram of its split feature,
+// left = parent - right, exact integers), so a row costs its candidate bits' atomics only.
+template <bool REC, bool DERIVE>
 __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restrict__ rows_v, int level,
                                                  const int32_t* __restrict__ wl) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -276,11 +279,13 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restr
       w = packed ? (uint32_t)e >> RF_WSHIFT : (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
       y = p.Y[r] & RF_M62;
     }
-    my_n += w;
-    uint64_t yy = y;
-    while (yy) {
-      atomicAdd(&S[__builtin_ctzll(yy)], w);
-      yy &= yy - 1;
+    if (!DERIVE) {
+      my_n += w;
+      uint64_t yy = y;
+      while (yy) {
+        atomicAdd(&S[__builtin_ctzll(yy)], w);
+        yy &= yy - 1;
+      }
     }
     if (!split) continue;
     for (int wd = 0; wd < p.W; ++wd) {
@@ -297,17 +302,38 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restr
       }
     }
   }
-  for (int o = 32; o > 0; o >>= 1) my_n += __shfl_xor(my_n, o);
-  if ((threadIdx.x & 63) == 0) atomicAdd(nn, my_n);
+  if (!DERIVE) {
+    for (int o = 32; o > 0; o >>= 1) my_n += __shfl_xor(my_n, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(nn, my_n);
+  }
   __syncthreads();
   uint32_t* dst = p.acc + ((int64_t)t * nodesL + nd) * rec;
   const int used = split ? rec : 68;
+  const int lo = DERIVE ? 68 : 0;  // S / n (words 0..67) already hold the derived totals
   if (B == 1) {
-    for (int i = threadIdx.x; i < used; i += blockDim.x) dst[i] = lds[i];
+    for (int i = lo + threadIdx.x; i < used; i += blockDim.x) dst[i] = lds[i];
   } else {
-    for (int i = threadIdx.x; i < used; i += blockDim.x)
+    for (int i = lo + threadIdx.x; i < used; i += blockDim.x)
       if (lds[i]) atomicAdd(&dst[i], lds[i]);
   }
+}
+
+// Level >= 1 node totals from the parent's record (DERIVE histograms): the parent's rf_split left the
+// winning candidate slot c in its record word 65; node index 2i+1 (even nd) is the x_f = 0 child.
+// One wavefront per (tree, node); lane j < 64 writes S[j], lane 0 also n.
+__global__ void __launch_bounds__(64) rf_child_totals(RfParams p, const uint32_t* __restrict__ prev, int level) {
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int t = blockIdx.y, nd = blockIdx.x, node = first + nd;
+  const int lane = threadIdx.x;
+  if (p.seg[((int64_t)t * p.nodes + node) * 2 + 1] < 0) return;  // under an unsplit parent: no record
+  const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
+  const uint32_t* P = prev + ((int64_t)t * (nodesL >> 1) + (nd >> 1)) * rec;
+  const int c = (int)P[65];
+  const bool right = nd & 1;
+  const uint32_t sr = P[68 + kp + c * 64 + lane], nr = P[68 + c];
+  uint32_t* dst = p.acc + ((int64_t)t * nodesL + nd) * rec;
+  dst[lane] = right ? sr : P[lane] - sr;
+  if (lane == 0) dst[64] = right ? nr : P[64] - nr;
 }
 
 // K8 on the matrix cores (binary features, W == 1, k <= 15 candidates): the node histogram is one
@@ -443,7 +469,7 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
     return;
   }
   const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
-  const uint32_t* A = p.acc + ((int64_t)t * nodesL + nd) * rec;
+  uint32_t* A = p.acc + ((int64_t)t * nodesL + nd) * rec;
   const uint32_t n = A[64];
   const uint32_t Sj = lane < 62 ? A[lane] : 0u;
   float* vo = p.value + ((int64_t)t * p.nodes + node) * 64;
@@ -451,7 +477,7 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
   if (lane == 0) p.cover[(int64_t)t * p.nodes + node] = (float)n;
   const bool can_split = level < p.max_depth && n >= (uint32_t)(2 * p.min_leaf) && n > 0;
   double best = 0.0;
-  int bf = -1;
+  int bf = -1, bc = -1;
   if (can_split) {
     uint64_t s2 = (uint64_t)Sj * Sj;
     for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
@@ -472,6 +498,7 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
       if (g > best || (g == best && bf >= 0 && f < bf)) {
         best = g;
         bf = f;
+        bc = c;
       }
     }
     // a split must reduce impurity by more than rounding noise
@@ -480,6 +507,7 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
   if (lane == 0) {
     *fo = (int16_t)bf;
     p.gain[(int64_t)t * p.nodes + node] = bf >= 0 ? best : 0.0;
+    A[65] = bf >= 0 ? (uint32_t)bc : 0u;  // candidate slot of the split (rf_child_totals)
   }
 }
 
@@ -625,7 +653,7 @@ static void rf_shape(int64_t N, int level, int& B, int& nt) {
 
 EM_API int64_t em_rf_acc_words(int T, int max_depth, int k_feat) {
   if (T < 1 || max_depth < 0 || max_depth > 14 || k_feat < 1 || k_feat > RF_MAXF) return -1;
-  return (int64_t)T * (1ll << max_depth) * rec_words(k_feat);
+  return 2 * (int64_t)T * (1ll << max_depth) * rec_words(k_feat);  // two levels' records (rf_child_totals)
 }
 
 // Native level-wise driver: all T trees advance one level per (prep, hist, split, partition) round.
@@ -644,11 +672,15 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const size_t lds = (size_t)rec * 4;
   if (lds > 160 * 1024 - 8192) return EM_ERR_ARG;
   static bool attr = false;
-  static int mfma_env = -1;
+  static int mfma_env = -1, derive_env = 1;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)rf_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)rf_hist<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
-    (void)hipFuncSetAttribute((const void*)rf_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)rf_hist<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 8192);
+    (void)hipFuncSetAttribute((const void*)rf_hist<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 8192);
+    (void)hipFuncSetAttribute((const void*)rf_hist<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
     (void)hipFuncSetAttribute((const void*)rf_hist_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
@@ -657,6 +689,8 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     // operands bit by bit, not in the MFMAs
     const char* e = std::getenv("EM_RF_MFMA");
     mfma_env = (e && e[0] == '1') ? 1 : 0;
+    const char* d = std::getenv("EM_RF_DERIVE");  // 0: accumulate node totals at every level (A/B)
+    derive_env = (d && d[0] == '0') ? 0 : 1;
     attr = true;
   }
   // record-form row lists for one-word features (rows_a/rows_b hold 16 B per row: em_rf_row_bytes);
@@ -665,8 +699,10 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const bool rec_rows = em_rf_row_bytes(W, F, N) == 16;
   const bool use_mfma = rec_rows && mfma_env && k_feat <= 15;
   const size_t lds_mfma = (size_t)(((rec + 3) & ~3) * 4) + 4096 + 4 * 1024;
+  uint32_t* accs[2] = {acc, acc + (int64_t)T * (1ll << max_depth) * rec};
+  const bool derive = derive_env && !use_mfma;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
-             cover, cand, acc, lrc};
+             cover, cand, accs[0], lrc};
   (void)hipMemsetAsync(lrc, 0, (size_t)T * 2 * sizeof(int32_t), stream);
   {
     int B, nt;
@@ -691,13 +727,22 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;  // kept rows per tree <= N
     const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
     (void)B;
-    (void)hipMemsetAsync(acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
+    p.acc = accs[level & 1];
+    (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
+    const bool dl = derive && level > 0;
+    if (dl) hipLaunchKernelGGL(rf_child_totals, dim3(nodesL, T), dim3(64), 0, stream, p, accs[(level - 1) & 1], level);
     if (use_mfma)
       hipLaunchKernelGGL(rf_hist_mfma, dim3(G), dim3(nt), lds_mfma, stream, p, (const RfRec*)rin, level, (const int32_t*)wl);
+    else if (dl && level == max_depth)
+      ;  // the last level needs node totals only: all derived
+    else if (rec_rows && dl)
+      hipLaunchKernelGGL((rf_hist<true, true>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
     else if (rec_rows)
-      hipLaunchKernelGGL(rf_hist<true>, dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
+      hipLaunchKernelGGL((rf_hist<true, false>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
+    else if (dl)
+      hipLaunchKernelGGL((rf_hist<false, true>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
     else
-      hipLaunchKernelGGL(rf_hist<false>, dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
+      hipLaunchKernelGGL((rf_hist<false, false>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
     hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level);
     EM_CHECK_LAUNCH();
     if (level == max_depth) break;
