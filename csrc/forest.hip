@@ -105,30 +105,51 @@ __host__ __device__ inline int rec_words(int k) { return 68 + ((k + 3) & ~3) + 6
 // is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
 template <bool REC>
 __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restrict__ rows_v) {
+  // chunks of RR x RF_NT rows: every thread hashes RR rows (all hashes / loads in flight), one count
+  // exchange and one atomic reservation per chunk; the count arrays are double-buffered, so a chunk
+  // costs two barriers (was three per RF_NT rows)
+  constexpr int RR = 4;
   const int t = blockIdx.y, B = gridDim.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __shared__ int wcnt[4];
-  __shared__ int base;
+  __shared__ int wcnt[2][RR][4];
+  __shared__ int base[2];
   int32_t* out = static_cast<int32_t*>(rows_v) + (int64_t)t * p.N;
   RfRec* outr = static_cast<RfRec*>(rows_v) + (int64_t)t * p.N;
   const int64_t r0 = p.N * blockIdx.x / B, r1 = p.N * (blockIdx.x + 1) / B;
-  for (int64_t c = r0; c < r1; c += RF_NT) {
-    const int64_t r = c + threadIdx.x;
-    const int w = r < r1 ? row_weight(p.bootstrap, p.seed, t + p.t_off, r) : 0;
-    const bool keep = w > 0;
-    const uint64_t bal = __ballot(keep);
-    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-    if (lane == 0) wcnt[wv] = __builtin_popcountll(bal);
-    __syncthreads();
-    if (threadIdx.x == 0) base = atomicAdd(&p.lrc[(int64_t)t * 2], wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3]);
-    __syncthreads();
-    int off = base;
-    for (int i = 0; i < wv; ++i) off += wcnt[i];
-    if (keep) {
-      if constexpr (REC) outr[off + pre] = rf_make_rec(p.X[r], p.Y[r], (uint32_t)w);
-      else out[off + pre] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w << RF_WSHIFT)) : (int32_t)r;
+  int par = 0;
+  for (int64_t c = r0; c < r1; c += RR * RF_NT, par ^= 1) {
+    int w[RR], pre[RR];
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {
+      const int64_t r = c + k * RF_NT + threadIdx.x;
+      w[k] = r < r1 ? row_weight(p.bootstrap, p.seed, t + p.t_off, r) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {
+      const uint64_t bal = __ballot(w[k] > 0);
+      pre[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+      if (lane == 0) wcnt[par][k][wv] = __builtin_popcountll(bal);
     }
     __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+#pragma unroll
+      for (int k = 0; k < RR; ++k) tot += wcnt[par][k][0] + wcnt[par][k][1] + wcnt[par][k][2] + wcnt[par][k][3];
+      base[par] = atomicAdd(&p.lrc[(int64_t)t * 2], tot);
+    }
+    __syncthreads();
+    int off = base[par];
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {
+      int o = off;
+      for (int i = 0; i < wv; ++i) o += wcnt[par][k][i];
+      if (w[k] > 0) {
+        const int64_t r = c + k * RF_NT + threadIdx.x;
+        if constexpr (REC) outr[o + pre[k]] = rf_make_rec(p.X[r], p.Y[r], (uint32_t)w[k]);
+        else out[o + pre[k]] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w[k] << RF_WSHIFT)) : (int32_t)r;
+      }
+      off += wcnt[par][k][0] + wcnt[par][k][1] + wcnt[par][k][2] + wcnt[par][k][3];
+    }
   }
 }
 
