@@ -153,6 +153,21 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
   }
 }
 
+// the node's candidate features: partial Fisher-Yates on a hashed stream, as the oracle
+EM_DEVICE void rf_node_cands(const RfParams& p, int t, int node, int16_t* __restrict__ co) {
+  int arr[RF_MAXF];
+  for (int i = 0; i < p.F; ++i) arr[i] = i;
+  const int kk = p.k_feat < p.F ? p.k_feat : p.F;
+  for (int i = 0; i < kk; ++i) {
+    const uint64_t h = hash3(p.seed ^ 0x5EEDF00Dull, ((uint64_t)(t + p.t_off) << 32) | (uint64_t)node, (uint64_t)i);
+    const int j = i + (int)(h % (uint64_t)(p.F - i));
+    const int tmp = arr[i];
+    arr[i] = arr[j];
+    arr[j] = tmp;
+    co[i] = (int16_t)arr[i];
+  }
+}
+
 // One thread per (tree, node of this level): child segments from the parent's partition counters,
 // then the node's candidate features (partial Fisher-Yates on a hashed stream, as the oracle).
 __global__ void rf_level_prep(RfParams p, int level) {
@@ -177,18 +192,18 @@ __global__ void rf_level_prep(RfParams p, int level) {
   sg[0] = start;
   sg[1] = count;
   if (count < 0 || level >= p.max_depth) return;
-  int arr[RF_MAXF];
-  for (int i = 0; i < p.F; ++i) arr[i] = i;
-  const int kk = p.k_feat < p.F ? p.k_feat : p.F;
-  int16_t* co = p.cand + ((int64_t)t * nodesL + nd) * p.k_feat;
-  for (int i = 0; i < kk; ++i) {
-    const uint64_t h = hash3(p.seed ^ 0x5EEDF00Dull, ((uint64_t)(t + p.t_off) << 32) | (uint64_t)node, (uint64_t)i);
-    const int j = i + (int)(h % (uint64_t)(p.F - i));
-    const int tmp = arr[i];
-    arr[i] = arr[j];
-    arr[j] = tmp;
-    co[i] = (int16_t)arr[i];
-  }
+  rf_node_cands(p, t, node, p.cand + ((int64_t)t * nodesL + nd) * p.k_feat);
+}
+
+// Candidates of every node of `level` into cand_out (present or not): the fused partition of level - 1
+// accumulates the children's histograms before rf_level_prep(level) runs (which then writes the same
+// candidates again: they depend on (seed, tree, node) only).
+__global__ void rf_level_cands(RfParams p, int level, int16_t* __restrict__ cand_out) {
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)p.T * nodesL) return;
+  const int t = (int)(gid / nodesL), nd = (int)(gid - (int64_t)t * nodesL);
+  rf_node_cands(p, t, first + nd, cand_out + ((int64_t)t * nodesL + nd) * p.k_feat);
 }
 
 // Level work lists.  Deep levels are very unbalanced (a one-hot split sends ~90 % of a node's rows to
@@ -535,10 +550,14 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
 // K10: children row lists, (blocks x nodes x trees) workgroups: left rows (x_f = 0) fill the parent
 // segment from its start, right rows from its end; every 256-row chunk reserves its ranges with one
 // atomic per side on the node's counters (lrc), which rf_level_prep turns into the child segments.
-template <bool REC>
+// HIST (record rows, derived node totals): while a record moves to its child, its candidate bits are
+// also added to that child's histogram (cnt / hist words of the child's record in acc_next, LDS partials
+// merged by integer atomics), so level + 1 needs no histogram pass over its rows.
+template <bool REC, bool HIST>
 __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __restrict__ rin_v,
                                                       void* __restrict__ rout_v, int level,
-                                                      const int32_t* __restrict__ wl) {
+                                                      const int32_t* __restrict__ wl, uint32_t* __restrict__ acc_next,
+                                                      const int16_t* __restrict__ cand_next) {
   using E = typename std::conditional<REC, RfRec, int32_t>::type;
   const E* rin = static_cast<const E*>(rin_v);
   E* rout = static_cast<E*>(rout_v);
@@ -551,6 +570,25 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
   const int start = sg[0], count = sg[1];
   const int f = p.feat[(int64_t)t * p.nodes + node];
   if (f < 0 || count < 0) return;
+  extern __shared__ __attribute__((aligned(16))) uint32_t chl[];  // HIST: [2 children][rec]
+  __shared__ int8_t cslot[2][64];
+  __shared__ uint64_t cmk[2];
+  const int kf = p.k_feat, rec = rec_words(kf), kp = (kf + 3) & ~3;
+  if (HIST) {
+    for (int i = threadIdx.x; i < 2 * rec; i += blockDim.x) chl[i] = 0u;
+    if (threadIdx.x < 2) {
+      const int s = threadIdx.x;
+      const int16_t* co = cand_next + ((int64_t)t * (2 * nodesL) + 2 * nd + s) * kf;
+      uint64_t m = 0;
+      const int kk = kf < p.F ? kf : p.F;
+      for (int i = 0; i < kk; ++i) {
+        cslot[s][co[i]] = (int8_t)i;
+        m |= 1ull << co[i];
+      }
+      cmk[s] = m;
+    }
+    __syncthreads();
+  }
   // chunks of 4 x blockDim rows: 4 ballots per wave (row k of the thread = c + k*blockDim + tid), one
   // LDS count exchange and one atomic reservation per side per chunk (instead of per blockDim rows);
   // the small count arrays are double-buffered so a chunk needs two barriers
@@ -611,6 +649,37 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
         lo += lc[buf][k][q];
         roff += rc[buf][k][q];
       }
+    }
+    if constexpr (HIST && REC) {
+#pragma unroll
+      for (int k2 = 0; k2 < RR; ++k2) {
+        if (!have[k2]) continue;
+        const int sd = right[k2] ? 1 : 0;
+        const uint32_t w = rf_rec_w(r[k2]);
+        const uint64_t y = r[k2].y & RF_M62;
+        uint64_t xx = r[k2].x & RF_M62 & cmk[sd];
+        uint32_t* cnt = chl + sd * rec + 68;
+        uint32_t* hist = cnt + kp;
+        while (xx) {
+          const int sl = cslot[sd][__builtin_ctzll(xx)];
+          xx &= xx - 1;
+          atomicAdd(&cnt[sl], w);
+          uint64_t y2 = y;
+          while (y2) {
+            atomicAdd(&hist[sl * 64 + __builtin_ctzll(y2)], w);
+            y2 &= y2 - 1;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (HIST) {
+    __syncthreads();
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      uint32_t* dst = acc_next + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * rec;
+      for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x)
+        if (chl[sd * rec + i]) atomicAdd(&dst[i], chl[sd * rec + i]);
     }
   }
 }
@@ -674,7 +743,9 @@ static void rf_shape(int64_t N, int level, int& B, int& nt) {
 
 EM_API int64_t em_rf_acc_words(int T, int max_depth, int k_feat) {
   if (T < 1 || max_depth < 0 || max_depth > 14 || k_feat < 1 || k_feat > RF_MAXF) return -1;
-  return 2 * (int64_t)T * (1ll << max_depth) * rec_words(k_feat);  // two levels' records (rf_child_totals)
+  // two levels' records (rf_child_totals) + a second candidate buffer (the fused partition fills the
+  // next level's candidates while the current level's are still in use)
+  return 2 * (int64_t)T * (1ll << max_depth) * rec_words(k_feat) + ((int64_t)T * (1ll << max_depth) * k_feat + 1) / 2;
 }
 
 // Native level-wise driver: all T trees advance one level per (prep, hist, split, partition) round.
@@ -693,7 +764,7 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const size_t lds = (size_t)rec * 4;
   if (lds > 160 * 1024 - 8192) return EM_ERR_ARG;
   static bool attr = false;
-  static int mfma_env = -1, derive_env = 1;
+  static int mfma_env = -1, derive_env = 1, fuse_env = 1;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)rf_hist<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
@@ -712,6 +783,10 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     mfma_env = (e && e[0] == '1') ? 1 : 0;
     const char* d = std::getenv("EM_RF_DERIVE");  // 0: accumulate node totals at every level (A/B)
     derive_env = (d && d[0] == '0') ? 0 : 1;
+    const char* fz = std::getenv("EM_RF_FUSE");  // 0: separate histogram pass at every level (A/B)
+    fuse_env = (fz && fz[0] == '0') ? 0 : 1;
+    (void)hipFuncSetAttribute((const void*)rf_partition<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 8192);
     attr = true;
   }
   // record-form row lists for one-word features (rows_a/rows_b hold 16 B per row: em_rf_row_bytes);
@@ -721,7 +796,9 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const bool use_mfma = rec_rows && mfma_env && k_feat <= 15;
   const size_t lds_mfma = (size_t)(((rec + 3) & ~3) * 4) + 4096 + 4 * 1024;
   uint32_t* accs[2] = {acc, acc + (int64_t)T * (1ll << max_depth) * rec};
+  int16_t* cands[2] = {cand, reinterpret_cast<int16_t*>(acc + 2 * (int64_t)T * (1ll << max_depth) * rec)};
   const bool derive = derive_env && !use_mfma;
+  const bool fuse = derive && fuse_env && rec_rows;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
              cover, cand, accs[0], lrc};
   (void)hipMemsetAsync(lrc, 0, (size_t)T * 2 * sizeof(int32_t), stream);
@@ -742,17 +819,21 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     int B, nt;
     rf_shape(kept, level, B, nt);
     const int64_t tn = (int64_t)T * nodesL;
+    p.acc = accs[level & 1];  // this level's node records and candidate lists (double-buffered)
+    p.cand = cands[level & 1];
     hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level);
     hipLaunchKernelGGL(rf_worklist, dim3(1), dim3(1024), 0, stream, p, level, wl);
     // grid: an upper bound of the work list (the kernels exit past wl[tn])
     const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;  // kept rows per tree <= N
     const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
     (void)B;
-    p.acc = accs[level & 1];
-    (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
+    const bool fused_prev = fuse && level >= 1 && level < max_depth;  // built by partition(level - 1)
+    if (!fused_prev) (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
     const bool dl = derive && level > 0;
     if (dl) hipLaunchKernelGGL(rf_child_totals, dim3(nodesL, T), dim3(64), 0, stream, p, accs[(level - 1) & 1], level);
-    if (use_mfma)
+    if (fused_prev)
+      ;  // cnt / hist words were accumulated by the fused partition of the previous level
+    else if (use_mfma)
       hipLaunchKernelGGL(rf_hist_mfma, dim3(G), dim3(nt), lds_mfma, stream, p, (const RfRec*)rin, level, (const int32_t*)wl);
     else if (dl && level == max_depth)
       ;  // the last level needs node totals only: all derived
@@ -768,12 +849,21 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     EM_CHECK_LAUNCH();
     if (level == max_depth) break;
     (void)hipMemsetAsync(lrc, 0, (size_t)tn * 2 * sizeof(int32_t), stream);
-    if (rec_rows)
-      hipLaunchKernelGGL(rf_partition<true>, dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
-                         (const int32_t*)wl);
-    else
-      hipLaunchKernelGGL(rf_partition<false>, dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
-                         (const int32_t*)wl);
+    if (fuse && level + 1 < max_depth) {
+      const int64_t tn2 = 2 * tn;
+      int16_t* cn = cands[(level + 1) & 1];
+      hipLaunchKernelGGL(rf_level_cands, dim3((unsigned)((tn2 + 127) / 128)), dim3(128), 0, stream, p, level + 1, cn);
+      uint32_t* an = accs[(level + 1) & 1];  // = the records of level - 1, already read by rf_child_totals(level)
+      (void)hipMemsetAsync(an, 0, (size_t)tn2 * rec * sizeof(uint32_t), stream);
+      hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), 2 * lds, stream, p, (const void*)rin, rout,
+                         level, (const int32_t*)wl, an, (const int16_t*)cn);
+    } else if (rec_rows) {
+      hipLaunchKernelGGL((rf_partition<true, false>), dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
+                         (const int32_t*)wl, (uint32_t*)nullptr, (const int16_t*)nullptr);
+    } else {
+      hipLaunchKernelGGL((rf_partition<false, false>), dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
+                         (const int32_t*)wl, (uint32_t*)nullptr, (const int16_t*)nullptr);
+    }
     EM_CHECK_LAUNCH();
     void* tmp = rin;
     rin = rout;
