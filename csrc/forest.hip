@@ -170,7 +170,7 @@ EM_DEVICE void rf_node_cands(const RfParams& p, int t, int node, int16_t* __rest
 
 // One thread per (tree, node of this level): child segments from the parent's partition counters,
 // then the node's candidate features (partial Fisher-Yates on a hashed stream, as the oracle).
-__global__ void rf_level_prep(RfParams p, int level) {
+__global__ void rf_level_prep(RfParams p, int level, int have_cands) {
   const int nodesL = 1 << level, first = nodesL - 1;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)p.T * nodesL) return;
@@ -191,13 +191,13 @@ __global__ void rf_level_prep(RfParams p, int level) {
   }
   sg[0] = start;
   sg[1] = count;
-  if (count < 0 || level >= p.max_depth) return;
+  if (count < 0 || level >= p.max_depth || have_cands) return;  // have_cands: rf_level_cands drew them
   rf_node_cands(p, t, node, p.cand + ((int64_t)t * nodesL + nd) * p.k_feat);
 }
 
 // Candidates of every node of `level` into cand_out (present or not): the fused partition of level - 1
-// accumulates the children's histograms before rf_level_prep(level) runs (which then writes the same
-// candidates again: they depend on (seed, tree, node) only).
+// accumulates the children's histograms before rf_level_prep(level) runs, so they are drawn here (they
+// depend on (seed, tree, node) only) and rf_level_prep(level) skips them.
 __global__ void rf_level_cands(RfParams p, int level, int16_t* __restrict__ cand_out) {
   const int nodesL = 1 << level, first = nodesL - 1;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -821,13 +821,14 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     const int64_t tn = (int64_t)T * nodesL;
     p.acc = accs[level & 1];  // this level's node records and candidate lists (double-buffered)
     p.cand = cands[level & 1];
-    hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level);
+    const bool fused_prev = fuse && level >= 1 && level < max_depth;  // built by partition(level - 1)
+    hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level,
+                       (int)fused_prev);
     hipLaunchKernelGGL(rf_worklist, dim3(1), dim3(1024), 0, stream, p, level, wl);
     // grid: an upper bound of the work list (the kernels exit past wl[tn])
     const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;  // kept rows per tree <= N
     const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
     (void)B;
-    const bool fused_prev = fuse && level >= 1 && level < max_depth;  // built by partition(level - 1)
     if (!fused_prev) (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
     const bool dl = derive && level > 0;
     if (dl) hipLaunchKernelGGL(rf_child_totals, dim3(nodesL, T), dim3(64), 0, stream, p, accs[(level - 1) & 1], level);
