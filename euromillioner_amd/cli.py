@@ -46,6 +46,7 @@ _FLAGS = {
     "--comm-dtype": "dist.comm_dtype",
     "--fault-at-step": "dist.fault_at_step", "--fault-rank": "dist.fault_rank",
     "--check-sync-every": "dist.check_sync_every", "--avg-frequency": "dist.avg_frequency",
+    "--max-restarts": "dist.max_restarts",
     "--profile-dir": "log.profile_dir", "--profile-steps": "log.profile_steps",
     "--ckpt": "ckpt.path", "--resume": "ckpt.resume", "--ckpt-every": "ckpt.every",
     "--log-level": "log.level", "--device": "device",
@@ -126,9 +127,13 @@ def main(argv=None) -> int:
             log.error(f"invalid configuration: {e}")
             return 2
         if must_spawn:
-            log.info(f"launching {world} ranks (127.0.0.1 rendezvous)")
-            return launch.spawn([sys.executable, "-m", "euromillioner_amd"] + argv, world,
-                                timeout_s=float(os.environ.get("EUROM_LAUNCH_TIMEOUT", "86400")))
+            log.info(f"launching {world} ranks (127.0.0.1 rendezvous)"
+                     + (f", up to {cfg.dist.max_restarts} restart(s)" if cfg.dist.max_restarts else ""))
+            base = [sys.executable, "-m", "euromillioner_amd"] + argv
+            # a restarted job continues from the last checkpoint (ckpt.path) when there is one
+            again = base + ["--resume", "auto"] if cfg.ckpt.path and not cfg.ckpt.resume else base
+            return launch.spawn(base, world, timeout_s=float(os.environ.get("EUROM_LAUNCH_TIMEOUT", "86400")),
+                                max_restarts=int(cfg.dist.max_restarts), restart_argv=again)
     try:
         if a.cmd == "run":
             from .pipeline import run_reference_pipeline

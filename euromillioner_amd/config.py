@@ -118,6 +118,7 @@ class DistConfig:
     fault_rank: int | None = None
     check_sync_every: int = 0  # cross-rank parameter checksum assert every k steps (0 = off)
     avg_frequency: int = 0  # >0: parameter averaging every k local steps (Spark ParameterAveraging parity)
+    max_restarts: int = 0  # self-launched --dp N jobs: restart every rank (with --resume auto) after a failure
 
 
 @dataclasses.dataclass

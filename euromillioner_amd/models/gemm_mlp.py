@@ -88,7 +88,9 @@ class GemmMLPTrainer:
         self.sizes = tuple(int(s) for s in sizes)
         self.padded = (64 * self.lags,) + tuple(_pad_hidden(h, activation, dtype) for h in self.sizes[1:-1]) + (64,)
         self.activation, self.loss_name, self.group = activation, loss, process_group
-        self.bucket_elems = max(1 << 16, int(bucket_mb * (1 << 20) // 4))
+        # whole multiples of 8 elements: every bucket of the bf16 wire then starts 32-B aligned (the
+        # fp32 -> bf16 cast takes 16-B aligned fp32 sources; flat ranges start at multiples of 8)
+        self.bucket_elems = max(1 << 16, int(bucket_mb * (1 << 20) // 4) // 8 * 8)
         self.offsets = []
         off = 0
         for kp, np_ in zip(self.padded[:-1], self.padded[1:]):

@@ -124,10 +124,14 @@ class RangeAllReducer:
                  cast=None):
         self.flat, self.bucket_elems, self.group = flat, max(1, int(bucket_elems)), group
         self.wire, self.cast = wire, cast
+        if wire is not None:  # each bucket's cast needs a 16-B aligned fp32 start: whole multiples of 8
+            self.bucket_elems = max(8, self.bucket_elems // 8 * 8)
         self.handles: list = []
         self.launched: list[tuple[int, int]] = []
 
     def ready(self, a: int, c: int) -> None:
+        if self.wire is not None and a % 4:
+            raise ValueError(f"bf16-wire range must start at a multiple of 4 elements (got {a})")
         for s0 in range(a, c, self.bucket_elems):
             s1 = min(c, s0 + self.bucket_elems)
             if self.wire is not None:

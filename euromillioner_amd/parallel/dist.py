@@ -9,7 +9,8 @@ one 8-GPU xGMI node.  CPU tests use ``gloo``.
   always 127.0.0.1 for single-node runs;
 * ``timeout`` so a dead peer raises instead of hanging (SURVEY.md §5.3);
 * test-only fault injection: ``--fault-at-step k --fault-rank r`` makes rank r exit
-  with code 17 at step k.
+  with code 17 at step k -- on the first attempt of a job only (a job restarted by
+  ``parallel/launch.py --max-restarts`` or torchrun must not fail again at the same step).
 """
 from __future__ import annotations
 
@@ -72,8 +73,11 @@ def shutdown(info: DistInfo) -> None:
 
 
 def maybe_inject_fault(step: int, info: DistInfo, at_step: int | None, at_rank: int | None) -> None:
-    if at_step is not None and step == int(at_step) and (at_rank is None or int(at_rank) == info.rank):
-        os._exit(17)
+    if at_step is None or step != int(at_step) or (at_rank is not None and int(at_rank) != info.rank):
+        return
+    if os.environ.get("EUROM_RESTART", "0") != "0" or os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != "0":
+        return  # a restarted job: the injected fault already happened
+    os._exit(17)
 
 
 def all_reduce_mean_(t: torch.Tensor, info: DistInfo) -> torch.Tensor:

@@ -12,7 +12,14 @@ Rules that keep the launch safe on a GPU node:
 * every child gets ``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``LOCAL_WORLD_SIZE`` and a 127.0.0.1
   rendezvous (``MASTER_ADDR``/``MASTER_PORT``) plus ``EUROM_LAUNCHED=1``;
 * the first child that fails (or the whole job passing ``timeout_s``) kills the others' process
-  groups; the parent returns the failing child's exit code (124 for a timeout), never 0.
+  groups; the parent returns the failing child's exit code (124 for a timeout), never 0;
+* elastic restart (``--max-restarts k``): after a rank failure the parent stops the
+  job and starts ALL ranks again as fresh child processes (new rendezvous port), up to ``k`` times,
+  with ``restart_argv`` (the trainers pass ``--resume auto``, so the new job continues from the last
+  checkpoint).  Children see ``EUROM_RESTART=i`` (0 on the first attempt; test-only fault injection
+  fires only there).  Each restart is logged; once the restarts are used up the job exits with the
+  failing rank's code.  This replaces the reference's swallow-and-exit-0 handler
+  (``/root/reference/src/main/java/com/euromillioner/Main.java:144-147``).
 """
 from __future__ import annotations
 
@@ -24,6 +31,7 @@ import sys
 import time
 
 LAUNCHED_ENV = "EUROM_LAUNCHED"
+RESTART_ENV = "EUROM_RESTART"
 
 
 def free_port() -> int:
@@ -32,12 +40,12 @@ def free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def rank_env(rank: int, world: int, port: int, base: dict | None = None) -> dict:
-    """Environment of rank ``rank`` of a ``world``-rank single-node job."""
+def rank_env(rank: int, world: int, port: int, base: dict | None = None, attempt: int = 0) -> dict:
+    """Environment of rank ``rank`` of a ``world``-rank single-node job (``attempt``: restart index)."""
     env = dict(os.environ if base is None else base)
     env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
                 "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
-                "MASTER_PORT": str(port), LAUNCHED_ENV: "1"})
+                "MASTER_PORT": str(port), LAUNCHED_ENV: "1", RESTART_ENV: str(attempt)})
     # dmabuf IPC is the only kind the host driver supports (RCCL / xGMI peer buffers)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return env
@@ -64,22 +72,50 @@ def requested_world(requested: int | None) -> tuple[int, bool]:
     return 1, False
 
 
+def restart_attempt() -> int:
+    """Which (re)start of a self-launched job this process belongs to (0 = the first)."""
+    try:
+        return int(os.environ.get(RESTART_ENV, "0"))
+    except ValueError:
+        return 0
+
+
 def spawn(argv: list[str], world: int, timeout_s: float = 3600.0, env: dict | None = None,
-          quiet_ranks: bool = False, poll_s: float = 0.2) -> int:
-    """Run ``argv`` as ``world`` ranks; return 0 iff every rank exited 0.
+          quiet_ranks: bool = False, poll_s: float = 0.2, max_restarts: int = 0,
+          restart_argv: list[str] | None = None) -> int:
+    """Run ``argv`` as ``world`` ranks; return 0 iff every rank of the last attempt exited 0.
 
     ``quiet_ranks``: ranks > 0 get stdout discarded (their stderr still shows), so rank 0's
     output (e.g. the bench JSON line) is the only stdout of the job.
+    ``max_restarts``: after a failed attempt, start every rank again (``restart_argv`` if given)
+    at most this many times.  A job-level timeout is never retried.
     """
     if world < 1:
         raise ValueError("world must be >= 1")
+    if max_restarts < 0:
+        raise ValueError("max_restarts must be >= 0")
+    t0 = time.monotonic()
+    attempt = 0
+    while True:
+        cmd = argv if attempt == 0 or not restart_argv else restart_argv
+        rc = _run_once(cmd, world, t0, timeout_s, env, quiet_ranks, poll_s, attempt)
+        if rc == 0 or rc == 124 or attempt >= max_restarts:
+            if rc != 0 and max_restarts > 0 and rc != 124:
+                sys.stderr.write(f"[launch] giving up after {attempt} restart(s); exit {rc}\n")
+            return rc
+        attempt += 1
+        sys.stderr.write(f"[launch] restart {attempt}/{max_restarts}: starting all {world} ranks again "
+                         f"(previous attempt exited {rc})\n")
+        sys.stderr.flush()
+
+
+def _run_once(argv, world, t0, timeout_s, env, quiet_ranks, poll_s, attempt) -> int:
     port = free_port()
     procs: list[subprocess.Popen] = []
     for r in range(world):
         out = subprocess.DEVNULL if (quiet_ranks and r > 0) else None
-        procs.append(subprocess.Popen(argv, env=rank_env(r, world, port, env), stdout=out,
+        procs.append(subprocess.Popen(argv, env=rank_env(r, world, port, env, attempt), stdout=out,
                                       start_new_session=True))
-    t0 = time.monotonic()
     rc_final = 0
     try:
         live = set(range(world))
@@ -96,7 +132,7 @@ def spawn(argv: list[str], world: int, timeout_s: float = 3600.0, env: dict | No
             if live and time.monotonic() - t0 > timeout_s:
                 sys.stderr.write(f"[launch] job exceeded {timeout_s:.0f}s; stopping all ranks\n")
                 _kill_all(procs)
-                rc_final = rc_final or 124
+                rc_final = 124
                 break
             if live:
                 time.sleep(poll_s)

@@ -50,6 +50,20 @@ class _Engine:
     def evaluate(self, offset: int, n: int) -> dict:
         raise NotImplementedError
 
+    n_local = 0  # local steps taken (parameter-averaging phase; restored on resume)
+    avg_k = 0
+
+    def finish(self) -> None:
+        """End of training: with --avg-frequency k, average once more unless the last local step
+        just did (Spark's ParameterAveragingTrainingMaster averages at the end of every fit), so the
+        final evaluation, the checkpoint and the cross-rank check see one model."""
+        if self.avg_k > 0 and self.n_local % self.avg_k != 0:
+            self.average_parameters()
+            self.n_local = 0
+
+    def average_parameters(self) -> None:
+        pass
+
 
 def _checksum(flat: torch.Tensor) -> torch.Tensor:
     """Order-sensitive integer checksum of a float buffer (bit-exact comparison across ranks)."""
@@ -442,6 +456,7 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
         start_step = int(resume["extra"].get("step", 0))
         if "opt" in resume:
             engine.load_optimizer_state(resume["opt"])
+        engine.n_local = start_step  # keeps the --avg-frequency phase of the interrupted run
         log.info(f"resumed from {resume_path} at step {start_step}")
     log.info(f"mlp {'->'.join(map(str, sizes))} engine={engine.name} device={dev} world={info.world} "
              f"train={margin} (shard {shard}) val={n_samples - margin} batch={global_b} steps={steps}")
@@ -487,9 +502,11 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
             off += int(wperm[k] if m.shuffle else k) * local_b
         loss_t = engine.step(idx, off, local_b, global_b)
         done += 1
+        last = step == steps - 1
+        if last:
+            engine.finish()
         if cfg.dist.check_sync_every and (step + 1) % cfg.dist.check_sync_every == 0:
             check_sync(engine, info)
-        last = step == steps - 1
         if (m.eval_every and (step + 1) % m.eval_every == 0) or last:
             n_val = n_samples - margin if not device_data else min(n_samples - margin, 1 << 24)
             ev = engine.evaluate(margin, n_val) if n_samples > margin else {}

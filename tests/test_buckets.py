@@ -44,10 +44,15 @@ flat = torch.zeros(rows * K + 10)
 whole = (dz @ x.t()).reshape(-1).clone()
 dist.all_reduce(whole)
 out = {{}}
+def aligned_cast(s, d):  # the HIP cast (em_cast_f32_bf16) rejects fp32 sources that are not 16-B aligned
+    assert s.data_ptr() % 16 == 0, s.data_ptr()
+    return d.copy_(s)
 for wire_kind in ("fp32", "bf16"):
     flat.zero_()
     wire = torch.zeros_like(flat, dtype=torch.bfloat16) if wire_kind == "bf16" else None
-    red = RangeAllReducer(flat, bucket_elems=5000, wire=wire, cast=lambda s, d: d.copy_(s))
+    # an odd bucket size (what --bucket-mb 10.1 gives): the bf16 wire rounds it to whole 8-element groups
+    red = RangeAllReducer(flat, bucket_elems=5000 if wire is None else 5003, wire=wire, cast=aligned_cast)
+    assert wire is None or red.bucket_elems % 8 == 0
     gw = flat[:rows * K].view(rows, K)
     for r0, r1 in plan_panels(rows, K, 5000, ncu=2, tile_m=64, tile_n=32):
         gw[r0:r1] = dz[r0:r1] @ x.t()   # this panel is final ...

@@ -139,6 +139,49 @@ def test_parameter_averaging_mode_stays_in_sync(tmp_path):
     assert _params(p)[3]["step"] == 8
 
 
+def test_parameter_averaging_final_average(tmp_path):
+    """steps % k != 0: the run still ends on one averaged model (final check_sync passes, and the
+    checkpoint rank 0 writes is the average every rank holds)."""
+    p = str(tmp_path / "avg7.zip")
+    outs = _launch(_train_argv(["--steps", "7", "--batch", "128", "--avg-frequency", "3",
+                                "--check-sync-every", "7", "--ckpt", p]), 2)
+    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    assert _params(p)[3]["step"] == 7
+
+
+def _cli(args, timeout=400):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    return subprocess.run(args, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                          timeout=timeout)
+
+
+def test_elastic_restart_resumes_bit_identical(tmp_path):
+    """--dp 2 --max-restarts 1: rank 1 dies at step 5, the launcher restarts both ranks from the step-4
+    checkpoint (--resume auto) and the job ends with exit 0 and the same parameters, bit for bit, as
+    an uninterrupted run."""
+    ref, got = str(tmp_path / "ref.zip"), str(tmp_path / "restarted.zip")
+    common = ["--steps", "9", "--batch", "128", "--lr", "0.01", "--dp", "2", "--ckpt-every", "2"]
+    r = _cli(_train_argv(common + ["--ckpt", ref]))
+    assert r.returncode == 0, r.stdout[-3000:]
+    r = _cli(_train_argv(common + ["--ckpt", got, "--fault-at-step", "5", "--fault-rank", "1",
+                                   "--max-restarts", "1", "--timeout", "60"]))
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "restart 1/1" in r.stdout and "resumed from" in r.stdout
+    a, b = _params(ref), _params(got)
+    assert b[3]["step"] == 9
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y), np.abs(x - y).max()
+
+
+def test_no_restart_fails_loudly(tmp_path):
+    """The same fault with --max-restarts 0: the job exits non-zero (rank 1's code 17)."""
+    r = _cli(_train_argv(["--steps", "9", "--batch", "128", "--dp", "2", "--ckpt", str(tmp_path / "x.zip"),
+                          "--ckpt-every", "2", "--fault-at-step", "5", "--fault-rank", "1", "--timeout", "60"]))
+    assert r.returncode == 17, r.stdout[-3000:]
+    assert "restart" not in r.stdout.replace("restarts", "")
+
+
 def test_sync_check_detects_divergence(tmp_path):
     """Local steps that are never averaged diverge; the checker must fail loudly."""
     outs = _launch(_train_argv(["--steps", "3", "--batch", "128", "--avg-frequency", "1000",
