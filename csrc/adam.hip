@@ -12,46 +12,13 @@
 // straight 48 KB copy).  Modes let DP insert an RCCL all-reduce between the slab
 // reduction and the update.
 #include "common.h"
+#include "mlp_adam.h"
 #include "xgmi.h"
 
 namespace {
 
-constexpr int IN = 64, HID = 128, OUT = 64;
-constexpr int P_W2 = IN * HID, P_B2 = P_W2 + HID * OUT, P_TOTAL = P_B2 + OUT;
-constexpr int W1T_RS = 144, W2P_RS = 272, W2Q_RS = 144;  // padded image rows (csrc/mlp_fused.hip)
-constexpr int IMG_W1T = 0, IMG_W2P = IMG_W1T + 128 * W1T_RS, IMG_W2Q = IMG_W2P + 64 * W2P_RS, IMG_B2 = IMG_W2Q + 128 * W2Q_RS;
-
-// true for padding slots that must stay exactly zero (W1 row 63, W2 cols 62/63, b2[62/63])
-EM_DEVICE bool mlp_pad_slot(int p) {
-  if (p < P_W2) return (p >> 7) == 63;
-  if (p < P_B2) return ((p - P_W2) & 63) >= 62;
-  return (p - P_B2) >= 62;
-}
-
-EM_DEVICE void mlp_pack_one(int p, float val, uint8_t* img) {
-  const uint16_t b = f2bf_bits(val);
-  if (p < P_W2) {  // W1[f][c] -> W1T image row c, feature f
-    const int f = p >> 7, c = p & 127;
-    const uint32_t off = IMG_W1T + c * W1T_RS + (f >> 3) * 16 + (f & 7) * 2;
-    *reinterpret_cast<uint16_t*>(img + off) = b;
-  } else if (p < P_B2) {  // W2[c][o]
-    const int q = p - P_W2, c = q >> 6, o = q & 63;
-    {  // W2P: row o, hid c = 32t + perm(s,h,j)
-      const int t = c >> 5, cc = c & 31, s = cc >> 4, a = (cc >> 3) & 1, hh = (cc >> 2) & 1, bb = cc & 3;
-      const int j = 4 * a + bb, k16 = (2 * t + s) * 2 + hh;
-      const uint32_t off = IMG_W2P + o * W2P_RS + k16 * 16 + j * 2;
-      *reinterpret_cast<uint16_t*>(img + off) = b;
-    }
-    {  // W2Q: row c, out o = 32u + perm(s,h,j)
-      const int u = o >> 5, oo = o & 31, s = oo >> 4, a = (oo >> 3) & 1, hh = (oo >> 2) & 1, bb = oo & 3;
-      const int j = 4 * a + bb, k8 = (2 * u + s) * 2 + hh;
-      const uint32_t off = IMG_W2Q + c * W2Q_RS + k8 * 16 + j * 2;
-      *reinterpret_cast<uint16_t*>(img + off) = b;
-    }
-  } else {
-    *reinterpret_cast<float*>(img + IMG_B2 + (p - P_B2) * 4) = val;
-  }
-}
+using mlp::P_TOTAL;
+using mlp::IMG_BYTES;
 
 // 4 threads per parameter (slab-split), 64 parameters per 256-thread block.
 // Bias-correction step counter kept on the device: every block reads `step` first; the last block
@@ -73,12 +40,6 @@ EM_DEVICE void adam_end(int* state, int t) {
   }
 }
 
-// 1 - beta^t through the native v_log_f32 / v_exp_f32 (about 1 ulp each): powf's edge-case handling
-// was ~0.35 us of dependent latency per launch, on the critical path behind the step-counter load.
-EM_DEVICE float bias_correction(float beta, int t) {
-  return 1.f - __builtin_amdgcn_exp2f((float)t * __builtin_amdgcn_logf(beta));
-}
-
 // Step-counter modes (the `mode` argument's bit 2, EM_ADAM_PRE): without it every launch reads
 // state[0] + 1 and the last block to draw a ticket publishes it (adam_end); with it the producer
 // of this step's gradients already advanced state[0] (mlp_fused.hip advance_step), so the counter
@@ -93,21 +54,18 @@ EM_DEVICE void adam_apply_loaded(int p, float g, float w0, float m0, float v0, i
                                  uint8_t* __restrict__ mlp_img) {
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
   const float bc1 = bias_correction(b1, tstep), bc2 = bias_correction(b2, tstep);
-  if (mlp_img && mlp_pad_slot(p)) {
+  if (mlp_img && mlp::pad_slot(p)) {
     params[p] = 0.f;
     m[p] = 0.f;
     v[p] = 0.f;
-    mlp_pack_one(p, 0.f, mlp_img);
+    mlp::pack_one(p, 0.f, mlp_img);
   } else {
-    float w = w0;
-    g += wd * w;
-    const float mm = b1 * m0 + (1.f - b1) * g;
-    const float vv = b2 * v0 + (1.f - b2) * g * g;
+    float mm = m0, vv = v0;
+    const float w = adam_math(g, w0, mm, vv, lr, b1, b2, eps, wd, bc1, bc2);
     m[p] = mm;
     v[p] = vv;
-    w -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
     params[p] = w;
-    if (mlp_img) mlp_pack_one(p, w, mlp_img);
+    if (mlp_img) mlp::pack_one(p, w, mlp_img);
   }
 }
 
@@ -171,11 +129,13 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
   if (!pre) adam_end(state, tstep);
 }
 
-// Vectorised slab reduction (P % 64 == 0, stride % 4 == 0): 256 threads per 64 parameters, thread
-// t = (slab group g = t >> 4, quad q = t & 15) sums float4 quads of slabs g, g + 16, ... with all of
-// its loads in flight (16-B loads: 4x fewer memory instructions than one float per thread).  The
-// fixed summation order keeps the result bitwise reproducible.
-constexpr int A4_T = 256, A4_G = 16;
+// Vectorised slab reduction (P % 64 == 0, stride % 4 == 0): 128 threads per 64 parameters, thread
+// t = (slab group g = t >> 4, quad q = t & 15) sums float4 quads of slabs g, g + 8, g + 16, ... in that
+// order (32 16-B loads in flight per thread for 256 slabs), then thread (quad, e) adds the 8 group
+// sums in group order.  This is exactly the summation order of the train kernel's in-launch Adam
+// epilogue (csrc/mlp_fused.hip epi_adam), so the split path (train -> em_adam_slab) and the one-launch
+// step produce bit-identical gradients.
+constexpr int A4_T = 128, A4_G = 8;
 __global__ void __launch_bounds__(A4_T)
 adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, float grad_scale,
                   float* __restrict__ params, float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io,
@@ -202,17 +162,18 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
     m0 = m[p];
     v0 = v[p];
   }
-  f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
-  int sl = g;
-  for (; sl + 15 * A4_G < nslab; sl += 16 * A4_G) {
-    f32x4 t[16];
+  f32x4 acc = f32x4{};
+  for (int j0 = 0; g + A4_G * j0 < nslab; j0 += 32) {
+    f32x4 t[32];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t[k] = *reinterpret_cast<const f32x4*>(src + (size_t)(sl + k * A4_G) * stride);
+    for (int k = 0; k < 32; ++k) {
+      const int sl = g + A4_G * (j0 + k);
+      t[k] = sl < nslab ? *reinterpret_cast<const f32x4*>(src + (size_t)sl * stride) : f32x4{};
+    }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc[k & 3] += t[k];
+    for (int k = 0; k < 32; ++k) acc += t[k];
   }
-  for (; sl < nslab; sl += A4_G) acc[0] += *reinterpret_cast<const f32x4*>(src + (size_t)sl * stride);
-  part[g][q] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  part[g][q] = acc;
   __syncthreads();
   if (blockIdx.x == 0 && loss_slabs && loss_out && threadIdx.x >= 64 && threadIdx.x < 128) {
     float l = 0.f;
@@ -253,7 +214,7 @@ adam_xgmi_kernel(XgmiDesc d, int P, float* __restrict__ params, float* __restric
 __global__ void mlp_pack_kernel(const float* __restrict__ params, uint8_t* __restrict__ img) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P_TOTAL) return;
-  mlp_pack_one(p, mlp_pad_slot(p) ? 0.f : params[p], img);
+  mlp::pack_one(p, mlp::pad_slot(p) ? 0.f : params[p], img);
 }
 
 // plain multi-tensor-style Adam over a flat buffer (generic path: K6 for any model).  G = float, or

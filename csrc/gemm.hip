@@ -311,7 +311,7 @@ template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, int wm, int wn, int m0, int n0,
                           void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
                           const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                          float beta) {
+                          float beta, float* __restrict__ colpart, int N) {
   const int r = lane & 31, h = lane >> 5;
   // bf16 outputs go through a per-wave transposed LDS tile T[64 cols][32 rows] (ds_write_b64 of 4
   // consecutive rows per lane), then leave as 16-B coalesced stores: C rows via ds_read_b64_tr_b16
@@ -323,6 +323,7 @@ EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, i
   char* tb = smem + wave * WEPI;
   char* yb = tb + 64 * TS;
   const int colw = n0 + wn * 64;
+  float cs[2] = {0.f, 0.f};  // column sums of the epilogue values over the wave's 128 rows (colpart)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // unrolled: acc[i] must stay statically indexed (no scratch)
     const int rowb = m0 + wm * 128 + 32 * i;  // first row of this block
@@ -354,6 +355,7 @@ EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, i
             v = g_fn<FN>(v + bv);
           }
           x[e] = v;
+          cs[j] += v;
           if (!OUT_BF16) {
             float* cp = reinterpret_cast<float*>(C) + (int64_t)(rowb + lr) * ldc + colw + lc;
             *cp = beta != 0.f ? v + beta * *cp : v;
@@ -392,6 +394,13 @@ EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, i
     }
     wave_lds_sync();  // T / Y blocks are rewritten by the next block
   }
+  if (colpart) {  // bias gradient partials: row (m0 + 128 wm) / 128 of the [M / 128][N] fp32 partial array
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float t = xhalf_sum(cs[j]);
+      if (h == 0) colpart[(int64_t)((m0 >> 7) + wm) * N + colw + 32 * j + r] = t;
+    }
+  }
 }
 
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
@@ -399,7 +408,7 @@ __global__ void __launch_bounds__(G_NT, 1)
 gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                   void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                   const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta) {
+                  float beta, float* __restrict__ colpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -453,7 +462,7 @@ gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   }
 
   g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
-                                         alpha, beta);
+                                         alpha, beta, colpart, N);
 }
 
 // ============================================================================================
@@ -518,7 +527,7 @@ __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                   void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                   const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta) {
+                  float beta, float* __restrict__ colpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -615,7 +624,7 @@ gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
-                                         alpha, beta);
+                                         alpha, beta, colpart, N);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -641,13 +650,14 @@ template <int OUT_BF16, int FN, int DACT, int HAS_CT, int NBT>
 EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave, int lane, int rowbase, int colw,
                             void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
                             const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                            float beta) {
+                            float beta, float* __restrict__ colpart, int N) {
   constexpr int TS = 80;
   constexpr int YS = 144;
   constexpr int WEPI = 64 * TS + 32 * YS;
   char* tb = smem + wave * WEPI;
   char* yb = tb + 64 * TS;
   const int c16 = lane & 15, r4 = 4 * (lane >> 4);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of the epilogue values over the wave's 128 rows (colpart)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rowb = rowbase + 32 * i;
@@ -680,6 +690,7 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
             v = g_fn<FN>(v + bv);
           }
           x[e] = v;
+          cs[nb] += v;
           if (!OUT_BF16) {
             float* cp = reinterpret_cast<float*>(C) + (int64_t)(rowb + lr) * ldc + colw + lc;
             *cp = beta != 0.f ? v + beta * *cp : v;
@@ -714,6 +725,15 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
       }
     }
     wave_lds_sync();
+  }
+  if (colpart) {  // bias gradient partials: the four 16-lane row groups hold the same columns
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      float t = cs[nb];
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      if (lane < 16) colpart[(int64_t)(rowbase >> 7) * N + colw + 16 * nb + c16] = t;
+    }
   }
 }
 
@@ -752,7 +772,7 @@ __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                     void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                     const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                    float beta) {
+                    float beta, float* __restrict__ colpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t st_acc[8] = {}, st_t0 = 0, st_a = 0, st_b = 0;
   (void)st_acc;
@@ -931,7 +951,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   __syncthreads();
   if (G_STAMPS) G_MARK(st_b);
   g_epilogue16<OUT_BF16, FN, DACT, HAS_CT, 4>(acc, 0, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, C, ldc, CT,
-                                              ldct, bias, mask, ldm, alpha, beta);
+                                              ldct, bias, mask, ldm, alpha, beta, colpart, N);
 #if G_STAMPS
   {
     uint64_t t;
@@ -947,7 +967,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
              int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
-             int64_t ldm, float alpha, float beta) {
+             int64_t ldm, float alpha, float beta, float* colpart) {
   static bool attr = false;
   static const bool pp = !getenv_flag_off("EM_GEMM_PP");
   static const bool m16 = !getenv_flag_off("EM_GEMM_MFMA16");
@@ -978,16 +998,17 @@ int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf
     attr = true;
   }
   hipLaunchKernelGGL(kern, grid, dim3(G_NT), G_LDS, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm,
-                     alpha, beta);
+                     alpha, beta, colpart);
   return 0;
 }
 
 // runtime (out, act/dact, ct) -> one of 15 instantiations
 int g_dispatch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
                int64_t ldc, int c_bf16, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act,
-               const __bf16* mask, int64_t ldm, int dact, float alpha, float beta) {
+               const __bf16* mask, int64_t ldm, int dact, float alpha, float beta, float* colpart) {
 #define EM_G(OB, FN, DA, CTV) \
-  return g_launch<OB, FN, DA, CTV>(grid, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, beta)
+  return g_launch<OB, FN, DA, CTV>(grid, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, beta, \
+                                   colpart)
   if (!c_bf16) {
     if (act != ACT_NONE || mask || CT) return EM_ERR_ARG;
     EM_G(0, ACT_NONE, 0, 0);
@@ -1086,14 +1107,39 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const __bf16* __res
   }
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ part, int chunks, int N, float* __restrict__ out,
-                                    int accumulate, float scale) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= N) return;
+// Fixed-order sum of fp32 partial rows [chunks][N] -> out[N] (+ accumulate, * scale): 64 columns x 16
+// chunk groups per 1024-thread block; group g sums chunks g, g + 16, ... with 8 loads in flight, then
+// the 16 group sums are added in group order (bit-reproducible, and one round of loads deep instead
+// of a serial walk over the chunks).  Used for the colsum partials and for the GEMM epilogue's fused
+// bias-gradient partials (em_gemm_bf16_cs).
+constexpr int CR_COLS = 64, CR_G = 16;
+__global__ void __launch_bounds__(CR_COLS * CR_G) colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
+                                                                      float* __restrict__ out, int accumulate,
+                                                                      float scale) {
+  __shared__ float red[CR_G][CR_COLS];
+  const int c = threadIdx.x % CR_COLS, g = threadIdx.x / CR_COLS;
+  const int col = blockIdx.x * CR_COLS + c;
   float s = 0.f;
-  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * N + col];
-  s *= scale;
-  out[col] = accumulate ? out[col] + s : s;
+  if (col < N) {
+    int k = g;
+    for (; k + 7 * CR_G < chunks; k += 8 * CR_G) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(k + u * CR_G) * N + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < chunks; k += CR_G) s += part[(int64_t)k * N + col];
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    float t = red[0][c];
+#pragma unroll
+    for (int q = 1; q < CR_G; ++q) t += red[q][c];
+    t *= scale;
+    out[col] = accumulate ? out[col] + t : t;
+  }
 }
 
 // row sums of a bf16 [R][C] matrix (bias gradients from a transposed dZ copy): one wavefront per row
@@ -1243,13 +1289,25 @@ wgrad_skinny_reduce_kernel(const float* __restrict__ part, int S, int J, int W, 
 static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                      int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
                      int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, int splits, int kstep,
-                     int64_t c_split, hipStream_t stream);
+                     int64_t c_split, hipStream_t stream, float* colpart = nullptr);
 
 EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                         int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
                         int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, hipStream_t stream) {
   return gemm_impl(A, lda, a_kc, B, ldb, b_kc, C, ldc, c_bf16, M, N, K, bias, act, mask, ldm, dact, alpha, beta, ct,
                    ldct, 1, K, 0, stream);
+}
+
+// The same GEMM on the 256-tile path with the epilogue's column sums (K3 bias gradient, fused): colpart
+// receives fp32 [M / 128][N] partials -- row p = sum over output rows 128p .. 128p + 127 of the final
+// epilogue values (after act' for dgrad), before the bf16 rounding.  em_colpart_reduce sums them.
+EM_API int em_gemm_bf16_cs(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
+                           int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
+                           int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, float* colpart,
+                           hipStream_t stream) {
+  if (!colpart || ((uintptr_t)colpart & 3)) return EM_ERR_ARG;
+  return gemm_impl(A, lda, a_kc, B, ldb, b_kc, C, ldc, c_bf16, M, N, K, bias, act, mask, ldm, dact, alpha, beta, ct,
+                   ldct, 1, K, 0, stream, colpart);
 }
 
 // Split-K on the any-layout kernel: `splits` slices of `kstep` (multiple of 64) along K, slice s writing
@@ -1266,7 +1324,7 @@ EM_API int em_gemm_bf16_splitk(const void* A, int64_t lda, int a_kc, const void*
 static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                      int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
                      int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, int splits, int kstep,
-                     int64_t c_split, hipStream_t stream) {
+                     int64_t c_split, hipStream_t stream, float* colpart) {
   if (!A || !B || !C || M < 0 || N < 0 || K < 0 || act < 0 || act > 3) return EM_ERR_ARG;
   if (mask && (dact < 1 || dact > 3)) return EM_ERR_ARG;
   if (M == 0 || N == 0) return 0;
@@ -1286,12 +1344,12 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
   if (big) {
     const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
                               ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
-                              beta);
+                              beta, colpart);
     if (rc) return rc;
     EM_CHECK_LAUNCH();
     return 0;
   }
-  if (ct) return EM_ERR_ARG;  // the transposed copy is only produced by the 256 path
+  if (ct || colpart) return EM_ERR_ARG;  // the transposed copy / column partials: 256 path only
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const __bf16* a = (const __bf16*)A;
   const __bf16* b = (const __bf16*)B;
@@ -1332,8 +1390,19 @@ EM_API int em_colsum_bf16(const void* X, int64_t ldx, int M, int N, float* out, 
                        ldx, M, N, ws);
     EM_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, ws, chunks, N, out, accumulate,
-                     scale);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + CR_COLS - 1) / CR_COLS), dim3(CR_COLS * CR_G), 0, stream, ws,
+                     chunks, N, out, accumulate, scale);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[n] (+)= scale * sum_p part[p][n], fixed order (the em_gemm_bf16_cs bias-gradient partials)
+EM_API int em_colpart_reduce(const float* part, int nparts, int N, float* out, int accumulate, float scale,
+                             hipStream_t stream) {
+  if (!part || !out || nparts < 0 || N < 0) return EM_ERR_ARG;
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + CR_COLS - 1) / CR_COLS), dim3(CR_COLS * CR_G), 0, stream, part,
+                     nparts, N, out, accumulate, scale);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -172,6 +172,8 @@ class GemmMLPTrainer:
                   "logits": torch.empty(B, 64, dtype=torch.float32, device=dev),
                   "part": torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=dev),
                   "colsum_ws": torch.empty(max(1, (B + 511) // 512) * max(P), dtype=torch.float32, device=dev),
+                  # bias-gradient partials [B / 128][N] written by the 256-tile dgrad epilogue (fused K3 bias grad)
+                  "colpart": torch.empty(max(1, B // 128) * max(P), dtype=torch.float32, device=dev),
                   "plan": plan,
                   # transposed copies for the big wgrads: X_i^T (= Y_{i-1}^T) and dZ_i^T
                   "actt": {i: torch.empty(P[i], B, dtype=torch.bfloat16, device=dev)
@@ -251,6 +253,8 @@ class GemmMLPTrainer:
                     dz = LF.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
             return dz
         plan = ws["plan"]
+        B = dz.shape[0]
+        fused_bias = set()  # layers whose bias gradient the previous dgrad's epilogue already summed
         for i in reversed(range(L)):
             gw, gbias = self._views(self.grads, i)
             beta = 1.0 if accumulate else 0.0
@@ -262,20 +266,29 @@ class GemmMLPTrainer:
                     LIN.linear_wgrad_nt(ws["dzt"][i][r0:r1], ws["actt"][i], out=gw[r0:r1], beta=beta)
                     if on_ready is not None:
                         on_ready(a + r0 * K, a + r1 * K)
-                LIN.rowsum(ws["dzt"][i], out=gbias, accumulate=accumulate)
+                if i not in fused_bias:
+                    LIN.rowsum(ws["dzt"][i], out=gbias, accumulate=accumulate)
             else:
                 LIN.linear_wgrad(dz, inputs[i], out=gw, beta=beta)
                 if on_ready is not None:
                     on_ready(a, b_off)
-                LIN.colsum(dz, out=gbias, accumulate=accumulate, ws=ws["colsum_ws"])
+                if i not in fused_bias:
+                    LIN.colsum(dz, out=gbias, accumulate=accumulate, ws=ws["colsum_ws"])
             if on_ready is not None:
                 on_ready(b_off, c)
             if i > 0:
                 w, _ = self._views(self.shadow, i)
                 if plan["dgrad"][i]:
                     wt = LIN.transpose(w, out=ws["wt"][i])
+                    # K3 bias gradient of layer i - 1 fused into this dgrad's epilogue: per-128-row column
+                    # sums of dZ_{i-1} (fp32, before the bf16 store), then one fixed-order reduce
+                    part = ws["colpart"] if B % 128 == 0 else None
                     dz = LIN.linear_dgrad_nt(dz, wt, inputs[i], self.activation, out=ws["dz"][i - 1],
-                                             ct=ws["dzt"].get(i - 1))
+                                             ct=ws["dzt"].get(i - 1), colpart=part)
+                    if part is not None:
+                        _, gb_prev = self._views(self.grads, i - 1)
+                        LIN.colpart_reduce(part, B // 128, self.padded[i], gb_prev, accumulate=accumulate)
+                        fused_bias.add(i - 1)
                 else:
                     dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
         return dz

@@ -88,11 +88,17 @@ class DrawMLP(nn.Module):
 
 
 class FusedSmallMLP:
-    """Flagship trainer: 62->128->62 ReLU MLP, bf16 MFMA compute, fp32 master weights + Adam."""
+    """Flagship trainer: 62->128->62 ReLU MLP, bf16 MFMA compute, fp32 master weights + Adam.
+
+    Single process: ONE launch per optimizer step (``fused_mlp.train_step``: the slab reduction and
+    Adam run inside the train kernel, overlapping its slowest workgroups).  ``fused_adam=False`` (or
+    ``EUROM_FUSED_ADAM=0``) keeps the two-launch form (train kernel, then ``em_adam_slab``), which
+    gives bit-identical parameters.  Data parallel: train kernel -> all-reduce -> Adam."""
 
     def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
-                 state_dict: dict | None = None, process_group=None, comm: str = "auto"):
+                 state_dict: dict | None = None, process_group=None, comm: str = "auto",
+                 fused_adam: bool | None = None):
         from ..ops import fused_mlp as FM
         from ..ops import _native as N
 
@@ -122,6 +128,12 @@ class FusedSmallMLP:
         self.loss_slabs = torch.zeros(self.nslab_max, dtype=torch.float32, device=dev)
         self.grad_io = torch.zeros(P + 1, dtype=torch.float32, device=dev)  # [grads..., loss]
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sync = torch.zeros(FM.SYNC_WORDS, dtype=torch.int32, device=dev)  # one-launch step protocol words
+        import os
+
+        if fused_adam is None:
+            fused_adam = os.environ.get("EUROM_FUSED_ADAM", "1") != "0"
+        self.fused_adam = bool(fused_adam)
         FM.pack(self.params, self.img)
         self._checked = False
         # DP gradient all-reduce: "xgmi" = one-shot peer-memory reduction fused into the Adam
@@ -161,16 +173,22 @@ class FusedSmallMLP:
         """One optimizer step over B local samples (``draws`` = feature masks from :meth:`prepare`);
         returns the (global) mean loss as a device tensor."""
         FM = self.FM
-        # the train kernel advances the Adam step counter (one store), so no Adam launch below draws a
-        # grid-wide ticket for it (pre=True)
-        nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
-                                  offset=offset, sidx=sidx, check=not self._checked, step=self.state)
-        self._checked = True
         gb = global_batch if global_batch is not None else B * self.world
         scale = 1.0 / max(gb, 1)
         if self.loss_name == "bce":
             scale /= 62.0
         lscale = 1.0 / max(gb, 1) / (62.0 if self.loss_name == "bce" else 1.0)
+        if self.group is None and self.fused_adam:
+            FM.train_step(draws, B, self.img, self.slabs, self.loss_slabs, self.params, self.m, self.v, self.hp,
+                          self.state, self.sync, self.loss_out, scale, lscale, loss=self.loss_name, offset=offset,
+                          sidx=sidx, check=not self._checked)
+            self._checked = True
+            return self.loss_out
+        # the train kernel advances the Adam step counter (one store), so no Adam launch below draws a
+        # grid-wide ticket for it (pre=True)
+        nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
+                                  offset=offset, sidx=sidx, check=not self._checked, step=self.state)
+        self._checked = True
         if self.group is None:
             FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=0,
                          img=self.img, loss_slabs=self.loss_slabs, loss_out=self.loss_out, loss_scale=lscale, pre=True)
@@ -196,19 +214,24 @@ class FusedSmallMLP:
         """True when a step can be replayed from a hipGraph: single GPU, xGMI, or the RCCL path
         (an RCCL all-reduce is a stream-ordered kernel, captured like any other: the step has no
         host sync, so the fallback does not pay ~4 Python launches per 90 us step).  gloo
-        collectives run on the host and are never captured; ``EUROM_RCCL_GRAPH=0`` opts out."""
+        collectives run on the host and are never captured.  Captured RCCL steps have only been checked
+        against eager steps on a 1-rank group (the pool's boxes have one GPU), so replaying them is
+        opt-in: ``EUROM_RCCL_GRAPH=1``."""
         if self.group is None or self.xgmi is not None:
             return True
         import os
 
         import torch.distributed as dist
 
-        return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "1") != "0"
+        return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "0") == "1"
 
     def check_comm(self) -> None:
-        """Raise if an xGMI wait timed out (synchronises)."""
+        """Raise if an xGMI wait or a one-launch step's cross-workgroup wait timed out (synchronises)."""
         if self.xgmi is not None:
             self.xgmi.check()
+        if int(self.sync[self.FM.SYNC_ERR].item()) != 0:
+            raise RuntimeError("fused step: a workgroup's gradient slab never arrived (timeout); parameters of "
+                               "that step were left unchanged")
 
     def close(self) -> None:
         if self.xgmi is not None:

@@ -31,6 +31,10 @@ N.register_signatures({
                                      N._i32, N._i32, N._i32, N._i32, N._f32, N._i32, N._i32, N._i64, N._c_void_p]),
     "em_wgrad_skinny": (N._i32, [N._c_void_p, N._i64, N._c_void_p, N._i64, N._i32, N._i32, N._i32, N._c_void_p,
                                  N._i64, N._i32, N._f32, N._f32, N._c_void_p, N._i32, N._i32, N._c_void_p]),
+    "em_gemm_bf16_cs": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64,
+                                 N._i32, N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32,
+                                 N._f32, N._f32, N._c_void_p, N._i64, N._c_void_p, N._c_void_p]),
+    "em_colpart_reduce": (N._i32, [N._c_void_p, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p]),
     "em_colsum_ws_floats": (N._i32, [N._i32, N._i32]),
     "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p,
                                 N._c_void_p]),
@@ -73,9 +77,12 @@ def big_ok(M: int, N_: int, K: int) -> bool:
 
 def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Tensor, M: int, N_: int, K: int,
          bias: torch.Tensor | None = None, act: str = "none", dact_src: torch.Tensor | None = None,
-         dact: str = "relu", alpha: float = 1.0, beta: float = 0.0, ct: torch.Tensor | None = None) -> torch.Tensor:
+         dact: str = "relu", alpha: float = 1.0, beta: float = 0.0, ct: torch.Tensor | None = None,
+         colpart: torch.Tensor | None = None) -> torch.Tensor:
     """Raw K1-K3 launch.  ``a``/``b`` are bf16 in their storage shape; ``out`` fp32 or bf16 [M, N].
-    ``ct`` (bf16 [N, M], 256-path only) receives a transposed copy of the output."""
+    ``ct`` (bf16 [N, M], 256-path only) receives a transposed copy of the output.
+    ``colpart`` (fp32, >= M / 128 * N, 256-path only) receives the epilogue's column sums per 128 output
+    rows (the fused bias gradient of a dgrad: ``colpart_reduce`` sums them)."""
     for t, nm in ((a, "a"), (b, "b")):
         N.check_cuda(t, nm, torch.bfloat16, contiguous=False)
         if not is_aligned(t):
@@ -101,11 +108,30 @@ def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Te
         N.check_cuda(ct, "ct", torch.bfloat16, contiguous=False)
         if not (a_kc and b_kc and big_ok(M, N_, K)) or tuple(ct.shape) != (N_, M) or not is_aligned(ct):
             raise ValueError("ct needs the 256-tile NT path and an aligned bf16 [N, M] buffer")
-    N.call("em_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kc), b.data_ptr(), b.stride(0), int(b_kc),
-           out.data_ptr(), out.stride(0), int(out.dtype == torch.bfloat16), M, N_, K,
-           bias.data_ptr() if bias is not None else None, ACTS[act],
-           dact_src.data_ptr() if dact_src is not None else None, ldm, ACTS[dact] if dact_src is not None else 0,
-           float(alpha), float(beta), ct.data_ptr() if ct is not None else None, ct.stride(0) if ct is not None else 0,
+    args = (a.data_ptr(), a.stride(0), int(a_kc), b.data_ptr(), b.stride(0), int(b_kc),
+            out.data_ptr(), out.stride(0), int(out.dtype == torch.bfloat16), M, N_, K,
+            bias.data_ptr() if bias is not None else None, ACTS[act],
+            dact_src.data_ptr() if dact_src is not None else None, ldm, ACTS[dact] if dact_src is not None else 0,
+            float(alpha), float(beta), ct.data_ptr() if ct is not None else None, ct.stride(0) if ct is not None else 0)
+    if colpart is not None:
+        N.check_cuda(colpart, "colpart", torch.float32)
+        if not (a_kc and b_kc and big_ok(M, N_, K)) or colpart.numel() < (M // 128) * N_:
+            raise ValueError("colpart needs the 256-tile NT path and M / 128 * N floats")
+        N.call("em_gemm_bf16_cs", *args, colpart.data_ptr(), N.stream_handle(out.device))
+    else:
+        N.call("em_gemm_bf16", *args, N.stream_handle(out.device))
+    return out
+
+
+def colpart_reduce(part: torch.Tensor, nparts: int, n: int, out: torch.Tensor, accumulate: bool = False,
+                   scale: float = 1.0) -> torch.Tensor:
+    """``out[:n] (+)= scale * part.view(nparts, n).sum(0)`` in a fixed order (bias gradient from the
+    partials a ``colpart`` GEMM wrote)."""
+    N.check_cuda(part, "part", torch.float32)
+    N.check_cuda(out, "out", torch.float32)
+    if part.numel() < nparts * n or out.numel() < n:
+        raise ValueError("colpart_reduce: buffer too small")
+    N.call("em_colpart_reduce", part.data_ptr(), int(nparts), int(n), out.data_ptr(), int(accumulate), float(scale),
            N.stream_handle(out.device))
     return out
 
@@ -135,15 +161,17 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, act:
 
 
 def linear_dgrad_nt(dz: torch.Tensor, wt: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",
-                    out: torch.Tensor | None = None, ct: torch.Tensor | None = None) -> torch.Tensor:
-    """dgrad from a transposed weight copy ``wt`` [K, N] (256-tile NT path): ``(dz @ wt.T) * act'(y_prev)``."""
+                    out: torch.Tensor | None = None, ct: torch.Tensor | None = None,
+                    colpart: torch.Tensor | None = None) -> torch.Tensor:
+    """dgrad from a transposed weight copy ``wt`` [K, N] (256-tile NT path): ``(dz @ wt.T) * act'(y_prev)``;
+    ``colpart`` gets the bias-gradient partials of the result (see :func:`gemm`)."""
     M, N_ = dz.shape
     K = wt.shape[0]
     if out is None:
         out = empty_aligned(M, K, torch.bfloat16, dz.device)
     if dact in ("none", "identity"):
         y_prev = None
-    return gemm(dz, True, wt, True, out, M, K, N_, dact_src=y_prev, dact=dact, ct=ct)
+    return gemm(dz, True, wt, True, out, M, K, N_, dact_src=y_prev, dact=dact, ct=ct, colpart=colpart)
 
 
 def linear_wgrad_nt(dzt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None,

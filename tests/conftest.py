@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run through gpurun)")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "perf: performance guard (timing; tolerant of box-to-box variance)")
 
 
 def pytest_collection_modifyitems(config, items):

@@ -183,9 +183,10 @@ def test_no_restart_fails_loudly(tmp_path):
 
 
 def test_sync_check_detects_divergence(tmp_path):
-    """Local steps that are never averaged diverge; the checker must fail loudly."""
-    outs = _launch(_train_argv(["--steps", "3", "--batch", "128", "--avg-frequency", "1000",
-                                "--check-sync-every", "3"]), 2)
+    """Local steps that are not averaged yet diverge; the checker (step 2, long before the first
+    averaging point and the end-of-run average) must fail loudly."""
+    outs = _launch(_train_argv(["--steps", "4", "--batch", "128", "--avg-frequency", "1000",
+                                "--check-sync-every", "2"]), 2)
     assert all(rc != 0 for rc, _ in outs)
     assert any("diverged" in o for _, o in outs)
 

@@ -24,14 +24,24 @@ def _ref_grads(sd, ds_numbers, offset, B, loss, bf16=True):
     return l.item(), {"l1.weight": W1.grad, "l1.bias": b1.grad, "l2.weight": W2.grad, "l2.bias": b2.grad}, z.detach()
 
 
-@pytest.fixture(params=[6, 4], ids=["v6", "v4"])
-def kernel(request):
-    """Run the test on the producer/consumer kernel (v6, default) and the hidden-split pairs (v4)."""
+@pytest.fixture(params=["one-launch", "split"])
+def kernel(request, monkeypatch):
+    """Run the test on both step forms: the one-launch step (train kernel with the in-launch Adam
+    epilogue, the default) and the split form (train kernel, then em_adam_slab)."""
+    monkeypatch.setenv("EUROM_FUSED_ADAM", "1" if request.param == "one-launch" else "0")
+    yield request.param
+
+
+def _assert_grads_close(gk, gr, tol=1e-2):
+    """Per tensor (W1, b1, W2, b2 views of the flat gradient), relative L2 error <= tol against the
+    fp32 reference built from the same bf16-rounded operands: a single zeroed bias column (1/62 of b2)
+    or weight row moves its tensor's error by >= ~10 %."""
     from euromillioner_amd.ops import fused_mlp as FM
 
-    prev = FM.select_kernel(request.param)
-    yield request.param
-    FM.select_kernel(prev)
+    got, ref = FM.unflatten(gk), FM.unflatten(FM.flatten(gr, device="cuda"))
+    for name in ("l1.weight", "l1.bias", "l2.weight", "l2.bias"):
+        err = float((got[name] - ref[name]).norm() / ref[name].norm().clamp_min(1e-30))
+        assert err < tol, (name, err)
 
 
 @pytest.fixture(scope="module")
@@ -52,10 +62,8 @@ def test_fused_grads_match_reference(data, loss, B, offset, kernel):
     m = FusedSmallMLP(loss=loss, seed=5)
     lk, gk = m.grads(draws, B, offset=offset)
     lr_, gr, _ = _ref_grads(m.state_dict(), ds.numbers, offset, B, loss)
-    gflat = FM.flatten(gr, device="cuda")
     assert abs(lk - lr_) <= 2e-3 * max(1.0, abs(lr_)), (lk, lr_)
-    err = (gk - gflat).norm() / gflat.norm()
-    assert err < 2e-2, float(err)
+    _assert_grads_close(gk, gr)
     # padding slots carry exactly zero gradient
     assert float((gk * (1 - FM.pad_mask("cuda"))).abs().max()) == 0.0
 
@@ -101,8 +109,9 @@ def test_fused_adam_matches_torch(data):
 
 
 def test_step_counter_advanced_by_train_kernel(data, kernel):
-    """FusedSmallMLP.step: the train kernel advances the Adam step counter and Adam reads it without
-    a ticket (pre mode).  Must equal the ticket path (gradient via mode 1, Adam via mode 2) bit for bit."""
+    """FusedSmallMLP.step (one launch: the in-launch Adam advances the counter; split: the train kernel
+    advances it and Adam reads it without a ticket) must equal the ticket path (gradient via mode 1,
+    Adam via mode 2) bit for bit: both slab reductions sum in the same fixed order."""
     from euromillioner_amd.models.mlp import FusedSmallMLP
     from euromillioner_amd.ops import fused_mlp as FM
 
@@ -204,18 +213,57 @@ def test_fused_grads_property_random_batches(kernel):
         m = models[loss]
         lk, gk = m.grads(draws, B, offset=offset)
         lr_, gr, _ = _ref_grads(m.state_dict(), ds.numbers, offset, B, loss)
-        gflat = FM.flatten(gr, device="cuda")
         assert abs(lk - lr_) <= 2e-3 * max(1.0, abs(lr_)), (B, offset, loss, lk, lr_)
-        err = float((gk - gflat).norm() / gflat.norm())
-        assert err < 2e-2, (B, offset, loss, err)
+        # a handful of samples: per-tensor norms are dominated by a few bf16 roundings of dZ
+        _assert_grads_close(gk, gr, tol=1e-2 if B >= 256 else 3e-2)
 
     check()
 
 
-def test_select_kernel_rejects_unknown():
-    from euromillioner_amd.ops import fused_mlp as FM
+def test_one_launch_step_equals_split_step(data):
+    """The one-launch step (slab reduction + Adam inside the train kernel, cross-workgroup hand-off)
+    and the split step (train kernel, then em_adam_slab) give bit-identical parameters, moments,
+    weight images, losses and step counters over several steps and batch sizes (grid sizes 1..256)."""
+    from euromillioner_amd.models.mlp import FusedSmallMLP
 
-    with pytest.raises(ValueError):
-        FM.select_kernel(7)
-    prev = FM.select_kernel(4)
-    assert FM.select_kernel(prev) == 4
+    _, draws = data
+    for loss in ("softmax", "bce"):
+        a = FusedSmallMLP(loss=loss, seed=6, lr=3e-3, fused_adam=True)
+        b = FusedSmallMLP(loss=loss, seed=6, lr=3e-3, fused_adam=False)
+        for it, B in enumerate((5000, 37, 128, 129, 4096, 1)):
+            la = float(a.step(draws, B, offset=13 * it).item())
+            lb = float(b.step(draws, B, offset=13 * it).item())
+            assert la == lb, (loss, B, la, lb)
+        torch.cuda.synchronize()
+        a.check_comm()
+        assert int(a.state[0]) == int(b.state[0]) == 6
+        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+        assert torch.equal(a.img, b.img)
+
+
+def test_one_launch_step_replays_from_graph(data):
+    """hipGraph capture of the one-launch step (the bench's form): replays equal eager steps bit for
+    bit, i.e. the epoch-tagged flags / dequeue head / step counter re-arm themselves every launch."""
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    _, draws = data
+    a = FusedSmallMLP(loss="softmax", seed=8, lr=3e-3)
+    b = FusedSmallMLP(loss="softmax", seed=8, lr=3e-3)
+    B = 4096
+    a.step(draws, B, offset=0)  # first launch eager (argument checks), then capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            a.step(draws, B, offset=100)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(5):
+        g.replay()
+    b.step(draws, B, offset=0)
+    for _ in range(5):
+        b.step(draws, B, offset=100)
+    torch.cuda.synchronize()
+    a.check_comm()
+    assert int(a.state[0]) == int(b.state[0]) == 6
+    assert torch.equal(a.params, b.params) and torch.equal(a.img, b.img)

@@ -18,6 +18,38 @@ def _rel(a, b):
 
 
 ACT = {"none": lambda x: x, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}
+DACT = {"relu": lambda y: (y > 0).float(), "sigmoid": lambda y: y * (1 - y), "tanh": lambda y: 1 - y * y}
+
+
+def _bf16_chain_grads(tr, X, Y, loss="softmax"):
+    """fp32 reference of the GEMM trainer's step with the SAME bf16 roundings the kernels apply: bf16
+    weights (the shadow), bf16 hidden activations and bf16 dL/dZ between layers; fp32 accumulation,
+    fp32 weight / bias gradients.  What remains between it and the kernels is fp32 summation order, so
+    a per-tensor tolerance of 1e-2 is tight: one zeroed bias column or weight row fails it."""
+    sd = tr.state_dict()
+    n_layers = len(tr.sizes) - 1
+    Ws = [_bf(sd[f"layers.{i}.weight"].cuda().float()) for i in range(n_layers)]
+    bs = [sd[f"layers.{i}.bias"].cuda().float() for i in range(n_layers)]
+    hs = [X.cuda()]
+    for i in range(n_layers - 1):
+        hs.append(_bf(ACT[tr.activation](hs[-1] @ Ws[i].t() + bs[i])))
+    logits = (hs[-1] @ Ws[-1].t() + bs[-1]).detach().requires_grad_()
+    lv = L.LOSSES[loss](logits, Y.cuda())
+    lv.backward()
+    dz = _bf(logits.grad)
+    out = {}
+    for i in reversed(range(n_layers)):
+        out[f"layers.{i}.weight"] = dz.t() @ hs[i]
+        out[f"layers.{i}.bias"] = dz.sum(0)
+        if i > 0:
+            dz = _bf((dz @ Ws[i]) * DACT[tr.activation](hs[i]))
+    return lv.item(), out
+
+
+def _assert_tight(gk, ref, tol=1e-2):
+    for n, g in ref.items():
+        err = _rel(gk[n], g)
+        assert err < tol, (n, err)
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 200, 70), (128, 128, 64), (1, 7, 5), (517, 1030, 333)])
@@ -148,6 +180,7 @@ def test_gemm_trainer_grads_match_drawmlp(data, sizes):
     assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
     for n, p in ref.named_parameters():
         assert _rel(gk[n].cpu(), p.grad) < 5e-2, n
+    _assert_tight(gk, _bf16_chain_grads(tr, X, Y)[1])
     # the pads of the flat buffers stay zero
     sd = tr.state_dict()
     for n, p in ref.named_parameters():
@@ -246,6 +279,29 @@ def test_gemm_trainer_big_plan_matches_drawmlp(data):
     assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
     for n, p in ref.named_parameters():
         assert _rel(gk[n].cpu(), p.grad) < 5e-2, n
+    # the bias gradients of layers 0 and 1 come from the 256-tile dgrad epilogues (fused colsum partials)
+    _assert_tight(gk, _bf16_chain_grads(tr, X, Y)[1])
+
+
+def test_fused_bias_partials_catch_a_dropped_column(data):
+    """The tight reference rejects a bias gradient with ONE column zeroed (the check the fused
+    bias-gradient epilogue is held to): mutation test of _assert_tight itself."""
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+
+    ds, masks = data
+    sizes, B, off = (62, 512, 256, 62), 1024, 3
+    tr = GemmMLPTrainer(sizes, seed=2)
+    X = torch.from_numpy(multi_hot(ds.numbers[off:off + B])).float()
+    Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).float()
+    _, gk = tr.grads_only(masks, B, offset=off)
+    ref = _bf16_chain_grads(tr, X, Y)[1]
+    _assert_tight(gk, ref)
+    for name in ("layers.0.bias", "layers.1.bias", "layers.2.bias"):
+        bad = dict(gk)
+        bad[name] = gk[name].clone()
+        bad[name][int(gk[name].abs().argmax())] = 0.0
+        with pytest.raises(AssertionError):
+            _assert_tight(bad, ref)
 
 
 @pytest.mark.parametrize("M,N,K,big", [(256, 512, 256, True), (128, 96, 128, False), (300, 200, 300, False)])
@@ -328,6 +384,7 @@ def test_gemm_trainer_odd_wide_layers_take_the_tile_path(data):
     assert abs(lk - l.item()) < 1e-2 * max(1, l.item())
     for n, p in ref.named_parameters():
         assert _rel(gk[n].cpu(), p.grad) < 5e-2, n
+    _assert_tight(gk, _bf16_chain_grads(tr, X, Y)[1])
     tr.step(masks, B, offset=off)
     torch.cuda.synchronize()
     w1, _ = tr._views(tr.params, 1)  # [1024, 1024]: rows/cols 1000.. are padding

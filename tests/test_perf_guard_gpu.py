@@ -10,7 +10,7 @@ catch a structural regression (e.g. the run-time staging-lead flag in the GEMM's
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.perf]
 
 
 def _time(fn, iters):
@@ -39,7 +39,12 @@ def test_gemm_256_tile_within_reach_of_hipblaslt():
         t_ours = _time(lambda: LIN.linear_fwd(x, w, None, "none", out=y), 10)
         t_lib = _time(lambda: torch.nn.functional.linear(x, w), 10)
         best = max(best, t_lib / t_ours)
-    assert best > 0.82, f"256-tile GEMM at {best:.2f} x hipBLASLt throughput (measured 0.88-0.90)"
+    # 0.75: below the box-to-box spread (~15 %, profiles/gemm_box_variance.md) of the 0.88-0.90 measured;
+    # EUROM_PERF_GEMM_FLOOR=0.82 restores the tighter structural guard on a known box
+    import os
+
+    floor = float(os.environ.get("EUROM_PERF_GEMM_FLOOR", "0.75"))
+    assert best > floor, f"256-tile GEMM at {best:.2f} x hipBLASLt throughput (measured 0.88-0.90)"
 
 
 def test_fused_step_time():

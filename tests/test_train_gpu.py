@@ -92,10 +92,13 @@ def test_dp_code_path_on_one_rank_matches_local(engine):
     assert torch.allclose(dp.params, local.params, atol=1e-6, rtol=0), float((dp.params - local.params).abs().max())
 
 
-def test_rccl_step_replays_from_a_hipgraph():
+def test_rccl_step_replays_from_a_hipgraph(monkeypatch):
     """The fused model's RCCL fallback (slab reduce -> RCCL all-reduce -> Adam) is graph-safe: steps
-    captured in one hipGraph and replayed equal the same steps run eagerly on a local model."""
+    captured in one hipGraph and replayed equal the same steps run eagerly on a local model
+    (opt-in, EUROM_RCCL_GRAPH=1, until a multi-GPU node confirms it at world > 1)."""
     import torch
+
+    monkeypatch.setenv("EUROM_RCCL_GRAPH", "1")
 
     from euromillioner_amd.data.draws import DrawSet
     from euromillioner_amd.models.mlp import FusedSmallMLP

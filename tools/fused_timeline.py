@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Per-block wall-clock timeline of the fused v4 train kernel inside a 10-launch hipGraph (steady clock).
-Needs a V4_STAMPS=1 build.  Prints, per batch size, the spread of block entry, prologue, loop and fold
-times of the LAST launch of the graph, plus the per-role phase split."""
+"""Per-block wall-clock timeline of the fused train kernel (csrc/mlp_fused.hip) inside a 10-launch
+hipGraph (steady clock).  Needs a diagnostic build: ``python -m euromillioner_amd._build --define
+FUSED_STAMPS=1`` into a side library (EUROM_NATIVE_LIB), never the shipped one -- the stamps drain LDS
+counters at every mark.  Prints, per batch size, the spread of block entry, prologue, loop and slab-write
+times of the LAST launch of the graph, the per-XCD-group loop medians and the forward / backward wave
+phase split (s_memtime cycles, ``Stamps`` marks 0-9)."""
 from __future__ import annotations
 
 import os
@@ -10,10 +13,10 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PHASES = ["F1+relu+Himg", "F2 own", "wait H", "F2 partner+Ximg", "loss part1", "wait stats", "dz+pack+D2",
-          "wait dz", "B1+mask", "dW+db2"]
+NAMES = ["F wait slot", "F X+F1+H", "F F2", "F loss", "F D2+signal",
+         "B wait full", "B reads", "B B1+dW2+db2", "B mask", "B dW1T"]
 
 
 def main():
@@ -54,20 +57,11 @@ def main():
         xcd = np.arange(nslab) % 8
         print("   loop median per blockIdx%8:", " ".join("%.1f" % np.median(loop[xcd == k]) for k in range(8)))
         st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
-        if os.environ.get("EM_FUSED_V6") == "1":
-            names = ["F wait slot", "F X+F1+H", "F F2", "F loss", "F D2+signal",
-                     "B wait full", "B reads+B1+mask", "B dW2+db2+bx", "B signal", "B dW1T"]
-            for nm, ws in (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5])):
-                v = st[:, ws, :].reshape(-1, 10).mean(0)
-                tot = v.sum()
-                print(f"   {nm}: {tot / 1e3:.1f} k cycles/wave; " +
-                      ", ".join(f"{n} {x / 1e3:.1f}k" for n, x in zip(names, v) if x > 0))
-            continue
-        for role in (0, 1):
-            v = st[:, role::2, :].reshape(-1, 10).mean(0)
+        for nm, ws in (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5])):  # wave -> role map of the kernel
+            v = st[:, ws, :].reshape(-1, 10).mean(0)
             tot = v.sum()
-            print(f"   role {role}: {tot / 1e3:.1f} k cycles/wave; " +
-                  ", ".join(f"{n} {x / tot * 100:.0f}%" for n, x in zip(PHASES, v)))
+            print(f"   {nm}: {tot / 1e3:.1f} k cycles/wave; " +
+                  ", ".join(f"{n} {x / 1e3:.1f}k" for n, x in zip(NAMES, v) if x > 0))
 
 
 if __name__ == "__main__":
