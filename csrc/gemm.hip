@@ -1075,6 +1075,182 @@ __global__ void __launch_bounds__(256) transpose_kernel(const __bf16* __restrict
   }
 }
 
+// ============================================================================================
+// Skinny-K GEMM (K = 64 or 128): the wide MLP's first-layer forward (X[B,64] W0ᵀ) and last-layer
+// dgrad (dZ[B,64] W2) write a [B, 8192] bf16 output plus its transposed copy, with almost no
+// arithmetic (2 GB written per 8 MFLOP-ish tile work).  On the 256-tile ping-pong kernel (1 block /
+// CU, 226 VGPRs, epilogue serialized per wave) they ran at 2.9-3.4 TB/s.  This kernel is built for
+// the store stream instead: 128 x 128 tiles, 4 waves (2 x 2, 64 x 64 each, 16 MFMAs), <= 128 VGPRs
+// and 40 KB of LDS so 4 workgroups share a CU and hide each other's epilogue latencies.
+//   * the whole K of the tile is staged once (register staging, XOR-swizzled [128][64] images);
+//   * epilogue per wave: act'(mask) via ds_read_b64_tr_b16 of a staged 64 x 64 mask block (4 rows of
+//     one column per read = the accumulator layout), bf16 values into a [col][row] image T, then C
+//     rows (128 B per row: two transposed reads per 16 B) and C^T rows (128 B straight from T);
+//   * optional column sums (fused bias gradient, same [M / 128][N] partial format as the 256 path).
+constexpr int K64_BM = 128, K64_BN = 128, K64_NT = 256;
+constexpr int K64_TS = 144;                          // bytes per T row: 64 bf16 + 16 pad
+constexpr int K64_WEPI = 64 * K64_TS;                // 9216 B per wave
+constexpr int K64_LDS = 4 * K64_WEPI + 4 * 8 * 1024;  // T images + staged 64 x 64 mask blocks (8 KB / wave)
+static_assert(K64_LDS >= 2 * K64_BM * 64 * 2, "operand tiles must fit");
+
+template <int FN, int DACT, int HAS_CT>
+__global__ void __launch_bounds__(K64_NT, 4)
+gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                __bf16* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
+                const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
+                float* __restrict__ colpart) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = N / K64_BN;
+  const int bid = xcd_remap(blockIdx.x, (M / K64_BM) * tiles_n);
+  const int m0 = (bid / tiles_n) * K64_BM, n0 = (bid % tiles_n) * K64_BN;
+  const int r = lane & 31, h = lane >> 5;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  for (int k0 = 0; k0 < K; k0 += 64) {
+    u32x4 rs[4];  // one staging set for both operands (keeps the kernel at <= 128 VGPRs, 4 blocks / CU)
+    if (k0) __syncthreads();  // the previous K tile's fragments are read
+    load_tile<1>(A, lda, m0, k0, M, K, tid, rs);
+    store_tile<1>(smem, tid, rs);
+    load_tile<1>(B, ldb, n0, k0, N, K, tid, rs);
+    store_tile<1>(smem + K64_BM * 128, tid, rs);
+    __syncthreads();
+    const char* la = smem;
+    const char* lb = smem + K64_BM * 128;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 a0 = frag<1>(la, wm * 64 + r, s, lane), a1 = frag<1>(la, wm * 64 + 32 + r, s, lane);
+      const bf16x8 b0 = frag<1>(lb, wn * 64 + r, s, lane), b1 = frag<1>(lb, wn * 64 + 32 + r, s, lane);
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+    }
+  }
+  __syncthreads();  // operand tiles dead: the LDS becomes the epilogue images
+
+  char* tb = smem + wave * K64_WEPI;
+  char* yb = smem + 4 * K64_WEPI + wave * 8192;  // [64 rows][64 cols] bf16, 128-B rows, 16-B chunk ^= row & 7
+  const int rowb = m0 + wm * 64, colw = n0 + wn * 64;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, gq = lane >> 4;
+  if (DACT) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {  // 512 chunks of 16 B: rows q >> 3, chunk q & 7
+      const int q = lane + 64 * t, row = q >> 3, ch = q & 7;
+      *reinterpret_cast<u32x4*>(yb + row * 128 + ((ch ^ (row & 7)) << 4)) =
+          *reinterpret_cast<const u32x4*>(mask + (int64_t)(rowb + row) * ldm + colw + ch * 8);
+    }
+    wave_lds_sync();
+  }
+  float cs[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int lc = 32 * j + r;
+    const float bv = (!DACT && bias) ? bias[colw + lc] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int lr = 32 * i + 8 * g + 4 * h;  // the lane's 4 consecutive rows lr .. lr + 3, column lc
+        float y[4] = {0.f, 0.f, 0.f, 0.f};
+        if (DACT) {  // transposed read: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3
+          const int rr = 32 * i + 8 * g + 4 * (gq >> 1) + q4, cc = 32 * j + 16 * (gq & 1) + 4 * p4;
+          const s16x4 m4 = lds_tr16(yb, (uint32_t)(rr * 128 + (((cc >> 3) ^ (rr & 7)) << 4) + (cc & 7) * 2));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[e] = bf16_bits_to_f32((uint16_t)m4[e]);
+        }
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = alpha * acc[i][j][4 * g + e];
+          v = DACT ? v * g_dfn<FN>(y[e]) : g_fn<FN>(v + bv);
+          x[e] = v;
+          cs[j] += v;
+        }
+        *reinterpret_cast<u32x2*>(tb + lc * K64_TS + lr * 2) = u32x2{pack2(x[0], x[1]), pack2(x[2], x[3])};
+      }
+  }
+  wave_lds_sync();
+  // C rows: per iteration a 16-lane group writes 16 rows x 8 columns (one 16-B store per lane)
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int cb = 8 * it, r0 = 16 * gq;
+    const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * K64_TS + (r0 + 4 * p4) * 2));
+    const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * K64_TS + (r0 + 4 * p4) * 2));
+    *reinterpret_cast<bf16x8*>(C + (int64_t)(rowb + r0 + i16) * ldc + colw + cb) = cat_tr(lo, hi);
+  }
+  if (HAS_CT) {  // C^T row = one column of the block: 64 rows = 128 B straight from T
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = lane + 64 * k, col = q >> 3, part = q & 7;
+      *reinterpret_cast<u32x4*>(CT + (int64_t)(colw + col) * ldct + rowb + part * 8) =
+          *reinterpret_cast<const u32x4*>(tb + col * K64_TS + part * 16);
+    }
+  }
+  if (colpart) {  // bias-gradient partials, row (m0 >> 7) of [M / 128][N]: the two wm waves add via LDS
+#pragma unroll
+    for (int j = 0; j < 2; ++j) cs[j] = xhalf_sum(cs[j]);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2 wn][64 cols] of the wm = 1 waves
+    if (wm == 1 && h == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[wn * 64 + 32 * j + r] = cs[j];
+    }
+    __syncthreads();
+    if (wm == 0 && h == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        colpart[(int64_t)(m0 >> 7) * N + colw + 32 * j + r] = cs[j] + red[wn * 64 + 32 * j + r];
+    }
+  }
+}
+
+template <int FN, int DACT, int HAS_CT>
+int k64_launch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
+               __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask, int64_t ldm,
+               float alpha, float* colpart) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_k64_kernel<FN, DACT, HAS_CT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, K64_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), K64_LDS, st,
+                     A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart);
+  return 0;
+}
+
+// runtime (act / dact, ct) -> instantiation; bf16 output only
+int k64_dispatch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
+                 __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act, const __bf16* mask,
+                 int64_t ldm, int dact, float alpha, float* colpart) {
+#define EM_K(FN, DA, CTV) \
+  return k64_launch<FN, DA, CTV>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart)
+  const bool ct = CT != nullptr;
+  if (mask) {
+    if (act != ACT_NONE) return EM_ERR_ARG;
+    switch (dact) {
+      case ACT_RELU: if (ct) EM_K(ACT_RELU, 1, 1); else EM_K(ACT_RELU, 1, 0);
+      case ACT_SIGMOID: if (ct) EM_K(ACT_SIGMOID, 1, 1); else EM_K(ACT_SIGMOID, 1, 0);
+      case ACT_TANH: if (ct) EM_K(ACT_TANH, 1, 1); else EM_K(ACT_TANH, 1, 0);
+      default: return EM_ERR_ARG;
+    }
+  }
+  switch (act) {
+    case ACT_NONE: if (ct) EM_K(ACT_NONE, 0, 1); else EM_K(ACT_NONE, 0, 0);
+    case ACT_RELU: if (ct) EM_K(ACT_RELU, 0, 1); else EM_K(ACT_RELU, 0, 0);
+    case ACT_SIGMOID: if (ct) EM_K(ACT_SIGMOID, 0, 1); else EM_K(ACT_SIGMOID, 0, 0);
+    case ACT_TANH: if (ct) EM_K(ACT_TANH, 0, 1); else EM_K(ACT_TANH, 0, 0);
+    default: return EM_ERR_ARG;
+  }
+#undef EM_K
+}
+
 // column sums of a bf16 [M][N] matrix (bias gradients), deterministic two-pass:
 // pass 1: block (column group of 512, row chunk of CS_ROWS) -> fp32 partial [chunk][N]
 // pass 2: fixed-order sum over chunks (+ optional accumulate / scale)
@@ -1341,6 +1517,16 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
   const bool big = splits == 1 && a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
                    (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL") &&
                    (c_bf16 || (act == ACT_NONE && !mask));  // fp32 + act / act' epilogues: any-layout kernel
+  // skinny K (64 / 128) with a bf16 output: the store-stream kernel (see gemm_k64_kernel); EM_GEMM_K64=0
+  // keeps the 256-tile path for A/B
+  static const bool k64_on = !getenv_flag_off("EM_GEMM_K64");
+  if (big && k64_on && c_bf16 && (K == 64 || K == 128) && beta == 0.f) {
+    const int rc = k64_dispatch(stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, (__bf16*)C, ldc, (__bf16*)ct,
+                                ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha, colpart);
+    if (rc) return rc;
+    EM_CHECK_LAUNCH();
+    return 0;
+  }
   if (big) {
     const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
                               ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,

@@ -256,7 +256,10 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
 constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[N] | done0[N] | done1[N]
-constexpr int V6_RING = V6_FLAGS + 128;  // [2 units][3 slots][16 KB]
+// scaled target tables (FUSED_FASTY): nibble -> 4 x {0, -1/5} (main), {0, -1/2} (stars) and the
+// nibble of outputs 48-51 that straddles the groups ({-1/5, -1/5, -1/2, -1/2} per bit)
+constexpr int V6_YM = V6_FLAGS + 128, V6_YS = V6_YM + 256, V6_YMS = V6_YS + 256;
+constexpr int V6_RING = V6_YMS + 256;  // [2 units][3 slots][16 KB]
 constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_RSLOTS * V6_SLOT;
 // byte offset of ring slot `slot` of unit `unit`
 EM_DEVICE uint32_t v6_slot(int unit, int slot) {
@@ -267,6 +270,9 @@ constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 204
 static_assert(V6_LDS <= 163840 && V6_RING % 16 == 0, "v6 LDS budget");
 static_assert(IMG_BYTES == 54528 && IMG_BYTES % 16 == 0, "image size (ops/fused_mlp.py IMG_BYTES)");
 constexpr int V6_SPIN_LIMIT = 1 << 20;  // ~50 ms of polling: a legitimate wait is microseconds
+#ifndef FUSED_FASTY
+#define FUSED_FASTY 0  // 2: scaled target tables only (A/B diagnostic; standard 5 + 2 draws only)
+#endif
 
 // wait until the LDS counter at off reaches target (skipped once a wait has failed: the launch then
 // drains quickly and reports NaN)
@@ -302,7 +308,12 @@ EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
 // and 58-63 straddle the group edges), so every statically classified element emits only its own
 // group's ops (a select-form "x ? v : 0" fed into an fma would have to be kept: fma(0, inf, a) is
 // NaN).  Max / sum / target-dot reductions run as independent partial chains.
-template <int YL, typename Hook>
+//
+// FAST (every sample of the tile has 5 main / 2 star targets, or none: a padding row -- i.e. every
+// real Euromillions draw): the targets are read from tables that already hold -y / n_group, so
+// dZ2 = p - y / n is ONE fma per output and the target logit sum needs no per-group split
+// (32 multiplies and the star chain fewer per tile than the general form).
+template <int YL, bool FAST, typename Hook>
 EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
                                 float& loss_acc, Hook&& hook) {
   constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
@@ -310,7 +321,9 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      int base = YL;
+      if (FAST) base = (u == 0 || g < 2) ? V6_YM : (g == 2 && h == 0) ? V6_YMS : V6_YS;
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + base + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
       yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
     }
   };
@@ -381,19 +394,25 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
       } else if (c0 == 1) {
         e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL));
         ss[i & 1] += e;
-        ts[i & 1] = __builtin_fmaf(yb1[i], v, ts[i & 1]);
+        if (FAST) tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);
+        else ts[i & 1] = __builtin_fmaf(yb1[i], v, ts[i & 1]);
       }
     } else if (c0 == 0) {
       e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, h0 ? nmL : nsL));
-      const float ty = yb1[i] * v;
       s1p[i & 1] = h0 ? s1p[i & 1] + e : s1p[i & 1];
       ss[i & 1] = h0 ? ss[i & 1] : ss[i & 1] + e;
-      tm[i & 3] = h0 ? tm[i & 3] + ty : tm[i & 3];
-      ts[i & 1] = h0 ? ts[i & 1] : ts[i & 1] + ty;
+      if (FAST) {  // main (h = 0) or star (h = 1): the table already carries the group's -1 / n
+        tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);
+      } else {
+        const float ty = yb1[i] * v;
+        tm[i & 3] = h0 ? tm[i & 3] + ty : tm[i & 3];
+        ts[i & 1] = h0 ? ts[i & 1] : ts[i & 1] + ty;
+      }
     } else {
       e = h0 ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL)) : 0.f;
       ss[i & 1] += e;
-      ts[i & 1] = h0 ? __builtin_fmaf(yb1[i], v, ts[i & 1]) : ts[i & 1];
+      if (FAST) tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);  // pad targets are 0: adds 0
+      else ts[i & 1] = h0 ? __builtin_fmaf(yb1[i], v, ts[i & 1]) : ts[i & 1];
     }
     dz[1][i] = e;
   }
@@ -412,18 +431,20 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     for (int i = 0; i < 16; ++i) {
       const int c0 = out_cls(u, i, 0), c1 = out_cls(u, i, 1);
       const float fm = u == 0 ? f0 : f1;
+      const float ym = FAST ? yb[i] : yb[i] * ni_m, ys = FAST ? yb[i] : yb[i] * ni_s;
       if (c0 == c1) {
-        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, yb[i] * ni_m);
-        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
+        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, ym);
+        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, ys);
         if (c0 == 2) dz[u][i] = 0.f;
       } else if (c0 == 0) {
-        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? fm : f_s, yb[i] * (h0 ? ni_m : ni_s));
+        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? fm : f_s, FAST ? yb[i] : yb[i] * (h0 ? ni_m : ni_s));
       } else {  // the pad lanes' e is 0 and their target bit (outputs 62/63) is 0
-        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
+        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, ys);
       }
     }
   }
-  float l = -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
+  float l = FAST ? ((tm[0] + tm[1]) + (tm[2] + tm[3]))
+                 : -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
   if (h == 0)
     l += (nm ? M + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
   loss_acc += l;
@@ -530,7 +551,16 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
           __builtin_amdgcn_sched_barrier(0);
         }
       };
-      v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, lt, hook);
+      // wave-uniform: FAST when every sample of the tile has 5 + 2 targets (or is padding)
+      const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
+      const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);
+      const int ns = __builtin_popcount(thi & 0x3FFC0000u);
+      const bool std_draw = (nm == 5 || nm == 0) && (ns == 2 || ns == 0);
+      (void)std_draw;
+      if (FUSED_FASTY == 2)  // diagnostic A/B build: scaled tables only (valid for standard draws only)
+        v6_softmax_split<V6_YLUT, true>(smem, z2, tmask, h, dz, lt, hook);
+      else
+        v6_softmax_split<V6_YLUT, false>(smem, z2, tmask, h, dz, lt, hook);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
@@ -892,7 +922,13 @@ mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
     for (int k = 0; k < KK; ++k)
       if (tid + 512 * k < N16) dst[tid + 512 * k] = v[k];
   }
-  if (tid < 64) reinterpret_cast<float*>(smem + V6_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
+  if (tid < 64) {
+    const float bit = (float)(((tid >> 2) >> (tid & 3)) & 1);
+    reinterpret_cast<float*>(smem + V6_YLUT)[tid] = bit;
+    reinterpret_cast<float*>(smem + V6_YM)[tid] = -0.2f * bit;
+    reinterpret_cast<float*>(smem + V6_YS)[tid] = -0.5f * bit;
+    reinterpret_cast<float*>(smem + V6_YMS)[tid] = ((tid & 3) < 2 ? -0.2f : -0.5f) * bit;
+  }
   if (tid < 32) {
     const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
     reinterpret_cast<uint32_t*>(smem + V6_XLUT)[tid] =

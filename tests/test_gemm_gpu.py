@@ -203,9 +203,11 @@ def test_gemm_trainer_learns_planted(data):
     assert ev["acc"] > ev["trivial_acc"], ev
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 256, 4096)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 256, 4096), (1024, 2048, 64),
+                                   (768, 512, 128)])
 @pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh"])
 def test_big_nt_forward_with_transposed_copy(M, N, K, act):
+    """K = 64 / 128 shapes run the skinny-K store-stream kernel (gemm_k64_kernel), the others the 256 tile."""
     from euromillioner_amd.ops import linear as LIN
 
     assert LIN.big_ok(M, N, K)
@@ -245,6 +247,39 @@ def test_big_nt_dgrad_and_wgrad(dact):
     gw = LIN.linear_wgrad_nt(LIN.transpose(dz), LIN.transpose(x))
     assert _rel(gw, dz.float().t() @ x.float()) < 1e-5
     assert _rel(LIN.rowsum(LIN.transpose(dz)), dz.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("dact,K", [("relu", 64), ("sigmoid", 128), ("relu", 768), ("tanh", 256)])
+def test_dgrad_fused_bias_partials(dact, K):
+    """The dgrad epilogue's column sums (fused bias gradient): colpart rows = sums over 128 output
+    rows of the fp32 epilogue values; the fixed-order reduce equals dZ.sum(0) of the reference, and
+    the bf16 output / transposed copy are unchanged by the extra work.  K = 64 / 128 exercise the
+    skinny-K kernel (wave pairs combined through LDS), the others the 256-tile epilogue."""
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(K)
+    M, Kout = 1024, 512  # dz [M, K] (K = the reduction width) -> out [M, Kout]
+    dz = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(dz.shape[1], Kout, device="cuda", generator=g) / dz.shape[1] ** 0.5).bfloat16()
+    y = ACT[dact](torch.randn(M, Kout, device="cuda", generator=g)).bfloat16()
+    wt = LIN.transpose(w)
+    ct = torch.empty(Kout, M, dtype=torch.bfloat16, device="cuda")
+    part = torch.full(((M // 128) * Kout,), float("nan"), device="cuda")
+    out = LIN.linear_dgrad_nt(dz, wt, y, dact, ct=ct, colpart=part)
+    yf = y.float()
+    ref = (dz.float() @ w.float()) * ((yf > 0).float() if dact == "relu" else yf * (1 - yf) if dact == "sigmoid"
+                                       else 1 - yf * yf)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    assert torch.equal(ct, out.t())
+    assert torch.isfinite(part).all()  # every partial row written
+    db = torch.empty(Kout, device="cuda")
+    LIN.colpart_reduce(part, M // 128, Kout, db)
+    assert _rel(db, ref.sum(0)) < 1e-4, _rel(db, ref.sum(0))
+    blocks = ref.view(M // 128, 128, Kout).sum(1)
+    assert _rel(part.view(M // 128, Kout), blocks) < 1e-4
+    db2 = db.clone()
+    LIN.colpart_reduce(part, M // 128, Kout, db2, accumulate=True)
+    assert torch.allclose(db2, 2 * db, rtol=1e-6, atol=1e-6)
 
 
 def test_wgrad_split_k_and_colsum_big_batch():
