@@ -16,6 +16,8 @@
 //   K11 gbdt_predict    ensemble traversal over binned rows
 //   K13 gbdt_metric     logloss / rmse / error partial sums -> per-round history
 // Node numbering is heap order (children 2i+1, 2i+2); status 0 unused / 1 split / 2 leaf.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -94,24 +96,24 @@ __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restr
 // Cells: feature f owns bins [foff[f], foff[f+1]) of a compact axis of C = foff[F] cells (a one-hot
 // lag feature has 2 cells, "day" 31 ...), so a (task, node) histogram of the reference features is
 // ~200 cells (3 KB of double pairs) instead of F x max_bins.
-// Work split (deterministic, no atomics): block = (row chunk, task, tile); tile = FT features x NTn
-// nodes.  Thread (p, fl) owns feature f0 + fl for the p-th contiguous sub-range of the chunk's rows
-// and accumulates its private LDS copy in row order; the P copies are folded in p order and the
-// chunks by gbdt_chunk_reduce in chunk order.  Two features that induce the same partition of the
-// rows therefore get bit-identical sums (exact gain ties keep breaking towards the lower feature).
-// Per row a thread does one 16-B LDS read-modify-write; the chain is latency-bound per thread and is
-// hidden by occupancy: the tile plan keeps the LDS footprint <= ~48 KB (3+ blocks per CU).
-constexpr int HIST_MAX_CHUNK = 1024;        // rows staged in LDS per piece
-constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // doubles of per-chunk partials (1 GiB) per level
-constexpr int HIST_LDS_BUDGET = 36 * 1024;  // per-block histogram copies (+ 10 B/row staging)
-constexpr int HIST_STAGE_LDS = 24 * 1024;   // per-block row staging (node, g, h, bins) when bins are staged
+// Work split: block = (row chunk, task, tile); tile = FT features x NTn nodes; thread (p, fl) owns
+// feature f0 + fl for the p-th contiguous sub-range of each staged piece of the chunk's rows.
+// Two forms, chosen per fit by the host (models/gbdt.py quant_bits):
+//  * exact (fp64, gbdt_hist): no atomics -- every thread accumulates its private LDS copy in row
+//    order, the P copies are folded in p order and the chunks by gbdt_chunk_reduce in chunk order,
+//    so two features that induce the same partition of the rows get bit-identical sums (exact gain
+//    ties keep breaking towards the lower feature).  Per row a thread does one 16-B LDS
+//    read-modify-write; that serial chain bounds the kernel (1.17 ms per level at 183k rows x 62
+//    tasks, profiles/README.md).
+//  * fixed point (gbdt_hist_q): g and h are quantised per row to int64 (q = rint(x * 2^s), s chosen
+//    so that any sum over the n rows stays below 2^61) and accumulated with non-returning LDS
+//    integer atomics into ONE shared copy: integer addition is exact and order-free, so the sums
+//    are deterministic without the per-thread copies or the serial chain, and the numpy oracle
+//    reproduces them exactly (models/gbdt.py _quant_hist).
+constexpr int HIST_MAX_CHUNK = 1024;             // rows staged in LDS per piece
+constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // 8-byte words of per-chunk partials (1 GiB) per level
+constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (+ staged rows)
 
-// STAGE = 1 (opt-in, see plan_hist): the piece's bin rows are staged in LDS too, with wide
-// coalesced loads by the whole block, so the per-row chain runs on LDS only.  It does not pay: the
-// 8 byte loads in flight per wave of the STAGE = 0 form are not what bounds a large level, the
-// serial per-thread LDS update chain is.  Either way, per 8 rows every input is read before the 8
-// cell updates.  Rows go to copies exactly as in STAGE = 0 for the same piece size.
-template <int STAGE>
 __global__ void __launch_bounds__(256)
 gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
@@ -129,17 +131,15 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   float* sg = reinterpret_cast<float*>(smem + (size_t)P * per * sizeof(double));
   float* sh = sg + piece;
   int16_t* sn = reinterpret_cast<int16_t*>(sh + piece);
-  uint32_t* sbw = reinterpret_cast<uint32_t*>(sn + ((piece + 1) & ~1));  // staged bin words (STAGE)
   const int64_t base = (int64_t)t * n;
   const int nth = f1 - f0;
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
   const int f = f0 + (p < P ? fl : 0);
   double* my = hist + (size_t)(p < P ? p : 0) * per + (foff[f] - c0) * 2;
   // the block's rows [c*chunk, +chunk) in staged pieces of <= piece rows: per piece the rows'
-  // (node, g, h) (and bins) go to LDS once, shared by every feature thread, then thread (p, fl) adds
-  // the p-th contiguous part of the piece to its copy in row order
+  // (node, g, h) go to LDS once, shared by every feature thread, then thread (p, fl) adds the p-th
+  // contiguous part of the piece to its copy in row order
   const int rb = c * chunk, re = min(n, rb + chunk);
-  const int64_t nbytes = (int64_t)n * F;
   for (int r0 = rb; r0 < re; r0 += piece) {
     const int r1 = min(re, r0 + piece);
     __syncthreads();  // the previous piece's staging is consumed
@@ -148,38 +148,10 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
       sh[r - r0] = h[base + r];
       sn[r - r0] = (int16_t)(node[base + r] - first - n0);  // tile-relative node (outside -> skipped)
     }
-    int boff = 0;  // byte offset of row r0 inside the staged words
-    if (STAGE) {
-      const int64_t b0 = (int64_t)r0 * F, w0 = b0 >> 2;
-      boff = (int)(b0 & 3);
-      const int nw = (int)((((int64_t)r1 * F + 3) >> 2) - w0);
-      const bool tail = (w0 + nw) * 4 > nbytes;  // the array's last word, partly past its end
-      const int nwl = nw - (tail ? 1 : 0);        // words loaded whole
-      // range-checked buffer loads of the piece's words
-      const int64_t left = nbytes - w0 * 4;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(bins + w0 * 4), 0, (int)(left < 0x7FFFFFF0 ? left : 0x7FFFFFF0), 0x00020000);
-      int i = threadIdx.x;
-      for (; i + 3 * (int)blockDim.x < nwl; i += 4 * blockDim.x) {
-        uint32_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (i + u * blockDim.x) * 4, 0, 0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) sbw[i + u * blockDim.x] = v[u];
-      }
-      for (; i < nwl; i += blockDim.x) sbw[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, i * 4, 0, 0);
-      // a buffer load of a word that runs past the array end returns 0 in full: that word bytewise
-      if (threadIdx.x == 0 && tail) {
-        uint32_t v = 0;
-        for (int64_t q = (w0 + nw - 1) * 4; q < nbytes; ++q) v |= (uint32_t)bins[q] << (8 * (q & 3));
-        sbw[nw - 1] = v;
-      }
-    }
     __syncthreads();
     if (p < P) {
       const int len = r1 - r0, sub = (len + P - 1) / P;
       const int a0 = min(len, p * sub), a1 = min(len, a0 + sub);
-      const uint8_t* colL = reinterpret_cast<const uint8_t*>(sbw) + boff + f;  // STAGE: row r at colL[(r - r0) * F]
       const uint8_t* col = bins + (int64_t)r0 * F + f;
       int r = a0;
       // 8 rows' inputs first, then their 8 updates in row order (sums bitwise = the plain loop)
@@ -188,7 +160,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
         float gv[8], hv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          b[u] = STAGE ? colL[(r + u) * F] : col[(int64_t)(r + u) * F];
+          b[u] = col[(int64_t)(r + u) * F];
           nd[u] = sn[r + u];
           gv[u] = sg[r + u];
           hv[u] = sh[r + u];
@@ -204,7 +176,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
       for (; r < a1; ++r) {
         const int nd = sn[r];
         if ((unsigned)nd >= (unsigned)NTn) continue;
-        double* e = my + (nd * ldsC + (STAGE ? colL[r * F] : col[(int64_t)r * F])) * 2;
+        double* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
         e[0] += (double)sg[r];
         e[1] += (double)sh[r];
       }
@@ -228,10 +200,88 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   }
 }
 
+// fixed-point value of x * 2^s (x a float, |x * 2^s| < 2^62): the product is exact (power-of-two
+// scale), rint rounds half to even like numpy's np.rint, and the int64 conversion of an integral
+// double is exact
+EM_DEVICE long long quantise(float x, double scale) { return (long long)__builtin_rint((double)x * scale); }
+
+__global__ void __launch_bounds__(256)
+gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
+            const int16_t* __restrict__ node, const int* __restrict__ foff, long long* __restrict__ partial, int T,
+            int n, int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, double qscale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int c = blockIdx.x, t = blockIdx.y;
+  const int nft = (F + FT - 1) / FT;
+  const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
+  const int f0 = ft * FT, f1 = min(F, f0 + FT), n0 = nt * NTn;
+  const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
+  long long* hist = reinterpret_cast<long long*>(smem);  // [NTn][ldsC][2], shared by all P phases
+  const int per = NTn * ldsC * 2;
+  for (int i = threadIdx.x; i < per; i += blockDim.x) hist[i] = 0;
+  long long* sq = hist + per;  // staged rows: (qg, qh) pairs, then the tile-relative node ids
+  int16_t* sn = reinterpret_cast<int16_t*>(sq + 2 * piece);
+  const int64_t base = (int64_t)t * n;
+  const int nth = f1 - f0;
+  const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
+  const int f = f0 + (p < P ? fl : 0);
+  long long* my = hist + (foff[f] - c0) * 2;
+  const int rb = c * chunk, re = min(n, rb + chunk);
+  for (int r0 = rb; r0 < re; r0 += piece) {
+    const int r1 = min(re, r0 + piece);
+    __syncthreads();  // the previous piece's staging is consumed (first pass: the zeroing is done)
+    for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
+      sq[2 * (r - r0)] = quantise(g[base + r], qscale);
+      sq[2 * (r - r0) + 1] = quantise(h[base + r], qscale);
+      sn[r - r0] = (int16_t)(node[base + r] - first - n0);
+    }
+    __syncthreads();
+    if (p < P) {
+      const int len = r1 - r0;
+      const uint8_t* col = bins + (int64_t)r0 * F + f;
+      int r = p;  // phases interleave rows, so the P waves of a row read neighbouring bin bytes
+      for (; r + 7 * P < len; r += 8 * P) {
+        int b[8], nd[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          b[u] = col[(int64_t)(r + u * P) * F];
+          nd[u] = sn[r + u * P];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if ((unsigned)nd[u] >= (unsigned)NTn) continue;
+          long long* e = my + (nd[u] * ldsC + b[u]) * 2;
+          const long long qg = sq[2 * (r + u * P)], qh = sq[2 * (r + u * P) + 1];
+          __hip_atomic_fetch_add(e, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(e + 1, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      for (; r < len; r += P) {
+        const int nd = sn[r];
+        if ((unsigned)nd >= (unsigned)NTn) continue;
+        long long* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
+        __hip_atomic_fetch_add(e, sq[2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(e + 1, sq[2 * r + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  __syncthreads();
+  long long* out = partial + ((int64_t)c * T + t) * (int64_t)nodesL * C * 2;
+  const int nn = min(NTn, nodesL - n0);
+  for (int i = threadIdx.x; i < nn * Ct; i += blockDim.x) {
+    const int nd = i / Ct, cc = i - nd * Ct;
+    const long long* e = hist + (nd * ldsC + cc) * 2;
+    long long* o = out + ((int64_t)(n0 + nd) * C + c0 + cc) * 2;
+    o[0] = e[0];
+    o[1] = e[1];
+  }
+}
+
 // fold the per-chunk histograms into chunk 0 in chunk order (single-GPU and DP paths alike)
-__global__ void gbdt_chunk_reduce(double* __restrict__ partial, int nchunks, int64_t S) {
+template <typename A>
+__global__ void gbdt_chunk_reduce(A* __restrict__ partial, int nchunks, int64_t S) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S; e += (int64_t)gridDim.x * blockDim.x) {
-    double acc = partial[e];
+    A acc = partial[e];
     for (int c = 1; c < nchunks; ++c) acc += partial[(int64_t)c * S + e];
     partial[e] = acc;
   }
@@ -242,23 +292,29 @@ __global__ void gbdt_chunk_reduce(double* __restrict__ partial, int nchunks, int
 // Thread <-> feature: a sequential left-sum over the feature's bins (bin order), XGBoost loss_chg
 // at every candidate "bin <= b", first maximum kept; then a block arg-max where the larger gain
 // wins and equal gains go to the lower feature == numpy's first argmax in (feature, bin) order.
+// A = double (exact form) or long long (fixed point, value = q * qinv): the fixed-point form keeps
+// the left sums and the node totals (feature 0's cells, every level) in integers and converts each
+// to double once, so GR = (Gn - GL) is exact as well.
+template <typename A>
 __global__ void __launch_bounds__(256)
-gbdt_split(const double* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
+gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
            int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
-           int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw) {
+           int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
+           double qinv) {
+  constexpr bool Q = std::is_same<A, long long>::value;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
   int8_t* st = status + (int64_t)t * NN;
   if (st[i] != 2) return;  // block-uniform
-  const double* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
+  const A* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
   if (nchunks > 1) {  // per-chunk partials: fold this node's cells into LDS in chunk order (== gbdt_chunk_reduce)
-    double* fold = reinterpret_cast<double*>(smem);
+    A* fold = reinterpret_cast<A*>(smem);
     for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
-      double acc = hs[e];
+      A acc = hs[e];
       int c = 1;
       for (; c + 8 <= nchunks; c += 8) {  // 8 independent loads in flight, added in chunk order
-        double v[8];
+        A v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = hs[(int64_t)(c + u) * cstride + e];
 #pragma unroll
@@ -270,21 +326,29 @@ gbdt_split(const double* __restrict__ hist, int nchunks, int64_t cstride, const 
     __syncthreads();
     hs = fold;
   }
-  __shared__ double sGn[2];
+  auto val = [qinv](A x) -> double {
+    if constexpr (Q)
+      return (double)x * qinv;
+    else
+      return x;
+  };
+  __shared__ A sGn[2];
   __shared__ double rv[4];
   __shared__ int rf[4], rb[4];
-  __shared__ double rgl[4], rhl[4];
+  __shared__ A rgl[4], rhl[4];
   if (threadIdx.x == 0) {
-    double Gn, Hn;
-    if (level == 0) {  // root totals: feature 0's cells in bin order
-      Gn = 0.0;
-      Hn = 0.0;
+    A Gn, Hn;
+    if (Q || level == 0) {  // node totals: feature 0's cells in bin order
+      Gn = 0;
+      Hn = 0;
       for (int c = foff[0]; c < foff[1]; ++c) {
         Gn += hs[2 * c];
         Hn += hs[2 * c + 1];
       }
-      G[(int64_t)t * NN] = Gn;
-      H[(int64_t)t * NN] = Hn;
+      if (level == 0) {
+        G[(int64_t)t * NN] = val(Gn);
+        H[(int64_t)t * NN] = val(Hn);
+      }
     } else {
       Gn = G[(int64_t)t * NN + i];
       Hn = H[(int64_t)t * NN + i];
@@ -293,25 +357,28 @@ gbdt_split(const double* __restrict__ hist, int nchunks, int64_t cstride, const 
     sGn[1] = Hn;
   }
   __syncthreads();
-  const double Gn = sGn[0], Hn = sGn[1];
+  const A Gna = sGn[0], Hna = sGn[1];
+  const double Gn = val(Gna), Hn = val(Hna);
   const double root = Gn * Gn / (Hn + lam);
-  double best = -INFINITY, bGL = 0.0, bHL = 0.0;
+  double best = -INFINITY;
+  A bGL = 0, bHL = 0;
   int bf = 0x7fffffff, bb = 0;
   for (int f = threadIdx.x; f < F; f += blockDim.x) {
     const int ca = foff[f], cb = foff[f + 1];
-    double GL = 0.0, HL = 0.0;
+    A GLa = 0, HLa = 0;
     for (int c = ca; c < cb - 1; ++c) {  // the last bin is never a candidate (nothing to its right)
-      GL += hs[2 * c];
-      HL += hs[2 * c + 1];
-      const double GR = Gn - GL, HR = Hn - HL;
+      GLa += hs[2 * c];
+      HLa += hs[2 * c + 1];
+      const double GL = val(GLa), HL = val(HLa);
+      const double GR = val(Gna - GLa), HR = val(Hna - HLa);
       if (HL >= mcw && HR >= mcw) {
         const double gn = GL * GL / (HL + lam) + GR * GR / (HR + lam) - root;
         if (gn > best) {  // strict: the lower bin of this feature keeps ties
           best = gn;
           bf = f;
           bb = c - ca;
-          bGL = GL;
-          bHL = HL;
+          bGL = GLa;
+          bHL = HLa;
         }
       }
     }
@@ -320,7 +387,8 @@ gbdt_split(const double* __restrict__ hist, int nchunks, int64_t cstride, const 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const double ov = __shfl_xor(best, o), ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
+    const double ov = __shfl_xor(best, o);
+    const A ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
     const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o);
     if (ov > best || (ov == best && of < bf)) {
       best = ov;
@@ -356,10 +424,10 @@ gbdt_split(const double* __restrict__ hist, int nchunks, int64_t cstride, const 
       const int l = 2 * i + 1, r = 2 * i + 2;
       st[l] = 2;
       st[r] = 2;
-      G[(int64_t)t * NN + l] = bGL;
-      H[(int64_t)t * NN + l] = bHL;
-      G[(int64_t)t * NN + r] = Gn - bGL;
-      H[(int64_t)t * NN + r] = Hn - bHL;
+      G[(int64_t)t * NN + l] = val(bGL);
+      H[(int64_t)t * NN + l] = val(bHL);
+      G[(int64_t)t * NN + r] = val(Gna - bGL);
+      H[(int64_t)t * NN + r] = val(Hna - bHL);
     }
   }
 }
@@ -525,14 +593,15 @@ inline int grid_for(int64_t total, int bs = 256) {
 // ------------------------------------------------------------------ host-side histogram plan
 namespace {
 struct HistPlan {
-  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece, stage;
+  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece;
   size_t lds;
 };
 
-// Tile plan of one level: widest feature tile (then fewest node tiles) whose P private copies fit
-// the LDS budget; P (row phases, 1..4) fills a 256-thread block when F is small.  Chunks are sized
-// so a level launches ~4096 blocks (all 256 CUs busy even for the reference's ~930 rows).
-bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
+// Tile plan of one level: widest feature tile (then fewest node tiles) whose histogram copies fit
+// the LDS budget (P private copies in the exact form, one shared copy in the fixed-point form); P
+// (row phases, 1..4) fills a 256-thread block when F is small.  Chunks are sized so a level launches
+// ~4096 blocks (all 256 CUs busy even for the reference's ~930 rows).
+bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, HistPlan& pl) {
   const int nodesL = 1 << level;
   for (int NTn = nodesL; NTn >= 1; NTn >>= 1) {
     for (int FT = F < 256 ? F : 256;; FT = (FT + 1) / 2) {
@@ -544,7 +613,7 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
       int P = 256 / FT;
       P = P > 4 ? 4 : (P < 1 ? 1 : P);
       for (; P >= 1; --P)
-        if ((int64_t)P * NTn * maxC * 16 <= HIST_LDS_BUDGET) break;
+        if ((int64_t)(quant ? 1 : P) * NTn * maxC * 16 <= HIST_LDS_BUDGET) break;
       if (P >= 1) {
         pl.FT = FT;
         pl.NTn = NTn;
@@ -564,16 +633,9 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
         chunk = chunk < 64 ? 64 : chunk;
         pl.chunk = (int)chunk;
         pl.nchunks = (int)((n + chunk - 1) / chunk);
-        // pieces: rows staged per pass; with bins staged (F + 10 B/row) they fill <= HIST_STAGE_LDS
-        // (opt-in, EM_GBDT_HIST_STAGE=1: measured slower, 1316 vs 1170 us per level at 183k rows x 62
-        // tasks, equal at the reference's 928 rows -- the per-row LDS update chain, not the byte loads,
-        // bounds this kernel)
-        static const bool stage_on = getenv("EM_GBDT_HIST_STAGE") && getenv("EM_GBDT_HIST_STAGE")[0] == '1';
-        int piece = (int)(HIST_STAGE_LDS / (F + 10)) & ~15;
-        pl.stage = stage_on && piece >= 64;
-        pl.piece = pl.stage ? (piece < HIST_MAX_CHUNK ? piece : HIST_MAX_CHUNK) : HIST_MAX_CHUNK;
-        pl.lds = (size_t)P * NTn * maxC * 16 + (size_t)pl.piece * 10 + 4 +
-                 (pl.stage ? (((size_t)pl.piece * F + 8) & ~(size_t)3) + 4 : 0);
+        pl.piece = HIST_MAX_CHUNK;
+        // staged rows: (g, h) floats + node id (exact); (qg, qh) int64 + node id (fixed point)
+        pl.lds = (size_t)(quant ? 1 : P) * NTn * maxC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4;
         return true;
       }
       if (FT == 1) break;
@@ -583,32 +645,44 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, HistPlan& pl) {
 }
 
 int64_t partial_need(int level, int n, int T, int F, const int* foff) {
-  HistPlan pl;
-  if (!plan_hist(level, n, T, F, foff, pl)) return -1;
-  return (int64_t)pl.nchunks * T * (1 << level) * foff[F] * 2;
+  HistPlan pl;  // the fixed-point plan never has more chunks (same tiles or wider)
+  if (!plan_hist(level, n, T, F, foff, false, pl)) return -1;
+  HistPlan pq;
+  if (!plan_hist(level, n, T, F, foff, true, pq)) return -1;
+  const int64_t nch = pl.nchunks > pq.nchunks ? pl.nchunks : pq.nchunks;
+  return nch * T * (1 << level) * foff[F] * 2;
 }
 
-// K8 for one level: per-chunk histograms, then folded into partial[0 : T*nodesL*C*2]
+// K8 for one level: per-chunk histograms, then folded into partial[0 : T*nodesL*C*2] (8-byte words:
+// doubles, or int64 when qscale != 0)
 // fold = false leaves the per-chunk partials for gbdt_split to fold (small chunk counts); *nchunks_out
 // = the number of partial copies left in `partial` (1 after a fold)
 constexpr int SPLIT_FOLD_MAX_CHUNKS = 32, SPLIT_FOLD_MAX_LDS = 32 * 1024;
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
-                      bool fold, int* nchunks_out, hipStream_t stream) {
+                      bool fold, double qscale, int* nchunks_out, hipStream_t stream) {
+  const bool quant = qscale != 0.0;
   HistPlan pl;
-  if (!plan_hist(level, n, T, F, foff_h, pl)) return EM_ERR_ARG;
+  if (!plan_hist(level, n, T, F, foff_h, quant, pl)) return EM_ERR_ARG;
   const int C = foff_h[F];
   const int64_t S = (int64_t)T * (1 << level) * C * 2;
   if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
-  if (pl.stage)
-    hipLaunchKernelGGL(gbdt_hist<1>, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g,
-                       h, node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
+  const dim3 grid(pl.nchunks, T, pl.nft * pl.ntn);
+  if (quant)
+    hipLaunchKernelGGL(gbdt_hist_q, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d,
+                       reinterpret_cast<long long*>(partial), T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
+                       pl.ldsC, pl.piece, qscale);
   else
-    hipLaunchKernelGGL(gbdt_hist<0>, dim3(pl.nchunks, T, pl.nft * pl.ntn), dim3(pl.threads), pl.lds, stream, bins, g,
-                       h, node, foff_d, partial, T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
+    hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
+                       C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
   const bool split_folds = !fold && pl.nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
-  if (pl.nchunks > 1 && !split_folds)
-    hipLaunchKernelGGL(gbdt_chunk_reduce, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
+  if (pl.nchunks > 1 && !split_folds) {
+    if (quant)
+      hipLaunchKernelGGL(gbdt_chunk_reduce<long long>, dim3(grid_for(S)), dim3(256), 0, stream,
+                         reinterpret_cast<long long*>(partial), pl.nchunks, S);
+    else
+      hipLaunchKernelGGL(gbdt_chunk_reduce<double>, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
+  }
   *nchunks_out = split_folds ? pl.nchunks : 1;
   EM_CHECK_LAUNCH();
   return 0;
@@ -652,10 +726,14 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
                        int metric, float eta, float lam, float gamma, float mcw, float subsample, uint32_t seed,
                        float* g, float* h, int16_t* node, double* partial, int64_t partial_doubles, double* Gs,
                        double* Hs, double* mpart, int8_t* status, int16_t* feat, uint8_t* sbin, float* leaf,
-                       float* gainv, float* cover, float* hist_out, hipStream_t stream) {
+                       float* gainv, float* cover, float* hist_out, int quant_bits, hipStream_t stream) {
   if (!bins || !Y || !margin || n <= 0 || F <= 0 || !valid_foff(foff_h, F) || !foff_d || T <= 0 || max_depth < 1 ||
-      max_depth > 12 || r0 < 0 || r1 < r0)
+      max_depth > 12 || r0 < 0 || r1 < r0 || quant_bits < 0 || quant_bits > 61)
     return EM_ERR_ARG;
+  // fixed-point histograms (quant_bits = s > 0): the caller guarantees |g|, |h| <= 1 and n < 2^(61-s),
+  // so every per-cell and per-node sum of q = rint(x * 2^s) stays below 2^61 in magnitude
+  if (quant_bits && (obj == OBJ_SQERR || (int64_t)n >= (1ll << (61 - quant_bits)))) return EM_ERR_ARG;
+  const double qscale = quant_bits ? ldexp(1.0, quant_bits) : 0.0, qinv = quant_bits ? ldexp(1.0, -quant_bits) : 0.0;
   const int NN = (1 << (max_depth + 1)) - 1;
   const int C = foff_h[F];
   const int64_t TN = (int64_t)T * n;
@@ -674,12 +752,18 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       const int nodesL = 1 << level;
       int nch = 1;
       const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles,
-                                       false, &nch, stream);
+                                       false, qscale, &nch, stream);
       if (rc) return rc;
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
       const int64_t cstride = (int64_t)T * nodesL * C * 2;
-      hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), nch > 1 ? (size_t)C * 16 : 0, stream, partial, nch,
-                         cstride, foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw);
+      const size_t slds = nch > 1 ? (size_t)C * 16 : 0;
+      if (quant_bits)
+        hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, stream,
+                           reinterpret_cast<const long long*>(partial), nch, cstride, foff_d, T, F, C, level, NN, Gs,
+                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv);
+      else
+        hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, stream, partial, nch, cstride,
+                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0);
       hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, st, fe, sb,
                          level);
     }
@@ -755,7 +839,7 @@ EM_API int em_gbdt_dp_level_hist(int level, const uint8_t* bins, const float* g,
     return EM_ERR_ARG;
   int nch = 1;
   const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles, true,
-                                   &nch, stream);
+                                   0.0, &nch, stream);
   if (rc) return rc;
   EM_CHECK_LAUNCH();
   *len_out = (int64_t)T * (1 << level) * foff_h[F] * 2;
@@ -772,8 +856,8 @@ EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* 
   const int nodesL = 1 << level;
   const int64_t TN = (int64_t)T * n;
   const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
-  hipLaunchKernelGGL(gbdt_split, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C, level,
-                     NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw);
+  hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C,
+                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
                      sbin, level);
   EM_CHECK_LAUNCH();

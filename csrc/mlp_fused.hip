@@ -256,10 +256,7 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
 constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[N] | done0[N] | done1[N]
-// scaled target tables (FUSED_FASTY): nibble -> 4 x {0, -1/5} (main), {0, -1/2} (stars) and the
-// nibble of outputs 48-51 that straddles the groups ({-1/5, -1/5, -1/2, -1/2} per bit)
-constexpr int V6_YM = V6_FLAGS + 128, V6_YS = V6_YM + 256, V6_YMS = V6_YS + 256;
-constexpr int V6_RING = V6_YMS + 256;  // [2 units][3 slots][16 KB]
+constexpr int V6_RING = V6_FLAGS + 128;  // [2 units][3 slots][16 KB]
 constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_RSLOTS * V6_SLOT;
 // byte offset of ring slot `slot` of unit `unit`
 EM_DEVICE uint32_t v6_slot(int unit, int slot) {
@@ -270,9 +267,6 @@ constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 204
 static_assert(V6_LDS <= 163840 && V6_RING % 16 == 0, "v6 LDS budget");
 static_assert(IMG_BYTES == 54528 && IMG_BYTES % 16 == 0, "image size (ops/fused_mlp.py IMG_BYTES)");
 constexpr int V6_SPIN_LIMIT = 1 << 20;  // ~50 ms of polling: a legitimate wait is microseconds
-#ifndef FUSED_FASTY
-#define FUSED_FASTY 0  // 2: scaled target tables only (A/B diagnostic; standard 5 + 2 draws only)
-#endif
 
 // wait until the LDS counter at off reaches target (skipped once a wait has failed: the launch then
 // drains quickly and reports NaN)
@@ -308,12 +302,7 @@ EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
 // and 58-63 straddle the group edges), so every statically classified element emits only its own
 // group's ops (a select-form "x ? v : 0" fed into an fma would have to be kept: fma(0, inf, a) is
 // NaN).  Max / sum / target-dot reductions run as independent partial chains.
-//
-// FAST (every sample of the tile has 5 main / 2 star targets, or none: a padding row -- i.e. every
-// real Euromillions draw): the targets are read from tables that already hold -y / n_group, so
-// dZ2 = p - y / n is ONE fma per output and the target logit sum needs no per-group split
-// (32 multiplies and the star chain fewer per tile than the general form).
-template <int YL, bool FAST, typename Hook>
+template <int YL, typename Hook>
 EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
                                 float& loss_acc, Hook&& hook) {
   constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
@@ -321,9 +310,7 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      int base = YL;
-      if (FAST) base = (u == 0 || g < 2) ? V6_YM : (g == 2 && h == 0) ? V6_YMS : V6_YS;
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + base + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
       yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
     }
   };
@@ -334,7 +321,8 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
   const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
   float tm[4] = {0.f, 0.f, 0.f, 0.f}, ts[2] = {0.f, 0.f};
-  // ---- tile 0: outputs 0..31, all main ----
+  // ---- tile 0: outputs 0..31, all main.  step(j), j = 0..7, is issued between tile 1's F2 MFMAs by
+  // the caller (hook): in-order issue lets the VALU run only between MFMAs in program order ----
   float m0 = 0.f, s0 = 0.f, nL = 0.f;
   float mm0[4], sm[4] = {0.f, 0.f, 0.f, 0.f}, yb0[16];
   auto step = [&](int j) {
@@ -381,40 +369,37 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   float s1p[2] = {0.f, 0.f}, ss[2] = {0.f, 0.f};
   float yb1[16];
   targets(1, yb1);
+  {
+    float (&yb)[16] = yb1;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
-    const float v = z2[1][i];
-    float e = 0.f;
-    if (c0 == c1) {
-      if (c0 == 0) {
-        e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nmL));
-        s1p[i & 1] += e;
-        tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);
-      } else if (c0 == 1) {
-        e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL));
-        ss[i & 1] += e;
-        if (FAST) tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);
-        else ts[i & 1] = __builtin_fmaf(yb1[i], v, ts[i & 1]);
-      }
-    } else if (c0 == 0) {
-      e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, h0 ? nmL : nsL));
-      s1p[i & 1] = h0 ? s1p[i & 1] + e : s1p[i & 1];
-      ss[i & 1] = h0 ? ss[i & 1] : ss[i & 1] + e;
-      if (FAST) {  // main (h = 0) or star (h = 1): the table already carries the group's -1 / n
-        tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);
-      } else {
-        const float ty = yb1[i] * v;
+    for (int i = 0; i < 16; ++i) {
+      const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
+      const float v = z2[1][i];
+      float e = 0.f;
+      if (c0 == c1) {
+        if (c0 == 0) {
+          e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nmL));
+          s1p[i & 1] += e;
+          tm[i & 3] = __builtin_fmaf(yb[i], v, tm[i & 3]);
+        } else if (c0 == 1) {
+          e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL));
+          ss[i & 1] += e;
+          ts[i & 1] = __builtin_fmaf(yb[i], v, ts[i & 1]);
+        }
+      } else if (c0 == 0) {
+        e = __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, h0 ? nmL : nsL));
+        const float ty = yb[i] * v;
+        s1p[i & 1] = h0 ? s1p[i & 1] + e : s1p[i & 1];
+        ss[i & 1] = h0 ? ss[i & 1] : ss[i & 1] + e;
         tm[i & 3] = h0 ? tm[i & 3] + ty : tm[i & 3];
         ts[i & 1] = h0 ? ts[i & 1] : ts[i & 1] + ty;
+      } else {
+        e = h0 ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL)) : 0.f;
+        ss[i & 1] += e;
+        ts[i & 1] = h0 ? __builtin_fmaf(yb[i], v, ts[i & 1]) : ts[i & 1];
       }
-    } else {
-      e = h0 ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, L2E, nsL)) : 0.f;
-      ss[i & 1] += e;
-      if (FAST) tm[i & 3] = __builtin_fmaf(yb1[i], v, tm[i & 3]);  // pad targets are 0: adds 0
-      else ts[i & 1] = h0 ? __builtin_fmaf(yb1[i], v, ts[i & 1]) : ts[i & 1];
+      dz[1][i] = e;
     }
-    dz[1][i] = e;
   }
   const float s1 = xhalf_sum(s1p[0] + s1p[1]), s_s = xhalf_sum(ss[0] + ss[1]);
   // ---- online merge of the main group: M = max(m0, m1), S = a0 s0 + a1 s1 ----
@@ -431,20 +416,18 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     for (int i = 0; i < 16; ++i) {
       const int c0 = out_cls(u, i, 0), c1 = out_cls(u, i, 1);
       const float fm = u == 0 ? f0 : f1;
-      const float ym = FAST ? yb[i] : yb[i] * ni_m, ys = FAST ? yb[i] : yb[i] * ni_s;
       if (c0 == c1) {
-        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, ym);
-        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, ys);
+        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, yb[i] * ni_m);
+        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
         if (c0 == 2) dz[u][i] = 0.f;
       } else if (c0 == 0) {
-        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? fm : f_s, FAST ? yb[i] : yb[i] * (h0 ? ni_m : ni_s));
+        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? fm : f_s, yb[i] * (h0 ? ni_m : ni_s));
       } else {  // the pad lanes' e is 0 and their target bit (outputs 62/63) is 0
-        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, ys);
+        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
       }
     }
   }
-  float l = FAST ? ((tm[0] + tm[1]) + (tm[2] + tm[3]))
-                 : -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
+  float l = -(((tm[0] + tm[1]) + (tm[2] + tm[3])) * inv_m + (ts[0] + ts[1]) * inv_s);
   if (h == 0)
     l += (nm ? M + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
   loss_acc += l;
@@ -483,12 +466,13 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     for (int kk = 0; kk < 8; ++kk) w2r[u][kk] = lds_frag(smem, w2p_off(32 * u + r, kk * 2 + h));
   __syncthreads();  // every forward wave holds its weights: the W1ᵀ / W2ᵀ images are free (recycled slots)
   st.start();
-  for (int k = F; k < K; k += 2) {
-    const int slot = k % V6_NSLOT;
+  // (one tile as a lambda called from the loop below: written inline in the loop, the same body
+  // compiles to 9 more VALU per tile -- slot addresses recomputed -- and measured 3 % slower)
+  auto ftile = [&](int k, int slot, int knext) {
     const bool valid = (U + k * nunits) * 32 + r < B;
     const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
     const uint64_t tmask = valid ? ntg : 0ull;
-    fetch(k + 2, nin, ntg);
+    fetch(knext, nin, ntg);
     const uint32_t SB = v6_slot(unit, slot);
     if (k >= V6_NSLOT) {  // the slot's previous tile (k - 4) must be consumed by both backward waves
       v6_wait(smem, FL + (V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
@@ -534,41 +518,34 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
         z2[u][4 * g + 0] = b[0]; z2[u][4 * g + 1] = b[1]; z2[u][4 * g + 2] = b[2]; z2[u][4 * g + 3] = b[3];
       }
     auto f2mfma = [&](int u, int kk) { z2[u] = mfma32(w2r[u][kk], hT[kk >> 1][kk & 1], z2[u]); };
-    float dz[2][16];
-    float lt = 0.f;  // this lane's loss terms of the tile
+    // softmax: tile 0's chain first; tile 1's chain is issued by the softmax hook, one MFMA per step
+    // of tile 0's statistics (sched_barrier fences pin that order)
+    auto hook = [&](auto&& step) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f2mfma(1, j);
+        __builtin_amdgcn_sched_barrier(0);
+        step(j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
     if (LOSS == 0) {
-      // tile 0's chain first; tile 1's chain is issued by the softmax hook, one MFMA per step of tile
-      // 0's statistics (sched_barrier fences pin that order)
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) f2mfma(0, kk);
-      st.mark(2);
-      auto hook = [&](auto&& step) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          f2mfma(1, j);
-          __builtin_amdgcn_sched_barrier(0);
-          step(j);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      // wave-uniform: FAST when every sample of the tile has 5 + 2 targets (or is padding)
-      const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
-      const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);
-      const int ns = __builtin_popcount(thi & 0x3FFC0000u);
-      const bool std_draw = (nm == 5 || nm == 0) && (ns == 2 || ns == 0);
-      (void)std_draw;
-      if (FUSED_FASTY == 2)  // diagnostic A/B build: scaled tables only (valid for standard draws only)
-        v6_softmax_split<V6_YLUT, true>(smem, z2, tmask, h, dz, lt, hook);
-      else
-        v6_softmax_split<V6_YLUT, false>(smem, z2, tmask, h, dz, lt, hook);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
         for (int u = 0; u < 2; ++u) f2mfma(u, kk);
-      st.mark(2);
-      bce_tile_loss<V6_YLUT>(smem, z2, tmask, valid, h, dz, lt);
     }
+    st.mark(2);
+
+    float dz[2][16];
+    float lt = 0.f;  // this lane's loss terms of the tile
+    if (LOSS == 0)
+      v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, lt, hook);
+    else
+      bce_tile_loss<V6_YLUT>(smem, z2, tmask, valid, h, dz, lt);
     loss_acc += lt;
     st.mark(3);
 
@@ -587,7 +564,8 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
       }
     lds_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
-  }
+  };
+  for (int k = F; k < K; k += 2) ftile(k, k % V6_NSLOT, k + 2);
 }
 
 // backward wave of hidden half RHO: every tile of the unit's stream.  Every LDS read of the tile
@@ -754,8 +732,8 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
 // slabs, loading every slab as soon as its flag shows up, i.e. while the slow workgroups are still
 // computing.  The slowest workgroup draws no chunk; the critical path after its loop is its slab
 // publish plus one 256-byte read per waiting chunk and the Adam arithmetic.
-//   * bit-reproducible: a chunk's parameter p is sum_{g=0..7} (sum_{j} slab[g + 8 j][p]) in this
-//     fixed order whatever the arrival order and whichever workgroup takes the chunk;
+//   * bit-reproducible: a chunk's parameter p is sum_{g=0..15} (sum_{i} slab[g + 16 i][p]) in the
+//     fixed order of em_adam_slab whatever the arrival order and whichever workgroup takes the chunk;
 //   * placement-independent: flags and slab words are stored sc1 and loaded sc1 by the wave that
 //     polled them (the loss words after a workgroup barrier); no XCD co-location is assumed;
 //   * replay-safe (hipGraph): flags are tagged with a launch epoch (never reset); the workgroup that
@@ -818,7 +796,7 @@ EM_DEVICE void epi_adam(char* smem, const float* __restrict__ slabs, const float
                         const AdamEpi& a, int tag, int tstep, int tid) {
   const int lane = tid & 63, g = tid >> 6, nslab = gridDim.x;
   int* SCH = reinterpret_cast<int*>(smem + V6_RED + 1024);        // dequeued chunk
-  float* PART = reinterpret_cast<float*>(smem + V6_RED + 1152);   // [8][64] per-wave partial sums
+  float* PART = reinterpret_cast<float*>(smem + V6_RED + 1152);   // [16][64] per-group partial sums
   int* BAD = reinterpret_cast<int*>(smem + V6_RED + 1088);
   // publish: every storing wave drained its sc1 slab stores; then ONE lane raises the flag
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -845,10 +823,27 @@ EM_DEVICE void epi_adam(char* smem, const float* __restrict__ slabs, const float
 #pragma unroll
     for (int j = 0; j < 32; ++j) v[j] = 0.f;
     const bool ok = epi_gather(slabs, a.sync, nslab, g, lane, p0, tag, v);
-    float s = v[0];
+    // wave g holds slab groups g (slabs g + 16 i = v[2i]) and g + 8 (slabs g + 8 + 16 i = v[2i + 1]);
+    // each group is summed exactly as em_adam_slab's thread of that group sums it (adam.hip
+    // adam_slab4_kernel: four interleaved accumulators over a full block of 16 slabs, else one
+    // sequential tail accumulator; absent slabs are +0)
 #pragma unroll
-    for (int j = 1; j < 32; ++j) s += v[j];  // slabs g, g + 8, ... in order (absent ones are +0)
-    PART[g * 64 + lane] = s;
+    for (int par = 0; par < 2; ++par) {
+      const int grp = g + 8 * par;
+      float s;
+      if (grp + 240 < nslab) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i & 3] += v[2 * i + par];
+        s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      } else {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc += v[2 * i + par];
+        s = (acc + 0.f) + (0.f + 0.f);
+      }
+      PART[grp * 64 + lane] = s;
+    }
     if (!ok) {
       BAD[0] = 1;
       if (lane == 0) __hip_atomic_store(a.sync + SYNC_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -857,9 +852,9 @@ EM_DEVICE void epi_adam(char* smem, const float* __restrict__ slabs, const float
     const bool bad = BAD[0] != 0;
     if (tid < 64) {
       const int p = p0 + tid;
-      float gs = PART[tid];
+      float gs = 0.f;
 #pragma unroll
-      for (int k = 1; k < 8; ++k) gs += PART[k * 64 + tid];
+      for (int k = 0; k < 16; ++k) gs += PART[k * 64 + tid];
       if (!bad) {
         const float lr = a.hp[0], b1 = a.hp[1], b2 = a.hp[2], eps = a.hp[3], wd = a.hp[4];
         if (mlp::pad_slot(p)) {
@@ -891,11 +886,11 @@ EM_DEVICE void epi_adam(char* smem, const float* __restrict__ slabs, const float
 
 // EPI 0: slabs only (em_adam_slab reduces them, or the DP paths all-reduce them first);
 // EPI 1: slabs + in-launch Adam (single-process training, AdamEpi above)
+// (the train kernel keeps its short argument block; the step kernel adds the Adam arguments)
 template <int LOSS, int EPI>
-__global__ void __launch_bounds__(512, 1)
-mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
-                          const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
-                          float* __restrict__ loss_slabs, int* __restrict__ step, AdamEpi epi) {
+__device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                                         int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                                         float* __restrict__ loss_slabs, int* __restrict__ step, const AdamEpi& epi) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t ts[4] = {};  // FUSED_STAMPS: 100 MHz wall-clock marks (entry, prologue done, loop done, slab written)
   if (FUSED_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -925,9 +920,6 @@ mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
   if (tid < 64) {
     const float bit = (float)(((tid >> 2) >> (tid & 3)) & 1);
     reinterpret_cast<float*>(smem + V6_YLUT)[tid] = bit;
-    reinterpret_cast<float*>(smem + V6_YM)[tid] = -0.2f * bit;
-    reinterpret_cast<float*>(smem + V6_YS)[tid] = -0.5f * bit;
-    reinterpret_cast<float*>(smem + V6_YMS)[tid] = ((tid & 3) < 2 ? -0.2f : -0.5f) * bit;
   }
   if (tid < 32) {
     const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
@@ -989,6 +981,22 @@ mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __r
     for (int k = 0; k < 4; ++k) slab_spare[128 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
   }
   if (EPI) epi_adam(smem, slabs, loss_slabs, epi, tag, tstep, tid);
+}
+
+template <int LOSS>
+__global__ void __launch_bounds__(512, 1)
+mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
+                          const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                          float* __restrict__ loss_slabs, int* __restrict__ step) {
+  train_v6<LOSS, 0>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step, AdamEpi{});
+}
+
+template <int LOSS>
+__global__ void __launch_bounds__(512, 1)
+mlp_fused_step_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
+                         const uint8_t* __restrict__ wimg, float* __restrict__ slabs, float* __restrict__ loss_slabs,
+                         AdamEpi epi) {
+  train_v6<LOSS, 1>(masks, sidx, B, offset, wimg, slabs, loss_slabs, nullptr, epi);
 }
 
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
@@ -1063,10 +1071,12 @@ EM_API int em_mlp_fused_lds_bytes() { return V6_LDS; }
 EM_API int em_mlp_fused_sync_words() { return SYNC_WORDS; }
 
 namespace {
-template <int LOSS, int EPI>
+template <int LOSS>
 void set_lds_attr() {
-  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, EPI>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            V6_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_step_v6_kernel<LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            V6_LDS);
 }
 int check_train_args(const uint64_t*& draws, const int32_t* sidx, int64_t B, int64_t& offset, const void* wimg,
                      float* slabs, float* loss_slabs, int nslab) {
@@ -1079,10 +1089,8 @@ int check_train_args(const uint64_t*& draws, const int32_t* sidx, int64_t B, int
     return EM_ERR_ARG;
   static bool attrs = false;
   if (!attrs) {
-    set_lds_attr<0, 0>();
-    set_lds_attr<1, 0>();
-    set_lds_attr<0, 1>();
-    set_lds_attr<1, 1>();
+    set_lds_attr<0>();
+    set_lds_attr<1>();
     attrs = true;
   }
   return 0;
@@ -1096,15 +1104,14 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
                               const void* wimg, float* slabs, float* loss_slabs, int nslab, int loss_kind,
                               int* step, hipStream_t stream) {
   if (int e = check_train_args(draws, sidx, B, offset, wimg, slabs, loss_slabs, nslab)) return e;
-  const AdamEpi none{};
   const int Bi = (int)B, oi = (int)offset;
   const uint8_t* w = (const uint8_t*)wimg;
   if (loss_kind == 0)
-    hipLaunchKernelGGL((mlp_fused_train_v6_kernel<0, 0>), dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, step, none);
+    hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
+                       slabs, loss_slabs, step);
   else
-    hipLaunchKernelGGL((mlp_fused_train_v6_kernel<1, 0>), dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, step, none);
+    hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
+                       slabs, loss_slabs, step);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1122,11 +1129,11 @@ EM_API int em_mlp_fused_step(const uint64_t* draws, const int32_t* sidx, int64_t
   const int Bi = (int)B, oi = (int)offset;
   const uint8_t* w = (const uint8_t*)wimg;
   if (loss_kind == 0)
-    hipLaunchKernelGGL((mlp_fused_train_v6_kernel<0, 1>), dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, nullptr, epi);
+    hipLaunchKernelGGL(mlp_fused_step_v6_kernel<0>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
+                       slabs, loss_slabs, epi);
   else
-    hipLaunchKernelGGL((mlp_fused_train_v6_kernel<1, 1>), dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, nullptr, epi);
+    hipLaunchKernelGGL(mlp_fused_step_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
+                       slabs, loss_slabs, epi);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -228,6 +228,43 @@ def gradients(objective: str, margin: np.ndarray, y: np.ndarray):
     raise ValueError(f"unsupported objective {objective}")
 
 
+# ----------------------------------------------------------------------------- histogram modes
+HIST_MODES = ("auto", "exact", "quant")
+QUANT_MIN_ROWS = 32768  # "auto": fixed-point histograms from this many rows on (reference config: 928 rows -> exact)
+_QUANT_SPLIT = 26  # oracle: q = hi * 2^26 + lo, so both halves' float64 GEMM sums stay exact integers
+
+
+def quant_bits(objective: str, n: int, mode: str = "auto", distributed: bool = False) -> int:
+    """Fixed-point scale s of the histogram sums (0 = exact fp64 sums).
+
+    Quantised form (csrc/gbdt.hip gbdt_hist_q): q = rint(x * 2^s) per row for x in {g, h}; the
+    logistic and softmax objectives have |g| <= 1 and 0 < h <= 0.5, so with n < 2^(61-s) every sum
+    of q over rows stays below 2^61 and integer accumulation is exact in any order.  s = 61 -
+    ceil(log2(n+1)) keeps 2^-s at or below the float32 ulp of any |g| >= 2^-20.  Squared error
+    (unbounded g) and the data-parallel path (fp64 all-reduce of the histograms) stay exact."""
+    if mode not in HIST_MODES:
+        raise ValueError(f"hist_mode must be one of {HIST_MODES}")
+    if mode == "exact" or distributed or objective == "reg:squarederror":
+        return 0
+    if (mode == "auto" and n < QUANT_MIN_ROWS) or n >= 1 << 26:
+        return 0
+    return 61 - max(1, int(n).bit_length())  # bit_length(n) == ceil(log2(n + 1))
+
+
+def _quantise(x: np.ndarray, s: int) -> np.ndarray:
+    return np.rint(x.astype(np.float64) * (2.0 ** s)).astype(np.int64)
+
+
+def _int_hist(onehot: np.ndarray, Zq: np.ndarray) -> np.ndarray:
+    """Exact onehot.T @ Zq for int64 Zq (|entries| <= 2^s, n rows, quant_bits' bound n * 2^s < 2^61,
+    n < 2^26): two float64 GEMMs of the 26-bit halves, whose partial sums are integers below 2^53 in
+    any order."""
+    hi = Zq >> _QUANT_SPLIT
+    lo = Zq & ((1 << _QUANT_SPLIT) - 1)
+    return ((onehot.T @ hi.astype(np.float64)).astype(np.int64) << _QUANT_SPLIT) + \
+        (onehot.T @ lo.astype(np.float64)).astype(np.int64)
+
+
 # ----------------------------------------------------------------------------- numpy oracle
 def _best_split_hist(hg, hh, G, H, lam, mcw):
     """hg/hh: [F, B] node histograms.  Returns (gain, f, bin, GL, HL) or None."""
@@ -314,7 +351,8 @@ class GBDT:
 
     def __init__(self, eta=1.0, max_depth=3, objective="reg:logistic", subsample=1.0, gamma=1.0,
                  reg_lambda=1.0, min_child_weight=1.0, base_score=0.5, nround=500, max_bin=256,
-                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1, num_class=0, nthread=0):
+                 eval_metric="logloss", seed=0, backend="auto", log=None, log_every=1, num_class=0, nthread=0,
+                 hist_mode="auto"):
         if objective not in OBJECTIVES:
             raise ValueError(f"objective must be one of {OBJECTIVES}")
         self.eta, self.max_depth, self.objective = float(eta), int(max_depth), objective
@@ -326,6 +364,9 @@ class GBDT:
         if objective in MULTI and eval_metric in ("logloss", "error"):
             self.eval_metric = "m" + eval_metric  # XGBoost's multi-class defaults: mlogloss / merror
         self.backend = backend
+        if hist_mode not in HIST_MODES:
+            raise ValueError(f"hist_mode must be one of {HIST_MODES}")
+        self.hist_mode = hist_mode  # histogram sums: exact fp64 or fixed point (quant_bits); both engines agree
         self.log, self.log_every = log, log_every
         self.trees: TreeArrays | None = None
         self.cuts = None
@@ -441,12 +482,18 @@ class GBDT:
         red = dp.sum_ if dp is not None else (lambda a: a)
         hist = []
         tix = np.arange(T)
+        qs = quant_bits(self.objective, n, self.hist_mode, dp is not None)
+        inv = 2.0 ** -qs
+        self.quant_bits_used = qs
         for rnd in range(R):
             g, h = gradients(self.objective, margin, Y32)
             if self.subsample < 1.0:
                 keep = (rng.random((n, T)) < self.subsample).astype(np.float32)
                 g, h = g * keep, h * keep
-            g64, h64 = g.astype(np.float64), h.astype(np.float64)
+            if qs:  # fixed point: integer sums, exact in any order (== gbdt_hist_q)
+                g64, h64 = _quantise(g, qs), _quantise(h, qs)
+            else:
+                g64, h64 = g.astype(np.float64), h.astype(np.float64)
             node = np.zeros((n, T), dtype=np.int64)
             st = np.zeros((T, NN), np.int8)
             st[:, 0] = 2
@@ -455,28 +502,40 @@ class GBDT:
             gain = np.zeros((T, NN))
             Gs = np.zeros((T, NN))
             Hs = np.zeros((T, NN))
-            Gs[:, 0], Hs[:, 0] = red(g64.sum(0)), red(h64.sum(0))
+            if not qs:
+                Gs[:, 0], Hs[:, 0] = red(g64.sum(0)), red(h64.sum(0))
             for depth in range(D):
                 first, nl = 2 ** depth - 1, 2 ** depth
                 rel = node - first  # [n, T]
                 act = (rel >= 0) & (rel < nl)
                 col = np.where(act, tix[None, :] * nl + rel, 0)
-                Zg = np.zeros((n, T * nl))
-                Zh = np.zeros((n, T * nl))
+                Zg = np.zeros((n, T * nl), dtype=g64.dtype)
+                Zh = np.zeros((n, T * nl), dtype=h64.dtype)
                 rows = np.nonzero(act)
                 Zg[rows[0], col[rows]] = g64[rows]
                 Zh[rows[0], col[rows]] = h64[rows]
-                HG = red(onehot.T @ Zg)  # [sum bins, T*nl]; C4: all-reduced under DP
-                HH = red(onehot.T @ Zh)
+                if qs:
+                    HG, HH = _int_hist(onehot, Zg), _int_hist(onehot, Zh)
+                else:
+                    HG = red(onehot.T @ Zg)  # [sum bins, T*nl]; C4: all-reduced under DP
+                    HH = red(onehot.T @ Zh)
                 # segmented prefix sums: left sums for "bin <= b" of feature f, all columns at once
                 CG, CH = np.cumsum(HG, axis=0), np.cumsum(HH, axis=0)
-                baseg = np.where(rowseg_start[:, None] > 0, CG[np.maximum(rowseg_start - 1, 0)], 0.0)
-                baseh = np.where(rowseg_start[:, None] > 0, CH[np.maximum(rowseg_start - 1, 0)], 0.0)
+                baseg = np.where(rowseg_start[:, None] > 0, CG[np.maximum(rowseg_start - 1, 0)], 0)
+                baseh = np.where(rowseg_start[:, None] > 0, CH[np.maximum(rowseg_start - 1, 0)], 0)
                 GL, HL = CG - baseg, CH - baseh
                 cols_t = np.repeat(tix, nl)
                 cols_i = np.tile(np.arange(nl), T) + first
-                Gn, Hn = Gs[cols_t, cols_i], Hs[cols_t, cols_i]
-                GR, HR = Gn[None, :] - GL, Hn[None, :] - HL
+                if qs:  # node totals = feature 0's cells; every sum converted to double once
+                    Gnq, Hnq = CG[off[1] - 1], CH[off[1] - 1]
+                    GR, HR = (Gnq[None, :] - GL).astype(np.float64) * inv, (Hnq[None, :] - HL).astype(np.float64) * inv
+                    GL, HL = GL.astype(np.float64) * inv, HL.astype(np.float64) * inv
+                    Gn, Hn = Gnq.astype(np.float64) * inv, Hnq.astype(np.float64) * inv
+                    if depth == 0:
+                        Gs[:, 0], Hs[:, 0] = Gn, Hn
+                else:
+                    Gn, Hn = Gs[cols_t, cols_i], Hs[cols_t, cols_i]
+                    GR, HR = Gn[None, :] - GL, Hn[None, :] - HL
                 ok = valid_row[:, None] & (HL >= self.mcw) & (HR >= self.mcw) & (st[cols_t, cols_i] == 2)[None, :]
                 with np.errstate(divide="ignore", invalid="ignore"):
                     gn = GL * GL / (HL + self.lam) + GR * GR / (HR + self.lam) - (Gn * Gn / (Hn + self.lam))[None, :]
@@ -490,7 +549,7 @@ class GBDT:
                     l, r = 2 * i + 1, 2 * i + 2
                     st[t, l] = st[t, r] = 2
                     Gs[t, l], Hs[t, l] = GL[rrow, c], HL[rrow, c]
-                    Gs[t, r], Hs[t, r] = Gs[t, i] - GL[rrow, c], Hs[t, i] - HL[rrow, c]
+                    Gs[t, r], Hs[t, r] = GR[rrow, c], HR[rrow, c]
                 # partition
                 nd = node
                 k = (st[tix[None, :], nd] == 1) & act

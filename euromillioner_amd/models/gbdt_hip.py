@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from ..ops import _native as N
-from .gbdt import TreeArrays, apply_bins
+from .gbdt import TreeArrays, apply_bins, quant_bits
 
 _v, _i, _i64, _f, _u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint32
 
@@ -23,7 +23,7 @@ class _Eval(ctypes.Structure):
 
 N.register_signatures({
     "em_gbdt_fit": (_i, [_v, _v, _i, _i, _v, _v, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f,
-                         _f, _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
+                         _f, _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _i, _v]),
     "em_gbdt_partial_doubles": (_i64, [_i, _i, _i, _v, _i]),
     "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
     "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
@@ -109,6 +109,8 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
         _fit_dp_rounds(model, dp, d_bins, d_Y, n, F, cells, T, margin, ev_names, ev_keep, g, h, node, partial, Gs, Hs,
                        mpart, status, feat, sbin, leaf, gain, cover, history, stream)
     r0 = R if dp is not None else 0
+    qbits = quant_bits(model.objective, n, model.hist_mode, dp is not None)
+    model.quant_bits_used = qbits
     while r0 < R:
         r1 = min(R, r0 + rounds_per_call)
         N.call("em_gbdt_fit", d_bins.data_ptr(), d_Y.data_ptr(), n, F, cells.hp, cells.dev.data_ptr(), T,
@@ -117,7 +119,7 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
                model.gamma, model.mcw, model.subsample, model.seed & 0xFFFFFFFF, g.data_ptr(), h.data_ptr(),
                node.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
                status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), gain.data_ptr(),
-               cover.data_ptr(), hist.data_ptr(), stream)
+               cover.data_ptr(), hist.data_ptr(), qbits, stream)
         hh = hist.view(R, 1 + len(ev_names))[r0:r1].cpu().numpy()
         for i, rnd in enumerate(range(r0, r1)):
             rec = {"round": rnd}

@@ -264,3 +264,82 @@ def test_hip_engine_deep_many_bins_matches_oracle():
     assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
     assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)
     assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-5
+
+
+# ----------------------------------------------------------------------------- fixed-point histograms
+def test_quant_bits_rule():
+    assert G.quant_bits("reg:logistic", 928) == 0  # reference config: exact fp64 sums
+    assert G.quant_bits("reg:logistic", 183500) == 61 - 18  # 2^17 < 183500 < 2^18
+    assert G.quant_bits("multi:softprob", 40000) == 61 - 16
+    assert G.quant_bits("reg:squarederror", 183500) == 0  # unbounded g: always exact
+    assert G.quant_bits("reg:logistic", 183500, distributed=True) == 0  # DP all-reduces fp64
+    assert G.quant_bits("reg:logistic", 183500, mode="exact") == 0
+    assert G.quant_bits("reg:logistic", 500, mode="quant") == 61 - 9
+    with pytest.raises(ValueError):
+        G.quant_bits("reg:logistic", 10, mode="fast")
+
+
+def test_int_hist_is_exact():
+    """The oracle's integer histogram (two float64 GEMMs of 26-bit halves) equals exact integer sums
+    at the largest magnitudes quant_bits allows."""
+    rng = np.random.default_rng(0)
+    n, C, K = 5000, 40, 7
+    s = G.quant_bits("reg:logistic", n, mode="quant")
+    Z = rng.integers(-(1 << s), (1 << s) + 1, size=(n, K), dtype=np.int64)
+    Z[:, 0] = 1 << s  # worst case: every row at the bound
+    onehot = np.zeros((n, C))
+    onehot[np.arange(n), rng.integers(0, C, n)] = 1.0
+    onehot[:, 0] = 1.0
+    exact = onehot.astype(np.int64).T @ Z  # int64 matmul: exact (|sums| < 2^61)
+    assert np.array_equal(G._int_hist(onehot, Z), exact)
+
+
+@pytest.mark.parametrize("obj", ["reg:logistic", "multi:softprob"])
+def test_quantised_oracle_tracks_exact(obj):
+    """hist_mode="quant" changes only the rounding of the histogram sums (2^-s ~ 1e-13 here): the
+    trees of the first rounds are the exact-mode trees and the losses agree to ~1e-9."""
+    if obj == "reg:logistic":
+        X, y = _ref_data()
+    else:
+        X, y = _multi_data(1500, seed=3)
+    n = int(0.7 * len(y))
+    kw = dict(objective=obj, nround=6, max_depth=3, eta=0.5, gamma=0.0, backend="numpy")
+    a = G.GBDT(hist_mode="exact", **kw).fit(X[:n], y[:n], evals={"test": (X[n:], y[n:])})
+    b = G.GBDT(hist_mode="quant", **kw).fit(X[:n], y[:n], evals={"test": (X[n:], y[n:])})
+    assert a.quant_bits_used == 0 and b.quant_bits_used > 40
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, rtol=1e-6, atol=1e-9)
+    assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-6
+
+
+def test_quantised_sums_are_order_free():
+    """Permuting the rows leaves every fixed-point tree bit-identical (integer sums), which is what
+    lets the device accumulate them with order-free atomics."""
+    X, y = _ref_data()
+    kw = dict(nround=4, max_depth=3, eta=0.5, gamma=0.0, backend="numpy", hist_mode="quant")
+    perm = np.random.default_rng(1).permutation(len(y))
+    a = G.GBDT(**kw).fit(X, y)
+    b = G.GBDT(**kw).fit(X[perm], y[perm])
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.array_equal(a.trees.leaf, b.trees.leaf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obj", ["reg:logistic", "multi:softprob"])
+def test_hip_quantised_matches_oracle(obj):
+    """Fixed-point device histograms (LDS int64 atomics) == the oracle's quantised mode, bit for bit
+    in the tree structure, on a multi-chunk, multi-piece problem."""
+    ds = DrawSet.synthetic(n=40001, seed=5, planted=0.9, calendar=False)
+    X = multi_hot(ds.numbers[:-1])
+    if obj == "reg:logistic":
+        Y = multi_hot(ds.numbers[1:])[:, :9]
+    else:
+        Y = (ds.numbers[1:, 0] % 5).astype(np.float64)
+    kw = dict(objective=obj, nround=5, eta=0.5, max_depth=3, gamma=0.0, hist_mode="quant")
+    a = G.GBDT(backend="numpy", **kw).fit(X[:36000], Y[:36000], evals={"test": (X[36000:], Y[36000:])})
+    b = G.GBDT(backend="hip", **kw).fit(X[:36000], Y[:36000], evals={"test": (X[36000:], Y[36000:])})
+    assert b.backend_used == "hip" and b.quant_bits_used == a.quant_bits_used > 0
+    assert np.array_equal(a.trees.status, b.trees.status)
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)
+    assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-5

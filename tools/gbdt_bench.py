@@ -34,16 +34,24 @@ def main():
         X, Y, _ = gbdt_dataset(ds, cfg)
         m = int(0.7 * len(X))
         res = {"case": name, "rows": m, "features": X.shape[1], "tasks": Y.shape[1], "rounds": rounds}
-        for be in (["hip", "numpy"] if with_numpy and not only and not hip_only else ["hip"]):
+        runs = [("hip", "auto")]
+        if n is not None:  # large case: the exact fp64 histogram form too (auto = fixed point here)
+            runs.append(("hip", "exact"))
+        if with_numpy and not only and not hip_only:
+            runs.append(("numpy", "auto"))
+        for be, mode in runs:
             if be == "hip":  # exclude one-time GPU context / code-object load from the timing
-                GBDT.from_params(cfg.gbdt_params(), nround=2, backend=be).fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
-            g = GBDT.from_params(cfg.gbdt_params(), nround=rounds, backend=be)
+                GBDT.from_params(cfg.gbdt_params(), nround=2, backend=be, hist_mode=mode).fit(
+                    X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
+            g = GBDT.from_params(cfg.gbdt_params(), nround=rounds, backend=be, hist_mode=mode)
             t0 = time.perf_counter()
             g.fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
             dt = time.perf_counter() - t0
-            res[f"{be}_s"] = round(dt, 3)
-            res[f"{be}_test_logloss"] = g.history[-1]["test"]
-            res[f"{be}_trees_per_s"] = round(rounds * Y.shape[1] / dt, 1)
+            key = be if mode == "auto" else f"{be}_{mode}"
+            res[f"{key}_s"] = round(dt, 3)
+            res[f"{key}_test_logloss"] = g.history[-1]["test"]
+            res[f"{key}_trees_per_s"] = round(rounds * Y.shape[1] / dt, 1)
+            res[f"{key}_quant_bits"] = int(getattr(g, "quant_bits_used", 0))
         print(json.dumps(res), flush=True)
 
 
