@@ -119,6 +119,9 @@ def _parse():
     ap.add_argument("--model", default="mlp", choices=["mlp", "mlp-wide"],
                     help="mlp = 62->128->62 (headline, fused kernel); mlp-wide = 62->8192->8192->62 (GEMM path)")
     ap.add_argument("--hidden", default=None, help="GEMM-path hidden sizes, e.g. 8192,8192")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype: bf16 (headline: fused kernel / bf16 GEMM engine) or fp32 (the exact-fp32 "
+                         "MFMA GEMM engine, csrc/gemm_f32.hip, for either model)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks sharing one GPU)")
     ap.add_argument("--device-data-gb", type=float, default=0.0,
@@ -226,7 +229,7 @@ def main():
         a.graph = 0  # per-step offsets walk the whole training shard
 
     B = a.batch
-    if a.accum < 1 or (a.accum > 1 and a.model != "mlp-wide"):
+    if a.accum < 1 or (a.accum > 1 and a.model != "mlp-wide" and a.dtype != "fp32"):
         raise SystemExit("--accum applies to --model mlp-wide (the fused kernel takes any batch directly)")
     BS = B * a.accum  # samples per GPU per optimizer step
     n_train = sh.train[1] - sh.train[0]
@@ -240,13 +243,13 @@ def main():
     def boff(i):
         return tr_skip + ((i * spread) % n_off) * BS
     sizes = (62, 128, 62)
-    if a.model == "mlp-wide":
+    if a.model == "mlp-wide" or a.dtype == "fp32":
         from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
 
-        hidden = tuple(int(h) for h in (a.hidden or "8192,8192").split(","))
+        hidden = tuple(int(h) for h in (a.hidden or ("8192,8192" if a.model == "mlp-wide" else "128")).split(","))
         sizes = (62,) + hidden + (62,)
         model = GemmMLPTrainer(sizes, dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group,
-                               bucket_mb=a.bucket_mb, comm_dtype=a.comm_dtype)
+                               bucket_mb=a.bucket_mb, comm_dtype=a.comm_dtype, dtype=a.dtype)
         model.broadcast_parameters()
 
         def step(i):
@@ -372,7 +375,7 @@ def main():
     desc = "mlp " + "->".join(str(x) for x in sizes) + " relu, " + (
         "grouped softmax-CE" if a.loss == "softmax" else "sigmoid-BCE")
     extra = {}
-    if a.model == "mlp-wide":
+    if a.model == "mlp-wide" or a.dtype == "fp32":
         tf = model.flops_per_sample() * BS / (ms / 1000.0) / 1e12
         extra = {"tflops_per_gpu": tf, "flops_per_sample": model.flops_per_sample()}
         if a.accum > 1:
@@ -391,7 +394,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": a.dtype,
             "data": ("synthetic, generated on the GPU: one seeded Euromillions draw sequence of %d draws "
                      "(%d per GPU%s), planted Markov p=%.2f, shared by all ranks; positional 70/30 split, "
                      "contiguous shard per rank; random-init weights"
@@ -400,6 +403,8 @@ def main():
             "config": {"model": desc,
                        "global_batch": BS * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
+                       "engine": ("gemm_f32" if a.dtype == "fp32" else "gemm" if a.model == "mlp-wide"
+                                  else a.impl),
                        "graph_steps": C if use_graph else 0,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
                        **({"comm_dtype": a.comm_dtype, "bucket_mb": a.bucket_mb} if a.model == "mlp-wide" else {}),

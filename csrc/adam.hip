@@ -49,11 +49,12 @@ constexpr int EM_ADAM_PRE = 4;
 // torch.optim.Adam update of parameter p with gradient g (pad slots of the MLP image pinned to 0).
 // w0/m0/v0 are params[p]/m[p]/v[p], loaded by the caller (the slab kernel issues those loads
 // before its slab reduction so their latency overlaps it).
-EM_DEVICE void adam_apply_loaded(int p, float g, float w0, float m0, float v0, int tstep, float* __restrict__ params,
-                                 float* __restrict__ m, float* __restrict__ v, const float* __restrict__ hp,
-                                 uint8_t* __restrict__ mlp_img) {
+// bc1 / bc2: the step's bias corrections (bias_correction(beta, t)), computed by the caller where
+// their latency hides (adam_slab4_kernel: while its slab loads are in flight)
+EM_DEVICE void adam_apply_bc(int p, float g, float w0, float m0, float v0, float bc1, float bc2,
+                             float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
+                             const float* __restrict__ hp, uint8_t* __restrict__ mlp_img) {
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
-  const float bc1 = bias_correction(b1, tstep), bc2 = bias_correction(b2, tstep);
   if (mlp_img && mlp::pad_slot(p)) {
     params[p] = 0.f;
     m[p] = 0.f;
@@ -67,6 +68,13 @@ EM_DEVICE void adam_apply_loaded(int p, float g, float w0, float m0, float v0, i
     params[p] = w;
     if (mlp_img) mlp::pack_one(p, w, mlp_img);
   }
+}
+
+EM_DEVICE void adam_apply_loaded(int p, float g, float w0, float m0, float v0, int tstep, float* __restrict__ params,
+                                 float* __restrict__ m, float* __restrict__ v, const float* __restrict__ hp,
+                                 uint8_t* __restrict__ mlp_img) {
+  adam_apply_bc(p, g, w0, m0, v0, bias_correction(hp[1], tstep), bias_correction(hp[2], tstep), params, m, v, hp,
+                mlp_img);
 }
 
 EM_DEVICE void adam_apply(int p, float g, int tstep, float* __restrict__ params, float* __restrict__ m,
@@ -163,13 +171,22 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
     v0 = v[p];
   }
   f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
+  float bc1 = 1.f, bc2 = 1.f;  // bias corrections: their fp64 chain runs under the slab loads below
   int sl = g;
   for (; sl + 15 * A4_G < nslab; sl += 16 * A4_G) {
     f32x4 t[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) t[k] = *reinterpret_cast<const f32x4*>(src + (size_t)(sl + k * A4_G) * stride);
+    if (sl == g && mode != 1 && threadIdx.x < 64) {
+      bc1 = bias_correction(hp[1], tstep);
+      bc2 = bias_correction(hp[2], tstep);
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[k & 3] += t[k];
+  }
+  if (nslab <= g + 15 * A4_G && mode != 1 && threadIdx.x < 64) {  // (no full block of slabs above)
+    bc1 = bias_correction(hp[1], tstep);
+    bc2 = bias_correction(hp[2], tstep);
   }
   for (; sl < nslab; sl += A4_G) acc[0] += *reinterpret_cast<const f32x4*>(src + (size_t)sl * stride);
   part[g][q] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
@@ -187,7 +204,7 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
     for (int k = 0; k < A4_G; ++k) t += part[k][pq][e];
     const float gsum = t * grad_scale;
     if (mode == 1) grad_io[p] = gsum;
-    else adam_apply_loaded(p, gsum, w0, m0, v0, tstep, params, m, v, hp, mlp_img);
+    else adam_apply_bc(p, gsum, w0, m0, v0, bc1, bc2, params, m, v, hp, mlp_img);
   }
   if (mode != 1 && !pre) adam_end(state, tstep);
 }

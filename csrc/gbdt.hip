@@ -113,6 +113,7 @@ __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restr
 constexpr int HIST_MAX_CHUNK = 1024;             // rows staged in LDS per piece
 constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // 8-byte words of per-chunk partials (1 GiB) per level
 constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (+ staged rows)
+constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
 
 __global__ void __launch_bounds__(256)
 gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
@@ -205,10 +206,20 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
 // double is exact
 EM_DEVICE long long quantise(float x, double scale) { return (long long)__builtin_rint((double)x * scale); }
 
+// LDS layout of the fixed-point form: two planes (g sums, then h sums) of 8-byte cells, so a lane's
+// atomic touches one 8-byte word, and one pad cell after every feature's bins: with the compact
+// layout a one-hot feature's cells sit 2 words apart, lanes f and f + 16 of a wave share a bank pair
+// and every atomic is replayed 4-8 times; the pad makes the per-feature stride 3 words (odd).
+// Cell (feature f, bin b) of tile node nd: plane[nd * ldsW + (foff[f] - c0) + (f - f0) + b]; the
+// node's row total sits in its last cell, plane[nd * ldsW + ldsW - 1].
+// Bin 0 is never accumulated: each p-phase has one extra "total" lane that adds every row of the
+// node, and bin 0 of a feature is written out as total - (its other bins), exact in integers.  For
+// the multi-hot draw features (a number is drawn in ~7 of 62 columns) that removes ~90 % of the
+// atomics' active lanes.
 __global__ void __launch_bounds__(256)
 gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
             const int16_t* __restrict__ node, const int* __restrict__ foff, long long* __restrict__ partial, int T,
-            int n, int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, double qscale) {
+            int n, int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsW, int piece, double qscale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int c = blockIdx.x, t = blockIdx.y;
@@ -216,20 +227,44 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
   const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
   const int f0 = ft * FT, f1 = min(F, f0 + FT), n0 = nt * NTn;
   const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
-  long long* hist = reinterpret_cast<long long*>(smem);  // [NTn][ldsC][2], shared by all P phases
-  const int per = NTn * ldsC * 2;
-  for (int i = threadIdx.x; i < per; i += blockDim.x) hist[i] = 0;
-  long long* sq = hist + per;  // staged rows: (qg, qh) pairs, then the tile-relative node ids
+  long long* hist = reinterpret_cast<long long*>(smem);  // [2 planes][NTn][ldsW], shared by all P phases
+  const int per = NTn * ldsW;
+  for (int i = threadIdx.x; i < 2 * per; i += blockDim.x) hist[i] = 0;
+  long long* sq = hist + 2 * per;  // staged rows: (qg, qh) pairs, the tile-relative node ids, the bin rows
   int16_t* sn = reinterpret_cast<int16_t*>(sq + 2 * piece);
+  u32x4* sbw = reinterpret_cast<u32x4*>(smem + (((size_t)(2 * per + 2 * piece) * 8 + (size_t)piece * 2 + 15) & ~15));
+  const int64_t nbytes = (int64_t)n * F;
   const int64_t base = (int64_t)t * n;
-  const int nth = f1 - f0;
+  const int nth = f1 - f0 + 1;  // the tile's features + the total lane
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
-  const int f = f0 + (p < P ? fl : 0);
-  long long* my = hist + (foff[f] - c0) * 2;
+  const bool tot = fl == nth - 1;
+  const int f = f0 + ((p < P && !tot) ? fl : 0);
+  long long* my = tot ? hist + ldsW - 2 : hist + (foff[f] - c0) + (f - f0);  // total lane: "bin 1" = last cell
   const int rb = c * chunk, re = min(n, rb + chunk);
   for (int r0 = rb; r0 < re; r0 += piece) {
     const int r1 = min(re, r0 + piece);
     __syncthreads();  // the previous piece's staging is consumed (first pass: the zeroing is done)
+    // the piece's bin rows: 16-B words covering bytes [r0 F, r1 F), all loads in flight at once
+    // (range-checked buffer loads: words past the end of the array read as 0)
+    const int64_t w0 = ((int64_t)r0 * F) >> 4;
+    const int boff = (int)(((int64_t)r0 * F) & 15);
+    const int nw = (int)((((int64_t)r1 * F + 15) >> 4) - w0);
+    {
+      const int64_t left = nbytes - w0 * 16;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(bins + w0 * 16), 0, (int)(left < 0x7FFFFFF0 ? left : 0x7FFFFFF0), 0x00020000);
+      // a word running past the array's end would read as 0 in full: that one is assembled bytewise
+      const bool tail = (w0 + nw) * 16 > nbytes;
+      for (int i = threadIdx.x; i < nw - (tail ? 1 : 0); i += blockDim.x)
+        sbw[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, i * 16, 0, 0));
+      if (tail && threadIdx.x == 0) {
+        uint8_t* wb = reinterpret_cast<uint8_t*>(sbw + nw - 1);
+        for (int k = 0; k < 16; ++k) {
+          const int64_t q = (w0 + nw - 1) * 16 + k;
+          wb[k] = q < nbytes ? bins[q] : 0;
+        }
+      }
+    }
     for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
       sq[2 * (r - r0)] = quantise(g[base + r], qscale);
       sq[2 * (r - r0) + 1] = quantise(h[base + r], qscale);
@@ -238,30 +273,31 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
     __syncthreads();
     if (p < P) {
       const int len = r1 - r0;
-      const uint8_t* col = bins + (int64_t)r0 * F + f;
+      const uint8_t* col = reinterpret_cast<const uint8_t*>(sbw) + boff + f;  // row r at col[r * F]
       int r = p;  // phases interleave rows, so the P waves of a row read neighbouring bin bytes
       for (; r + 7 * P < len; r += 8 * P) {
         int b[8], nd[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          b[u] = col[(int64_t)(r + u * P) * F];
+          b[u] = tot ? 1 : col[(r + u * P) * F];
           nd[u] = sn[r + u * P];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          if ((unsigned)nd[u] >= (unsigned)NTn) continue;
-          long long* e = my + (nd[u] * ldsC + b[u]) * 2;
+          if ((unsigned)nd[u] >= (unsigned)NTn || b[u] == 0) continue;
+          long long* e = my + nd[u] * ldsW + b[u];
           const long long qg = sq[2 * (r + u * P)], qh = sq[2 * (r + u * P) + 1];
           __hip_atomic_fetch_add(e, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add(e + 1, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(e + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       for (; r < len; r += P) {
         const int nd = sn[r];
-        if ((unsigned)nd >= (unsigned)NTn) continue;
-        long long* e = my + (nd * ldsC + col[(int64_t)r * F]) * 2;
+        const int bb = tot ? 1 : col[r * F];
+        if ((unsigned)nd >= (unsigned)NTn || bb == 0) continue;
+        long long* e = my + nd * ldsW + bb;
         __hip_atomic_fetch_add(e, sq[2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(e + 1, sq[2 * r + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(e + per, sq[2 * r + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
   }
@@ -270,10 +306,21 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
   const int nn = min(NTn, nodesL - n0);
   for (int i = threadIdx.x; i < nn * Ct; i += blockDim.x) {
     const int nd = i / Ct, cc = i - nd * Ct;
-    const long long* e = hist + (nd * ldsC + cc) * 2;
+    int fi = f0;  // the feature of compact cell c0 + cc (its pad cells precede it)
+    while (foff[fi + 1] <= c0 + cc) ++fi;
+    const long long* e = hist + nd * ldsW + cc + (fi - f0);
+    long long vg = e[0], vh = e[per];
+    if (c0 + cc == foff[fi]) {  // bin 0: the node's total minus the feature's other bins
+      vg = hist[nd * ldsW + ldsW - 1];
+      vh = hist[per + nd * ldsW + ldsW - 1];
+      for (int k = 1; k < foff[fi + 1] - foff[fi]; ++k) {
+        vg -= e[k];
+        vh -= e[per + k];
+      }
+    }
     long long* o = out + ((int64_t)(n0 + nd) * C + c0 + cc) * 2;
-    o[0] = e[0];
-    o[1] = e[1];
+    o[0] = vg;
+    o[1] = vh;
   }
 }
 
@@ -604,24 +651,26 @@ struct HistPlan {
 bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, HistPlan& pl) {
   const int nodesL = 1 << level;
   for (int NTn = nodesL; NTn >= 1; NTn >>= 1) {
-    for (int FT = F < 256 ? F : 256;; FT = (FT + 1) / 2) {
+    for (int FT = F < (quant ? 255 : 256) ? F : (quant ? 255 : 256);; FT = (FT + 1) / 2) {
       int maxC = 0;
       for (int f0 = 0; f0 < F; f0 += FT) {
         const int f1 = f0 + FT < F ? f0 + FT : F;
         maxC = foff[f1] - foff[f0] > maxC ? foff[f1] - foff[f0] : maxC;
       }
-      int P = 256 / FT;
+      const int lanes = FT + (quant ? 1 : 0);  // fixed point: + the total lane per phase
+      const int W = maxC + (quant ? FT + 1 : 0);  // fixed point: + a pad cell per feature + the total cell
+      int P = 256 / lanes;
       P = P > 4 ? 4 : (P < 1 ? 1 : P);
       for (; P >= 1; --P)
-        if ((int64_t)(quant ? 1 : P) * NTn * maxC * 16 <= HIST_LDS_BUDGET) break;
+        if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= HIST_LDS_BUDGET) break;
       if (P >= 1) {
         pl.FT = FT;
         pl.NTn = NTn;
         pl.P = P;
-        pl.ldsC = maxC;
+        pl.ldsC = W;
         pl.nft = (F + FT - 1) / FT;
         pl.ntn = nodesL / NTn;
-        pl.threads = ((FT * P + 63) / 64) * 64;
+        pl.threads = ((lanes * P + 63) / 64) * 64;
         // chunks: ~4096 blocks per level, >= 64 rows each, and the per-chunk partials within the cap
         const int64_t per_chunk = (int64_t)T * pl.nft * pl.ntn;
         const int64_t S = (int64_t)T * nodesL * foff[F] * 2;
@@ -633,9 +682,13 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
         chunk = chunk < 64 ? 64 : chunk;
         pl.chunk = (int)chunk;
         pl.nchunks = (int)((n + chunk - 1) / chunk);
-        pl.piece = HIST_MAX_CHUNK;
-        // staged rows: (g, h) floats + node id (exact); (qg, qh) int64 + node id (fixed point)
-        pl.lds = (size_t)(quant ? 1 : P) * NTn * maxC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4;
+        // staged rows: (g, h) floats + node id (exact); (qg, qh) int64 + node id + the piece's bin
+        // rows (fixed point: ~16 KB of bins per piece, fetched with 16-B loads)
+        pl.piece = quant ? ((HIST_QBIN_LDS / F) & ~15) : HIST_MAX_CHUNK;
+        if (pl.piece > HIST_MAX_CHUNK) pl.piece = HIST_MAX_CHUNK;
+        if (pl.piece < 16) pl.piece = 16;
+        pl.lds = (size_t)(quant ? 1 : P) * NTn * pl.ldsC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4 +
+                 (quant ? ((size_t)pl.piece * F + 32 + 15) / 16 * 16 : 0);
         return true;
       }
       if (FT == 1) break;

@@ -180,51 +180,124 @@ __global__ void onehot_lags_kernel(const uint64_t* __restrict__ masks, const int
   }
 }
 
-// K10: loss + dL/dlogits for the GEMM-path MLPs.  One wavefront per sample, lane j = output j
-// (62 live lanes; 62/63 are padding and get dz = 0).  dz is written bf16 (the next GEMM's
-// operand) already scaled by grad_scale (1/global_batch); per-block loss sums -> partials.
+// K10: loss + dL/dlogits for the GEMM-path MLPs.  16 lanes per sample, lane q = outputs 4q..4q+3
+// (one 16-B load of the logit row per lane: a wave reads 4 whole rows), group statistics as
+// 16-lane butterfly reductions, grid-stride over 4-sample wave groups.  Outputs 62/63 are padding
+// (dz = 0).  dz is written already scaled by grad_scale (1/global_batch) as the next GEMM's operand
+// type; partials[w] = the loss of samples 4w..4w+3 summed in sample order.
+EM_DEVICE float g16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+  return v;
+}
+EM_DEVICE float g16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 16));
+  return v;
+}
+
 template <typename T>  // dz element type: __bf16 (bf16 GEMM path) or float (fp32 path)
-__global__ void loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __restrict__ masks,
-                                 const int32_t* __restrict__ sidx, int64_t B, int64_t offset, int loss_kind,
-                                 float grad_scale, T* __restrict__ dz, int ldz, float* __restrict__ partials) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __shared__ float red[4];
-  const int64_t s = (int64_t)blockIdx.x * 4 + w;
-  float loss = 0.f;
-  if (s < B) {
-    const int64_t idx = sidx ? (int64_t)sidx[s] : offset + s;
-    const uint64_t tm = masks[idx + 1] & (MAIN_BITS | STAR_BITS);
-    const bool live = lane < 62;
-    const float z = live ? logits[s * ld + lane] : 0.f;
-    const float y = live ? (float)((tm >> lane) & 1ull) : 0.f;
-    float g = 0.f;
-    if (loss_kind == 0) {
-      const bool main = lane < 50;
-      const float mx_m = wave_max(main ? z : -INFINITY);
-      const float mx_s = wave_max(live && !main ? z : -INFINITY);
-      const float mx = main ? mx_m : mx_s;
-      const float e = live ? __expf(z - mx) : 0.f;
-      const float se_m = wave_sum(main ? e : 0.f), se_s = wave_sum(live && !main ? e : 0.f);
-      const float se = main ? se_m : se_s;
-      // target counts as wave sums: a lane-selected pair of 64-bit popcounts here produced wrong
-      // counts for some waves on gfx950 (ROCm 7.2; ISA looked right, results were nondeterministic)
-      const float sy_m = wave_sum(main ? y : 0.f), sy_s = wave_sum(live && !main ? y : 0.f);
-      const float sy = main ? sy_m : sy_s;
-      const float inv = 1.f / fmaxf(sy, 1.f);
-      const float p = e / se;
-      g = live ? (p * sy - y) * inv : 0.f;
-      loss = wave_sum(live ? -y * (z - mx - __logf(se)) * inv : 0.f);
-    } else {
-      const float sg = 1.f / (1.f + __expf(-z));
-      g = live ? (sg - y) * (1.f / 62.f) : 0.f;
-      const float l = fmaxf(z, 0.f) - z * y + __logf(1.f + __expf(-fabsf(z)));
-      loss = wave_sum(live ? l : 0.f) * (1.f / 62.f);
+__global__ void __launch_bounds__(256)
+loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __restrict__ masks,
+                 const int32_t* __restrict__ sidx, int64_t B, int64_t offset, int loss_kind, float grad_scale,
+                 T* __restrict__ dz, int ldz, float* __restrict__ partials) {
+  const int lane = threadIdx.x & 63, q = lane & 15, sub = lane >> 4;
+  const int64_t ngroups = (B + 3) / 4;
+  for (int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; gw < ngroups;
+       gw += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int64_t s = gw * 4 + sub;
+    const bool ok = s < B;
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    uint64_t tm = 0;
+    if (ok) {
+      const int64_t idx = sidx ? (int64_t)sidx[s] : offset + s;
+      tm = masks[idx + 1] & (MAIN_BITS | STAR_BITS);
+      if ((ld & 3) == 0) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(logits + s * ld + 4 * q);
+        z[0] = v[0]; z[1] = v[1]; z[2] = v[2]; z[3] = v[3];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = 4 * q + k < 62 ? logits[s * ld + 4 * q + k] : 0.f;
+      }
     }
-    dz[s * ldz + lane] = (T)(g * grad_scale);
+    float y[4], g[4];
+    bool live[4], mn[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = 4 * q + k;
+      live[k] = o < 62;
+      mn[k] = o < 50;
+      y[k] = live[k] ? (float)((tm >> o) & 1ull) : 0.f;
+      if (!live[k]) z[k] = 0.f;
+    }
+    float loss = 0.f;
+    if (loss_kind == 0) {
+      float am = -INFINITY, as = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (mn[k]) am = fmaxf(am, z[k]);
+        else if (live[k]) as = fmaxf(as, z[k]);
+      }
+      const float mx_m = g16_max(am), mx_s = g16_max(as);
+      float e[4], sm = 0.f, ss = 0.f, ym = 0.f, ys = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        e[k] = live[k] ? __expf(z[k] - (mn[k] ? mx_m : mx_s)) : 0.f;
+        if (mn[k]) {
+          sm += e[k];
+          ym += y[k];
+        } else {
+          ss += e[k];
+          ys += y[k];
+        }
+      }
+      const float se_m = g16_sum(sm), se_s = g16_sum(ss), sy_m = g16_sum(ym), sy_s = g16_sum(ys);
+      const float inv_m = 1.f / fmaxf(sy_m, 1.f), inv_s = 1.f / fmaxf(sy_s, 1.f);
+      const float lse_m = mx_m + __logf(se_m), lse_s = mx_s + __logf(se_s);
+      float l = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float se = mn[k] ? se_m : se_s, sy = mn[k] ? sy_m : sy_s, inv = mn[k] ? inv_m : inv_s;
+        g[k] = live[k] ? (e[k] / se * sy - y[k]) * inv : 0.f;
+        l += live[k] ? -y[k] * (z[k] - (mn[k] ? lse_m : lse_s)) * inv : 0.f;
+      }
+      loss = g16_sum(l);
+    } else {
+      float l = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float sg = 1.f / (1.f + __expf(-z[k]));
+        g[k] = live[k] ? (sg - y[k]) * (1.f / 62.f) : 0.f;
+        l += live[k] ? fmaxf(z[k], 0.f) - z[k] * y[k] + __logf(1.f + __expf(-fabsf(z[k]))) : 0.f;
+      }
+      loss = g16_sum(l) * (1.f / 62.f);
+    }
+    if (ok) {
+      T d4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d4[k] = (T)(g[k] * grad_scale);
+      T* d = dz + s * ldz + 4 * q;
+      if ((ldz & 3) == 0) {  // one 16-B (fp32) / 8-B (bf16) store per lane
+        if constexpr (sizeof(T) == 4) {
+          f32x4 v;
+          __builtin_memcpy(&v, d4, 16);
+          *reinterpret_cast<f32x4*>(d) = v;
+        } else {
+          uint64_t v;
+          __builtin_memcpy(&v, d4, 8);
+          *reinterpret_cast<uint64_t*>(d) = v;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = d4[k];
+      }
+    }
+    // the wave's 4 sample losses in sample order (a sample past B contributes +0)
+    const float l0 = __shfl(loss, 0), l1 = __shfl(loss, 16), l2 = __shfl(loss, 32), l3 = __shfl(loss, 48);
+    const int64_t s0 = gw * 4;
+    if (lane == 0)
+      partials[gw] = ((l0 + (s0 + 1 < B ? l1 : 0.f)) + (s0 + 2 < B ? l2 : 0.f)) + (s0 + 3 < B ? l3 : 0.f);
   }
-  if (lane == 0) red[w] = loss;
-  __syncthreads();
-  if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 }  // namespace
@@ -270,13 +343,21 @@ EM_API int em_onehot_encode_f32(const uint64_t* draws, const int32_t* sidx, int6
   return 0;
 }
 
+namespace {
+// 16 samples per 256-thread block; at most 4096 blocks (16 per CU), grid-stride beyond
+unsigned loss_grad_blocks(int64_t B) {
+  const int64_t nb = (B + 15) / 16;
+  return (unsigned)(nb < 4096 ? nb : 4096);
+}
+}  // namespace
+
 EM_API int em_loss_grad(const float* logits, int ld, const uint64_t* masks, const int32_t* sidx, int64_t B,
                         int64_t offset, int loss_kind, float grad_scale, void* dz, int ldz, float* partials,
                         hipStream_t stream) {
   if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
     return EM_ERR_ARG;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(loss_grad_kernel<__bf16>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks,
+  hipLaunchKernelGGL(loss_grad_kernel<__bf16>, dim3(loss_grad_blocks(B)), dim3(256), 0, stream, logits, ld, masks,
                      sidx, B, offset, loss_kind, grad_scale, (__bf16*)dz, ldz, partials);
   EM_CHECK_LAUNCH();
   return 0;
@@ -288,7 +369,7 @@ EM_API int em_loss_grad_f32(const float* logits, int ld, const uint64_t* masks, 
   if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
     return EM_ERR_ARG;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(loss_grad_kernel<float>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, stream, logits, ld, masks,
+  hipLaunchKernelGGL(loss_grad_kernel<float>, dim3(loss_grad_blocks(B)), dim3(256), 0, stream, logits, ld, masks,
                      sidx, B, offset, loss_kind, grad_scale, dz, ldz, partials);
   EM_CHECK_LAUNCH();
   return 0;

@@ -115,6 +115,9 @@ class GemmMLPTrainer:
         self._ws_cache: dict[int, dict] = {}
         self._checked = False
         self.panel_ncu: int | None = None  # (tests: pretend a smaller GPU to get several wgrad panels)
+        # (tools/wide_overlap.py: a factory (flat, bucket_elems) -> object with ready(a, c) / wait() that
+        # stands in for the all-reduce on one GPU, e.g. a side-stream reduce-copy per bucket)
+        self.comm_emulator = None
         self.last_buckets: list[tuple[int, int]] = []
 
     # ------------------------------------------------------------------ layout
@@ -329,7 +332,9 @@ class GemmMLPTrainer:
             self.grads[self.P:] += part.sum()
         self.grads[self.P:].mul_(1.0 / gb)
         red = None
-        if self.group is not None:
+        if self.comm_emulator is not None and self.group is None:
+            red = self.comm_emulator(self.grads, self.bucket_elems)
+        elif self.group is not None:
             import torch.distributed as dist
 
             from ..parallel.buckets import RangeAllReducer
@@ -341,7 +346,7 @@ class GemmMLPTrainer:
         self._backward(dz, inputs, ws, red.ready if red is not None else None, accumulate=accum > 1)
         if red is not None:
             red.wait()
-            self.last_buckets = red.launched
+            self.last_buckets = list(red.launched)
         g = self.grads_bf16 if self.grads_bf16 is not None else self.grads[:self.P]
         FM.adam_flat(self.params, g, self.m, self.v, self.hp, self.state, 1.0, shadow=self.shadow)
         return self.grads[self.P:]

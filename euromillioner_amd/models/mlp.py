@@ -90,10 +90,12 @@ class DrawMLP(nn.Module):
 class FusedSmallMLP:
     """Flagship trainer: 62->128->62 ReLU MLP, bf16 MFMA compute, fp32 master weights + Adam.
 
-    Single process: ONE launch per optimizer step (``fused_mlp.train_step``: the slab reduction and
-    Adam run inside the train kernel, overlapping its slowest workgroups).  ``fused_adam=False`` (or
-    ``EUROM_FUSED_ADAM=0``) keeps the two-launch form (train kernel, then ``em_adam_slab``), which
-    gives bit-identical parameters.  Data parallel: train kernel -> all-reduce -> Adam."""
+    Single process: two launches per optimizer step (train kernel, then ``em_adam_slab``).
+    ``fused_adam=True`` (or ``EUROM_FUSED_ADAM=1``) runs the one-launch form instead
+    (``fused_mlp.train_step``: the slab reduction and Adam inside the train kernel, overlapping its
+    slowest workgroups) -- bit-identical parameters, but measured 4.3 us per step slower on MI355X
+    (93.3 vs 89.0 us, docs/DESIGN.md), so it is opt-in.  Data parallel: train kernel -> all-reduce
+    -> Adam."""
 
     def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
@@ -132,7 +134,7 @@ class FusedSmallMLP:
         import os
 
         if fused_adam is None:
-            fused_adam = os.environ.get("EUROM_FUSED_ADAM", "1") != "0"
+            fused_adam = os.environ.get("EUROM_FUSED_ADAM", "0") == "1"
         self.fused_adam = bool(fused_adam)
         FM.pack(self.params, self.img)
         self._checked = False

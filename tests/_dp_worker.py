@@ -27,8 +27,52 @@ def _identical(t: torch.Tensor, world: int) -> bool:
     return all(torch.equal(allv[0], a) for a in allv)
 
 
+def wide_case(dev, rank, world):
+    """Wide GEMM trainer, data parallel with the bf16 wire and >= 3 async wgrad panels per hidden
+    layer (panel_ncu pretends a 4-CU GPU): every rank ends bit-identical, and the parameters track a
+    single-process run on the concatenated batch (the wire rounds the gradient to bf16, so Adam's
+    per-element step may differ in magnitude, never by more than 2 lr per step)."""
+    from euromillioner_amd.data.device_gen import generate_masks
+    from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
+
+    steps, B, lr = 3, 2048, 2e-3
+    sizes = (62, 1024, 1024, 62)
+    draws = generate_masks(world * B * steps + 16, seed=23, planted=0.8, device=dev)
+    g = GemmMLPTrainer(sizes, dev, lr=lr, seed=0, process_group=dist.group.WORLD, bucket_mb=0.25,
+                       comm_dtype="bf16")
+    g.panel_ncu = 4
+    g.broadcast_parameters()
+    panels = g.wgrad_panels(1)
+    for i in range(steps):
+        g.step(draws, B, offset=(i * world + rank) * B)
+    torch.cuda.synchronize()
+    out = {"rank": rank, "world": world, "panels": len(panels), "wire_bf16": g.grads_bf16 is not None,
+           "buckets": len(g.last_buckets), "identical": _identical(g.params, world)}
+    if rank == 0:
+        ref = GemmMLPTrainer(sizes, dev, lr=lr, seed=0)
+        for i in range(steps):
+            ref.step(draws, world * B, offset=i * world * B)
+        torch.cuda.synchronize()
+        d = (ref.params - g.params).abs()
+        out.update(max_diff=float(d.max()), mean_diff=float(d.mean()), lr=lr, steps=steps)
+    return out
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if os.environ.get("DP_CASE") == "wide":
+        backend = os.environ.get("DP_BACKEND", "nccl")
+        dev = torch.device("cuda", rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        out = wide_case(dev, rank, world)
+        print("DP_RESULT " + json.dumps(out), flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     backend = os.environ.get("DP_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", rank % ndev)

@@ -28,12 +28,12 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def _run(world: int, backend: str, timeout: int = 180):
+def _run(world: int, backend: str, timeout: int = 180, case: str = ""):
     port = _port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DP_BACKEND=backend,
+                   MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DP_BACKEND=backend, DP_CASE=case,
                    HSA_ENABLE_IPC_MODE_LEGACY="0")
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_dp_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
@@ -74,3 +74,18 @@ def test_rccl_data_parallel(world):
 def test_gloo_data_parallel_rehearsal():
     """Same worker, gloo group (host all-reduce of device tensors); ranks may share one GPU."""
     _check(_run(2, "gloo"), expect_xgmi=None)
+
+
+@pytest.mark.parametrize("world,backend", [(1, "gloo"), (2, "nccl"), (4, "nccl"), (8, "nccl")])
+def test_wide_dp_panels_bf16_wire(world, backend):
+    """Wide GEMM trainer (62->1024->1024->62) with the bf16 gradient wire and 4 async wgrad panels on
+    the 1024x1024 layer: ranks bit-identical, tracking the single-process run on the concatenated batch."""
+    if backend == "nccl" and _ndev() < world:
+        pytest.skip(f"RCCL world {world} needs {world} GPUs (this box has {_ndev()})")
+    res = _run(world, backend, case="wide")
+    for r in res:
+        assert r["identical"] and r["wire_bf16"] and r["panels"] >= 3, r
+        assert r["buckets"] >= r["panels"] + 2, r  # the hidden wgrad's panels + the other layers' ranges
+    r0 = res[0]
+    assert r0["max_diff"] <= 2 * r0["lr"] * r0["steps"] + 1e-6, r0
+    assert r0["mean_diff"] <= 0.05 * r0["lr"], r0
