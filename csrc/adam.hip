@@ -253,7 +253,42 @@ adam_flat_kernel(float* __restrict__ params, const G* __restrict__ grad, float* 
   const int tstep = adam_begin(state);
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
   const float bc1 = bias_correction(b1, tstep), bc2 = bias_correction(b2, tstep);
-  for (int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += (int64_t)gridDim.x * blockDim.x * 4) {
+  // AF_U float4 groups per thread per pass, every load of the pass issued before the first update
+  // (one group per pass left a single 64-B round trip in flight per thread: 4.4 TB/s on 67 M params)
+  constexpr int AF_U = 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  for (; i0 + (AF_U - 1) * stride + 4 <= n; i0 += AF_U * stride) {
+    f32x4 w[AF_U], g[AF_U], mm[AF_U], vv[AF_U];
+#pragma unroll
+    for (int u = 0; u < AF_U; ++u) {
+      const int64_t i4 = i0 + u * stride;
+      w[u] = *reinterpret_cast<const f32x4*>(params + i4);
+      g[u] = load_grad4<G>(grad + i4);
+      mm[u] = *reinterpret_cast<const f32x4*>(m + i4);
+      vv[u] = *reinterpret_cast<const f32x4*>(v + i4);
+    }
+#pragma unroll
+    for (int u = 0; u < AF_U; ++u) {
+      const int64_t i4 = i0 + u * stride;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gg = g[u][k] * grad_scale + wd * w[u][k];
+        mm[u][k] = b1 * mm[u][k] + (1.f - b1) * gg;
+        vv[u][k] = b2 * vv[u][k] + (1.f - b2) * gg * gg;
+        w[u][k] -= lr * (mm[u][k] / bc1) / (sqrtf(vv[u][k] / bc2) + eps);
+      }
+      *reinterpret_cast<f32x4*>(params + i4) = w[u];
+      *reinterpret_cast<f32x4*>(m + i4) = mm[u];
+      *reinterpret_cast<f32x4*>(v + i4) = vv[u];
+      if (shadow) {
+        bf16x4 sb;
+        sb[0] = (__bf16)w[u][0]; sb[1] = (__bf16)w[u][1]; sb[2] = (__bf16)w[u][2]; sb[3] = (__bf16)w[u][3];
+        *reinterpret_cast<bf16x4*>(shadow + i4) = sb;
+      }
+    }
+  }
+  for (int64_t i4 = i0; i4 < n; i4 += stride) {
     if (i4 + 4 <= n) {
       f32x4 w = *reinterpret_cast<const f32x4*>(params + i4);
       f32x4 g = load_grad4<G>(grad + i4);

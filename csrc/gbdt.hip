@@ -16,7 +16,9 @@
 //   K11 gbdt_predict    ensemble traversal over binned rows
 //   K13 gbdt_metric     logloss / rmse / error partial sums -> per-round history
 // Node numbering is heap order (children 2i+1, 2i+2); status 0 unused / 1 split / 2 leaf.
+#include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 
@@ -218,17 +220,23 @@ EM_DEVICE long long quantise(float x, double scale) { return (long long)__builti
 // atomics' active lanes.
 __global__ void __launch_bounds__(256)
 gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
-            const int16_t* __restrict__ node, const int* __restrict__ foff, long long* __restrict__ partial, int T,
-            int n, int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsW, int piece, double qscale) {
+            const int16_t* __restrict__ node, const int* __restrict__ foff, const int* __restrict__ fmap,
+            const int* __restrict__ gfoff, long long* __restrict__ partial, int T, int n, int F, int Fs, int C,
+            int level, int chunk, int FT, int NTn, int P, int ldsW, int piece, double qscale, int R) {
+  // features: the Fs features of a sub-problem (foff: their compact cells; fmap: sub -> row column,
+  // null = identity; gfoff: the full problem's cells, where the output goes); F = bytes per bin row.
+  // R replicas of each node's cells (phase p uses p % R): with few features per tile the phases of a
+  // wave are consecutive rows, whose calendar bins (and the total lane) hit the same word otherwise.
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int c = blockIdx.x, t = blockIdx.y;
-  const int nft = (F + FT - 1) / FT;
+  const int nft = (Fs + FT - 1) / FT;
   const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
-  const int f0 = ft * FT, f1 = min(F, f0 + FT), n0 = nt * NTn;
+  const int f0 = ft * FT, f1 = min(Fs, f0 + FT), n0 = nt * NTn;
   const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
-  long long* hist = reinterpret_cast<long long*>(smem);  // [2 planes][NTn][ldsW], shared by all P phases
-  const int per = NTn * ldsW;
+  long long* hist = reinterpret_cast<long long*>(smem);  // [2 planes][NTn][R][ldsW], shared by all P phases
+  const int NW = R * ldsW;                                // words per node
+  const int per = NTn * NW;
   for (int i = threadIdx.x; i < 2 * per; i += blockDim.x) hist[i] = 0;
   long long* sq = hist + 2 * per;  // staged rows: (qg, qh) pairs, the tile-relative node ids, the bin rows
   int16_t* sn = reinterpret_cast<int16_t*>(sq + 2 * piece);
@@ -239,7 +247,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
   const bool tot = fl == nth - 1;
   const int f = f0 + ((p < P && !tot) ? fl : 0);
-  long long* my = tot ? hist + ldsW - 2 : hist + (foff[f] - c0) + (f - f0);  // total lane: "bin 1" = last cell
+  long long* my = hist + (p % R) * ldsW + (tot ? ldsW - 2 : (foff[f] - c0) + (f - f0));  // total: "bin 1" = last
   const int rb = c * chunk, re = min(n, rb + chunk);
   for (int r0 = rb; r0 < re; r0 += piece) {
     const int r1 = min(re, r0 + piece);
@@ -273,7 +281,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
     __syncthreads();
     if (p < P) {
       const int len = r1 - r0;
-      const uint8_t* col = reinterpret_cast<const uint8_t*>(sbw) + boff + f;  // row r at col[r * F]
+      const uint8_t* col = reinterpret_cast<const uint8_t*>(sbw) + boff + (fmap ? fmap[f] : f);  // row r: col[r F]
       int r = p;  // phases interleave rows, so the P waves of a row read neighbouring bin bytes
       for (; r + 7 * P < len; r += 8 * P) {
         int b[8], nd[8];
@@ -285,7 +293,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           if ((unsigned)nd[u] >= (unsigned)NTn || b[u] == 0) continue;
-          long long* e = my + nd[u] * ldsW + b[u];
+          long long* e = my + nd[u] * NW + b[u];
           const long long qg = sq[2 * (r + u * P)], qh = sq[2 * (r + u * P) + 1];
           __hip_atomic_fetch_add(e, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_fetch_add(e + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -295,7 +303,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
         const int nd = sn[r];
         const int bb = tot ? 1 : col[r * F];
         if ((unsigned)nd >= (unsigned)NTn || bb == 0) continue;
-        long long* e = my + nd * ldsW + bb;
+        long long* e = my + nd * NW + bb;
         __hip_atomic_fetch_add(e, sq[2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(e + per, sq[2 * r + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -308,19 +316,119 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
     const int nd = i / Ct, cc = i - nd * Ct;
     int fi = f0;  // the feature of compact cell c0 + cc (its pad cells precede it)
     while (foff[fi + 1] <= c0 + cc) ++fi;
-    const long long* e = hist + nd * ldsW + cc + (fi - f0);
-    long long vg = e[0], vh = e[per];
+    auto cell = [&](int k, int plane) {  // cell k of this node summed over the replicas
+      long long v = 0;
+      for (int q = 0; q < R; ++q) v += hist[plane * per + nd * NW + q * ldsW + k];
+      return v;
+    };
+    const int k0 = cc + (fi - f0);
+    long long vg = cell(k0, 0), vh = cell(k0, 1);
     if (c0 + cc == foff[fi]) {  // bin 0: the node's total minus the feature's other bins
-      vg = hist[nd * ldsW + ldsW - 1];
-      vh = hist[per + nd * ldsW + ldsW - 1];
+      vg = cell(ldsW - 1, 0);
+      vh = cell(ldsW - 1, 1);
       for (int k = 1; k < foff[fi + 1] - foff[fi]; ++k) {
-        vg -= e[k];
-        vh -= e[per + k];
+        vg -= cell(k0 + k, 0);
+        vh -= cell(k0 + k, 1);
       }
     }
-    long long* o = out + ((int64_t)(n0 + nd) * C + c0 + cc) * 2;
+    const int fo = fmap ? fmap[fi] : fi;
+    long long* o = out + ((int64_t)(n0 + nd) * C + gfoff[fo] + (c0 + cc - foff[fi])) * 2;
     o[0] = vg;
     o[1] = vh;
+  }
+}
+
+// One-hot (2-bin) features of the fixed-point form, one ROW per lane: a row's set bits (bmask, packed
+// once per fit by gbdt_pack_bits) are walked with find-first-set, so every atomic instruction carries
+// one live (row, feature) pair per lane instead of the ~7 of 64 of the lane-per-feature form.  LDS per
+// tile node: [bin-1 cell of each one-hot feature j | the node total], two planes (g, h).  Bin 0 goes
+// out as total - bin 1 (exact in integers).  Same chunks and partial layout as gbdt_hist_q.
+__global__ void gbdt_pack_bits(const uint8_t* __restrict__ bins, int n, int F, const int* __restrict__ bfeat, int nb,
+                               int WB, uint64_t* __restrict__ bmask) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)n * WB;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / WB;
+    const int w = (int)(i - r * WB);
+    uint64_t m = 0;
+    for (int j = 0; j < 64 && w * 64 + j < nb; ++j) m |= (uint64_t)(bins[r * F + bfeat[w * 64 + j]] != 0) << j;
+    bmask[i] = m;
+  }
+}
+
+constexpr int QB_ROWS = 4;  // rows per thread in flight
+constexpr int QB_REP = 4;   // replicas of a node's cells (lane & 3): neighbouring rows rarely share a word
+__global__ void __launch_bounds__(256)
+gbdt_hist_qb(const uint64_t* __restrict__ bmask, int WB, const int* __restrict__ bcell, int nb,
+             const float* __restrict__ g, const float* __restrict__ h, const int16_t* __restrict__ node,
+             long long* __restrict__ partial, int T, int n, int C, int level, int chunk, int NTn, double qscale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nodesL = 1 << level, first = nodesL - 1;
+  const int c = blockIdx.x, t = blockIdx.y, n0 = blockIdx.z * NTn;
+  // per node: QB_REP replicas of [bin-1 cell of each one-hot feature j | total], each padded to an
+  // odd word count so the replicas start on different banks
+  const int W = (nb + 1) | 1;
+  const int per = NTn * QB_REP * W;
+  long long* hist = reinterpret_cast<long long*>(smem);
+  for (int i = threadIdx.x; i < 2 * per; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)t * n;
+  const int rep = threadIdx.x & (QB_REP - 1);
+  // lane-dependent start bit: at the k-th set bit, lanes of one wave sit on different features (the
+  // k-th smallest drawn number is otherwise the same few cells for every row of the wave)
+  const int rot = (int)((threadIdx.x * 37u) & 63u);
+  const int rb = c * chunk, re = min(n, rb + chunk);
+  for (int r0 = rb + (int)threadIdx.x; r0 < re; r0 += QB_ROWS * blockDim.x) {
+    int nd[QB_ROWS];
+    float gv[QB_ROWS], hv[QB_ROWS];
+    uint64_t m0[QB_ROWS];
+#pragma unroll
+    for (int u = 0; u < QB_ROWS; ++u) {  // every load of the thread's rows in flight
+      const int r = r0 + u * blockDim.x;
+      const bool ok = r < re;
+      nd[u] = ok ? node[base + r] - first - n0 : -1;
+      gv[u] = ok ? g[base + r] : 0.f;
+      hv[u] = ok ? h[base + r] : 0.f;
+      m0[u] = ok ? bmask[(int64_t)r * WB] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < QB_ROWS; ++u) {
+      if ((unsigned)nd[u] >= (unsigned)NTn) continue;
+      const long long qg = quantise(gv[u], qscale), qh = quantise(hv[u], qscale);
+      long long* pl = hist + (nd[u] * QB_REP + rep) * W;
+      __hip_atomic_fetch_add(pl + nb, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(pl + nb + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int r = r0 + u * blockDim.x;
+      for (int w = 0; w < WB; ++w) {
+        const uint64_t mw = w == 0 ? m0[u] : bmask[(int64_t)r * WB + w];
+        uint64_t m = rot ? (mw >> rot) | (mw << (64 - rot)) : mw;  // rotate right by rot
+        while (m) {
+          const int j = w * 64 + ((__builtin_ctzll(m) + rot) & 63);
+          m &= m - 1;
+          __hip_atomic_fetch_add(pl + j, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(pl + j + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  long long* out = partial + ((int64_t)c * T + t) * (int64_t)nodesL * C * 2;
+  const int nn = min(NTn, nodesL - n0);
+  for (int i = threadIdx.x; i < nn * nb; i += blockDim.x) {
+    const int nd = i / nb, j = i - nd * nb;
+    long long g1 = 0, h1 = 0, gt = 0, ht = 0;
+#pragma unroll
+    for (int q = 0; q < QB_REP; ++q) {
+      const long long* pl = hist + (nd * QB_REP + q) * W;
+      g1 += pl[j];
+      h1 += pl[per + j];
+      gt += pl[nb];
+      ht += pl[per + nb];
+    }
+    long long* o = out + ((int64_t)(n0 + nd) * C + bcell[j]) * 2;  // bcell = the feature's bin-0 cell
+    o[0] = gt - g1;
+    o[1] = ht - h1;
+    o[2] = g1;
+    o[3] = h1;
   }
 }
 
@@ -640,7 +748,7 @@ inline int grid_for(int64_t total, int bs = 256) {
 // ------------------------------------------------------------------ host-side histogram plan
 namespace {
 struct HistPlan {
-  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece;
+  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece, R = 1;
   size_t lds;
 };
 
@@ -648,8 +756,11 @@ struct HistPlan {
 // the LDS budget (P private copies in the exact form, one shared copy in the fixed-point form); P
 // (row phases, 1..4) fills a 256-thread block when F is small.  Chunks are sized so a level launches
 // ~4096 blocks (all 256 CUs busy even for the reference's ~930 rows).
-bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, HistPlan& pl) {
+bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, HistPlan& pl, int row_bytes = 0) {
+  // F features with cells foff[0..F]; row_bytes = bytes per bin row (0: F; a feature sub-problem's rows
+  // are the full rows)
   const int nodesL = 1 << level;
+  const int RB = row_bytes > 0 ? row_bytes : F;
   for (int NTn = nodesL; NTn >= 1; NTn >>= 1) {
     for (int FT = F < (quant ? 255 : 256) ? F : (quant ? 255 : 256);; FT = (FT + 1) / 2) {
       int maxC = 0;
@@ -659,15 +770,19 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
       }
       const int lanes = FT + (quant ? 1 : 0);  // fixed point: + the total lane per phase
       const int W = maxC + (quant ? FT + 1 : 0);  // fixed point: + a pad cell per feature + the total cell
-      int P = 256 / lanes;
-      P = P > 4 ? 4 : (P < 1 ? 1 : P);
+      int P = 256 / lanes;  // row phases: the exact form keeps P private copies (<= 4), the fixed-point
+      const int Pmax = quant ? 64 : 4;  // form one shared copy, so a few-feature tile fills the block with phases
+      P = P > Pmax ? Pmax : (P < 1 ? 1 : P);
+      // fixed point with >= 8 phases: 4 replicas (consecutive-row phases of one wave would hit the same words)
+      const int R = (quant && P >= 8) ? 4 : 1;
       for (; P >= 1; --P)
-        if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= HIST_LDS_BUDGET) break;
+        if ((int64_t)(quant ? R : P) * NTn * W * 16 <= HIST_LDS_BUDGET) break;
       if (P >= 1) {
         pl.FT = FT;
         pl.NTn = NTn;
         pl.P = P;
         pl.ldsC = W;
+        pl.R = R;
         pl.nft = (F + FT - 1) / FT;
         pl.ntn = nodesL / NTn;
         pl.threads = ((lanes * P + 63) / 64) * 64;
@@ -684,11 +799,11 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
         pl.nchunks = (int)((n + chunk - 1) / chunk);
         // staged rows: (g, h) floats + node id (exact); (qg, qh) int64 + node id + the piece's bin
         // rows (fixed point: ~16 KB of bins per piece, fetched with 16-B loads)
-        pl.piece = quant ? ((HIST_QBIN_LDS / F) & ~15) : HIST_MAX_CHUNK;
+        pl.piece = quant ? ((HIST_QBIN_LDS / RB) & ~15) : HIST_MAX_CHUNK;
         if (pl.piece > HIST_MAX_CHUNK) pl.piece = HIST_MAX_CHUNK;
         if (pl.piece < 16) pl.piece = 16;
-        pl.lds = (size_t)(quant ? 1 : P) * NTn * pl.ldsC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4 +
-                 (quant ? ((size_t)pl.piece * F + 32 + 15) / 16 * 16 : 0);
+        pl.lds = (size_t)(quant ? R : P) * NTn * pl.ldsC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4 +
+                 (quant ? ((size_t)pl.piece * RB + 32 + 15) / 16 * 16 : 0);
         return true;
       }
       if (FT == 1) break;
@@ -711,32 +826,76 @@ int64_t partial_need(int level, int n, int T, int F, const int* foff) {
 // fold = false leaves the per-chunk partials for gbdt_split to fold (small chunk counts); *nchunks_out
 // = the number of partial copies left in `partial` (1 after a fold)
 constexpr int SPLIT_FOLD_MAX_CHUNKS = 32, SPLIT_FOLD_MAX_LDS = 32 * 1024;
+// Fixed-point sparse form (em_gbdt_fit, quant_bits > 0, >= 8 one-hot features): one-hot features on
+// gbdt_hist_qb (row per lane over the packed bit masks), the others on gbdt_hist_q over their feature
+// sub-problem; both write their own cells of the same per-chunk partials.
+struct QuantAux {
+  int nb = 0, WB = 0;                 // one-hot features, 64-bit words per row mask
+  const int* bcell_d = nullptr;       // [nb] bin-0 cell of each one-hot feature (bin 1 follows)
+  const uint64_t* bmask_d = nullptr;  // [n][WB]
+  int Fm = 0;                         // the other features
+  std::vector<int> foffm_h;           // [Fm + 1] their compact cells
+  const int* foffm_d = nullptr;
+  const int* fmap_d = nullptr;        // [Fm] sub-feature -> bin-row column
+};
+
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
-                      bool fold, double qscale, int* nchunks_out, hipStream_t stream) {
+                      bool fold, double qscale, int* nchunks_out, hipStream_t stream, const QuantAux* qa = nullptr) {
   const bool quant = qscale != 0.0;
-  HistPlan pl;
-  if (!plan_hist(level, n, T, F, foff_h, quant, pl)) return EM_ERR_ARG;
   const int C = foff_h[F];
-  const int64_t S = (int64_t)T * (1 << level) * C * 2;
-  if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
-  const dim3 grid(pl.nchunks, T, pl.nft * pl.ntn);
-  if (quant)
-    hipLaunchKernelGGL(gbdt_hist_q, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d,
-                       reinterpret_cast<long long*>(partial), T, n, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
-                       pl.ldsC, pl.piece, qscale);
-  else
-    hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
-                       C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
-  const bool split_folds = !fold && pl.nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
-  if (pl.nchunks > 1 && !split_folds) {
+  const int nodesL = 1 << level;
+  const int64_t S = (int64_t)T * nodesL * C * 2;
+  long long* qpart = reinterpret_cast<long long*>(partial);
+  int nchunks = 0;
+  if (quant && qa && qa->nb > 0) {
+    HistPlan pm;
+    const bool multi = qa->Fm > 0;
+    if (multi && !plan_hist(level, n, T, qa->Fm, qa->foffm_h.data(), true, pm, F)) return EM_ERR_ARG;
+    int NTb = nodesL;
+    const int Wb = (qa->nb + 1) | 1;
+    while (NTb > 1 && (int64_t)2 * NTb * QB_REP * Wb * 8 > HIST_LDS_BUDGET) NTb >>= 1;
+    int64_t chunk;
+    if (multi) {
+      chunk = pm.chunk;
+    } else {
+      const int64_t per_chunk = (int64_t)T * (nodesL / NTb);
+      chunk = (n + (4096 + per_chunk - 1) / per_chunk - 1) / ((4096 + per_chunk - 1) / per_chunk);
+    }
+    const int64_t maxch = partial_doubles / S;  // chunks that fit the partial buffer
+    if (maxch < 1) return EM_ERR_ARG;
+    if ((n + chunk - 1) / chunk > maxch) chunk = (n + maxch - 1) / maxch;
+    if (chunk < 64) chunk = 64;
+    nchunks = (int)((n + chunk - 1) / chunk);
+    hipLaunchKernelGGL(gbdt_hist_qb, dim3(nchunks, T, nodesL / NTb), dim3(256), (size_t)2 * NTb * QB_REP * Wb * 8,
+                       stream, qa->bmask_d, qa->WB, qa->bcell_d, qa->nb, g, h, node, qpart, T, n, C, level,
+                       (int)chunk, NTb, qscale);
+    if (multi)
+      hipLaunchKernelGGL(gbdt_hist_q, dim3(nchunks, T, pm.nft * pm.ntn), dim3(pm.threads), pm.lds, stream, bins, g, h,
+                         node, qa->foffm_d, qa->fmap_d, foff_d, qpart, T, n, F, qa->Fm, C, level, (int)chunk, pm.FT,
+                         pm.NTn, pm.P, pm.ldsC, pm.piece, qscale, pm.R);
+  } else {
+    HistPlan pl;
+    if (!plan_hist(level, n, T, F, foff_h, quant, pl)) return EM_ERR_ARG;
+    if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
+    nchunks = pl.nchunks;
+    const dim3 grid(pl.nchunks, T, pl.nft * pl.ntn);
     if (quant)
-      hipLaunchKernelGGL(gbdt_chunk_reduce<long long>, dim3(grid_for(S)), dim3(256), 0, stream,
-                         reinterpret_cast<long long*>(partial), pl.nchunks, S);
+      hipLaunchKernelGGL(gbdt_hist_q, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d,
+                         (const int*)nullptr, foff_d, qpart, T, n, F, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
+                         pl.ldsC, pl.piece, qscale, pl.R);
     else
-      hipLaunchKernelGGL(gbdt_chunk_reduce<double>, dim3(grid_for(S)), dim3(256), 0, stream, partial, pl.nchunks, S);
+      hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d, partial, T, n,
+                         F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
   }
-  *nchunks_out = split_folds ? pl.nchunks : 1;
+  const bool split_folds = !fold && nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
+  if (nchunks > 1 && !split_folds) {
+    if (quant)
+      hipLaunchKernelGGL(gbdt_chunk_reduce<long long>, dim3(grid_for(S)), dim3(256), 0, stream, qpart, nchunks, S);
+    else
+      hipLaunchKernelGGL(gbdt_chunk_reduce<double>, dim3(grid_for(S)), dim3(256), 0, stream, partial, nchunks, S);
+  }
+  *nchunks_out = split_folds ? nchunks : 1;
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -790,6 +949,55 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   const int NN = (1 << (max_depth + 1)) - 1;
   const int C = foff_h[F];
   const int64_t TN = (int64_t)T * n;
+  // fixed point with >= 8 one-hot features: the sparse form (QuantAux); EM_GBDT_SPARSE=0 disables it
+  QuantAux qa;
+  void* qmem = nullptr;
+  static const bool sparse_on = !(getenv("EM_GBDT_SPARSE") && getenv("EM_GBDT_SPARSE")[0] == '0');
+  if (quant_bits && sparse_on) {
+    std::vector<int> bcell, bfeat, fmap;
+    qa.foffm_h.push_back(0);
+    for (int f = 0; f < F; ++f) {
+      const int nbins = foff_h[f + 1] - foff_h[f];
+      if (nbins == 2) {
+        bcell.push_back(foff_h[f]);
+        bfeat.push_back(f);
+      } else {
+        fmap.push_back(f);
+        qa.foffm_h.push_back(qa.foffm_h.back() + nbins);
+      }
+    }
+    if (bcell.size() >= 8) {
+      qa.nb = (int)bcell.size();
+      qa.WB = (qa.nb + 63) / 64;
+      qa.Fm = (int)fmap.size();
+      const size_t ints = 2 * (size_t)qa.nb + (size_t)qa.Fm + (size_t)qa.Fm + 1;
+      const size_t mask_off = (ints * 4 + 15) / 16 * 16;
+      if (hipError_t e = hipMalloc(&qmem, mask_off + (size_t)n * qa.WB * 8)) return (int)e;
+      std::vector<int> hostv;
+      hostv.insert(hostv.end(), bcell.begin(), bcell.end());
+      hostv.insert(hostv.end(), bfeat.begin(), bfeat.end());
+      hostv.insert(hostv.end(), fmap.begin(), fmap.end());
+      hostv.insert(hostv.end(), qa.foffm_h.begin(), qa.foffm_h.end());
+      int* dv = static_cast<int*>(qmem);
+      (void)hipMemcpyAsync(dv, hostv.data(), hostv.size() * 4, hipMemcpyHostToDevice, stream);
+      qa.bcell_d = dv;
+      qa.fmap_d = dv + 2 * qa.nb;
+      qa.foffm_d = dv + 2 * qa.nb + qa.Fm;
+      qa.bmask_d = reinterpret_cast<const uint64_t*>(static_cast<char*>(qmem) + mask_off);
+      hipLaunchKernelGGL(gbdt_pack_bits, dim3(grid_for((int64_t)n * qa.WB)), dim3(256), 0, stream, bins, n, F,
+                         dv + qa.nb, qa.nb, qa.WB, const_cast<uint64_t*>(qa.bmask_d));
+    }
+  }
+  struct Free {  // the scratch outlives every launch of this call: freed after the stream drains
+    void* p;
+    hipStream_t s;
+    ~Free() {
+      if (p) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(p);
+      }
+    }
+  } qfree{qmem, stream};
   for (int round = r0; round < r1; ++round) {
     int8_t* st = status + (int64_t)round * T * NN;
     int16_t* fe = feat + (int64_t)round * T * NN;
@@ -805,7 +1013,7 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       const int nodesL = 1 << level;
       int nch = 1;
       const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles,
-                                       false, qscale, &nch, stream);
+                                       false, qscale, &nch, stream, qa.nb ? &qa : nullptr);
       if (rc) return rc;
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
       const int64_t cstride = (int64_t)T * nodesL * C * 2;

@@ -110,7 +110,9 @@ __global__ void __launch_bounds__(FNT, 2)
 gemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                 float* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ bias, int act,
                 const float* __restrict__ Y, int64_t ldy, int dact, float alpha, float beta, int kstep,
-                int64_t c_split) {
+                int64_t c_split, float* __restrict__ colpart) {
+  // colpart (optional, no split-K): column sums of this tile's 128 output rows (the stored values)
+  // -> colpart[m0 / 128][n], fixed order: a lane's 32 rows, the two lane halves, then wm 0 + wm 1
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -166,6 +168,7 @@ gemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restric
   }
 
   // epilogue: accumulator register g of block (i, j) = row 8*(g>>2) + 4h + (g&3), column r
+  float cs[2] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -184,17 +187,29 @@ gemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restric
           v = f_act(v + bv, act);
         }
         float* cp = C + (int64_t)row * ldc + col;
-        *cp = beta != 0.f ? v + beta * *cp : v;
+        v = beta != 0.f ? v + beta * *cp : v;
+        *cp = v;
+        cs[j] += v;
       }
     }
+  if (colpart) {  // block-uniform
+    float* red = reinterpret_cast<float*>(smem);  // [2 wm][128 cols]; the K loop ended on a barrier
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float v = cs[j] + __shfl_xor(cs[j], 32);
+      if (h == 0) red[wm * 128 + wn * 64 + 32 * j + r] = v;
+    }
+    __syncthreads();
+    if (tid < 128 && n0 + tid < N) colpart[(int64_t)(m0 / FBM) * N + n0 + tid] = red[tid] + red[128 + tid];
+  }
 }
 
 template <int A_KC, int B_KC>
 void f_launch(dim3 grid, hipStream_t st, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
               int64_t ldc, int M, int N, int K, const float* bias, int act, const float* Y, int64_t ldy, int dact,
-              float alpha, float beta, int kstep, int64_t c_split) {
+              float alpha, float beta, int kstep, int64_t c_split, float* colpart) {
   hipLaunchKernelGGL((gemm_f32_kernel<A_KC, B_KC>), grid, dim3(FNT), F_LDS, st, A, lda, B, ldb, C, ldc, M, N, K, bias,
-                     act, Y, ldy, dact, alpha, beta, kstep, c_split);
+                     act, Y, ldy, dact, alpha, beta, kstep, c_split, colpart);
 }
 
 }  // namespace
@@ -204,8 +219,11 @@ void f_launch(dim3 grid, hipStream_t st, const float* A, int64_t lda, const floa
 EM_API int em_gemm_f32(const float* A, int64_t lda, int a_kc, const float* B, int64_t ldb, int b_kc, float* C,
                        int64_t ldc, int M, int N, int K, const float* bias, int act, const float* Y, int64_t ldy,
                        int dact, float alpha, float beta, int splits, int kstep, int64_t c_split,
-                       hipStream_t stream) {
-  if (!A || !B || !C || M < 0 || N < 0 || K < 0 || act < 0 || act > 3 || (dact && !Y) || splits < 1) return EM_ERR_ARG;
+                       float* colpart, hipStream_t stream) {
+  // colpart: [ceil(M / 128)][N] fp32 column sums of C per 128-row tile (bias gradient partials)
+  if (!A || !B || !C || M < 0 || N < 0 || K < 0 || act < 0 || act > 3 || (dact && !Y) || splits < 1 ||
+      (colpart && splits > 1))
+    return EM_ERR_ARG;
   if (M == 0 || N == 0) return 0;
   if (splits > 1 && (kstep <= 0 || (int64_t)kstep * splits < K || c_split < (int64_t)M * ldc || bias || act))
     return EM_ERR_ARG;
@@ -216,13 +234,17 @@ EM_API int em_gemm_f32(const float* A, int64_t lda, int a_kc, const float* B, in
   const int tiles = ((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (a_kc && b_kc)
-    f_launch<1, 1>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split);
+    f_launch<1, 1>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split,
+                   colpart);
   else if (a_kc)
-    f_launch<1, 0>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split);
+    f_launch<1, 0>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split,
+                   colpart);
   else if (b_kc)
-    f_launch<0, 1>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split);
+    f_launch<0, 1>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split,
+                   colpart);
   else
-    f_launch<0, 0>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split);
+    f_launch<0, 0>(grid, stream, A, lda, B, ldb, C, ldc, M, N, K, bias, act, Y, ldy, dact, alpha, beta, kstep, c_split,
+                   colpart);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -200,9 +200,13 @@ template <typename T>  // dz element type: __bf16 (bf16 GEMM path) or float (fp3
 __global__ void __launch_bounds__(256)
 loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __restrict__ masks,
                  const int32_t* __restrict__ sidx, int64_t B, int64_t offset, int loss_kind, float grad_scale,
-                 T* __restrict__ dz, int ldz, float* __restrict__ partials) {
+                 T* __restrict__ dz, int ldz, float* __restrict__ partials, float* __restrict__ colpart) {
+  // colpart (optional): this block's column sums of the written dz (as T-rounded values) ->
+  // colpart[blockIdx.x][64], fixed order (lane's samples in loop order, then the 4 sample slots of a
+  // wave, then the block's 4 waves): the last layer's bias gradient without another pass over dz
   const int lane = threadIdx.x & 63, q = lane & 15, sub = lane >> 4;
   const int64_t ngroups = (B + 3) / 4;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
   for (int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; gw < ngroups;
        gw += ((int64_t)gridDim.x * blockDim.x) >> 6) {
     const int64_t s = gw * 4 + sub;
@@ -275,7 +279,10 @@ loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __res
     if (ok) {
       T d4[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) d4[k] = (T)(g[k] * grad_scale);
+      for (int k = 0; k < 4; ++k) {
+        d4[k] = (T)(g[k] * grad_scale);
+        cs[k] += (float)d4[k];
+      }
       T* d = dz + s * ldz + 4 * q;
       if ((ldz & 3) == 0) {  // one 16-B (fp32) / 8-B (bf16) store per lane
         if constexpr (sizeof(T) == 4) {
@@ -297,6 +304,21 @@ loss_grad_kernel(const float* __restrict__ logits, int ld, const uint64_t* __res
     const int64_t s0 = gw * 4;
     if (lane == 0)
       partials[gw] = ((l0 + (s0 + 1 < B ? l1 : 0.f)) + (s0 + 2 < B ? l2 : 0.f)) + (s0 + 3 < B ? l3 : 0.f);
+  }
+  if (colpart) {
+    __shared__ float red[4][64];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v = cs[k];
+      v += __shfl_xor(v, 16);  // the wave's 4 sample slots (sub) of output 4q + k
+      v += __shfl_xor(v, 32);
+      if (sub == 0) red[w][4 * q + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64)
+      colpart[(int64_t)blockIdx.x * 64 + threadIdx.x] =
+          ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
   }
 }
 
@@ -345,32 +367,35 @@ EM_API int em_onehot_encode_f32(const uint64_t* draws, const int32_t* sidx, int6
 
 namespace {
 // 16 samples per 256-thread block; at most 4096 blocks (16 per CU), grid-stride beyond
+// (em_loss_grad_blocks: the colpart row count)
 unsigned loss_grad_blocks(int64_t B) {
   const int64_t nb = (B + 15) / 16;
   return (unsigned)(nb < 4096 ? nb : 4096);
 }
 }  // namespace
 
+EM_API int em_loss_grad_blocks(int64_t B) { return B > 0 ? (int)loss_grad_blocks(B) : 0; }
+
 EM_API int em_loss_grad(const float* logits, int ld, const uint64_t* masks, const int32_t* sidx, int64_t B,
                         int64_t offset, int loss_kind, float grad_scale, void* dz, int ldz, float* partials,
-                        hipStream_t stream) {
+                        float* colpart, hipStream_t stream) {
   if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
     return EM_ERR_ARG;
   if (B == 0) return 0;
   hipLaunchKernelGGL(loss_grad_kernel<__bf16>, dim3(loss_grad_blocks(B)), dim3(256), 0, stream, logits, ld, masks,
-                     sidx, B, offset, loss_kind, grad_scale, (__bf16*)dz, ldz, partials);
+                     sidx, B, offset, loss_kind, grad_scale, (__bf16*)dz, ldz, partials, colpart);
   EM_CHECK_LAUNCH();
   return 0;
 }
 
 EM_API int em_loss_grad_f32(const float* logits, int ld, const uint64_t* masks, const int32_t* sidx, int64_t B,
                             int64_t offset, int loss_kind, float grad_scale, float* dz, int ldz, float* partials,
-                            hipStream_t stream) {
+                            float* colpart, hipStream_t stream) {
   if (!logits || !masks || !dz || !partials || ld < 62 || ldz < 64 || B < 0 || loss_kind < 0 || loss_kind > 1)
     return EM_ERR_ARG;
   if (B == 0) return 0;
   hipLaunchKernelGGL(loss_grad_kernel<float>, dim3(loss_grad_blocks(B)), dim3(256), 0, stream, logits, ld, masks,
-                     sidx, B, offset, loss_kind, grad_scale, dz, ldz, partials);
+                     sidx, B, offset, loss_kind, grad_scale, dz, ldz, partials, colpart);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -162,6 +162,9 @@ class GemmMLPTrainer:
                   "dz": [torch.empty(B, n, dtype=f, device=dev) for n in P[1:]],
                   "logits": torch.empty(B, 64, dtype=f, device=dev),
                   "part": torch.empty(max((B + 3) // 4, 1), dtype=f, device=dev),
+                  # bias-gradient partials: of dz_last from the loss kernel, of dz_{i-1} from the dgrad epilogue
+                  "losscol": torch.empty(max(1, LIN.loss_grad_blocks(B)) * 64, dtype=f, device=dev),
+                  "colpart": torch.empty(max(1, -(-B // 128)) * max(P), dtype=f, device=dev),
                   "parts": {}}
             self._ws_cache = {B: ws}
         if ws is None:
@@ -174,6 +177,7 @@ class GemmMLPTrainer:
                   "dz": [torch.empty(B, n, dtype=torch.bfloat16, device=dev) for n in P[1:]],
                   "logits": torch.empty(B, 64, dtype=torch.float32, device=dev),
                   "part": torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=dev),
+                  "losscol": torch.empty(max(1, LIN.loss_grad_blocks(B)) * 64, dtype=torch.float32, device=dev),
                   "colsum_ws": torch.empty(max(1, (B + 511) // 512) * max(P), dtype=torch.float32, device=dev),
                   # bias-gradient partials [B / 128][N] written by the 256-tile dgrad epilogue (fused K3 bias grad)
                   "colpart": torch.empty(max(1, B // 128) * max(P), dtype=torch.float32, device=dev),
@@ -236,28 +240,37 @@ class GemmMLPTrainer:
         ncu = self.panel_ncu or N.cu_count(self.device)
         return plan_panels(self.padded[i + 1], self.padded[i], self.bucket_elems, ncu, LIN.BIG_M, LIN.BIG_N)
 
+    def _loss_bias(self, ws, B: int, accumulate: bool) -> None:
+        """Last layer's bias gradient from the loss kernel's per-block column partials."""
+        _, gbias = self._views(self.grads, len(self.offsets) - 1)
+        LIN.colpart_reduce(ws["losscol"], LIN.loss_grad_blocks(B), 64, gbias, accumulate=accumulate)
+
     def _backward(self, dz, inputs, ws, on_ready=None, accumulate: bool = False):
         """Last layer first: wgrad + bias grad into the flat gradient buffer (added to it when
         ``accumulate``: gradient accumulation over micro-batches), then dgrad (act' fused).
         ``on_ready(a, c)`` is called as soon as flat gradient range [a, c) is final: per row panel
-        of a 256-tile wgrad, per whole weight otherwise, then per bias."""
+        of a 256-tile wgrad, per whole weight otherwise, then per bias.  The last layer's bias
+        gradient is already in place (``_loss_bias``); every other bias gradient comes from the
+        partial column sums of the dgrad that produced its dZ."""
         L = len(self.offsets)
         if self.f32 and accumulate:
             raise ValueError("gradient accumulation runs on the bf16 path")
+        B = dz.shape[0]
         if self.f32:
             for i in reversed(range(L)):
                 gw, gbias = self._views(self.grads, i)
                 LF.linear_wgrad(dz, inputs[i], out=gw, parts_cache=ws["parts"])
-                torch.sum(dz, dim=0, out=gbias)
                 if on_ready is not None:
                     on_ready(self.offsets[i][0], self.offsets[i][2])
                 if i > 0:
                     w, _ = self._views(self.params, i)
-                    dz = LF.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
+                    dz = LF.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1],
+                                         colpart=ws["colpart"])
+                    _, gb_prev = self._views(self.grads, i - 1)
+                    LIN.colpart_reduce(ws["colpart"], -(-B // 128), self.padded[i], gb_prev)
             return dz
         plan = ws["plan"]
-        B = dz.shape[0]
-        fused_bias = set()  # layers whose bias gradient the previous dgrad's epilogue already summed
+        fused_bias = {L - 1}  # layers whose bias gradient is already summed (loss kernel / a dgrad epilogue)
         for i in reversed(range(L)):
             gw, gbias = self._views(self.grads, i)
             beta = 1.0 if accumulate else 0.0
@@ -315,7 +328,8 @@ class GemmMLPTrainer:
             off = offset + k * B
             logits, inputs = self._forward(masks, B, off, None, ws, train=True)
             dz, part = LIN.loss_grad(logits, self._tmasks(masks), B, self.loss_name, offset=off, grad_scale=1.0 / gb,
-                                     dz=ws["dz"][-1], partials=ws["part"])
+                                     dz=ws["dz"][-1], partials=ws["part"], colpart=ws["losscol"])
+            self._loss_bias(ws, B, accumulate=k > 0)
             if k == 0:
                 torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
             else:
@@ -324,8 +338,9 @@ class GemmMLPTrainer:
         last = offset + (accum - 1) * B
         logits, inputs = self._forward(masks, B, last, sidx, ws, train=True)
         dz, part = (LF if self.f32 else LIN).loss_grad(logits, self._tmasks(masks), B, self.loss_name, offset=last,
-                                                       sidx=sidx,
-                                                       grad_scale=1.0 / gb, dz=ws["dz"][-1], partials=ws["part"])
+                                                       sidx=sidx, grad_scale=1.0 / gb, dz=ws["dz"][-1],
+                                                       partials=ws["part"], colpart=ws["losscol"])
+        self._loss_bias(ws, B, accumulate=accum > 1)
         if accum == 1:
             torch.sum(part, dim=0, keepdim=True, out=self.grads[self.P:])
         else:
@@ -356,8 +371,9 @@ class GemmMLPTrainer:
         ws = self._ws(B)
         logits, inputs = self._forward(masks, B, offset, sidx, ws, train=True)
         dz, part = (LF if self.f32 else LIN).loss_grad(logits, self._tmasks(masks), B, self.loss_name, offset=offset,
-                                                       sidx=sidx,
-                                                       grad_scale=1.0 / B, dz=ws["dz"][-1], partials=ws["part"])
+                                                       sidx=sidx, grad_scale=1.0 / B, dz=ws["dz"][-1],
+                                                       partials=ws["part"], colpart=ws["losscol"])
+        self._loss_bias(ws, B, accumulate=False)
         self._backward(dz, inputs, ws)
         out = {k: v.clone() for k, v in self._logical(self.grads, flat_layer0=True).items()}
         return float(part.double().sum().item()) / B, out

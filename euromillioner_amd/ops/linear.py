@@ -41,7 +41,8 @@ N.register_signatures({
     "em_rowsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p]),
     "em_transpose_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i64, N._c_void_p]),
     "em_loss_grad": (N._i32, [N._c_void_p, N._i32, N._c_void_p, N._c_void_p, N._i64, N._i64, N._i32, N._f32,
-                              N._c_void_p, N._i32, N._c_void_p, N._c_void_p]),
+                              N._c_void_p, N._i32, N._c_void_p, N._c_void_p, N._c_void_p]),
+    "em_loss_grad_blocks": (N._i32, [N._i64]),
 })
 
 
@@ -306,8 +307,11 @@ def rowsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = 
 
 def loss_grad(logits: torch.Tensor, masks: torch.Tensor, B: int, loss: str = "softmax", offset: int = 0,
               sidx: torch.Tensor | None = None, grad_scale: float = 1.0, dz: torch.Tensor | None = None,
-              partials: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-    """K10: (dz bf16 [B, 64] = grad_scale * dL/dlogits, per-block loss sums [ceil(B/4)])."""
+              partials: torch.Tensor | None = None,
+              colpart: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """K10: (dz bf16 [B, 64] = grad_scale * dL/dlogits, per-block loss sums [ceil(B/4)]).
+    ``colpart`` (fp32, >= loss_grad_blocks(B) * 64): per-block column sums of dz for the last layer's
+    bias gradient (``colpart_reduce(colpart, loss_grad_blocks(B), 64, ...)``)."""
     from .fused_mlp import LOSS_KINDS, _check_draws
 
     _check_draws(masks, sidx, B, offset)
@@ -318,10 +322,20 @@ def loss_grad(logits: torch.Tensor, masks: torch.Tensor, B: int, loss: str = "so
         dz = torch.empty(B, 64, dtype=torch.bfloat16, device=logits.device)
     if partials is None:
         partials = torch.empty(max((B + 3) // 4, 1), dtype=torch.float32, device=logits.device)
+    if colpart is not None:
+        N.check_cuda(colpart, "colpart", torch.float32)
+        if colpart.numel() < loss_grad_blocks(B) * 64:
+            raise ValueError("colpart too small")
     N.call("em_loss_grad", logits.data_ptr(), logits.stride(0), masks.data_ptr(),
            sidx.data_ptr() if sidx is not None else None, B, offset, LOSS_KINDS[loss], float(grad_scale),
-           dz.data_ptr(), dz.stride(0), partials.data_ptr(), N.stream_handle(logits.device))
+           dz.data_ptr(), dz.stride(0), partials.data_ptr(), colpart.data_ptr() if colpart is not None else None,
+           N.stream_handle(logits.device))
     return dz, partials
+
+
+def loss_grad_blocks(B: int) -> int:
+    """Blocks (= colpart rows) of the K10 loss kernel for a batch of B."""
+    return int(N.query("em_loss_grad_blocks", int(B)))
 
 
 class _MLPFunction(torch.autograd.Function):

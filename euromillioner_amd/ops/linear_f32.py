@@ -15,11 +15,11 @@ from .linear import ACTS
 N.register_signatures({
     "em_gemm_f32": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64,
                              N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32, N._f32, N._f32,
-                             N._i32, N._i32, N._i64, N._c_void_p]),
+                             N._i32, N._i32, N._i64, N._c_void_p, N._c_void_p]),
     "em_onehot_encode_f32": (N._i32, [N._c_void_p, N._c_void_p, N._i64, N._i64, N._i32, N._i32, N._c_void_p,
                                       N._c_void_p]),
     "em_loss_grad_f32": (N._i32, [N._c_void_p, N._i32, N._c_void_p, N._c_void_p, N._i64, N._i64, N._i32, N._f32,
-                                  N._c_void_p, N._i32, N._c_void_p, N._c_void_p]),
+                                  N._c_void_p, N._i32, N._c_void_p, N._c_void_p, N._c_void_p]),
 })
 
 TILE = 128
@@ -34,9 +34,10 @@ def _check2d(t: torch.Tensor, name: str):
 def gemm_f32(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Tensor, M: int, N_: int, K: int,
              bias: torch.Tensor | None = None, act: str = "none", dact_src: torch.Tensor | None = None,
              dact: str = "relu", alpha: float = 1.0, beta: float = 0.0, splits: int = 1,
-             parts: torch.Tensor | None = None) -> torch.Tensor:
+             parts: torch.Tensor | None = None, colpart: torch.Tensor | None = None) -> torch.Tensor:
     """Raw launch.  ``splits > 1`` (no bias/act/dact): K is cut into slices written to ``parts``
-    ([splits, M, N] fp32) and summed into ``out`` (``out = alpha * sum + beta * out``)."""
+    ([splits, M, N] fp32) and summed into ``out`` (``out = alpha * sum + beta * out``).
+    ``colpart`` (splits == 1, fp32 >= ceil(M / 128) * N): per-128-row column sums of ``out``."""
     _check2d(a, "a")
     _check2d(b, "b")
     _check2d(out, "out")
@@ -55,6 +56,10 @@ def gemm_f32(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torc
             raise ValueError("dact_src must be [M, N]")
         ldy = dact_src.stride(0)
     st = N.stream_handle(out.device)
+    if colpart is not None:
+        N.check_cuda(colpart, "colpart", torch.float32)
+        if splits > 1 or colpart.numel() < -(-M // TILE) * N_:
+            raise ValueError("colpart needs splits == 1 and ceil(M / 128) * N floats")
     if splits > 1:
         if bias is not None or act != "none" or dact_src is not None:
             raise ValueError("split-K takes no epilogue")
@@ -62,7 +67,8 @@ def gemm_f32(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torc
         if parts is None or tuple(parts.shape) != (splits, M, N_) or not parts.is_contiguous():
             parts = torch.empty(splits, M, N_, dtype=torch.float32, device=out.device)
         N.call("em_gemm_f32", a.data_ptr(), a.stride(0), int(a_kc), b.data_ptr(), b.stride(0), int(b_kc),
-               parts.data_ptr(), N_, M, N_, K, None, 0, None, 0, 0, float(alpha), 0.0, splits, kstep, M * N_, st)
+               parts.data_ptr(), N_, M, N_, K, None, 0, None, 0, 0, float(alpha), 0.0, splits, kstep, M * N_, None,
+               st)
         if beta == 0.0:
             torch.sum(parts, dim=0, out=out) if out.is_contiguous() else out.copy_(parts.sum(0))
         else:
@@ -72,7 +78,7 @@ def gemm_f32(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torc
            out.data_ptr(), out.stride(0), M, N_, K, bias.data_ptr() if bias is not None else None,
            ACTS[dact] if dact_src is not None else ACTS[act],  # with dact_src the kernel's act names act'
            dact_src.data_ptr() if dact_src is not None else None, ldy, int(dact_src is not None),
-           float(alpha), float(beta), 1, 0, 0, st)
+           float(alpha), float(beta), 1, 0, 0, colpart.data_ptr() if colpart is not None else None, st)
     return out
 
 
@@ -82,10 +88,12 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, act:
     return gemm_f32(x, True, w, True, out, M, w.shape[0], K, bias=bias, act=act)
 
 
-def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor, act: str, out: torch.Tensor) -> torch.Tensor:
-    """``out = (dz @ w) * act'(y_prev)``; dz [M, N], w [N, K] (k-major as the B operand)."""
+def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor, act: str, out: torch.Tensor,
+                 colpart: torch.Tensor | None = None) -> torch.Tensor:
+    """``out = (dz @ w) * act'(y_prev)``; dz [M, N], w [N, K] (k-major as the B operand).  ``colpart``:
+    per-128-row column sums of ``out`` (the previous layer's bias gradient, ``colpart_reduce``)."""
     M, Nn = dz.shape
-    return gemm_f32(dz, True, w, False, out, M, w.shape[1], Nn, dact_src=y_prev, dact=act)
+    return gemm_f32(dz, True, w, False, out, M, w.shape[1], Nn, dact_src=y_prev, dact=act, colpart=colpart)
 
 
 def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor, parts_cache: dict | None = None) -> torch.Tensor:
@@ -120,8 +128,9 @@ def onehot(draws: torch.Tensor, B: int, offset: int = 0, which: int = 0, sidx: t
 
 def loss_grad(logits: torch.Tensor, masks: torch.Tensor, B: int, loss: str, offset: int = 0,
               sidx: torch.Tensor | None = None, grad_scale: float = 1.0, dz: torch.Tensor | None = None,
-              partials: torch.Tensor | None = None):
-    """K10 with an fp32 dL/dlogits [B, 64] (pre-scaled); returns (dz, per-block loss sums)."""
+              partials: torch.Tensor | None = None, colpart: torch.Tensor | None = None):
+    """K10 with an fp32 dL/dlogits [B, 64] (pre-scaled); returns (dz, per-block loss sums).
+    ``colpart``: per-block column sums of dz (see ``linear.loss_grad``)."""
     from . import fused_mlp as FM
 
     _check2d(logits, "logits")
@@ -131,5 +140,6 @@ def loss_grad(logits: torch.Tensor, masks: torch.Tensor, B: int, loss: str, offs
         partials = torch.empty((B + 3) // 4, dtype=torch.float32, device=logits.device)
     N.call("em_loss_grad_f32", logits.data_ptr(), logits.stride(0), masks.data_ptr(),
            sidx.data_ptr() if sidx is not None else None, B, offset, FM.LOSS_KINDS[loss], float(grad_scale),
-           dz.data_ptr(), dz.stride(0), partials.data_ptr(), N.stream_handle(logits.device))
+           dz.data_ptr(), dz.stride(0), partials.data_ptr(), colpart.data_ptr() if colpart is not None else None,
+           N.stream_handle(logits.device))
     return dz, partials[:(B + 3) // 4]

@@ -343,3 +343,24 @@ def test_hip_quantised_matches_oracle(obj):
     assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
     assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)
     assert abs(a.history[-1]["test"] - b.history[-1]["test"]) < 1e-5
+
+
+@pytest.mark.gpu
+def test_hip_quantised_mixed_features_match_oracle():
+    """The reference feature set (63 one-hot lag features + 3 calendar features with 12-196 bins) at
+    a size where both sparse passes run (row-per-lane one-hot kernel + lane-per-feature calendar
+    kernel, several chunks): trees bit-identical to the oracle's quantised mode."""
+    from euromillioner_amd import config as C
+    from euromillioner_amd.pipeline import gbdt_dataset
+
+    ds = DrawSet.synthetic(n=30001, seed=6, planted=0.5)
+    X, Y, _ = gbdt_dataset(ds, C.RunConfig())
+    Y = Y[:, :6]
+    m = 24000
+    kw = dict(nround=4, eta=1.0, max_depth=3, gamma=1.0, hist_mode="quant")
+    a = G.GBDT(backend="numpy", **kw).fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
+    b = G.GBDT(backend="hip", **kw).fit(X[:m], Y[:m], evals={"test": (X[m:], Y[m:])})
+    assert b.backend_used == "hip" and b.quant_bits_used == a.quant_bits_used > 0
+    assert np.array_equal(a.trees.status, b.trees.status)
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)

@@ -89,3 +89,26 @@ def test_onehot_lags_random(B, lags, offset, fp32):
     for k in range(lags):
         ref[:, 64 * k:64 * k + 62] = mh[offset + k:offset + k + B]
     assert torch.equal(out.float(), ref)
+
+
+def test_adam_bias_correction_exact_first_steps():
+    """From zero weights every Adam update is visible at full fp32 precision, so the first steps'
+    bias corrections (1 - beta^t, computed in fp64) must match torch.optim.Adam to ~fp32 rounding:
+    a native exp/log form of beta^t (~1e-4 relative error at small t) fails this by 10x."""
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    n = 4096
+    g = torch.Generator(device="cuda").manual_seed(7)
+    p = torch.zeros(n, device="cuda")
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    hp = torch.tensor([1e-2, 0.9, 0.999, 1e-8, 0.0], device="cuda")
+    state = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ref = p.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=1e-2, betas=(0.9, 0.999), eps=1e-8)
+    for _ in range(6):
+        gr = torch.randn(n, device="cuda", generator=g)
+        FM.adam_flat(p, gr, m, v, hp, state)
+        ref.grad = gr.clone()
+        opt.step()
+        torch.cuda.synchronize()
+        assert torch.allclose(p, ref.detach(), rtol=1e-5, atol=1e-9), float((p - ref.detach()).abs().max())

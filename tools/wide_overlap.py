@@ -64,6 +64,7 @@ def run(steps: int = 20, B: int = 1 << 16, bucket_mb: float = 25.0):
     peer = torch.randn(m.P + 1, device=dev)
     out = torch.empty_like(peer)
     for mode in ("none", "sidecopy", "serial", "none"):
+        m.last_buckets = []
         m.comm_emulator = None if mode == "none" else (
             lambda flat, be, s=(mode == "serial"): SideCopy(flat, be, side, peer, out, serial=s))
         for i in range(3):
@@ -86,8 +87,9 @@ def run(steps: int = 20, B: int = 1 << 16, bucket_mb: float = 25.0):
 
 def report(path: str):
     """Per mode (trace phases split at the 0.5 s sleeps): side-copy time and the fraction of it that
-    ran concurrently with compute-stream kernels, and each compute kernel's mean duration against
-    the first no-communication phase (what the concurrent copies cost the GEMMs)."""
+    ran concurrently with compute-stream kernels, and each compute kernel's time per step against
+    the first no-communication phase (what the concurrent copies cost the GEMMs; the panelled wgrad
+    is several launches per step in the communicating modes, one without)."""
     import csv
 
     rows = list(csv.DictReader(open(path)))
@@ -104,12 +106,13 @@ def report(path: str):
     modes = ["none", "sidecopy", "serial", "none(again)"]
     main = max(set(k[3] for k in ks), key=lambda s: sum(1 for k in ks if k[3] == s))
 
-    def per_kernel(ph):
+    def per_kernel(ph):  # compute-stream time per kernel name per optimizer step (Adam launches = steps)
         d = {}
         for k in ph:
             if k[3] == main:
                 d.setdefault(k[2][:80], []).append(k[1] - k[0])
-        return {n: sum(v) / len(v) / 1e3 for n, v in d.items()}
+        steps = max(1, sum(len(v) for n, v in d.items() if "adam" in n))
+        return {n: sum(v) / steps / 1e3 for n, v in d.items()}
     base = per_kernel(phases[0])
     for name, ph in zip(modes, phases):
         side = [k for k in ph if k[3] != main]
