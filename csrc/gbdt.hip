@@ -222,11 +222,11 @@ __global__ void __launch_bounds__(256)
 gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
             const int16_t* __restrict__ node, const int* __restrict__ foff, const int* __restrict__ fmap,
             const int* __restrict__ gfoff, long long* __restrict__ partial, int T, int n, int F, int Fs, int C,
-            int level, int chunk, int FT, int NTn, int P, int ldsW, int piece, double qscale, int R) {
+            int level, int chunk, int FT, int NTn, int P, int ldsW, int piece, double qscale) {
   // features: the Fs features of a sub-problem (foff: their compact cells; fmap: sub -> row column,
   // null = identity; gfoff: the full problem's cells, where the output goes); F = bytes per bin row.
-  // R replicas of each node's cells (phase p uses p % R): with few features per tile the phases of a
-  // wave are consecutive rows, whose calendar bins (and the total lane) hit the same word otherwise.
+  // (4 replicas of the cells for the phases of a wave measured 2.5x slower on the calendar
+  // sub-problem: lanes of one atomic on the same word are cheap, and the footprint forced node tiles)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int c = blockIdx.x, t = blockIdx.y;
@@ -234,9 +234,8 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
   const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
   const int f0 = ft * FT, f1 = min(Fs, f0 + FT), n0 = nt * NTn;
   const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
-  long long* hist = reinterpret_cast<long long*>(smem);  // [2 planes][NTn][R][ldsW], shared by all P phases
-  const int NW = R * ldsW;                                // words per node
-  const int per = NTn * NW;
+  long long* hist = reinterpret_cast<long long*>(smem);  // [2 planes][NTn][ldsW], shared by all P phases
+  const int per = NTn * ldsW;
   for (int i = threadIdx.x; i < 2 * per; i += blockDim.x) hist[i] = 0;
   long long* sq = hist + 2 * per;  // staged rows: (qg, qh) pairs, the tile-relative node ids, the bin rows
   int16_t* sn = reinterpret_cast<int16_t*>(sq + 2 * piece);
@@ -247,7 +246,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
   const bool tot = fl == nth - 1;
   const int f = f0 + ((p < P && !tot) ? fl : 0);
-  long long* my = hist + (p % R) * ldsW + (tot ? ldsW - 2 : (foff[f] - c0) + (f - f0));  // total: "bin 1" = last
+  long long* my = hist + (tot ? ldsW - 2 : (foff[f] - c0) + (f - f0));  // total lane: "bin 1" = the last cell
   const int rb = c * chunk, re = min(n, rb + chunk);
   for (int r0 = rb; r0 < re; r0 += piece) {
     const int r1 = min(re, r0 + piece);
@@ -293,7 +292,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           if ((unsigned)nd[u] >= (unsigned)NTn || b[u] == 0) continue;
-          long long* e = my + nd[u] * NW + b[u];
+          long long* e = my + nd[u] * ldsW + b[u];
           const long long qg = sq[2 * (r + u * P)], qh = sq[2 * (r + u * P) + 1];
           __hip_atomic_fetch_add(e, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_fetch_add(e + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -303,7 +302,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
         const int nd = sn[r];
         const int bb = tot ? 1 : col[r * F];
         if ((unsigned)nd >= (unsigned)NTn || bb == 0) continue;
-        long long* e = my + nd * NW + bb;
+        long long* e = my + nd * ldsW + bb;
         __hip_atomic_fetch_add(e, sq[2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(e + per, sq[2 * r + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -316,11 +315,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
     const int nd = i / Ct, cc = i - nd * Ct;
     int fi = f0;  // the feature of compact cell c0 + cc (its pad cells precede it)
     while (foff[fi + 1] <= c0 + cc) ++fi;
-    auto cell = [&](int k, int plane) {  // cell k of this node summed over the replicas
-      long long v = 0;
-      for (int q = 0; q < R; ++q) v += hist[plane * per + nd * NW + q * ldsW + k];
-      return v;
-    };
+    auto cell = [&](int k, int plane) { return hist[plane * per + nd * ldsW + k]; };
     const int k0 = cc + (fi - f0);
     long long vg = cell(k0, 0), vh = cell(k0, 1);
     if (c0 + cc == foff[fi]) {  // bin 0: the node's total minus the feature's other bins
@@ -356,18 +351,25 @@ __global__ void gbdt_pack_bits(const uint8_t* __restrict__ bins, int n, int F, c
 }
 
 constexpr int QB_ROWS = 4;  // rows per thread in flight
-constexpr int QB_REP = 4;   // replicas of a node's cells (lane & 3): neighbouring rows rarely share a word
+constexpr int QB_REP = 4;   // replicas of the one-hot cells and the total (lane & 3)
+constexpr int QB_MPRE = 4;  // multi-bin features whose bin bytes are loaded with the row's other inputs
+// The other (multi-bin) features ride along: per row one byte load and one atomic pair each, into
+// cells of their own (no replicas; consecutive rows mostly share a calendar bin, i.e. a word, and
+// lanes of one atomic on the same word are cheap).
+// LDS per tile node: [QB_REP x ((nb + 1) | 1) one-hot + total words][Cm multi-bin cells], two planes.
 __global__ void __launch_bounds__(256)
 gbdt_hist_qb(const uint64_t* __restrict__ bmask, int WB, const int* __restrict__ bcell, int nb,
-             const float* __restrict__ g, const float* __restrict__ h, const int16_t* __restrict__ node,
-             long long* __restrict__ partial, int T, int n, int C, int level, int chunk, int NTn, double qscale) {
+             const uint8_t* __restrict__ bins, int F, const int* __restrict__ fmap, const int* __restrict__ foffm,
+             const int* __restrict__ gfoff, int Fm, const float* __restrict__ g, const float* __restrict__ h,
+             const int16_t* __restrict__ node, long long* __restrict__ partial, int T, int n, int C, int level,
+             int chunk, int NTn, double qscale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int c = blockIdx.x, t = blockIdx.y, n0 = blockIdx.z * NTn;
-  // per node: QB_REP replicas of [bin-1 cell of each one-hot feature j | total], each padded to an
-  // odd word count so the replicas start on different banks
-  const int W = (nb + 1) | 1;
-  const int per = NTn * QB_REP * W;
+  const int W = (nb + 1) | 1;  // one replica: bin-1 cell of each one-hot feature, the total (odd word count)
+  const int Cm = Fm ? foffm[Fm] : 0;
+  const int NW = QB_REP * W + Cm;  // words per node
+  const int per = NTn * NW;
   long long* hist = reinterpret_cast<long long*>(smem);
   for (int i = threadIdx.x; i < 2 * per; i += blockDim.x) hist[i] = 0;
   __syncthreads();
@@ -378,7 +380,7 @@ gbdt_hist_qb(const uint64_t* __restrict__ bmask, int WB, const int* __restrict__
   const int rot = (int)((threadIdx.x * 37u) & 63u);
   const int rb = c * chunk, re = min(n, rb + chunk);
   for (int r0 = rb + (int)threadIdx.x; r0 < re; r0 += QB_ROWS * blockDim.x) {
-    int nd[QB_ROWS];
+    int nd[QB_ROWS], mb[QB_ROWS][QB_MPRE];
     float gv[QB_ROWS], hv[QB_ROWS];
     uint64_t m0[QB_ROWS];
 #pragma unroll
@@ -389,15 +391,25 @@ gbdt_hist_qb(const uint64_t* __restrict__ bmask, int WB, const int* __restrict__
       gv[u] = ok ? g[base + r] : 0.f;
       hv[u] = ok ? h[base + r] : 0.f;
       m0[u] = ok ? bmask[(int64_t)r * WB] : 0ull;
+#pragma unroll
+      for (int k = 0; k < QB_MPRE; ++k) mb[u][k] = (ok && k < Fm) ? bins[(int64_t)r * F + fmap[k]] : 0;
     }
 #pragma unroll
     for (int u = 0; u < QB_ROWS; ++u) {
       if ((unsigned)nd[u] >= (unsigned)NTn) continue;
       const long long qg = quantise(gv[u], qscale), qh = quantise(hv[u], qscale);
-      long long* pl = hist + (nd[u] * QB_REP + rep) * W;
+      long long* pn = hist + nd[u] * NW;
+      long long* pl = pn + rep * W;
       __hip_atomic_fetch_add(pl + nb, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_fetch_add(pl + nb + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const int r = r0 + u * blockDim.x;
+      for (int k = 0; k < Fm; ++k) {  // multi-bin features: their own cells, bin 0 derived at the end
+        const int b = k < QB_MPRE ? mb[u][k] : bins[(int64_t)r * F + fmap[k]];
+        if (b == 0) continue;
+        long long* e = pn + QB_REP * W + foffm[k] + b;
+        __hip_atomic_fetch_add(e, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(e + per, qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       for (int w = 0; w < WB; ++w) {
         const uint64_t mw = w == 0 ? m0[u] : bmask[(int64_t)r * WB + w];
         uint64_t m = rot ? (mw >> rot) | (mw << (64 - rot)) : mw;  // rotate right by rot
@@ -413,22 +425,43 @@ gbdt_hist_qb(const uint64_t* __restrict__ bmask, int WB, const int* __restrict__
   __syncthreads();
   long long* out = partial + ((int64_t)c * T + t) * (int64_t)nodesL * C * 2;
   const int nn = min(NTn, nodesL - n0);
-  for (int i = threadIdx.x; i < nn * nb; i += blockDim.x) {
+  auto total = [&](int nd, int plane) {
+    long long v = 0;
+#pragma unroll
+    for (int q = 0; q < QB_REP; ++q) v += hist[plane * per + nd * NW + q * W + nb];
+    return v;
+  };
+  for (int i = threadIdx.x; i < nn * nb; i += blockDim.x) {  // one-hot features: bin 0 = total - bin 1
     const int nd = i / nb, j = i - nd * nb;
-    long long g1 = 0, h1 = 0, gt = 0, ht = 0;
+    long long g1 = 0, h1 = 0;
 #pragma unroll
     for (int q = 0; q < QB_REP; ++q) {
-      const long long* pl = hist + (nd * QB_REP + q) * W;
-      g1 += pl[j];
-      h1 += pl[per + j];
-      gt += pl[nb];
-      ht += pl[per + nb];
+      g1 += hist[nd * NW + q * W + j];
+      h1 += hist[per + nd * NW + q * W + j];
     }
     long long* o = out + ((int64_t)(n0 + nd) * C + bcell[j]) * 2;  // bcell = the feature's bin-0 cell
-    o[0] = gt - g1;
-    o[1] = ht - h1;
+    o[0] = total(nd, 0) - g1;
+    o[1] = total(nd, 1) - h1;
     o[2] = g1;
     o[3] = h1;
+  }
+  for (int i = threadIdx.x; i < nn * Cm; i += blockDim.x) {  // multi-bin features
+    const int nd = i / Cm, cc = i - nd * Cm;
+    int k = 0;
+    while (foffm[k + 1] <= cc) ++k;
+    const long long* e = hist + nd * NW + QB_REP * W;
+    long long vg = e[cc], vh = e[per + cc];
+    if (cc == foffm[k]) {  // bin 0: the node's total minus the feature's other bins
+      vg = total(nd, 0);
+      vh = total(nd, 1);
+      for (int q = foffm[k] + 1; q < foffm[k + 1]; ++q) {
+        vg -= e[q];
+        vh -= e[per + q];
+      }
+    }
+    long long* o = out + ((int64_t)(n0 + nd) * C + gfoff[fmap[k]] + (cc - foffm[k])) * 2;
+    o[0] = vg;
+    o[1] = vh;
   }
 }
 
@@ -748,7 +781,7 @@ inline int grid_for(int64_t total, int bs = 256) {
 // ------------------------------------------------------------------ host-side histogram plan
 namespace {
 struct HistPlan {
-  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece, R = 1;
+  int chunk, nchunks, FT, NTn, P, ldsC, nft, ntn, threads, piece;
   size_t lds;
 };
 
@@ -773,16 +806,13 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
       int P = 256 / lanes;  // row phases: the exact form keeps P private copies (<= 4), the fixed-point
       const int Pmax = quant ? 64 : 4;  // form one shared copy, so a few-feature tile fills the block with phases
       P = P > Pmax ? Pmax : (P < 1 ? 1 : P);
-      // fixed point with >= 8 phases: 4 replicas (consecutive-row phases of one wave would hit the same words)
-      const int R = (quant && P >= 8) ? 4 : 1;
       for (; P >= 1; --P)
-        if ((int64_t)(quant ? R : P) * NTn * W * 16 <= HIST_LDS_BUDGET) break;
+        if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= HIST_LDS_BUDGET) break;
       if (P >= 1) {
         pl.FT = FT;
         pl.NTn = NTn;
         pl.P = P;
         pl.ldsC = W;
-        pl.R = R;
         pl.nft = (F + FT - 1) / FT;
         pl.ntn = nodesL / NTn;
         pl.threads = ((lanes * P + 63) / 64) * 64;
@@ -802,7 +832,7 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
         pl.piece = quant ? ((HIST_QBIN_LDS / RB) & ~15) : HIST_MAX_CHUNK;
         if (pl.piece > HIST_MAX_CHUNK) pl.piece = HIST_MAX_CHUNK;
         if (pl.piece < 16) pl.piece = 16;
-        pl.lds = (size_t)(quant ? R : P) * NTn * pl.ldsC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4 +
+        pl.lds = (size_t)(quant ? 1 : P) * NTn * pl.ldsC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4 +
                  (quant ? ((size_t)pl.piece * RB + 32 + 15) / 16 * 16 : 0);
         return true;
       }
@@ -849,31 +879,20 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
   long long* qpart = reinterpret_cast<long long*>(partial);
   int nchunks = 0;
   if (quant && qa && qa->nb > 0) {
-    HistPlan pm;
-    const bool multi = qa->Fm > 0;
-    if (multi && !plan_hist(level, n, T, qa->Fm, qa->foffm_h.data(), true, pm, F)) return EM_ERR_ARG;
     int NTb = nodesL;
-    const int Wb = (qa->nb + 1) | 1;
-    while (NTb > 1 && (int64_t)2 * NTb * QB_REP * Wb * 8 > HIST_LDS_BUDGET) NTb >>= 1;
-    int64_t chunk;
-    if (multi) {
-      chunk = pm.chunk;
-    } else {
-      const int64_t per_chunk = (int64_t)T * (nodesL / NTb);
-      chunk = (n + (4096 + per_chunk - 1) / per_chunk - 1) / ((4096 + per_chunk - 1) / per_chunk);
-    }
+    const int NWb = QB_REP * ((qa->nb + 1) | 1) + qa->foffm_h[qa->Fm];  // words per node
+    while (NTb > 1 && (int64_t)2 * NTb * NWb * 8 > HIST_LDS_BUDGET) NTb >>= 1;
+    const int64_t per_chunk = (int64_t)T * (nodesL / NTb);  // ~4096 blocks per level
+    const int64_t want = (4096 + per_chunk - 1) / per_chunk;
+    int64_t chunk = (n + want - 1) / want;
     const int64_t maxch = partial_doubles / S;  // chunks that fit the partial buffer
     if (maxch < 1) return EM_ERR_ARG;
     if ((n + chunk - 1) / chunk > maxch) chunk = (n + maxch - 1) / maxch;
     if (chunk < 64) chunk = 64;
     nchunks = (int)((n + chunk - 1) / chunk);
-    hipLaunchKernelGGL(gbdt_hist_qb, dim3(nchunks, T, nodesL / NTb), dim3(256), (size_t)2 * NTb * QB_REP * Wb * 8,
-                       stream, qa->bmask_d, qa->WB, qa->bcell_d, qa->nb, g, h, node, qpart, T, n, C, level,
-                       (int)chunk, NTb, qscale);
-    if (multi)
-      hipLaunchKernelGGL(gbdt_hist_q, dim3(nchunks, T, pm.nft * pm.ntn), dim3(pm.threads), pm.lds, stream, bins, g, h,
-                         node, qa->foffm_d, qa->fmap_d, foff_d, qpart, T, n, F, qa->Fm, C, level, (int)chunk, pm.FT,
-                         pm.NTn, pm.P, pm.ldsC, pm.piece, qscale, pm.R);
+    hipLaunchKernelGGL(gbdt_hist_qb, dim3(nchunks, T, nodesL / NTb), dim3(256), (size_t)2 * NTb * NWb * 8, stream,
+                       qa->bmask_d, qa->WB, qa->bcell_d, qa->nb, bins, F, qa->fmap_d, qa->foffm_d, foff_d, qa->Fm, g,
+                       h, node, qpart, T, n, C, level, (int)chunk, NTb, qscale);
   } else {
     HistPlan pl;
     if (!plan_hist(level, n, T, F, foff_h, quant, pl)) return EM_ERR_ARG;
@@ -883,7 +902,7 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
     if (quant)
       hipLaunchKernelGGL(gbdt_hist_q, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d,
                          (const int*)nullptr, foff_d, qpart, T, n, F, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
-                         pl.ldsC, pl.piece, qscale, pl.R);
+                         pl.ldsC, pl.piece, qscale);
     else
       hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d, partial, T, n,
                          F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
@@ -966,7 +985,9 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         qa.foffm_h.push_back(qa.foffm_h.back() + nbins);
       }
     }
-    if (bcell.size() >= 8) {
+    // sparse form only when one node's cells fit the LDS budget (many continuous features: dense form)
+    if (bcell.size() >= 8 && (int64_t)16 * (QB_REP * (((int)bcell.size() + 1) | 1) + qa.foffm_h.back()) <=
+                                 HIST_LDS_BUDGET) {
       qa.nb = (int)bcell.size();
       qa.WB = (qa.nb + 63) / 64;
       qa.Fm = (int)fmap.size();

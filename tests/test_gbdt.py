@@ -364,3 +364,21 @@ def test_hip_quantised_mixed_features_match_oracle():
     assert np.array_equal(a.trees.status, b.trees.status)
     assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
     assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hip_quantised_dense_form_matches_oracle():
+    """Continuous features only (no one-hot block): the fixed-point form runs the lane-per-feature
+    kernel over all features (staged bin rows, one shared LDS copy, derived bin 0); depth-6 trees
+    over 256-bin features stay bit-identical to the oracle's quantised mode."""
+    rng = np.random.default_rng(11)
+    n = 6000
+    X = rng.normal(size=(n, 12))
+    y = ((X[:, 0] + 0.5 * X[:, 3] * X[:, 5] + 0.3 * rng.normal(size=n)) > 0).astype(np.float64)
+    kw = dict(nround=4, max_depth=6, eta=0.5, gamma=0.0, min_child_weight=0.5, hist_mode="quant")
+    a = G.GBDT(backend="numpy", **kw).fit(X[:4500], y[:4500], evals={"test": (X[4500:], y[4500:])})
+    b = G.GBDT(backend="hip", **kw).fit(X[:4500], y[:4500], evals={"test": (X[4500:], y[4500:])})
+    assert b.backend_used == "hip" and b.quant_bits_used == a.quant_bits_used > 0
+    assert np.array_equal(a.trees.status, b.trees.status)
+    assert np.array_equal(a.trees.feat, b.trees.feat) and np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.allclose(a.trees.leaf, b.trees.leaf, atol=1e-5)

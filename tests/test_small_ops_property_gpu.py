@@ -111,4 +111,4 @@ def test_adam_bias_correction_exact_first_steps():
         ref.grad = gr.clone()
         opt.step()
         torch.cuda.synchronize()
-        assert torch.allclose(p, ref.detach(), rtol=1e-5, atol=1e-9), float((p - ref.detach()).abs().max())
+        assert torch.allclose(p, ref.detach(), rtol=5e-6, atol=5e-8), float((p - ref.detach()).abs().max())
