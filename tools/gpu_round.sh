@@ -1,0 +1,66 @@
+#!/bin/bash
+# Round-3 GPU measurements as named stages (run through gpurun; every GPU step has its own time
+# limit and a failing step ends the script).  Outputs under gpurun_out/round/<stage>/.
+#   bash tools/gpu_round.sh full            GPU suite + smoke() + driver-shape and default bench
+#   bash tools/gpu_round.sh fused-ab        same-box A/B: two-launch vs one-launch step (+ the round-2
+#                                           library when euromillioner_amd/lib/ab/old.so exists)
+#   bash tools/gpu_round.sh headline-prof   kernel trace + 2 PMC passes of the headline step, phase
+#                                           stamps when the FUSED_STAMPS side build lib/ab/stamps.so exists
+#   bash tools/gpu_round.sh gbdt            GBDT GPU tests, kernel trace of the 183k-row case, gbdt_bench
+#   bash tools/gpu_round.sh fp32            bench.py --dtype fp32 + kernel trace
+#   bash tools/gpu_round.sh wide            wide-MLP bench + kernel trace, one-GPU overlap rehearsal
+# Several stages run in order: bash tools/gpu_round.sh gbdt fp32
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+summ() { grep '^{' "$1" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$2', d['value'], d['ms_per_step'], (d.get('val') or {}).get('acc'))"; }
+for stage in "$@"; do
+  O=gpurun_out/round/$stage
+  mkdir -p $O
+  case $stage in
+  full)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 3; }
+    tail -1 $O/pytest.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 4; }
+    tail -1 $O/smoke.log
+    timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail $O/bench_driver.err; exit 5; }
+    timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 6; }
+    summ $O/bench_driver.json driver && summ $O/bench_default.json default || exit 7
+    ;;
+  fused-ab)
+    ARMS="split|EUROM_FUSED_ADAM=0;fused|EUROM_FUSED_ADAM=1"
+    [ -f euromillioner_amd/lib/ab/old.so ] && ARMS="old|EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/old.so;$ARMS"
+    rm -rf gpurun_out/ab
+    ARMS="$ARMS" ROUNDS=${ROUNDS:-3} bash tools/gpu_ab.sh || exit 8
+    cp gpurun_out/ab/results.jsonl $O/
+    ;;
+  headline-prof)
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 200 --warmup 5 --no-eval > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 9; }
+    timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $O/pmc1 -o run -- python bench.py --steps 20 --warmup 5 --no-eval --graph 0 > $O/pmc1.log 2>&1 || { tail -20 $O/pmc1.log; exit 10; }
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY --output-format csv -d $O/pmc2 -o run -- python bench.py --steps 20 --warmup 5 --no-eval --graph 0 > $O/pmc2.log 2>&1 || { tail -20 $O/pmc2.log; exit 11; }
+    if [ -f euromillioner_amd/lib/ab/stamps.so ]; then
+      EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/stamps.so TL_B=1048576 timeout -k 10 200 python tools/fused_timeline.py > $O/timeline.txt 2>&1 || { tail -20 $O/timeline.txt; exit 12; }
+      cat $O/timeline.txt
+    fi
+    ;;
+  gbdt)
+    timeout -k 10 400 python -u -m pytest tests/test_gbdt.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 13; }
+    tail -1 $O/pytest.log
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python tools/gbdt_bench.py 262k > $O/trace.log 2>&1 || { tail $O/trace.log; exit 14; }
+    timeout -k 10 300 python tools/gbdt_bench.py > $O/gbdt_bench.jsonl 2> $O/gbdt_bench.err || { tail $O/gbdt_bench.err; exit 15; }
+    cat $O/gbdt_bench.jsonl
+    ;;
+  fp32)
+    timeout -k 10 300 python bench.py --dtype fp32 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 16; }
+    summ $O/bench.json fp32 || exit 17
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --dtype fp32 --steps 20 --warmup 5 --no-eval > $O/trace.log 2>&1 || { tail $O/trace.log; exit 18; }
+    ;;
+  wide)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --model mlp-wide --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 19; }
+    summ $O/bench.json wide || exit 20
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/overlap -o run -- python tools/wide_overlap.py > $O/overlap.jsonl 2> $O/overlap.err || { tail $O/overlap.err; exit 21; }
+    python tools/wide_overlap.py report $O/overlap/run_kernel_trace.csv > $O/overlap_report.jsonl && cat $O/overlap.jsonl
+    ;;
+  *) echo "unknown stage $stage"; exit 2;;
+  esac
+done
