@@ -132,6 +132,14 @@ EM_DEVICE void lds_signal(char* smem, uint32_t flag_off, int value) {
 #ifndef FUSED_STAMPS
 #define FUSED_STAMPS 0
 #endif
+// A/B knobs (tools/build_variant.sh; profiles/r3/ab_knobs.jsonl): the ring wait's s_sleep (0 and 3 within
+// noise of 1) and the forward waves' priority (0: 8 % slower, 2: same as 1)
+#ifndef FUSED_SLEEP
+#define FUSED_SLEEP 1
+#endif
+#ifndef FUSED_FPRIO
+#define FUSED_FPRIO 1
+#endif
 struct Stamps {
   uint64_t last = 0;
   uint64_t acc[10] = {};
@@ -275,7 +283,7 @@ EM_DEVICE void v6_wait(const char* smem, uint32_t off, int target, bool& ok) {
   int spins = 0;
   while (__hip_atomic_load(reinterpret_cast<const int*>(smem + off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
          target) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(FUSED_SLEEP);
     if (++spins > V6_SPIN_LIMIT) {
       ok = false;
       return;
@@ -679,7 +687,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   };
   if (ROLE < 2) {
     float loss_acc = 0.f;
-    __builtin_amdgcn_s_setprio(1);  // forward waves bound the pipeline (+3 %)
+    __builtin_amdgcn_s_setprio(FUSED_FPRIO);  // forward waves bound the pipeline (+3 % at 1)
     v6_forward<LOSS, ROLE>(smem, masks, sidx, B, offset, unit, lane, loss_acc, ok, st);
     float lsum = wave_sum(loss_acc);
     if (!ok) lsum = __builtin_nanf("");
@@ -930,6 +938,7 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
   __syncthreads();
   // wave w runs on SIMD w % 4.  unit 0 = waves 0-3 (F0 F1 B0 B1), unit 1 = waves 4-7 (B0 B1 F0 F1):
   // every SIMD hosts one forward and one backward wave
+  // (pairing F and B of the same unit on a SIMD measured 1.5 % slower)
   const int unit = wave >> 2, wl = wave & 3;
   const int role = unit == 0 ? wl : (wl ^ 2);  // 0/1 forward f, 2/3 backward rho
   float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
