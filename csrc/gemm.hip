@@ -302,6 +302,21 @@ EM_DEVICE float g_dfn(float y) {  // activation derivative from the saved output
   return 1.f - y * y;
 }
 
+// ReLU activity bits, uint32 [M / 32][N]: bit (m & 31) of word (m >> 5) * N + n is output[m][n] > 0.
+// A forward epilogue with relu writes them next to its bf16 output; the relu dgrad of the layer above
+// reads one dword per lane and 32-row block instead of staging the 32 x 64 bf16 activation block.
+// Per 32-row block the lane of the 32x32 accumulator layout (column lc, rows 8g + 4h + e) holds bits
+// 8g + 4h + e; the 16x16 layout's lane (column lc, rows 16tm + 4(lane >> 4) + e) holds 16tm + 4(lane >> 4) + e.
+EM_DEVICE uint32_t or_xhalf(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (uint32_t)r[0] | (uint32_t)r[1];
+}
+EM_DEVICE uint32_t or_rows16(uint32_t v) {  // OR over the four 16-lane rows (same lane & 15)
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return or_xhalf((uint32_t)a[0] | (uint32_t)a[1]);
+}
+EM_DEVICE float bit_mul(uint32_t w, int b, float v) { return ((w >> b) & 1u) ? v : v * 0.f; }
+
 // OUT_BF16: 1 -> bf16 C (optionally + transposed C^T when HAS_CT), 0 -> fp32 C (+ beta * C_old)
 // FN: activation (DACT = 0, applied to alpha*acc + bias) or activation' (DACT = 1, multiplies
 // alpha*acc by act'(mask[m][n]))
@@ -311,7 +326,7 @@ template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, int wm, int wn, int m0, int n0,
                           void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
                           const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                          float beta, float* __restrict__ colpart, int N) {
+                          float beta, float* __restrict__ colpart, int N, uint32_t* __restrict__ bits) {
   const int r = lane & 31, h = lane >> 5;
   // bf16 outputs go through a per-wave transposed LDS tile T[64 cols][32 rows] (ds_write_b64 of 4
   // consecutive rows per lane), then leave as 16-B coalesced stores: C rows via ds_read_b64_tr_b16
@@ -324,10 +339,15 @@ EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, i
   char* yb = tb + 64 * TS;
   const int colw = n0 + wn * 64;
   float cs[2] = {0.f, 0.f};  // column sums of the epilogue values over the wave's 128 rows (colpart)
+  constexpr bool WBITS = !DACT && FN == ACT_RELU && OUT_BF16;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // unrolled: acc[i] must stay statically indexed (no scratch)
     const int rowb = m0 + wm * 128 + 32 * i;  // first row of this block
-    if (DACT) {
+    uint32_t bw[2] = {0u, 0u};  // DACT: the block's activity words of the lane's columns; WBITS: bits being built
+    if (DACT && bits) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bw[j] = bits[(int64_t)(rowb >> 5) * N + colw + 32 * j + r];
+    } else if (DACT) {
       const __bf16* ysrc = mask + (int64_t)rowb * ldm + colw;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -350,9 +370,10 @@ EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, i
           const int lr = 8 * g + 4 * h + e;
           float v = alpha * acc[i][j][4 * g + e];
           if (DACT) {
-            v *= g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
+            v = bits ? bit_mul(bw[j], lr, v) : v * g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
           } else {
             v = g_fn<FN>(v + bv);
+            if (WBITS) bw[j] |= (v > 0.f ? 1u : 0u) << (8 * g + e);
           }
           x[e] = v;
           cs[j] += v;
@@ -367,6 +388,13 @@ EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, i
           __builtin_memcpy(&pk, t4, 8);
           *reinterpret_cast<u32x2*>(tb + lc * TS + (8 * g + 4 * h) * 2) = pk;
         }
+      }
+    }
+    if (WBITS && bits) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t w = or_xhalf(bw[j] << (4 * h));
+        if (h == 0) bits[(int64_t)(rowb >> 5) * N + colw + 32 * j + r] = w;
       }
     }
     if (OUT_BF16) {
@@ -408,7 +436,7 @@ __global__ void __launch_bounds__(G_NT, 1)
 gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                   void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                   const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta, float* __restrict__ colpart) {
+                  float beta, float* __restrict__ colpart, uint32_t* __restrict__ bits) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -462,7 +490,7 @@ gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   }
 
   g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
-                                         alpha, beta, colpart, N);
+                                         alpha, beta, colpart, N, bits);
 }
 
 // ============================================================================================
@@ -527,7 +555,7 @@ __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                   void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                   const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta, float* __restrict__ colpart) {
+                  float beta, float* __restrict__ colpart, uint32_t* __restrict__ bits) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -624,7 +652,7 @@ gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
-                                         alpha, beta, colpart, N);
+                                         alpha, beta, colpart, N, bits);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -642,6 +670,10 @@ EM_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// G_CROW = 1: bf16 C rows leave through a row image, 8 lanes per 128-B row (see gemm_k64_kernel)
+#ifndef G_CROW
+#define G_CROW 1
+#endif
 // g_epilogue for the 16x16 accumulator layout: per 32-row block i the lane's values land in the
 // same transposed per-wave LDS tile T[64 cols][32 rows] (4 consecutive rows = one 8-B write), so
 // everything after the tile is shared with the 32x32 form.
@@ -650,7 +682,7 @@ template <int OUT_BF16, int FN, int DACT, int HAS_CT, int NBT>
 EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave, int lane, int rowbase, int colw,
                             void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
                             const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                            float beta, float* __restrict__ colpart, int N) {
+                            float beta, float* __restrict__ colpart, int N, uint32_t* __restrict__ bits) {
   constexpr int TS = 80;
   constexpr int YS = 144;
   constexpr int WEPI = 64 * TS + 32 * YS;
@@ -658,10 +690,15 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
   char* yb = tb + 64 * TS;
   const int c16 = lane & 15, r4 = 4 * (lane >> 4);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of the epilogue values over the wave's 128 rows (colpart)
+  constexpr bool WBITS = !DACT && FN == ACT_RELU && OUT_BF16;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rowb = rowbase + 32 * i;
-    if (DACT) {
+    uint32_t bw[4] = {0u, 0u, 0u, 0u};  // per 16-column group nb (see g_epilogue)
+    if (DACT && bits) {
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) bw[nb] = bits[(int64_t)(rowb >> 5) * N + colw + 16 * nb + c16];
+    } else if (DACT) {
       const __bf16* ysrc = mask + (int64_t)rowb * ldm + colw;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -685,9 +722,10 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
           const int lr = 16 * tm + r4 + e;
           float v = alpha * a[e];
           if (DACT) {
-            v *= g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
+            v = bits ? bit_mul(bw[nb], lr, v) : v * g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
           } else {
             v = g_fn<FN>(v + bv);
+            if (WBITS) bw[nb] |= (v > 0.f ? 1u : 0u) << (16 * tm + e);
           }
           x[e] = v;
           cs[nb] += v;
@@ -702,17 +740,36 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
         }
       }
     }
+    if (WBITS && bits) {
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const uint32_t w = or_rows16(bw[nb] << r4);
+        if (lane < 16) bits[(int64_t)(rowb >> 5) * N + colw + 16 * nb + c16] = w;
+      }
+    }
     if (OUT_BF16) {
       wave_lds_sync();
       const int gg = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int cb = 8 * (gg >> 1) + 16 * it;
-        const int r0 = 16 * (gg & 1);
+        const int r0 = 16 * (gg & 1), row = r0 + i16;
         const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * TS + (r0 + 4 * p4) * 2));
         const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * TS + (r0 + 4 * p4) * 2));
         const bf16x8 v8 = cat_tr(lo, hi);
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + r0 + i16) * ldc + colw + cb) = v8;
+        if (G_CROW)  // row image [32 rows][128 B] in the (consumed) Y block, chunk c of a row at c ^ (row & 7)
+          *reinterpret_cast<bf16x8*>(yb + row * 128 + (((cb >> 3) ^ (row & 7)) << 4)) = v8;
+        else
+          *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + row) * ldc + colw + cb) = v8;
+      }
+      if (G_CROW) {  // 8 lanes per 128-B row segment: each store covers 8 whole lines (gemm_k64_kernel CROW)
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = lane + 64 * k, row = q >> 3, ch = q & 7;
+          *reinterpret_cast<u32x4*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + row) * ldc + colw + ch * 8) =
+              *reinterpret_cast<const u32x4*>(yb + row * 128 + ((ch ^ (row & 7)) << 4));
+        }
       }
       if (HAS_CT) {
 #pragma unroll
@@ -772,7 +829,7 @@ __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                     void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                     const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                    float beta, float* __restrict__ colpart) {
+                    float beta, float* __restrict__ colpart, uint32_t* __restrict__ bits) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t st_acc[8] = {}, st_t0 = 0, st_a = 0, st_b = 0;
   (void)st_acc;
@@ -951,7 +1008,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   __syncthreads();
   if (G_STAMPS) G_MARK(st_b);
   g_epilogue16<OUT_BF16, FN, DACT, HAS_CT, 4>(acc, 0, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, C, ldc, CT,
-                                              ldct, bias, mask, ldm, alpha, beta, colpart, N);
+                                              ldct, bias, mask, ldm, alpha, beta, colpart, N, bits);
 #if G_STAMPS
   {
     uint64_t t;
@@ -967,7 +1024,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
 template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
              int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
-             int64_t ldm, float alpha, float beta, float* colpart) {
+             int64_t ldm, float alpha, float beta, float* colpart, uint32_t* bits) {
   static bool attr = false;
   static const bool pp = !getenv_flag_off("EM_GEMM_PP");
   static const bool m16 = !getenv_flag_off("EM_GEMM_MFMA16");
@@ -998,23 +1055,23 @@ int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf
     attr = true;
   }
   hipLaunchKernelGGL(kern, grid, dim3(G_NT), G_LDS, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm,
-                     alpha, beta, colpart);
+                     alpha, beta, colpart, bits);
   return 0;
 }
 
 // runtime (out, act/dact, ct) -> one of 15 instantiations
 int g_dispatch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
                int64_t ldc, int c_bf16, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act,
-               const __bf16* mask, int64_t ldm, int dact, float alpha, float beta, float* colpart) {
+               const __bf16* mask, int64_t ldm, int dact, float alpha, float beta, float* colpart, uint32_t* bits) {
 #define EM_G(OB, FN, DA, CTV) \
   return g_launch<OB, FN, DA, CTV>(grid, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, beta, \
-                                   colpart)
+                                   colpart, bits)
   if (!c_bf16) {
-    if (act != ACT_NONE || mask || CT) return EM_ERR_ARG;
+    if (act != ACT_NONE || mask || dact || CT || bits) return EM_ERR_ARG;
     EM_G(0, ACT_NONE, 0, 0);
   }
   const bool ct = CT != nullptr;
-  if (mask) {
+  if (mask || dact) {
     if (act != ACT_NONE) return EM_ERR_ARG;
     switch (dact) {
       case ACT_RELU: if (ct) EM_G(1, ACT_RELU, 1, 1); else EM_G(1, ACT_RELU, 1, 0);
@@ -1093,12 +1150,15 @@ constexpr int K64_WEPI = 64 * K64_TS;                // 9216 B per wave
 constexpr int K64_LDS = 4 * K64_WEPI + 4 * 8 * 1024;  // T images + staged 64 x 64 mask blocks (8 KB / wave)
 static_assert(K64_LDS >= 2 * K64_BM * 64 * 2, "operand tiles must fit");
 
-template <int FN, int DACT, int HAS_CT>
+// CROW = 1: the C rows go out row-contiguous -- the transposed reads of T land in a row image in the (then
+// free) mask block, and 8 lanes store one 128-B row segment, so a store instruction covers 8 whole lines
+// instead of 16 B of 64 lines (EM_K64_CROW=0: the direct form).
+template <int FN, int DACT, int HAS_CT, int CROW>
 __global__ void __launch_bounds__(K64_NT, 4)
 gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                 __bf16* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
                 const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                float* __restrict__ colpart) {
+                float* __restrict__ colpart, uint32_t* __restrict__ bits) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1138,7 +1198,14 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   char* yb = smem + 4 * K64_WEPI + wave * 8192;  // [64 rows][64 cols] bf16, 128-B rows, 16-B chunk ^= row & 7
   const int rowb = m0 + wm * 64, colw = n0 + wn * 64;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, gq = lane >> 4;
-  if (DACT) {
+  constexpr bool WBITS = !DACT && FN == ACT_RELU;
+  uint32_t bw[2][2] = {{0u, 0u}, {0u, 0u}};  // ReLU activity words [32-row block i][column half j] (g_epilogue)
+  if (DACT && bits) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bw[i][j] = bits[(int64_t)((rowb >> 5) + i) * N + colw + 32 * j + r];
+  } else if (DACT) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // 512 chunks of 16 B: rows q >> 3, chunk q & 7
       const int q = lane + 64 * t, row = q >> 3, ch = q & 7;
@@ -1158,7 +1225,7 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
       for (int g = 0; g < 4; ++g) {
         const int lr = 32 * i + 8 * g + 4 * h;  // the lane's 4 consecutive rows lr .. lr + 3, column lc
         float y[4] = {0.f, 0.f, 0.f, 0.f};
-        if (DACT) {  // transposed read: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3
+        if (DACT && !bits) {  // transposed read: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3
           const int rr = 32 * i + 8 * g + 4 * (gq >> 1) + q4, cc = 32 * j + 16 * (gq & 1) + 4 * p4;
           const s16x4 m4 = lds_tr16(yb, (uint32_t)(rr * 128 + (((cc >> 3) ^ (rr & 7)) << 4) + (cc & 7) * 2));
 #pragma unroll
@@ -1168,21 +1235,47 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float v = alpha * acc[i][j][4 * g + e];
-          v = DACT ? v * g_dfn<FN>(y[e]) : g_fn<FN>(v + bv);
+          if (DACT) {
+            v = bits ? bit_mul(bw[i][j], 8 * g + 4 * h + e, v) : v * g_dfn<FN>(y[e]);
+          } else {
+            v = g_fn<FN>(v + bv);
+            if (WBITS) bw[i][j] |= (v > 0.f ? 1u : 0u) << (8 * g + e);
+          }
           x[e] = v;
           cs[j] += v;
         }
         *reinterpret_cast<u32x2*>(tb + lc * K64_TS + lr * 2) = u32x2{pack2(x[0], x[1]), pack2(x[2], x[3])};
       }
   }
+  if (WBITS && bits) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t w = or_xhalf(bw[i][j] << (4 * h));
+        if (h == 0) bits[(int64_t)((rowb >> 5) + i) * N + colw + 32 * j + r] = w;
+      }
+  }
   wave_lds_sync();
-  // C rows: per iteration a 16-lane group writes 16 rows x 8 columns (one 16-B store per lane)
+  // C rows: per iteration a 16-lane group reads 16 rows x 8 columns (one 16-B piece per lane)
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
-    const int cb = 8 * it, r0 = 16 * gq;
+    const int cb = 8 * it, r0 = 16 * gq, row = r0 + i16;
     const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * K64_TS + (r0 + 4 * p4) * 2));
     const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * K64_TS + (r0 + 4 * p4) * 2));
-    *reinterpret_cast<bf16x8*>(C + (int64_t)(rowb + r0 + i16) * ldc + colw + cb) = cat_tr(lo, hi);
+    if (CROW)  // row image [64 rows][128 B], 16-B chunk c of row at c ^ (row & 7)
+      *reinterpret_cast<bf16x8*>(yb + row * 128 + ((it ^ (row & 7)) << 4)) = cat_tr(lo, hi);
+    else
+      *reinterpret_cast<bf16x8*>(C + (int64_t)(rowb + row) * ldc + colw + cb) = cat_tr(lo, hi);
+  }
+  if (CROW) {
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = lane + 64 * k, row = q >> 3, ch = q & 7;
+      *reinterpret_cast<u32x4*>(C + (int64_t)(rowb + row) * ldc + colw + ch * 8) =
+          *reinterpret_cast<const u32x4*>(yb + row * 128 + ((ch ^ (row & 7)) << 4));
+    }
   }
   if (HAS_CT) {  // C^T row = one column of the block: 64 rows = 128 B straight from T
 #pragma unroll
@@ -1210,29 +1303,33 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   }
 }
 
-template <int FN, int DACT, int HAS_CT>
+template <int FN, int DACT, int HAS_CT, int CROW>
 int k64_launch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
                __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask, int64_t ldm,
-               float alpha, float* colpart) {
+               float alpha, float* colpart, uint32_t* bits) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_k64_kernel<FN, DACT, HAS_CT>,
+    (void)hipFuncSetAttribute((const void*)gemm_k64_kernel<FN, DACT, HAS_CT, CROW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, K64_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), K64_LDS, st,
-                     A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart);
+  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT, CROW>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), K64_LDS, st,
+                     A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits);
   return 0;
 }
 
 // runtime (act / dact, ct) -> instantiation; bf16 output only
 int k64_dispatch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
                  __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act, const __bf16* mask,
-                 int64_t ldm, int dact, float alpha, float* colpart) {
-#define EM_K(FN, DA, CTV) \
-  return k64_launch<FN, DA, CTV>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart)
+                 int64_t ldm, int dact, float alpha, float* colpart, uint32_t* bits) {
+  static const bool crow = !getenv_flag_off("EM_K64_CROW");
+#define EM_K(FN, DA, CTV)                                                                                             \
+  return crow ? k64_launch<FN, DA, CTV, 1>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha,      \
+                                           colpart, bits)                                                              \
+              : k64_launch<FN, DA, CTV, 0>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha,      \
+                                           colpart, bits)
   const bool ct = CT != nullptr;
-  if (mask) {
+  if (mask || dact) {
     if (act != ACT_NONE) return EM_ERR_ARG;
     switch (dact) {
       case ACT_RELU: if (ct) EM_K(ACT_RELU, 1, 1); else EM_K(ACT_RELU, 1, 0);
@@ -1465,7 +1562,7 @@ wgrad_skinny_reduce_kernel(const float* __restrict__ part, int S, int J, int W, 
 static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                      int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
                      int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, int splits, int kstep,
-                     int64_t c_split, hipStream_t stream, float* colpart = nullptr);
+                     int64_t c_split, hipStream_t stream, float* colpart = nullptr, uint32_t* bits = nullptr);
 
 EM_API int em_gemm_bf16(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                         int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
@@ -1486,6 +1583,19 @@ EM_API int em_gemm_bf16_cs(const void* A, int64_t lda, int a_kc, const void* B, 
                    ldct, 1, K, 0, stream, colpart);
 }
 
+// The general form: optional column partials (as em_gemm_bf16_cs) and ReLU activity bits (uint32
+// [M / 32][N], bit m & 31 of word (m >> 5) * N + n = output[m][n] > 0): written when act is relu,
+// read in place of the saved activation when dact is relu and mask is null (64x less traffic than
+// the bf16 activation).
+EM_API int em_gemm_bf16_ex(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
+                           int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
+                           int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, float* colpart,
+                           uint32_t* bits, hipStream_t stream) {
+  if ((uintptr_t)colpart & 3) return EM_ERR_ARG;
+  return gemm_impl(A, lda, a_kc, B, ldb, b_kc, C, ldc, c_bf16, M, N, K, bias, act, mask, ldm, dact, alpha, beta, ct,
+                   ldct, 1, K, 0, stream, colpart, bits);
+}
+
 // Split-K on the any-layout kernel: `splits` slices of `kstep` (multiple of 64) along K, slice s writing
 // C + s * c_split (elements).  For small outputs with a huge reduction (64 x 8192 over a 64k batch).
 EM_API int em_gemm_bf16_splitk(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
@@ -1500,9 +1610,17 @@ EM_API int em_gemm_bf16_splitk(const void* A, int64_t lda, int a_kc, const void*
 static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb, int b_kc, void* C,
                      int64_t ldc, int c_bf16, int M, int N, int K, const float* bias, int act, const void* mask,
                      int64_t ldm, int dact, float alpha, float beta, void* ct, int64_t ldct, int splits, int kstep,
-                     int64_t c_split, hipStream_t stream, float* colpart) {
+                     int64_t c_split, hipStream_t stream, float* colpart, uint32_t* bits) {
   if (!A || !B || !C || M < 0 || N < 0 || K < 0 || act < 0 || act > 3) return EM_ERR_ARG;
   if (mask && (dact < 1 || dact > 3)) return EM_ERR_ARG;
+  // ReLU activity bits (see relu_bits_*): written by a bf16 forward with act relu, read instead of the
+  // saved activation by a relu dgrad; 256-tile / skinny-K paths only, M a multiple of 32
+  if (bits) {
+    const bool wr = act == ACT_RELU && !mask && dact == 0, rd = act == ACT_NONE && !mask && dact == ACT_RELU;
+    if (!(wr || rd) || !c_bf16 || (M & 31) || ((uintptr_t)bits & 3)) return EM_ERR_ARG;
+  } else if (dact && !mask) {
+    return EM_ERR_ARG;
+  }
   if (M == 0 || N == 0) return 0;
   // 16-byte vector loads need 8-element-aligned leading dimensions and base pointers
   if ((lda & 7) || (ldb & 7) || (((uintptr_t)A) & 15) || (((uintptr_t)B) & 15)) return EM_ERR_ARG;
@@ -1522,7 +1640,7 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
   static const bool k64_on = !getenv_flag_off("EM_GEMM_K64");
   if (big && k64_on && c_bf16 && (K == 64 || K == 128) && beta == 0.f) {
     const int rc = k64_dispatch(stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, (__bf16*)C, ldc, (__bf16*)ct,
-                                ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha, colpart);
+                                ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha, colpart, bits);
     if (rc) return rc;
     EM_CHECK_LAUNCH();
     return 0;
@@ -1530,12 +1648,12 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
   if (big) {
     const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
                               ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
-                              beta, colpart);
+                              beta, colpart, bits);
     if (rc) return rc;
     EM_CHECK_LAUNCH();
     return 0;
   }
-  if (ct || colpart) return EM_ERR_ARG;  // the transposed copy / column partials: 256 path only
+  if (ct || colpart || bits) return EM_ERR_ARG;  // transposed copy / column partials / bits: 256 path only
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const __bf16* a = (const __bf16*)A;
   const __bf16* b = (const __bf16*)B;

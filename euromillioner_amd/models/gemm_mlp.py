@@ -152,6 +152,14 @@ class GemmMLPTrainer:
         big_dgrad = [i > 0 and LIN.big_ok(B, P[i], P[i + 1]) for i in range(L)]
         return {"wgrad": big_wgrad, "dgrad": big_dgrad}
 
+    def _use_bits(self, plan: dict, B: int, i: int) -> bool:
+        """X_i's act' as activity bits: relu, both GEMMs on the 256-tile paths (EUROM_RELU_BITS=0: off)."""
+        import os
+
+        P = self.padded
+        return (self.activation == "relu" and plan["dgrad"][i] and B % 32 == 0
+                and LIN.big_ok(B, P[i], P[i - 1]) and os.environ.get("EUROM_RELU_BITS", "1") != "0")
+
     def _ws(self, B: int) -> dict:
         ws = self._ws_cache.get(B)
         if ws is None and self.f32:
@@ -188,7 +196,10 @@ class GemmMLPTrainer:
                   "dzt": {i: torch.empty(P[i + 1], B, dtype=torch.bfloat16, device=dev)
                           for i in range(L) if plan["wgrad"][i]},
                   "wt": {i: torch.empty(P[i], P[i + 1], dtype=torch.bfloat16, device=dev)
-                         for i in range(L) if plan["dgrad"][i]}}
+                         for i in range(L) if plan["dgrad"][i]},
+                  # relu activity bits of X_i (written by layer i - 1's forward, read by layer i's dgrad
+                  # instead of the bf16 X_i: 64x fewer bytes in the act' epilogue)
+                  "bits": {i: LIN.relu_bits(B, P[i], dev) for i in range(1, L) if self._use_bits(plan, B, i)}}
             self._ws_cache = {B: ws}  # keep one batch size resident
         return ws
 
@@ -229,7 +240,8 @@ class GemmMLPTrainer:
             last = i == L - 1
             out = ws["logits"] if last else ws["act"][i]
             ct = ws["actt"].get(i + 1) if train and not last else None  # X_{i+1}^T for layer i+1's wgrad
-            h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out, ct=ct)
+            bits = ws["bits"].get(i + 1) if train and not last else None
+            h = LIN.linear_fwd(h, w, bf, "none" if last else self.activation, out=out, ct=ct, bits=bits)
         return h, inputs
 
     def wgrad_panels(self, i: int) -> list[tuple[int, int]]:
@@ -300,7 +312,7 @@ class GemmMLPTrainer:
                     # sums of dZ_{i-1} (fp32, before the bf16 store), then one fixed-order reduce
                     part = ws["colpart"] if B % 128 == 0 else None
                     dz = LIN.linear_dgrad_nt(dz, wt, inputs[i], self.activation, out=ws["dz"][i - 1],
-                                             ct=ws["dzt"].get(i - 1), colpart=part)
+                                             ct=ws["dzt"].get(i - 1), colpart=part, bits=ws["bits"].get(i))
                     if part is not None:
                         _, gb_prev = self._views(self.grads, i - 1)
                         LIN.colpart_reduce(part, B // 128, self.padded[i], gb_prev, accumulate=accumulate)

@@ -34,6 +34,9 @@ N.register_signatures({
     "em_gemm_bf16_cs": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64,
                                  N._i32, N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32,
                                  N._f32, N._f32, N._c_void_p, N._i64, N._c_void_p, N._c_void_p]),
+    "em_gemm_bf16_ex": (N._i32, [N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64, N._i32, N._c_void_p, N._i64,
+                                 N._i32, N._i32, N._i32, N._i32, N._c_void_p, N._i32, N._c_void_p, N._i64, N._i32,
+                                 N._f32, N._f32, N._c_void_p, N._i64, N._c_void_p, N._c_void_p, N._c_void_p]),
     "em_colpart_reduce": (N._i32, [N._c_void_p, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p]),
     "em_colsum_ws_floats": (N._i32, [N._i32, N._i32]),
     "em_colsum_bf16": (N._i32, [N._c_void_p, N._i64, N._i32, N._i32, N._c_void_p, N._i32, N._f32, N._c_void_p,
@@ -71,6 +74,14 @@ def empty_aligned(r: int, c: int, dtype: torch.dtype, device) -> torch.Tensor:
 BIG_M, BIG_N, BIG_K = 256, 256, 64
 
 
+def relu_bits(M: int, N_: int, device) -> torch.Tensor:
+    """Buffer for the ReLU activity bits of an [M, N] activation (``gemm(bits=...)``): int32 [M / 32, N],
+    bit m % 32 of word [m // 32, n] is ``act[m, n] > 0``."""
+    if M % 32:
+        raise ValueError("relu bits need M % 32 == 0")
+    return torch.empty(M // 32, N_, dtype=torch.int32, device=device)
+
+
 def big_ok(M: int, N_: int, K: int) -> bool:
     """Shapes the 256x256 NT kernel takes (otherwise the 128x128 any-layout kernel runs)."""
     return M % BIG_M == 0 and N_ % BIG_N == 0 and K % BIG_K == 0 and K > 0
@@ -79,11 +90,13 @@ def big_ok(M: int, N_: int, K: int) -> bool:
 def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Tensor, M: int, N_: int, K: int,
          bias: torch.Tensor | None = None, act: str = "none", dact_src: torch.Tensor | None = None,
          dact: str = "relu", alpha: float = 1.0, beta: float = 0.0, ct: torch.Tensor | None = None,
-         colpart: torch.Tensor | None = None) -> torch.Tensor:
+         colpart: torch.Tensor | None = None, bits: torch.Tensor | None = None) -> torch.Tensor:
     """Raw K1-K3 launch.  ``a``/``b`` are bf16 in their storage shape; ``out`` fp32 or bf16 [M, N].
     ``ct`` (bf16 [N, M], 256-path only) receives a transposed copy of the output.
     ``colpart`` (fp32, >= M / 128 * N, 256-path only) receives the epilogue's column sums per 128 output
-    rows (the fused bias gradient of a dgrad: ``colpart_reduce`` sums them)."""
+    rows (the fused bias gradient of a dgrad: ``colpart_reduce`` sums them).
+    ``bits`` (:func:`relu_bits`, 256 path only): written by a bf16 forward with ``act="relu"``; read as
+    act' by a ``dact="relu"`` dgrad given no ``dact_src`` (1 bit per element instead of the bf16 activation)."""
     for t, nm in ((a, "a"), (b, "b")):
         N.check_cuda(t, nm, torch.bfloat16, contiguous=False)
         if not is_aligned(t):
@@ -105,6 +118,14 @@ def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Te
         if tuple(dact_src.shape) != (M, N_) or dact_src.stride(1) != 1:
             raise ValueError("dact_src must be bf16 [M, N] with unit column stride")
         ldm = dact_src.stride(0)
+    read_bits = bits is not None and dact_src is None and dact == "relu" and act in ("none", "identity")
+    if bits is not None:
+        N.check_cuda(bits, "bits", torch.int32)
+        if not (read_bits or (act == "relu" and dact_src is None)):
+            raise ValueError("bits: written by act='relu' or read by dact='relu' without dact_src")
+        if (out.dtype != torch.bfloat16 or not (a_kc and b_kc and big_ok(M, N_, K))
+                or tuple(bits.shape) != (M // 32, N_)):
+            raise ValueError("bits need the 256-tile NT path, a bf16 output and an int32 [M / 32, N] buffer")
     if ct is not None:
         N.check_cuda(ct, "ct", torch.bfloat16, contiguous=False)
         if not (a_kc and b_kc and big_ok(M, N_, K)) or tuple(ct.shape) != (N_, M) or not is_aligned(ct):
@@ -112,12 +133,17 @@ def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Te
     args = (a.data_ptr(), a.stride(0), int(a_kc), b.data_ptr(), b.stride(0), int(b_kc),
             out.data_ptr(), out.stride(0), int(out.dtype == torch.bfloat16), M, N_, K,
             bias.data_ptr() if bias is not None else None, ACTS[act],
-            dact_src.data_ptr() if dact_src is not None else None, ldm, ACTS[dact] if dact_src is not None else 0,
+            dact_src.data_ptr() if dact_src is not None else None, ldm,
+            ACTS[dact] if (dact_src is not None or read_bits) else 0,
             float(alpha), float(beta), ct.data_ptr() if ct is not None else None, ct.stride(0) if ct is not None else 0)
     if colpart is not None:
         N.check_cuda(colpart, "colpart", torch.float32)
         if not (a_kc and b_kc and big_ok(M, N_, K)) or colpart.numel() < (M // 128) * N_:
             raise ValueError("colpart needs the 256-tile NT path and M / 128 * N floats")
+    if bits is not None:
+        N.call("em_gemm_bf16_ex", *args, colpart.data_ptr() if colpart is not None else None, bits.data_ptr(),
+               N.stream_handle(out.device))
+    elif colpart is not None:
         N.call("em_gemm_bf16_cs", *args, colpart.data_ptr(), N.stream_handle(out.device))
     else:
         N.call("em_gemm_bf16", *args, N.stream_handle(out.device))
@@ -152,27 +178,31 @@ def transpose(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, act: str = "none",
                out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None,
-               ct: torch.Tensor | None = None) -> torch.Tensor:
-    """``act(x @ w.T + bias)``; x bf16 [M, K], w bf16 [N, K] (nn.Linear layout); ``ct`` gets the output^T."""
+               ct: torch.Tensor | None = None, bits: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(x @ w.T + bias)``; x bf16 [M, K], w bf16 [N, K] (nn.Linear layout); ``ct`` gets the output^T,
+    ``bits`` (relu) its activity bits."""
     M, K = x.shape
     N_ = w.shape[0]
     if out is None:
         out = empty_aligned(M, N_, out_dtype, x.device)
-    return gemm(x, True, w, True, out, M, N_, K, bias=bias, act=act, ct=ct)
+    return gemm(x, True, w, True, out, M, N_, K, bias=bias, act=act, ct=ct, bits=bits)
 
 
 def linear_dgrad_nt(dz: torch.Tensor, wt: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",
                     out: torch.Tensor | None = None, ct: torch.Tensor | None = None,
-                    colpart: torch.Tensor | None = None) -> torch.Tensor:
+                    colpart: torch.Tensor | None = None, bits: torch.Tensor | None = None) -> torch.Tensor:
     """dgrad from a transposed weight copy ``wt`` [K, N] (256-tile NT path): ``(dz @ wt.T) * act'(y_prev)``;
-    ``colpart`` gets the bias-gradient partials of the result (see :func:`gemm`)."""
+    ``colpart`` gets the bias-gradient partials of the result (see :func:`gemm`).  With ``bits`` (relu, from
+    the forward that wrote y_prev) act' comes from the activity bits and y_prev is not read."""
     M, N_ = dz.shape
     K = wt.shape[0]
     if out is None:
         out = empty_aligned(M, K, torch.bfloat16, dz.device)
     if dact in ("none", "identity"):
+        y_prev = bits = None
+    if bits is not None:
         y_prev = None
-    return gemm(dz, True, wt, True, out, M, K, N_, dact_src=y_prev, dact=dact, ct=ct, colpart=colpart)
+    return gemm(dz, True, wt, True, out, M, K, N_, dact_src=y_prev, dact=dact, ct=ct, colpart=colpart, bits=bits)
 
 
 def linear_wgrad_nt(dzt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None,

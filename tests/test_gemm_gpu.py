@@ -282,6 +282,46 @@ def test_dgrad_fused_bias_partials(dact, K):
     assert torch.allclose(db2, 2 * db, rtol=1e-6, atol=1e-6)
 
 
+def _pack_bits(y: torch.Tensor) -> torch.Tensor:
+    """(y > 0) packed as the kernels' activity bits: int32 [M / 32, N], bit k of word [r, n] = y[32r + k, n] > 0."""
+    M, N = y.shape
+    pos = (y.float() > 0).long().view(M // 32, 32, N)
+    words = (pos << torch.arange(32, device=y.device).view(1, 32, 1)).sum(1)
+    return torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 512, 64), (512, 768, 320), (1024, 256, 128)])
+def test_relu_bits_forward_and_dgrad(M, N, K):
+    """ReLU activity bits: the forward epilogue writes (y > 0) packed 32 rows per word next to an unchanged
+    bf16 output (K = 64 / 128: skinny-K kernel, else the 256 tile), and a relu dgrad reading the bits is
+    bit-identical (output, C^T, bias partials) to the one reading the bf16 activation, on both the skinny-K
+    (reduction 64) and the 256-tile (reduction 256) dgrad."""
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    bits = LIN.relu_bits(M, N, "cuda").fill_(0x5A5A5A5A)
+    y = LIN.linear_fwd(x, w, b, "relu", torch.bfloat16, bits=bits)
+    assert torch.equal(y, LIN.linear_fwd(x, w, b, "relu", torch.bfloat16))
+    assert torch.equal(bits, _pack_bits(y))
+    assert 0.3 < (y > 0).float().mean().item() < 0.7
+    for R in (64, 256):
+        dz = torch.randn(M, R, device="cuda", generator=g).bfloat16()
+        wt = LIN.transpose((torch.randn(R, N, device="cuda", generator=g) / R ** 0.5).bfloat16())
+        outs = []
+        for use_bits in (False, True):
+            ct = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
+            part = torch.full(((M // 128) * N,), float("nan"), device="cuda")
+            o = LIN.linear_dgrad_nt(dz, wt, y, "relu", ct=ct, colpart=part, bits=bits if use_bits else None)
+            outs.append((o, ct, part))
+        for a, c in zip(*outs):
+            assert torch.equal(a, c)
+    with pytest.raises(ValueError):
+        LIN.linear_fwd(x, w, b, "tanh", torch.bfloat16, bits=bits)
+
+
 def test_wgrad_split_k_and_colsum_big_batch():
     from euromillioner_amd.ops import linear as LIN
 
