@@ -44,7 +44,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 class _TorchBaseline:
-    """Same model/loss/optimizer in plain PyTorch (bf16 autocast GEMMs via hipBLASLt) — comparison only."""
+    """Same model/loss/optimizer in plain PyTorch (bf16 autocast or fp32 GEMMs via hipBLASLt) — comparison only."""
 
     def __init__(self, dev, a, draws, B, group):
         from euromillioner_amd.models.mlp import DrawMLP
@@ -57,13 +57,14 @@ class _TorchBaseline:
         self.y = torch.empty(B, 64, dtype=torch.bfloat16, device=dev)
         self.loss_out = torch.zeros(1, device=dev)
         self.grad_io = torch.zeros(1, device=dev)
+        self.bf16 = a.dtype == "bf16"  # fp32: plain fp32 GEMMs
 
     def step(self, off):
         FM = self.FM
         FM.onehot(self.draws, self.B, offset=off, which=0, out=self.x)
         FM.onehot(self.draws, self.B, offset=off, which=1, out=self.y)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            z = self.net(self.x[:, :62])
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.bf16):
+            z = self.net(self.x[:, :62].float())
         loss = self.net.loss(z.float(), self.y[:, :62])
         self.opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -114,14 +115,16 @@ def _parse():
                          "time has passed (the chip ramps its clock over the first ~100 ms of load; a training "
                          "run spends its life at the steady clock).  0 = exactly W warmup steps")
     ap.add_argument("--no-eval", action="store_true")
-    ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
-                    help="fused = our HIP kernels (headline); torch = plain PyTorch/hipBLASLt eager (comparison)")
+    ap.add_argument("--impl", default="fused", choices=["fused", "gemm", "torch"],
+                    help="fused = our HIP kernels (headline: the fused train kernel for --model mlp, the GEMM engine "
+                         "for mlp-wide); gemm = the per-layer GEMM engine for --model mlp too; torch = plain "
+                         "PyTorch/hipBLASLt eager (comparison)")
     ap.add_argument("--model", default="mlp", choices=["mlp", "mlp-wide"],
                     help="mlp = 62->128->62 (headline, fused kernel); mlp-wide = 62->8192->8192->62 (GEMM path)")
     ap.add_argument("--hidden", default=None, help="GEMM-path hidden sizes, e.g. 8192,8192")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                    help="compute dtype: bf16 (headline: fused kernel / bf16 GEMM engine) or fp32 (the exact-fp32 "
-                         "MFMA GEMM engine, csrc/gemm_f32.hip, for either model)")
+                    help="compute dtype: bf16 (headline) or fp32 (exact fp32 MFMA: the fused fp32 train kernel "
+                         "csrc/mlp_fused_f32.hip for --model mlp, the fp32 GEMM engine csrc/gemm_f32.hip otherwise)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks sharing one GPU)")
     ap.add_argument("--device-data-gb", type=float, default=0.0,
@@ -229,7 +232,8 @@ def main():
         a.graph = 0  # per-step offsets walk the whole training shard
 
     B = a.batch
-    if a.accum < 1 or (a.accum > 1 and a.model != "mlp-wide" and a.dtype != "fp32"):
+    gemm_engine = a.model == "mlp-wide" or a.impl == "gemm"
+    if a.accum < 1 or (a.accum > 1 and not gemm_engine):
         raise SystemExit("--accum applies to --model mlp-wide (the fused kernel takes any batch directly)")
     BS = B * a.accum  # samples per GPU per optimizer step
     n_train = sh.train[1] - sh.train[0]
@@ -243,7 +247,7 @@ def main():
     def boff(i):
         return tr_skip + ((i * spread) % n_off) * BS
     sizes = (62, 128, 62)
-    if a.model == "mlp-wide" or a.dtype == "fp32":
+    if gemm_engine:
         from euromillioner_amd.models.gemm_mlp import GemmMLPTrainer
 
         hidden = tuple(int(h) for h in (a.hidden or ("8192,8192" if a.model == "mlp-wide" else "128")).split(","))
@@ -255,7 +259,8 @@ def main():
         def step(i):
             return model.step(draws, B, offset=boff(i), accum=a.accum)
     elif a.impl == "fused":
-        model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group, comm=a.comm)
+        model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group, comm=a.comm,
+                              dtype=a.dtype)
         model.broadcast_parameters()
 
         def step(i):
@@ -375,7 +380,7 @@ def main():
     desc = "mlp " + "->".join(str(x) for x in sizes) + " relu, " + (
         "grouped softmax-CE" if a.loss == "softmax" else "sigmoid-BCE")
     extra = {}
-    if a.model == "mlp-wide" or a.dtype == "fp32":
+    if gemm_engine:
         tf = model.flops_per_sample() * BS / (ms / 1000.0) / 1e12
         extra = {"tflops_per_gpu": tf, "flops_per_sample": model.flops_per_sample()}
         if a.accum > 1:
@@ -403,8 +408,8 @@ def main():
             "config": {"model": desc,
                        "global_batch": BS * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
-                       "engine": ("gemm_f32" if a.dtype == "fp32" else "gemm" if a.model == "mlp-wide"
-                                  else a.impl),
+                       "engine": (("gemm_f32" if a.dtype == "fp32" else "gemm") if gemm_engine
+                                  else a.impl + ("_f32" if a.dtype == "fp32" else "")),
                        "graph_steps": C if use_graph else 0,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
                        **({"comm_dtype": a.comm_dtype, "bucket_mb": a.bucket_mb} if a.model == "mlp-wide" else {}),

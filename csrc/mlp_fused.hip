@@ -35,6 +35,7 @@
 
 #include "common.h"
 #include "mlp_adam.h"
+#include "mlp_loss.h"
 
 namespace {
 using mlp::IN, mlp::HID, mlp::OUT, mlp::P_W1, mlp::P_W2, mlp::P_B2, mlp::P_TOTAL;
@@ -67,9 +68,6 @@ EM_DEVICE bf16x8 lut_frag(const char* lut, uint64_t m, int q, int h) {
 EM_DEVICE uint32_t w1t_off(int row, int k8) { return IMG_W1T + row * W1T_RS + k8 * 16; }
 EM_DEVICE uint32_t w2p_off(int row, int k16) { return IMG_W2P + row * W2P_RS + k16 * 16; }
 EM_DEVICE uint32_t w2q_off(int row, int k8) { return IMG_W2Q + row * W2Q_RS + k8 * 16; }
-
-// o(u,i,h) = 32u + (i&3) + 8(i>>2) + 4h : output index held in register i of Z2ᵀ tile u
-EM_DEVICE constexpr int oo0(int i) { return (i & 3) + 8 * (i >> 2); }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -187,45 +185,6 @@ EM_DEVICE bf16x8 nib_xfrag(const char* smem, uint32_t w, int q) {
   return __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
 }
 
-// class of output o = 32 u + oo0(i) + 4h: 0 main, 1 star, 2 pad
-EM_DEVICE constexpr int out_cls(int u, int i, int h) {
-  return 32 * u + oo0(i) + 4 * h < 50 ? 0 : (32 * u + oo0(i) + 4 * h < 62 ? 1 : 2);
-}
-
-// Sigmoid-BCE loss + dZ2 of a whole 32-sample tile in ONE wave: the lane's 32 logits z2[u][i] (output
-// 32u + oo0(i) + 4h of sample r; lanes r and r + 32 share the sample).  Targets as {0,1} floats from
-// a 16-entry nibble table (YL): register group g of tile u holds outputs 32u + 8g + 4h .. +3 = one
-// nibble of the target mask.
-template <int YL>
-EM_DEVICE void bce_tile_loss(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, bool valid, int h,
-                             float (&dz)[2][16], float& loss_acc) {
-  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
-  float l = 0.f;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    float yb[16];
-    const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
-      yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = out_cls(u, i, h);
-      const float v = z2[u][i], y = yb[i];
-      const float en = __builtin_amdgcn_exp2f(-fabsf(v) * L2E);  // stable sigmoid / softplus
-      const float rp = __builtin_amdgcn_rcpf(1.f + en);
-      const float pr = v >= 0.f ? rp : en * rp;
-      const float sp = fmaxf(v, 0.f) + __builtin_amdgcn_logf(1.f + en) * LN2;
-      const bool okc = valid && c != 2;
-      dz[u][i] = okc ? (pr - y) : 0.f;
-      l += okc ? (sp - y * v) : 0.f;
-    }
-  }
-  loss_acc += l;
-}
-
 // ============================================================================================
 // v6: producer/consumer units -- forward waves feed backward waves through an LDS ring.
 //
@@ -298,169 +257,6 @@ EM_DEVICE int v6_unit_id(int unit) { return blockIdx.x * 2 + unit; }
 EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
   const int ntiles = (B + 31) / 32;
   return U < ntiles ? (ntiles - U + nunits - 1) / nunits : 0;
-}
-
-// Grouped softmax-CE of a whole tile in ONE wave (v6 forward), main-group statistics split per
-// output tile and merged online (flash-softmax style): tile 0's max / exp / sums need only Z2 tile
-// 0, so they run on the VALU while tile 1's F2 chain is still in the matrix pipe (the caller's hook
-// issues step(j) between tile 1's MFMAs; in-order issue overlaps only VALU that sits between MFMAs
-// in program order).  dZ2 of tile u carries its tile's rescale a_u = exp(m_u - M).
-// The class of the lane's element i of output tile u (main / star / pad) is a compile-time
-// constant except for 4 elements of tile 1 whose class depends on the lane half h (outputs 48-51
-// and 58-63 straddle the group edges), so every statically classified element emits only its own
-// group's ops (a select-form "x ? v : 0" fed into an fma would have to be kept: fma(0, inf, a) is
-// NaN).  Max / sum / target-dot reductions run as independent partial chains.
-// Packed fp32 pairs: the accumulator registers (i, i + 1), i even, are an aligned VGPR pair, so the
-// exp argument, the exp sums and the target dot of two outputs issue as ONE v_pk_fma_f32 / v_pk_add_f32
-// (full rate on the 2-wide packed path).  Elements (i, i + 1) of a tile share their class for both h
-// (out_cls), except where noted below.  38 fewer VALU per forward tile (494 -> 456); the same-box A/B
-// was within noise (89.4 vs 89.5 us, profiles/r3/ab_packed_softmax.jsonl): the forward wave's tile is
-// bound by its dependency chain, not by issue.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-EM_DEVICE f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-template <int YL, typename Hook>
-EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
-                                float& loss_acc, Hook&& hook) {
-  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
-  const f32x2 L2E2 = {L2E, L2E};
-  auto targets = [&](int u, float (&yb)[16]) {
-    const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
-      yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
-    }
-  };
-  auto zpair = [&](int u, int i) { return f32x2{z2[u][i], z2[u][i + 1]}; };
-  auto exp2 = [](f32x2 t) { return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)}; };
-  const bool h0 = h == 0;
-  const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
-  const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
-  const int ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
-  const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
-  const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
-  // target dots: tm[q] holds elements with (i & 3) >> 1 == q (x: even i, y: odd i), ts by i & 1
-  f32x2 tm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, ts = {0.f, 0.f};
-  // ---- tile 0: outputs 0..31, all main.  step(j), j = 0..7, is issued between tile 1's F2 MFMAs by
-  // the caller (hook): in-order issue lets the VALU run only between MFMAs in program order ----
-  float m0 = 0.f, s0 = 0.f;
-  f32x2 nL2 = {0.f, 0.f};
-  float mm0[4], yb0[16];
-  f32x2 sm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
-  auto step = [&](int j) {
-    if (j == 0) {
-      mm0[0] = z2[0][0]; mm0[1] = z2[0][1]; mm0[2] = z2[0][2]; mm0[3] = z2[0][3];
-#pragma unroll
-      for (int i = 4; i < 16; ++i) mm0[i & 3] = fmaxf(mm0[i & 3], z2[0][i]);
-      targets(0, yb0);
-    } else if (j == 1) {
-      m0 = xhalf_max(fmaxf(fmaxf(mm0[0], mm0[1]), fmaxf(mm0[2], mm0[3])));
-      nL2 = f32x2{-m0 * L2E, -m0 * L2E};
-    } else if (j < 6) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int i = 4 * (j - 2) + 2 * q;
-        const f32x2 zz = zpair(0, i);
-        const f32x2 e = exp2(pfma(zz, L2E2, nL2));
-        sm[q] += e;
-        tm[q] = pfma(f32x2{yb0[i], yb0[i + 1]}, zz, tm[q]);
-        dz[0][i] = e.x;
-        dz[0][i + 1] = e.y;
-      }
-    } else if (j == 6) {
-      s0 = xhalf_sum((sm[0].x + sm[0].y) + (sm[1].x + sm[1].y));
-    }
-  };
-  hook(step);
-  // ---- tile 1: outputs 32..63 (main 32..49, star 50..61, pad 62/63) ----
-  float mm[2] = {-3.0e38f, -3.0e38f}, ms[2] = {-3.0e38f, -3.0e38f};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
-    const float v = z2[1][i];
-    if (c0 == c1) {
-      if (c0 == 0) mm[i & 1] = fmaxf(mm[i & 1], v);
-      if (c0 == 1) ms[i & 1] = fmaxf(ms[i & 1], v);
-    } else if (c0 == 0) {  // main (h = 0) / star (h = 1)
-      mm[i & 1] = h0 ? fmaxf(mm[i & 1], v) : mm[i & 1];
-      ms[i & 1] = h0 ? ms[i & 1] : fmaxf(ms[i & 1], v);
-    } else {  // star (h = 0) / pad (h = 1)
-      ms[i & 1] = h0 ? fmaxf(ms[i & 1], v) : ms[i & 1];
-    }
-  }
-  const float m1 = xhalf_max(fmaxf(mm[0], mm[1]));
-  const float mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
-  const float nmL = -m1 * L2E, nsL = -mx_s * L2E;
-  const f32x2 nmL2 = {nmL, nmL}, nsL2 = {nsL, nsL};
-  f32x2 s1p = {0.f, 0.f}, ss = {0.f, 0.f};
-  float yb1[16];
-  targets(1, yb1);
-  {
-    float (&yb)[16] = yb1;
-#pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
-      static_assert(out_cls(1, 9, 0) == out_cls(1, 8, 0) && out_cls(1, 15, 1) == out_cls(1, 14, 1), "pair classes");
-      const f32x2 zz = zpair(1, i), yy = {yb[i], yb[i + 1]};
-      f32x2 e;
-      if (c0 == c1 && c0 == 0) {
-        e = exp2(pfma(zz, L2E2, nmL2));
-        s1p += e;
-        tm[(i & 3) >> 1] = pfma(yy, zz, tm[(i & 3) >> 1]);
-      } else if (c0 == c1 && c0 == 1) {
-        e = exp2(pfma(zz, L2E2, nsL2));
-        ss += e;
-        ts = pfma(yy, zz, ts);
-      } else if (c0 == 0) {  // main (h = 0) / star (h = 1): outputs 48/49 | 52/53
-        e = exp2(pfma(zz, L2E2, h0 ? nmL2 : nsL2));
-        const f32x2 ty = yy * zz;
-        s1p = h0 ? s1p + e : s1p;
-        ss = h0 ? ss : ss + e;
-        tm[(i & 3) >> 1] = h0 ? tm[(i & 3) >> 1] + ty : tm[(i & 3) >> 1];
-        ts = h0 ? ts : ts + ty;
-      } else {  // star (h = 0) / pad (h = 1): outputs 58/59 | 62/63
-        const f32x2 ex = exp2(pfma(zz, L2E2, nsL2));
-        e = h0 ? ex : f32x2{0.f, 0.f};
-        ss += e;
-        ts = h0 ? pfma(yy, zz, ts) : ts;
-      }
-      dz[1][i] = e.x;
-      dz[1][i + 1] = e.y;
-    }
-  }
-  const float s1 = xhalf_sum(s1p.x + s1p.y), s_s = xhalf_sum(ss.x + ss.y);
-  // ---- online merge of the main group: M = max(m0, m1), S = a0 s0 + a1 s1 ----
-  const float M = fmaxf(m0, m1);
-  const float a0 = __builtin_amdgcn_exp2f((m0 - M) * L2E), a1 = __builtin_amdgcn_exp2f((m1 - M) * L2E);
-  const float S = __builtin_fmaf(a0, s0, a1 * s1);
-  const float rS = nm ? __builtin_amdgcn_rcpf(S) : 0.f;
-  const float f0 = a0 * rS, f1 = a1 * rS, f_s = ns ? __builtin_amdgcn_rcpf(s_s) : 0.f;
-  const float ni_m = -inv_m, ni_s = -inv_s;
-  // (written per element: the compiler pairs these into v_pk_mul_f32 + v_pk_fma_f32 by itself, and the
-  // explicit f32x2 form compiled to 8 more VALU)
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const float (&yb)[16] = u == 0 ? yb0 : yb1;  // the targets, read once per tile
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c0 = out_cls(u, i, 0), c1 = out_cls(u, i, 1);
-      const float fm = u == 0 ? f0 : f1;
-      if (c0 == c1) {
-        if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, yb[i] * ni_m);
-        if (c0 == 1) dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
-        if (c0 == 2) dz[u][i] = 0.f;
-      } else if (c0 == 0) {
-        dz[u][i] = __builtin_fmaf(dz[u][i], h0 ? fm : f_s, yb[i] * (h0 ? ni_m : ni_s));
-      } else {  // the pad lanes' e is 0 and their target bit (outputs 62/63) is 0
-        dz[u][i] = __builtin_fmaf(dz[u][i], f_s, yb[i] * ni_s);
-      }
-    }
-  }
-  float l = -(((tm[0].x + tm[0].y) + (tm[1].x + tm[1].y)) * inv_m + (ts.x + ts.y) * inv_s);
-  if (h == 0)
-    l += (nm ? M + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? mx_s + __builtin_amdgcn_logf(s_s) * LN2 : 0.f);
-  loss_acc += l;
 }
 
 // forward wave F (0/1) of unit `unit`: tiles k = F, F + 2, ... of the unit's stream

@@ -100,12 +100,16 @@ class FusedSmallMLP:
     def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
                  state_dict: dict | None = None, process_group=None, comm: str = "auto",
-                 fused_adam: bool | None = None):
+                 fused_adam: bool | None = None, dtype: str = "bf16"):
         from ..ops import fused_mlp as FM
         from ..ops import _native as N
 
         if loss not in FM.LOSS_KINDS:
             raise ValueError(f"loss must be one of {list(FM.LOSS_KINDS)}")
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError("dtype must be bf16 or fp32")
+        # fp32: the exact-fp32 train kernel (csrc/mlp_fused_f32.hip) on the same slabs / Adam
+        self.dtype = dtype
         self.FM = FM
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -135,7 +139,7 @@ class FusedSmallMLP:
 
         if fused_adam is None:
             fused_adam = os.environ.get("EUROM_FUSED_ADAM", "0") == "1"
-        self.fused_adam = bool(fused_adam)
+        self.fused_adam = bool(fused_adam) and dtype == "bf16"  # the one-launch step is bf16 only
         FM.pack(self.params, self.img)
         self._checked = False
         # DP gradient all-reduce: "xgmi" = one-shot peer-memory reduction fused into the Adam
@@ -188,8 +192,7 @@ class FusedSmallMLP:
             return self.loss_out
         # the train kernel advances the Adam step counter (one store), so no Adam launch below draws a
         # grid-wide ticket for it (pre=True)
-        nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
-                                  offset=offset, sidx=sidx, check=not self._checked, step=self.state)
+        nslab = self._partials(draws, B, offset, sidx, check=not self._checked, step=self.state)
         self._checked = True
         if self.group is None:
             FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=0,
@@ -241,11 +244,18 @@ class FusedSmallMLP:
             self.xgmi.close()
             self.xgmi = None
 
+    def _partials(self, draws, B, offset, sidx, check=True, step=None) -> int:
+        """The train kernel of this model's dtype: per-workgroup gradient slabs; returns the grid size."""
+        if self.dtype == "fp32":
+            return self.FM.train_partials_f32(draws, B, self.params, self.slabs, self.loss_slabs,
+                                              loss=self.loss_name, offset=offset, sidx=sidx, check=check, step=step)
+        return self.FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
+                                      offset=offset, sidx=sidx, check=check, step=step)
+
     def grads(self, draws: torch.Tensor, B: int, offset: int = 0, sidx: torch.Tensor | None = None):
         """(mean loss, flat gradient) without updating — for tests / gradient checks."""
         FM = self.FM
-        nslab = FM.train_partials(draws, B, self.img, self.slabs, self.loss_slabs, loss=self.loss_name,
-                                  offset=offset, sidx=sidx)
+        nslab = self._partials(draws, B, offset, sidx)
         scale = 1.0 / B / (62.0 if self.loss_name == "bce" else 1.0)
         FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=1,
                      grad_io=self.grad_io, loss_slabs=self.loss_slabs, loss_out=self.grad_io[FM.P_TOTAL:],
@@ -255,6 +265,13 @@ class FusedSmallMLP:
 
     # ------------------------------------------------------------------ inference / eval
     def logits(self, draws: torch.Tensor, B: int, offset: int = 0, sidx=None) -> torch.Tensor:
+        if self.dtype == "fp32":  # evaluation in fp32 as well (torch fp32 GEMMs on the master weights)
+            FM = self.FM
+            x = FM.onehot(draws, B, offset=offset, which=0, sidx=sidx).float()
+            W1 = self.params[FM.P_W1:FM.P_W2].view(64, 128)
+            W2 = self.params[FM.P_W2:FM.P_B2].view(128, 64)
+            h = torch.relu(x @ W1 + W1[62])
+            return h @ W2 + self.params[FM.P_B2:FM.P_TOTAL]
         return self.FM.forward_logits(draws, B, self.img, offset=offset, sidx=sidx)
 
     def evaluate(self, draws: torch.Tensor, B: int, offset: int = 0, sidx=None, chunk: int = 1 << 22) -> dict:

@@ -136,6 +136,26 @@ def train_partials(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.
     return nslab
 
 
+def train_partials_f32(draws: torch.Tensor, B: int, params: torch.Tensor, slabs: torch.Tensor,
+                       loss_slabs: torch.Tensor, loss: str = "softmax", offset: int = 0,
+                       sidx: torch.Tensor | None = None, check: bool = True, step: torch.Tensor | None = None) -> int:
+    """:func:`train_partials` in exact fp32 (``csrc/mlp_fused_f32.hip``: every product a
+    v_mfma_f32_32x32x2_f32): reads the fp32 master ``params`` instead of the bf16 weight images and
+    writes the same per-workgroup gradient slabs.  Returns the grid size used."""
+    if check:
+        _check_draws(draws, sidx, B, offset)
+        N.check_cuda(params, "params", torch.float32)
+        if params.numel() != P_TOTAL:
+            raise ValueError("params must hold P_TOTAL floats")
+        if slabs.dim() != 2 or slabs.shape[1] != SLAB_STRIDE or loss_slabs.numel() < slabs.shape[0]:
+            raise ValueError("slabs must be [nslab, SLAB_STRIDE]")
+    nslab = max(1, min(slabs.shape[0], (B + 127) // 128))
+    N.call("em_mlp_fused_train_f32", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
+           params.data_ptr(), slabs.data_ptr(), loss_slabs.data_ptr(), nslab, LOSS_KINDS[loss],
+           step.data_ptr() if step is not None else None, N.stream_handle(draws.device))
+    return nslab
+
+
 def train_step(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.Tensor, loss_slabs: torch.Tensor,
                params: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor,
                sync: torch.Tensor, loss_out: torch.Tensor, grad_scale: float, loss_scale: float,

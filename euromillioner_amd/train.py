@@ -109,7 +109,7 @@ class _FusedEngine(_Engine):
         m = cfg.mlp
         self.model = FusedSmallMLP(info.device, loss=m.loss, lr=m.lr, betas=tuple(m.betas), eps=m.eps,
                                    weight_decay=m.weight_decay, state_dict={self._MAP[k]: v for k, v in sd.items()},
-                                   process_group=info.group)
+                                   process_group=info.group, dtype=m.dtype)
         self.masks = masks
 
     def step(self, idx, offset, B, global_batch):
@@ -376,10 +376,9 @@ def _mlp_sizes(cfg: RunConfig) -> tuple:
 def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
     if info.device.type != "cuda":
         return "torch"  # CPU plumbing path
-    if (sizes == (62, 128, 62) and cfg.mlp.activation == "relu" and cfg.mlp.dtype == "bf16"
-            and not cfg.dist.avg_frequency):
-        return "fused"  # the single-launch kernel is bf16; --dtype fp32 takes the fp32 MFMA GEMM engine
-    return "gemm"  # any stack, lag windows, fp32, parameter averaging
+    if sizes == (62, 128, 62) and cfg.mlp.activation == "relu" and not cfg.dist.avg_frequency:
+        return "fused"  # the fused train kernel: bf16 (mlp_fused.hip) or exact fp32 (mlp_fused_f32.hip)
+    return "gemm"  # any other stack, lag windows, parameter averaging
 
 
 def train_mlp(cfg: RunConfig) -> dict:

@@ -267,3 +267,46 @@ def test_one_launch_step_replays_from_graph(data):
     a.check_comm()
     assert int(a.state[0]) == int(b.state[0]) == 6
     assert torch.equal(a.params, b.params) and torch.equal(a.img, b.img)
+
+
+@pytest.mark.parametrize("loss", ["softmax", "bce"])
+@pytest.mark.parametrize("B,offset", [(4096, 0), (1000, 7), (37, 100), (70000, 3)])
+def test_fused_f32_grads_match_fp32_reference(data, loss, B, offset):
+    """The exact-fp32 train kernel (csrc/mlp_fused_f32.hip, v_mfma_f32_32x32x2_f32) against the fp32
+    PyTorch reference with UNROUNDED operands: only the summation order differs, so the tolerance is
+    3e-5 relative per tensor (the bf16 kernel is held to 1e-2).  70000 samples: several tiles per wave."""
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    ds, draws = data
+    if B + offset + 1 > ds.numbers.shape[0]:
+        ds = DrawSet.synthetic(n=B + offset + 16, seed=11, planted=0.6, calendar=False)
+        draws = FM.rows_to_masks(torch.from_numpy(ds.numbers).cuda())
+    m = FusedSmallMLP(loss=loss, seed=5, dtype="fp32")
+    lk, gk = m.grads(draws, B, offset=offset)
+    old = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        lr_, gr, zref = _ref_grads(m.state_dict(), ds.numbers, offset, B, loss, bf16=False)
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = old
+    assert abs(lk - lr_) <= 3e-5 * max(1.0, abs(lr_)), (lk, lr_)
+    _assert_grads_close(gk, gr, tol=3e-5)
+    assert float((gk * (1 - FM.pad_mask("cuda"))).abs().max()) == 0.0
+    lg = m.logits(draws, B, offset=offset)
+    assert torch.allclose(lg[:, :62], zref, atol=1e-5, rtol=1e-5)
+
+
+def test_fused_f32_steps_deterministic_and_learn(data):
+    """fp32 fused steps: bit-identical parameters across two runs (fixed-order slabs + Adam) and the
+    training loss falls on the planted data."""
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+
+    ds, draws = data
+    runs = []
+    for _ in range(2):
+        m = FusedSmallMLP(loss="softmax", seed=3, lr=3e-3, dtype="fp32")
+        losses = [float(m.step(draws, 4096, offset=64 * i).item()) for i in range(12)]
+        runs.append((m.params.clone(), losses))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert runs[0][1][-1] < runs[0][1][0], runs[0][1]

@@ -92,5 +92,12 @@ def test_fp32_cli_config_trains():
                                 "data.planted": 0.8, "mlp.steps": 80, "mlp.batch": 1024, "mlp.lr": 0.005,
                                 "mlp.eval_every": 0, "log.level": "WARN"}, environ={})
     res = train(cfg)
+    assert res["engine"] == "fused"  # 62->128->62 relu: the exact-fp32 fused kernel (csrc/mlp_fused_f32.hip)
+    assert res["val"]["acc"] > res["val"]["trivial_acc"], res["val"]
+    # any other stack takes the fp32 GEMM engine
+    cfg = C.build_config(None, {"model": "mlp", "device": "cuda", "mlp.dtype": "fp32", "mlp.hidden": [96],
+                                "data.n_draws": 6001, "data.planted": 0.8, "mlp.steps": 80, "mlp.batch": 1024,
+                                "mlp.lr": 0.005, "mlp.eval_every": 0, "log.level": "WARN"}, environ={})
+    res = train(cfg)
     assert res["engine"] == "gemm"
     assert res["val"]["acc"] > res["val"]["trivial_acc"], res["val"]
