@@ -44,8 +44,9 @@ constexpr int F32_B2 = F32_W2 + 128 * F32_RS2 * 4;           // 71680
 constexpr int F32_YLUT = F32_B2 + 256;                       // 16 x f32x4 target nibble table
 constexpr int F32_WAVE = F32_YLUT + 256;                     // per-wave staging
 constexpr int F32_DZ = 0, F32_T = 64 * F32_RST * 4, F32_MASK = 2 * 64 * F32_RST * 4;
-constexpr int F32_WAVE_BYTES = F32_MASK + 32 * 8;            // 18688
-constexpr int F32_LDS = F32_WAVE + 4 * F32_WAVE_BYTES;       // 146944
+constexpr int F32_ACC = F32_MASK + 32 * 8;                   // [64 lanes] db2 + [64 lanes] loss, kept in LDS
+constexpr int F32_WAVE_BYTES = F32_ACC + 2 * 64 * 4;         // 19200
+constexpr int F32_LDS = F32_WAVE + 4 * F32_WAVE_BYTES;       // 148992
 // end of launch: the fold image (register layout of the accumulators, conflict-free) reuses the LDS
 constexpr int F32_FOLD_FLOATS = 2 * 8 * 16 * 64 + 64;         // dW1T + dW2 partials + b2
 static_assert(F32_FOLD_FLOATS * 4 <= F32_LDS, "fold image must fit");
@@ -85,14 +86,17 @@ mlp_fused_train_f32_kernel(const uint64_t* __restrict__ masks, const int32_t* __
   float* DZI = reinterpret_cast<float*>(ws + F32_DZ);  // [64 o][36]: dZ2 of the tile
   float* TI = reinterpret_cast<float*>(ws + F32_T);    // [64 c][36]: half of H, then half of dZ1
   uint64_t* MI = reinterpret_cast<uint64_t*>(ws + F32_MASK);
+  // the lane's db2 (lane = output o) and loss sums live in LDS between tiles: as loop-carried registers
+  // the allocator spilled them to scratch inside the loop
+  float* ACC = reinterpret_cast<float*>(ws + F32_ACC);
+  ACC[lane] = 0.f;
+  ACC[64 + lane] = 0.f;
 
   f32x16 gw1[4][2], gw2[4][2];  // dW1T [c tile][f tile], dW2 [c tile][o tile]: the launch's accumulators
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int j = 0; j < 2; ++j) gw1[t][j] = gw2[t][j] = f32x16{};
-  float gb2 = 0.f;  // db2[lane] (lane = output o) summed over this wave's tiles
-  float loss_acc = 0.f;
 
   const int nwav = gridDim.x * 4, ntiles = (B + 31) / 32;
   for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += nwav) {
@@ -137,7 +141,7 @@ mlp_fused_train_f32_kernel(const uint64_t* __restrict__ masks, const int32_t* __
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) z1[t][i] = fmaxf(z1[t][i], 0.f);  // H
+      for (int i = 0; i < 16; ++i) z1[t][i] = z1[t][i] > 0.f ? z1[t][i] : 0.f;  // H (a select: fmaxf adds a canonicalize)
 
     // ---- F2: Z2[o][s] = b2 + sum over c = 32t + 8g + 4h + e of W2[c][o] H[c][s]
     f32x16 z2[2];
@@ -192,7 +196,7 @@ mlp_fused_train_f32_kernel(const uint64_t* __restrict__ masks, const int32_t* __
     } else {
       bce_tile_loss<F32_WAVE - 256>(smem, z2, valid ? tm : 0ull, valid, h, dz, lt);
     }
-    loss_acc += lt;
+    ACC[64 + lane] += lt;
 
     // ---- stage dZ2 [o][s]; db2 += its row sums (lane o sums its row in a fixed order)
 #pragma unroll
@@ -207,7 +211,7 @@ mlp_fused_train_f32_kernel(const uint64_t* __restrict__ masks, const int32_t* __
         const f32x4 v = *reinterpret_cast<const f32x4*>(DZI + lane * F32_RST + j0);
         rs += (v[0] + v[1]) + (v[2] + v[3]);
       }
-      gb2 += rs;
+      ACC[lane] += rs;
     }
 
     // ---- dW2[c][o] += sum_s H[c][s] dZ2[o][s], K = the tile's samples (s = j + 16h per lane)
@@ -290,6 +294,8 @@ mlp_fused_train_f32_kernel(const uint64_t* __restrict__ masks, const int32_t* __
   // ---- fold the four waves' partials in wave order, then one parameter-order slab
   __syncthreads();  // every wave is past its last LDS read of the weight and staging images
   float* FO = reinterpret_cast<float*>(smem);  // [2 (w1, w2)][8 (t, j)][16 i][64 lane] + b2[64]
+  const float gb2 = ACC[lane], loss_acc = ACC[64 + lane];
+  __syncthreads();
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
 #pragma unroll
