@@ -110,6 +110,9 @@ def _parse():
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="consecutive training steps captured per hipGraph (each a full fwd+bwd+Adam step); "
                          "0 = all timed steps up to 50 in one graph (one launch latency per chunk)")
+    ap.add_argument("--graph-chunks", default="",
+                    help="explicit hipGraph plan for the timed steps: comma-separated step counts summing to "
+                         "--steps, launched back to back (e.g. 1,19)")
     ap.add_argument("--warmup-ms", type=float, default=250.0,
                     help="after the W warmup steps, keep replaying untimed warmup steps until this much wall "
                          "time has passed (the chip ramps its clock over the first ~100 ms of load; a training "
@@ -305,6 +308,9 @@ def main():
         # profiles/README.md) is paid once per chunk instead of once per step.  Steps that do not
         # fill a chunk replay a 1-step graph.
         C = max(1, min(a.graph_steps if a.graph_steps > 0 else 50, a.steps))
+        chunks = [int(x) for x in a.graph_chunks.split(",") if x.strip()]
+        if chunks and (sum(chunks) != a.steps or min(chunks) < 1):
+            raise SystemExit("--graph-chunks must be positive step counts summing to --steps")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
 
@@ -318,12 +324,20 @@ def main():
         with torch.cuda.stream(s):
             g_c = capture(C)
             g_1 = capture(1)
+            g_by = {C: g_c, 1: g_1}
+            for n in chunks:
+                if n not in g_by:
+                    g_by[n] = capture(n)
         torch.cuda.current_stream().wait_stream(s)
         for _ in range(a.warmup - 1):
             g_1.replay()
         torch.cuda.synchronize()
         clock_warmup(g_c.replay, C)
-        plan = [(g_c, C)] * (a.steps // C) + [(g_1, 1)] * (a.steps % C)
+        if chunks:
+            C = max(chunks)
+            plan = [(g_by[n], n) for n in chunks]
+        else:
+            plan = [(g_c, C)] * (a.steps // C) + [(g_1, 1)] * (a.steps % C)
         runs = [(lambda g=g: g.replay(), n) for g, n in plan]
     else:
         wi = iter(range(a.warmup, 1 << 62))
