@@ -617,13 +617,14 @@ EM_DEVICE bool epi_gather(const float* __restrict__ slabs, const int* sync, int 
   return true;
 }
 
-// everything after this workgroup's slab is written (all 512 threads)
-EM_DEVICE void epi_adam(char* smem, const float* __restrict__ slabs, const float* __restrict__ loss_slabs,
+// everything after this workgroup's slab is written (all 512 threads); returns the chunks it processed
+EM_DEVICE int epi_adam(char* smem, const float* __restrict__ slabs, const float* __restrict__ loss_slabs,
                         const AdamEpi& a, int tag, int tstep, int tid) {
   const int lane = tid & 63, g = tid >> 6, nslab = gridDim.x;
   int* SCH = reinterpret_cast<int*>(smem + V6_RED + 1024);        // dequeued chunk
   float* PART = reinterpret_cast<float*>(smem + V6_RED + 1152);   // [16][64] per-group partial sums
   int* BAD = reinterpret_cast<int*>(smem + V6_RED + 1088);
+  int done = 0;
   // publish: every storing wave drained its sc1 slab stores; then ONE lane raises the flag
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -642,8 +643,9 @@ EM_DEVICE void epi_adam(char* smem, const float* __restrict__ slabs, const float
         __hip_atomic_store(a.sync + SYNC_EPOCH, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.state, tstep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      return;
+      return done;
     }
+    ++done;
     const int p0 = c * EPI_CHUNK;
     float v[32];
 #pragma unroll
@@ -807,7 +809,13 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
 #pragma unroll
     for (int k = 0; k < 4; ++k) slab_spare[128 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
   }
-  if (EPI) epi_adam(smem, slabs, loss_slabs, epi, tag, tstep, tid);
+  if (EPI) {
+    const int nchunks = epi_adam(smem, slabs, loss_slabs, epi, tag, tstep, tid);
+    if (FUSED_STAMPS && tid == 0) {  // epilogue end + chunks processed (tools/epi_timeline.py)
+      slab_spare[132] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      slab_spare[133] = (float)nchunks;
+    }
+  }
 }
 
 template <int LOSS>
