@@ -1,7 +1,11 @@
 """DL4J ModelSerializer-layout checkpoint: byte layout (golden), ordering, roundtrip.
 
 Parity with a real DL4J artifact is unpinned (no JVM / DL4J files offline); the layout
-assumptions are the ones documented in euromillioner_amd/ckpt/modelserializer.py."""
+assumptions are the ones documented in euromillioner_amd/ckpt/modelserializer.py.  One of them is
+the JSON type-info style of configuration.json: layers, activations, loss functions and the updater
+carry Jackson ``@class`` properties (the fully qualified class name).  DL4J 0.9.x may instead have
+written some of them as wrapper objects keyed by a short type name; no artifact here decides which,
+so the golden tests below pin this builder's own format, not DL4J's."""
 import io
 import struct
 import zipfile
