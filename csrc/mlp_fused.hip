@@ -1,5 +1,5 @@
 // K7 -- fused persistent small-MLP training step for MI355X (gfx950).
-// EM_BUILD_FLAGS: -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-use-amdgpu-trackers
+// EM_BUILD_FLAGS: -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-use-amdgpu-trackers -mllvm -amdgpu-schedule-metric-bias=0
 //
 // Model (BASELINE.json config 2): multi-hot 62-wide draw
 // vector -> Linear(62,128) -> ReLU -> Linear(128,62) -> grouped softmax-CE
