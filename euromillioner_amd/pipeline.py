@@ -174,7 +174,12 @@ def date_str(d) -> str:
 
 
 def next_draw_date(last: np.datetime64) -> np.datetime64:
-    d = last.astype(_dt.date) + _dt.timedelta(days=1)
-    while not (d.weekday() == 4 or (d.weekday() == 1 and d >= _dt.date(2011, 5, 10))):
-        d += _dt.timedelta(days=1)
-    return np.datetime64(d, "D")
+    """The next Euromillions draw day after ``last`` (Fridays; Tuesdays too from 2011-05-10).  Pure
+    datetime64 arithmetic: long synthetic sequences run past year 9999, where datetime.date cannot go."""
+    tuesdays_from = np.datetime64("2011-05-10", "D")
+    d = np.datetime64(last, "D") + np.timedelta64(1, "D")
+    while True:
+        wd = (int(d.astype(np.int64)) + 3) % 7  # 1970-01-01 was a Thursday; Monday = 0 as in date.weekday()
+        if wd == 4 or (wd == 1 and d >= tuesdays_from):
+            return d
+        d = d + np.timedelta64(1, "D")

@@ -136,3 +136,22 @@ def test_comm_dtype_flag_reaches_config_and_is_validated():
     cfg.dist.comm_dtype = "fp16"
     with pytest.raises(ValueError, match="comm_dtype"):
         C.validate(cfg)
+
+
+def test_next_draw_date_past_year_9999():
+    """Long synthetic sequences (millions of draws) run past year 9999, where datetime.date cannot go:
+    `predict` on a 2M-draw dataset failed with a TypeError before next_draw_date used datetime64 only."""
+    import datetime as dt
+
+    import numpy as np
+
+    from euromillioner_amd.pipeline import next_draw_date
+
+    for s in ["2004-02-13", "2011-05-06", "2011-05-10", "2011-05-13", "2026-10-16", "9999-12-30"]:
+        d = dt.date.fromisoformat(s) + dt.timedelta(days=1) if s != "9999-12-30" else None
+        if d is not None:
+            while not (d.weekday() == 4 or (d.weekday() == 1 and d >= dt.date(2011, 5, 10))):
+                d += dt.timedelta(days=1)
+            assert next_draw_date(np.datetime64(s, "D")) == np.datetime64(d, "D"), s
+    far = next_draw_date(np.datetime64("21173-01-26", "D"))
+    assert far > np.datetime64("21173-01-26", "D") and (int(far.astype(np.int64)) + 3) % 7 in (1, 4)
