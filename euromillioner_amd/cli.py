@@ -86,7 +86,7 @@ def build_parser() -> argparse.ArgumentParser:
     _add_common(p)
     p.add_argument("--model", default=None, choices=["mlp", "mlp-wide", "rf", "gbdt"])
     p = sub.add_parser("gen", help="write synthetic draws to CSV")
-    p.add_argument("--n", type=int, default=None)
+    p.add_argument("--n", "--n-draws", dest="n", type=int, default=None, help="draws to generate (same name as train --n-draws)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--planted", type=float, default=0.0)
     p.add_argument("--out", required=True)

@@ -155,3 +155,12 @@ def test_next_draw_date_past_year_9999():
             assert next_draw_date(np.datetime64(s, "D")) == np.datetime64(d, "D"), s
     far = next_draw_date(np.datetime64("21173-01-26", "D"))
     assert far > np.datetime64("21173-01-26", "D") and (int(far.astype(np.int64)) + 3) % 7 in (1, 4)
+
+
+def test_gen_accepts_n_draws_alias(tmp_path):
+    """`gen --n-draws` (the name `train` uses) is the same as `gen --n`."""
+    from euromillioner_amd import cli
+
+    out = tmp_path / "d.csv"
+    assert cli.main(["gen", "--n-draws", "300", "--out", str(out)]) == 0
+    assert len([ln for ln in out.read_text().splitlines() if ln.strip()]) >= 300
