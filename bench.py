@@ -46,6 +46,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 class _TorchBaseline:
     """Same model/loss/optimizer in plain PyTorch (bf16 autocast or fp32 GEMMs via hipBLASLt) — comparison only."""
 
+    # torch.optim.Adam (capturable=False) refuses hipGraph capture: the baseline runs eager launches
+    no_graph = True
+
     def __init__(self, dev, a, draws, B, group):
         from euromillioner_amd.models.mlp import DrawMLP
         from euromillioner_amd.ops import fused_mlp as FM
@@ -274,7 +277,8 @@ def main():
         def step(i):
             return model.step(boff(i))
 
-    use_graph = bool(a.graph) and (world == 1 or getattr(model, "graph_safe", False))
+    use_graph = bool(a.graph) and not getattr(model, "no_graph", False) and (
+        world == 1 or getattr(model, "graph_safe", False))
     loss_t = None
     tw = time.perf_counter()
     # warmup: with hipGraphs, one eager step (first-launch setup) and the other W-1 as replays of the
