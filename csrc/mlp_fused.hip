@@ -549,187 +549,17 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   }
 }
 
-// ============================================================================================
-// In-launch Adam (EPI = 1): the slab reduction and the optimizer step ride on the train launch.
-//
-// Without it a step is two launches: this kernel, then em_adam_slab (a 17 MB slab read, ~3.7 us,
-// plus a ~1.5 us kernel boundary) -- all of it after the SLOWEST workgroup's loop, which ends
-// ~4 us after the median one.  Here every workgroup, as soon as its own slab is written, publishes
-// it (write-through sc1 stores, every storing wave drained, one sc1 flag store: the R1 hand-off of
-// cdna_hip_programming.md §6 Guideline 16) and then becomes an Adam worker: it dequeues 64-parameter
-// chunks from a device counter (dequeue row of the MI355X price list) and sums each chunk over all
-// slabs, loading every slab as soon as its flag shows up, i.e. while the slow workgroups are still
-// computing.  The slowest workgroup draws no chunk; the critical path after its loop is its slab
-// publish plus one 256-byte read per waiting chunk and the Adam arithmetic.
-//   * bit-reproducible: a chunk's parameter p is sum_{g=0..15} (sum_{i} slab[g + 16 i][p]) in the
-//     fixed order of em_adam_slab whatever the arrival order and whichever workgroup takes the chunk;
-//   * placement-independent: flags and slab words are stored sc1 and loaded sc1 by the wave that
-//     polled them (the loss words after a workgroup barrier); no XCD co-location is assumed;
-//   * replay-safe (hipGraph): flags are tagged with a launch epoch (never reset); the workgroup that
-//     draws the LAST dequeue ticket of the launch (every other workgroup has drawn its final one, so
-//     all have read the epoch and the step counter at entry) resets the head, advances the epoch and
-//     publishes the Adam step counter for the next launch;
-//   * bounded: every poll gives up after EPI_TIMEOUT (wall clock), raises sync[ERR] and poisons the
-//     loss with NaN; the parameters of that step are left unchanged.
-constexpr int SYNC_FLAGS = 0, SYNC_MAXB = 1024, SYNC_HEAD = 1024, SYNC_EPOCH = 1025, SYNC_ERR = 1026;
-constexpr int SYNC_WORDS = 1040;  // the Python side allocates this many zeroed int32 (ops/fused_mlp.py)
-constexpr int EPI_CHUNK = 64, EPI_NCHUNK = P_TOTAL / EPI_CHUNK;  // 257
-static_assert(P_TOTAL % EPI_CHUNK == 0, "whole chunks");
-constexpr long long EPI_TIMEOUT = 200000000;  // wall_clock64 ticks (100 MHz): 2 s
-
-struct AdamEpi {
-  float* params;
-  float* m;
-  float* v;
-  const float* hp;  // {lr, beta1, beta2, eps, weight_decay}
-  int* state;       // {adam step, ticket}: state[0] is advanced by this launch
-  int* sync;        // SYNC_WORDS zeroed int32 (flags / head / epoch / error)
-  uint8_t* img;     // the weight images this launch read: the epilogue writes next step's
-  float* loss_out;  // mean loss of the step
-  float grad_scale, loss_scale;
-};
-
-EM_DEVICE int ld_sc1(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// wave g of the worker: v[j] = slab[g + 8 j][p0 + lane] for every slab j of this wave, each loaded as
-// soon as its flag carries this launch's tag.  Returns false on timeout.
-EM_DEVICE bool epi_gather(const float* __restrict__ slabs, const int* sync, int nslab, int g, int lane, int p0, int tag,
-                          float (&v)[32]) {
-  uint32_t need = 0;
-#pragma unroll
-  for (int j = 0; j < 32; ++j) need |= (g + 8 * j < nslab ? 1u : 0u) << j;
-  uint32_t have = 0;
-  long long t0 = 0;
-  while (have != need) {
-    int f = 0;
-    if (lane < 32 && ((need & ~have) >> lane & 1u)) f = ld_sc1(sync + SYNC_FLAGS + g + 8 * lane) == tag;
-    const uint32_t nw = (uint32_t)__ballot(f);
-    if (nw == 0) {
-      if (t0 == 0) t0 = wall_clock64();
-      else if (wall_clock64() - t0 > EPI_TIMEOUT) return false;
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-#pragma unroll
-    for (int j = 0; j < 32; ++j)
-      if (nw >> j & 1u)
-        v[j] = __hip_atomic_load(slabs + (size_t)(g + 8 * j) * SLAB_STRIDE + p0 + lane, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-    have |= nw;
-  }
-  return true;
-}
-
-// everything after this workgroup's slab is written (all 512 threads); returns the chunks it processed
-EM_DEVICE int epi_adam(char* smem, const float* __restrict__ slabs, const float* __restrict__ loss_slabs,
-                        const AdamEpi& a, int tag, int tstep, int tid) {
-  const int lane = tid & 63, g = tid >> 6, nslab = gridDim.x;
-  int* SCH = reinterpret_cast<int*>(smem + V6_RED + 1024);        // dequeued chunk
-  float* PART = reinterpret_cast<float*>(smem + V6_RED + 1152);   // [16][64] per-group partial sums
-  int* BAD = reinterpret_cast<int*>(smem + V6_RED + 1088);
-  int done = 0;
-  // publish: every storing wave drained its sc1 slab stores; then ONE lane raises the flag
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(a.sync + SYNC_FLAGS + blockIdx.x, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    BAD[0] = 0;
-  }
-  for (;;) {
-    if (tid == 0) SCH[0] = __hip_atomic_fetch_add(a.sync + SYNC_HEAD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int c = SCH[0];
-    __syncthreads();  // SCH is rewritten by the next dequeue
-    if (c >= EPI_NCHUNK) {
-      if (tid == 0 && c == EPI_NCHUNK + nslab - 1) {  // the launch's last ticket: reset for the next launch
-        __hip_atomic_store(a.sync + SYNC_HEAD, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.sync + SYNC_EPOCH, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.state, tstep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return done;
-    }
-    ++done;
-    const int p0 = c * EPI_CHUNK;
-    float v[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = 0.f;
-    const bool ok = epi_gather(slabs, a.sync, nslab, g, lane, p0, tag, v);
-    // wave g holds slab groups g (slabs g + 16 i = v[2i]) and g + 8 (slabs g + 8 + 16 i = v[2i + 1]);
-    // each group is summed exactly as em_adam_slab's thread of that group sums it (adam.hip
-    // adam_slab4_kernel: four interleaved accumulators over a full block of 16 slabs, else one
-    // sequential tail accumulator; absent slabs are +0)
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-      const int grp = g + 8 * par;
-      float s;
-      if (grp + 240 < nslab) {
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i & 3] += v[2 * i + par];
-        s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      } else {
-        float acc = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc += v[2 * i + par];
-        s = (acc + 0.f) + (0.f + 0.f);
-      }
-      PART[grp * 64 + lane] = s;
-    }
-    if (!ok) {
-      BAD[0] = 1;
-      if (lane == 0) __hip_atomic_store(a.sync + SYNC_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();  // every flag of every slab has been seen by some wave of this workgroup
-    const bool bad = BAD[0] != 0;
-    if (tid < 64) {
-      const int p = p0 + tid;
-      float gs = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) gs += PART[k * 64 + tid];
-      if (!bad) {
-        const float lr = a.hp[0], b1 = a.hp[1], b2 = a.hp[2], eps = a.hp[3], wd = a.hp[4];
-        if (mlp::pad_slot(p)) {
-          a.params[p] = 0.f;
-          a.m[p] = 0.f;
-          a.v[p] = 0.f;
-          mlp::pack_one(p, 0.f, a.img);
-        } else {
-          float mm = a.m[p], vv = a.v[p];
-          const float w = adam_math(gs * a.grad_scale, a.params[p], mm, vv, lr, b1, b2, eps, wd,
-                                    bias_correction(b1, tstep), bias_correction(b2, tstep));
-          a.m[p] = mm;
-          a.v[p] = vv;
-          a.params[p] = w;
-          mlp::pack_one(p, w, a.img);
-        }
-      }
-    } else if (c == 0 && tid < 128 && a.loss_out) {  // the step's loss: fixed-order sum of the per-slab losses
-      float l = 0.f;
-      for (int s2 = tid - 64; s2 < nslab; s2 += 64)
-        l += __hip_atomic_load(loss_slabs + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      l = wave_sum(l);
-      if (tid == 64) a.loss_out[0] = bad ? __builtin_nanf("") : l * a.loss_scale;
-    }
-    __syncthreads();  // PART / BAD are reused by the next chunk
-    if (tid == 0) BAD[0] = 0;
-  }
-}
-
-// EPI 0: slabs only (em_adam_slab reduces them, or the DP paths all-reduce them first);
-// EPI 1: slabs + in-launch Adam (single-process training, AdamEpi above)
-// (the train kernel keeps its short argument block; the step kernel adds the Adam arguments)
-template <int LOSS, int EPI>
+// Slabs only: em_adam_slab reduces them (or the DP paths all-reduce them first).  A one-launch form
+// with the slab reduction and Adam inside this kernel was measured 4.3 us per step slower (round 3,
+// docs/DESIGN.md §6b) and removed in round 4.
+template <int LOSS>
 __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                                          int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
-                                         float* __restrict__ loss_slabs, int* __restrict__ step, const AdamEpi& epi) {
+                                         float* __restrict__ loss_slabs, int* __restrict__ step) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t ts[4] = {};  // FUSED_STAMPS: 100 MHz wall-clock marks (entry, prologue done, loop done, slab written)
   if (FUSED_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
-  int tag = 0, tstep = 0;
-  if (EPI) {  // read at entry: the launch's last ticket holder rewrites both only after every workgroup is done
-    tag = ld_sc1(epi.sync + SYNC_EPOCH) + 1;
-    tstep = ld_sc1(epi.state) + 1;
-  } else if (step && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (step && blockIdx.x == 0 && threadIdx.x == 0) {
     // the optimizer's step counter (em_adam_slab pre mode): stream order puts this launch strictly
     // between two Adam launches, so one plain store here saves Adam a grid-wide ticket
     step[0] = step[0] + 1;
@@ -812,13 +642,6 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
 #pragma unroll
     for (int k = 0; k < 4; ++k) slab_spare[128 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
   }
-  if (EPI) {
-    const int nchunks = epi_adam(smem, slabs, loss_slabs, epi, tag, tstep, tid);
-    if (FUSED_STAMPS && tid == 0) {  // epilogue end + chunks processed (tools/epi_timeline.py)
-      slab_spare[132] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());
-      slab_spare[133] = (float)nchunks;
-    }
-  }
 }
 
 template <int LOSS>
@@ -826,15 +649,7 @@ __global__ void __launch_bounds__(512, 1)
 mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
                           const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                           float* __restrict__ loss_slabs, int* __restrict__ step) {
-  train_v6<LOSS, 0>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step, AdamEpi{});
-}
-
-template <int LOSS>
-__global__ void __launch_bounds__(512, 1)
-mlp_fused_step_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
-                         const uint8_t* __restrict__ wimg, float* __restrict__ slabs, float* __restrict__ loss_slabs,
-                         AdamEpi epi) {
-  train_v6<LOSS, 1>(masks, sidx, B, offset, wimg, slabs, loss_slabs, nullptr, epi);
+  train_v6<LOSS>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step);
 }
 
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
@@ -906,14 +721,11 @@ EM_API int em_mlp_fused_param_count() { return P_TOTAL; }
 EM_API int em_mlp_fused_slab_stride() { return SLAB_STRIDE; }
 EM_API int em_mlp_fused_image_bytes() { return IMG_BYTES; }
 EM_API int em_mlp_fused_lds_bytes() { return V6_LDS; }
-EM_API int em_mlp_fused_sync_words() { return SYNC_WORDS; }
 
 namespace {
 template <int LOSS>
 void set_lds_attr() {
   (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            V6_LDS);
-  (void)hipFuncSetAttribute((const void*)mlp_fused_step_v6_kernel<LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             V6_LDS);
 }
 int check_train_args(const uint64_t*& draws, const int32_t* sidx, int64_t B, int64_t& offset, const void* wimg,
@@ -950,28 +762,6 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
   else
     hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
                        slabs, loss_slabs, step);
-  EM_CHECK_LAUNCH();
-  return 0;
-}
-
-// The whole single-process optimizer step in ONE launch: train + slab reduction + Adam (+ the next
-// step's weight images into wimg) + the mean loss into loss_out.  sync: SYNC_WORDS zeroed int32,
-// owned by one model (never shared between two models that may run concurrently).
-EM_API int em_mlp_fused_step(const uint64_t* draws, const int32_t* sidx, int64_t B, int64_t offset, void* wimg,
-                             float* slabs, float* loss_slabs, int nslab, int loss_kind, float* params, float* m,
-                             float* v, const float* hp, int* state, int* sync, float* loss_out, float grad_scale,
-                             float loss_scale, hipStream_t stream) {
-  if (int e = check_train_args(draws, sidx, B, offset, wimg, slabs, loss_slabs, nslab)) return e;
-  if (!params || !m || !v || !hp || !state || !sync || nslab > 256) return EM_ERR_ARG;  // 8 waves x 32 slabs
-  const AdamEpi epi{params, m, v, hp, state, sync, (uint8_t*)wimg, loss_out, grad_scale, loss_scale};
-  const int Bi = (int)B, oi = (int)offset;
-  const uint8_t* w = (const uint8_t*)wimg;
-  if (loss_kind == 0)
-    hipLaunchKernelGGL(mlp_fused_step_v6_kernel<0>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, epi);
-  else
-    hipLaunchKernelGGL(mlp_fused_step_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, epi);
   EM_CHECK_LAUNCH();
   return 0;
 }

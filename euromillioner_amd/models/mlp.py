@@ -90,17 +90,15 @@ class DrawMLP(nn.Module):
 class FusedSmallMLP:
     """Flagship trainer: 62->128->62 ReLU MLP, bf16 MFMA compute, fp32 master weights + Adam.
 
-    Single process: two launches per optimizer step (train kernel, then ``em_adam_slab``).
-    ``fused_adam=True`` (or ``EUROM_FUSED_ADAM=1``) runs the one-launch form instead
-    (``fused_mlp.train_step``: the slab reduction and Adam inside the train kernel, overlapping its
-    slowest workgroups) -- bit-identical parameters, but measured 4.3 us per step slower on MI355X
-    (93.3 vs 89.0 us, docs/DESIGN.md), so it is opt-in.  Data parallel: train kernel -> all-reduce
-    -> Adam."""
+    Single process: two launches per optimizer step (train kernel, then ``em_adam_slab``).  A
+    one-launch form (slab reduction + Adam inside the train kernel) was bit-identical but measured
+    4.3 us per step slower on MI355X (93.3 vs 89.0 us, docs/DESIGN.md §6b) and was removed in round 4.
+    Data parallel: train kernel -> all-reduce -> Adam."""
 
     def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
                  state_dict: dict | None = None, process_group=None, comm: str = "auto",
-                 fused_adam: bool | None = None, dtype: str = "bf16"):
+                 dtype: str = "bf16"):
         from ..ops import fused_mlp as FM
         from ..ops import _native as N
 
@@ -134,12 +132,6 @@ class FusedSmallMLP:
         self.loss_slabs = torch.zeros(self.nslab_max, dtype=torch.float32, device=dev)
         self.grad_io = torch.zeros(P + 1, dtype=torch.float32, device=dev)  # [grads..., loss]
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.sync = torch.zeros(FM.SYNC_WORDS, dtype=torch.int32, device=dev)  # one-launch step protocol words
-        import os
-
-        if fused_adam is None:
-            fused_adam = os.environ.get("EUROM_FUSED_ADAM", "0") == "1"
-        self.fused_adam = bool(fused_adam) and dtype == "bf16"  # the one-launch step is bf16 only
         FM.pack(self.params, self.img)
         self._checked = False
         # DP gradient all-reduce: "xgmi" = one-shot peer-memory reduction fused into the Adam
@@ -184,12 +176,6 @@ class FusedSmallMLP:
         if self.loss_name == "bce":
             scale /= 62.0
         lscale = 1.0 / max(gb, 1) / (62.0 if self.loss_name == "bce" else 1.0)
-        if self.group is None and self.fused_adam:
-            FM.train_step(draws, B, self.img, self.slabs, self.loss_slabs, self.params, self.m, self.v, self.hp,
-                          self.state, self.sync, self.loss_out, scale, lscale, loss=self.loss_name, offset=offset,
-                          sidx=sidx, check=not self._checked)
-            self._checked = True
-            return self.loss_out
         # the train kernel advances the Adam step counter (one store), so no Adam launch below draws a
         # grid-wide ticket for it (pre=True)
         nslab = self._partials(draws, B, offset, sidx, check=not self._checked, step=self.state)
@@ -231,12 +217,9 @@ class FusedSmallMLP:
         return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "0") == "1"
 
     def check_comm(self) -> None:
-        """Raise if an xGMI wait or a one-launch step's cross-workgroup wait timed out (synchronises)."""
+        """Raise if an xGMI peer wait timed out (synchronises)."""
         if self.xgmi is not None:
             self.xgmi.check()
-        if int(self.sync[self.FM.SYNC_ERR].item()) != 0:
-            raise RuntimeError("fused step: a workgroup's gradient slab never arrived (timeout); parameters of "
-                               "that step were left unchanged")
 
     def close(self) -> None:
         if self.xgmi is not None:

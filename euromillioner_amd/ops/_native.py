@@ -38,13 +38,9 @@ _SIGS = {
     "em_mlp_fused_lds_bytes": (_i32, []),
     "em_mlp_fused_train": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p,
                                    _c_void_p]),
-    "em_mlp_fused_step": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32,
-                                  _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32,
-                                  _f32, _c_void_p]),
     "em_mlp_fused_train_f32": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32,
                                        _c_void_p, _c_void_p]),
     "em_mlp_fused_f32_lds_bytes": (_i32, []),
-    "em_mlp_fused_sync_words": (_i32, []),
     "em_mlp_fused_forward": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i32, _c_void_p]),
     "em_mlp_fused_pack": (_i32, [_c_void_p, _c_void_p, _c_void_p]),
     "em_mlp_fused_slab_stride": (_i32, []),

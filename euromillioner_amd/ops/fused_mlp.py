@@ -108,10 +108,6 @@ def _check_draws(draws: torch.Tensor, sidx: torch.Tensor | None, B: int, offset:
         raise ValueError(f"samples [{offset}, {offset + B}) + next draw exceed {n} draws")
 
 
-SYNC_WORDS = 1040  # == em_mlp_fused_sync_words(): flags / dequeue head / epoch / error of the one-launch step
-SYNC_ERR = 1026
-
-
 ADAM_PRE = 4  # em_adam_slab mode bit: step counter already advanced by the train kernel (csrc/adam.hip)
 
 
@@ -153,29 +149,6 @@ def train_partials_f32(draws: torch.Tensor, B: int, params: torch.Tensor, slabs:
     N.call("em_mlp_fused_train_f32", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
            params.data_ptr(), slabs.data_ptr(), loss_slabs.data_ptr(), nslab, LOSS_KINDS[loss],
            step.data_ptr() if step is not None else None, N.stream_handle(draws.device))
-    return nslab
-
-
-def train_step(draws: torch.Tensor, B: int, img: torch.Tensor, slabs: torch.Tensor, loss_slabs: torch.Tensor,
-               params: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor,
-               sync: torch.Tensor, loss_out: torch.Tensor, grad_scale: float, loss_scale: float,
-               loss: str = "softmax", offset: int = 0, sidx: torch.Tensor | None = None, check: bool = True) -> int:
-    """The whole single-process optimizer step in ONE launch (K7 + the in-launch K6 epilogue): forward,
-    loss, backward, the fixed-order slab reduction, Adam (advancing ``state[0]``), the next step's
-    bf16 weight images into ``img`` and the mean loss into ``loss_out``.  ``sync`` is the model's own
-    [SYNC_WORDS] int32 buffer (zeroed once; never shared by two models).  Returns the grid size."""
-    if check:
-        _check_draws(draws, sidx, B, offset)
-        N.check_cuda(sync, "sync", torch.int32)
-        if sync.numel() < SYNC_WORDS:
-            raise ValueError("sync must hold SYNC_WORDS int32")
-        if slabs.dim() != 2 or slabs.shape[1] != SLAB_STRIDE or loss_slabs.numel() < slabs.shape[0]:
-            raise ValueError("slabs must be [nslab, SLAB_STRIDE]")
-    nslab = max(1, min(slabs.shape[0], (B + 127) // 128, 256))
-    N.call("em_mlp_fused_step", draws.data_ptr(), sidx.data_ptr() if sidx is not None else None, B, offset,
-           img.data_ptr(), slabs.data_ptr(), loss_slabs.data_ptr(), nslab, LOSS_KINDS[loss], params.data_ptr(),
-           m.data_ptr(), v.data_ptr(), hp.data_ptr(), state.data_ptr(), sync.data_ptr(), loss_out.data_ptr(),
-           float(grad_scale), float(loss_scale), N.stream_handle(draws.device))
     return nslab
 
 

@@ -24,12 +24,11 @@ def _ref_grads(sd, ds_numbers, offset, B, loss, bf16=True):
     return l.item(), {"l1.weight": W1.grad, "l1.bias": b1.grad, "l2.weight": W2.grad, "l2.bias": b2.grad}, z.detach()
 
 
-@pytest.fixture(params=["one-launch", "split"])
-def kernel(request, monkeypatch):
-    """Run the test on both step forms: the one-launch step (train kernel with the in-launch Adam
-    epilogue, the default) and the split form (train kernel, then em_adam_slab)."""
-    monkeypatch.setenv("EUROM_FUSED_ADAM", "1" if request.param == "one-launch" else "0")
-    yield request.param
+@pytest.fixture
+def kernel():
+    """The optimizer step form under test: the train kernel, then em_adam_slab (the one-launch form
+    with an in-kernel Adam epilogue was measured slower and removed in round 4)."""
+    yield "split"
 
 
 def _assert_grads_close(gk, gr, tol=1e-2):
@@ -218,55 +217,6 @@ def test_fused_grads_property_random_batches(kernel):
         _assert_grads_close(gk, gr, tol=1e-2 if B >= 256 else 3e-2)
 
     check()
-
-
-def test_one_launch_step_equals_split_step(data):
-    """The one-launch step (slab reduction + Adam inside the train kernel, cross-workgroup hand-off)
-    and the split step (train kernel, then em_adam_slab) give bit-identical parameters, moments,
-    weight images, losses and step counters over several steps and batch sizes (grid sizes 1..256)."""
-    from euromillioner_amd.models.mlp import FusedSmallMLP
-
-    _, draws = data
-    for loss in ("softmax", "bce"):
-        a = FusedSmallMLP(loss=loss, seed=6, lr=3e-3, fused_adam=True)
-        b = FusedSmallMLP(loss=loss, seed=6, lr=3e-3, fused_adam=False)
-        for it, B in enumerate((5000, 37, 128, 129, 4096, 1)):
-            la = float(a.step(draws, B, offset=13 * it).item())
-            lb = float(b.step(draws, B, offset=13 * it).item())
-            assert la == lb, (loss, B, la, lb)
-        torch.cuda.synchronize()
-        a.check_comm()
-        assert int(a.state[0]) == int(b.state[0]) == 6
-        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
-        assert torch.equal(a.img, b.img)
-
-
-def test_one_launch_step_replays_from_graph(data):
-    """hipGraph capture of the one-launch step (the bench's form): replays equal eager steps bit for
-    bit, i.e. the epoch-tagged flags / dequeue head / step counter re-arm themselves every launch."""
-    from euromillioner_amd.models.mlp import FusedSmallMLP
-
-    _, draws = data
-    a = FusedSmallMLP(loss="softmax", seed=8, lr=3e-3)
-    b = FusedSmallMLP(loss="softmax", seed=8, lr=3e-3)
-    B = 4096
-    a.step(draws, B, offset=0)  # first launch eager (argument checks), then capture
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g, stream=s):
-            a.step(draws, B, offset=100)
-    torch.cuda.current_stream().wait_stream(s)
-    for _ in range(5):
-        g.replay()
-    b.step(draws, B, offset=0)
-    for _ in range(5):
-        b.step(draws, B, offset=100)
-    torch.cuda.synchronize()
-    a.check_comm()
-    assert int(a.state[0]) == int(b.state[0]) == 6
-    assert torch.equal(a.params, b.params) and torch.equal(a.img, b.img)
 
 
 @pytest.mark.parametrize("loss", ["softmax", "bce"])

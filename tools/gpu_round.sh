@@ -2,8 +2,6 @@
 # Round-3 GPU measurements as named stages (run through gpurun; every GPU step has its own time
 # limit and a failing step ends the script).  Outputs under gpurun_out/round/<stage>/.
 #   bash tools/gpu_round.sh full            GPU suite + smoke() + driver-shape and default bench
-#   bash tools/gpu_round.sh fused-ab        same-box A/B: two-launch vs one-launch step (+ the round-2
-#                                           library when euromillioner_amd/lib/ab/old.so exists)
 #   bash tools/gpu_round.sh headline-prof   kernel trace + 2 PMC passes of the headline step, phase
 #                                           stamps when the FUSED_STAMPS side build lib/ab/stamps.so exists
 #   bash tools/gpu_round.sh gbdt            GBDT GPU tests, kernel trace of the 183k-row case, gbdt_bench
@@ -26,13 +24,6 @@ for stage in "$@"; do
     timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail $O/bench_driver.err; exit 5; }
     timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 6; }
     summ $O/bench_driver.json driver && summ $O/bench_default.json default || exit 7
-    ;;
-  fused-ab)
-    ARMS="split|EUROM_FUSED_ADAM=0;fused|EUROM_FUSED_ADAM=1"
-    [ -f euromillioner_amd/lib/ab/old.so ] && ARMS="old|EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/old.so;$ARMS"
-    rm -rf gpurun_out/ab
-    ARMS="$ARMS" ROUNDS=${ROUNDS:-3} bash tools/gpu_ab.sh || exit 8
-    cp gpurun_out/ab/results.jsonl $O/
     ;;
   headline-prof)
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 200 --warmup 5 --no-eval > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 9; }
