@@ -17,6 +17,7 @@
 //   K13 gbdt_metric     logloss / rmse / error partial sums -> per-round history
 // Node numbering is heap order (children 2i+1, 2i+2); status 0 unused / 1 split / 2 leaf.
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -47,9 +48,19 @@ EM_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
+// Replayed rounds (em_gbdt_fit's hipGraph path): `rd` points at the device round counter and the
+// per-round tree arrays / history / predict range are offset by it in-kernel, so every round is the
+// same kernel sequence; the eager paths pass rd = nullptr and pre-offset pointers.
+EM_DEVICE int64_t rd_off(const int* rd, int64_t stride) { return rd ? (int64_t)(*rd) * stride : 0; }
+
 // per-round tree reset: status/feature/bin/gain cleared, every task's root opened (status 2)
 __global__ void gbdt_round_init(int8_t* __restrict__ st, int16_t* __restrict__ fe, uint8_t* __restrict__ sb,
-                                float* __restrict__ gn, int total, int NN) {
+                                float* __restrict__ gn, int total, int NN, const int* __restrict__ rd) {
+  const int64_t o = rd_off(rd, total);
+  st += o;
+  fe += o;
+  sb += o;
+  gn += o;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     st[i] = (i % NN) == 0 ? 2 : 0;
     fe[i] = -1;
@@ -66,7 +77,8 @@ __global__ void gbdt_init_margin(float* __restrict__ margin, int64_t total, floa
 // margin/g/h/node: [T][n]; Y: [n][T]
 __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restrict__ Y, float* __restrict__ g,
                           float* __restrict__ h, int16_t* __restrict__ node, int T, int n, int obj, float subsample,
-                          uint32_t seed, int round) {
+                          uint32_t seed, int round, const int* __restrict__ rd) {
+  if (rd) round = *rd;
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
@@ -488,8 +500,15 @@ __global__ void __launch_bounds__(256)
 gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
            int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
            int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
-           double qinv) {
+           double qinv, const int* __restrict__ rd) {
   constexpr bool Q = std::is_same<A, long long>::value;
+  {
+    const int64_t o = rd_off(rd, (int64_t)T * NN);
+    status += o;
+    feat += o;
+    sbin += o;
+    gain += o;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
@@ -622,7 +641,13 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
 
 __global__ void gbdt_partition(const uint8_t* __restrict__ bins, int16_t* __restrict__ node, int T, int n, int F,
                                int NN, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
-                               const uint8_t* __restrict__ sbin, int level) {
+                               const uint8_t* __restrict__ sbin, int level, const int* __restrict__ rd) {
+  {
+    const int64_t o = rd_off(rd, (int64_t)T * NN);
+    status += o;
+    feat += o;
+    sbin += o;
+  }
   const int first = (1 << level) - 1, last = (1 << (level + 1)) - 1;
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -639,9 +664,18 @@ __global__ void gbdt_partition(const uint8_t* __restrict__ bins, int16_t* __rest
 // one thread per task: prune (gamma) bottom-up, leaf values, cover
 __global__ void gbdt_finalize(int T, int NN, int max_depth, int8_t* __restrict__ status, int16_t* __restrict__ feat,
                               const float* __restrict__ gain, const double* __restrict__ G, const double* __restrict__ H,
-                              float* __restrict__ leaf, float* __restrict__ cover, double lam, float gamma, double eta) {
+                              float* __restrict__ leaf, float* __restrict__ cover, double lam, float gamma, double eta,
+                              const int* __restrict__ rd) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
+  {
+    const int64_t ro = rd_off(rd, (int64_t)T * NN);
+    status += ro;
+    feat += ro;
+    gain += ro;
+    leaf += ro;
+    cover += ro;
+  }
   int8_t* st = status + (int64_t)t * NN;
   const int64_t o = (int64_t)t * NN;
   for (int i = (1 << max_depth) - 2; i >= 0; --i) {
@@ -664,7 +698,10 @@ EM_DEVICE int leaf_ancestor(const int8_t* st, int nd) {
 }
 
 __global__ void gbdt_update(float* __restrict__ margin, const int16_t* __restrict__ node, int T, int n, int NN,
-                            const int8_t* __restrict__ status, const float* __restrict__ leaf) {
+                            const int8_t* __restrict__ status, const float* __restrict__ leaf,
+                            const int* __restrict__ rd) {
+  status += rd_off(rd, (int64_t)T * NN);
+  leaf += rd_off(rd, (int64_t)T * NN);
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i / n);
@@ -676,7 +713,12 @@ __global__ void gbdt_update(float* __restrict__ margin, const int16_t* __restric
 // K11: margin[t][r] += sum over trees k in [k0, k1) (task of tree k = k % T) — traversal on bins
 __global__ void gbdt_predict(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F, int NN,
                              int k0, int k1, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
-                             const uint8_t* __restrict__ sbin, const float* __restrict__ leaf) {
+                             const uint8_t* __restrict__ sbin, const float* __restrict__ leaf,
+                             const int* __restrict__ rd) {
+  if (rd) {  // trees of round *rd: [k0, k1) shifted by round * T
+    k0 += *rd * T;
+    k1 += *rd * T;
+  }
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
@@ -755,7 +797,9 @@ EM_DEVICE double block_sum_partials(const double* __restrict__ partial, int nb) 
 }
 
 __global__ void __launch_bounds__(256)
-gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int metric, float* __restrict__ out) {
+gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int metric, float* __restrict__ out,
+                  const int* __restrict__ rd = nullptr, int ostride = 0) {
+  out += rd_off(rd, ostride);
   const double s = block_sum_partials(partial, nb);
   if (threadIdx.x == 0) {
     double v = s / (double)(count > 0 ? count : 1);
@@ -925,6 +969,39 @@ bool valid_foff(const int* foff, int F) {
     if (foff[f + 1] - foff[f] < 1 || foff[f + 1] - foff[f] > 256) return false;
   return true;
 }
+
+__global__ void gbdt_round_set(int* rd, int v) {
+  if (threadIdx.x == 0) *rd = v;
+}
+__global__ void gbdt_round_advance(int* rd) {
+  if (threadIdx.x == 0) *rd += 1;
+}
+
+// every argument a captured round depends on (compared bytewise: zero-filled before use)
+struct GbdtGraphKey {
+  const void* p[18];
+  const void* ev[4][3];
+  int evn[4];
+  int i[9];
+  float f[5];
+  int64_t pd;
+  int foff[320];
+};
+struct GraphCache {
+  hipGraphExec_t exec = nullptr;
+  int* rd = nullptr;        // device round counter
+  hipStream_t cap = nullptr;  // capture stream (the caller's may be the legacy default stream)
+  int dev = -1;
+  GbdtGraphKey key;
+  void reset() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    exec = nullptr;
+  }
+};
+GraphCache& graph_cache() {
+  static GraphCache c;
+  return c;
+}
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
@@ -1019,58 +1096,116 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       }
     }
   } qfree{qmem, stream};
-  for (int round = r0; round < r1; ++round) {
-    int8_t* st = status + (int64_t)round * T * NN;
-    int16_t* fe = feat + (int64_t)round * T * NN;
-    uint8_t* sb = sbin + (int64_t)round * T * NN;
-    float* lf = leaf + (int64_t)round * T * NN;
-    float* gn = gainv + (int64_t)round * T * NN;
-    float* cv = cover + (int64_t)round * T * NN;
-    hipLaunchKernelGGL(gbdt_round_init, dim3(grid_for((int64_t)T * NN)), dim3(256), 0, stream, st, fe, sb, gn, T * NN,
-                       NN);
-    hipLaunchKernelGGL(gbdt_grad, dim3(grid_for(TN)), dim3(256), 0, stream, margin, Y, g, h, node, T, n, obj, subsample,
-                       seed, round);
+  // one round's kernel sequence.  rd == nullptr: the arrays of `round` are addressed from the host;
+  // rd = the device round counter: every round-dependent offset is taken in-kernel (round = 0 here),
+  // so the identical sequence is captured once and replayed for every round
+  auto enqueue_round = [&](int round, const int* rd, hipStream_t s) -> int {
+    const int64_t ro = (int64_t)round * T * NN;
+    int8_t* st = status + ro;
+    int16_t* fe = feat + ro;
+    uint8_t* sb = sbin + ro;
+    float* lf = leaf + ro;
+    float* gn = gainv + ro;
+    float* cv = cover + ro;
+    hipLaunchKernelGGL(gbdt_round_init, dim3(grid_for((int64_t)T * NN)), dim3(256), 0, s, st, fe, sb, gn, T * NN, NN,
+                       rd);
+    hipLaunchKernelGGL(gbdt_grad, dim3(grid_for(TN)), dim3(256), 0, s, margin, Y, g, h, node, T, n, obj, subsample,
+                       seed, round, rd);
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
       int nch = 1;
       const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles,
-                                       false, qscale, &nch, stream, qa.nb ? &qa : nullptr);
+                                       false, qscale, &nch, s, qa.nb ? &qa : nullptr);
       if (rc) return rc;
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
       const int64_t cstride = (int64_t)T * nodesL * C * 2;
       const size_t slds = nch > 1 ? (size_t)C * 16 : 0;
       if (quant_bits)
-        hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, stream,
+        hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, s,
                            reinterpret_cast<const long long*>(partial), nch, cstride, foff_d, T, F, C, level, NN, Gs,
-                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv);
+                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, rd);
       else
-        hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, stream, partial, nch, cstride,
-                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0);
-      hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, st, fe, sb,
-                         level);
+        hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, s, partial, nch, cstride,
+                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, rd);
+      hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, s, bins, node, T, n, F, NN, st, fe, sb,
+                         level, rd);
     }
-    hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, stream, T, NN, max_depth, st, fe, gn, Gs, Hs,
-                       lf, cv, (double)lam, gamma, (double)eta);
-    hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, stream, margin, node, T, n, NN, st, lf);
-    // metrics (train + evals)
+    hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, s, T, NN, max_depth, st, fe, gn, Gs, Hs, lf,
+                       cv, (double)lam, gamma, (double)eta, rd);
+    hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd);
+    // metrics (train + evals) into hist_out[round]
+    const int hs = 1 + n_evals;
+    float* ho = hist_out + (int64_t)round * hs;
     const int mb_train = grid_for(TN);
-    hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, stream, margin, Y, T, n, obj, metric, mpart);
-    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, stream, mpart, mb_train,
-                       metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, hist_out + (int64_t)round * (1 + n_evals));
+    hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, s, margin, Y, T, n, obj, metric, mpart);
+    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb_train,
+                       metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, ho, rd, hs);
     for (int e = 0; e < n_evals; ++e) {
       const int64_t TE = (int64_t)T * evals[e].n;
-      const int64_t k0 = (int64_t)round * T;
-      hipLaunchKernelGGL(gbdt_predict, dim3(grid_for(TE)), dim3(256), 0, stream, evals[e].bins, evals[e].margin, T,
-                         evals[e].n, F, NN, (int)k0, (int)(k0 + T), status, feat, sbin, leaf);
+      const int k0 = round * T;
+      hipLaunchKernelGGL(gbdt_predict, dim3(grid_for(TE)), dim3(256), 0, s, evals[e].bins, evals[e].margin, T,
+                         evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf, rd);
       const int mb = grid_for(TE);
-      hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, stream, evals[e].margin, evals[e].Y, T, evals[e].n, obj,
+      hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, s, evals[e].margin, evals[e].Y, T, evals[e].n, obj,
                          metric, mpart);
-      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, stream, mpart, mb,
-                         metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric,
-                         hist_out + (int64_t)round * (1 + n_evals) + 1 + e);
+      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb,
+                         metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric, ho + 1 + e, rd, hs);
     }
+    if (rd) hipLaunchKernelGGL(gbdt_round_advance, dim3(1), dim3(64), 0, s, const_cast<int*>(rd));
     EM_CHECK_LAUNCH();
+    return 0;
+  };
+  // Launch-bound fits (the reference's ~1k rows: ~20 tiny kernels per round) replay one captured
+  // round instead: host enqueue cost per round drops from ~20 launches to one graph launch.  The
+  // graph is cached across calls with the same arguments (the Python driver calls per 25 rounds);
+  // EM_GBDT_GRAPH=0 keeps the eager loop.  Same kernels and arguments: bit-identical trees.
+  static const bool graph_on = !(getenv("EM_GBDT_GRAPH") && getenv("EM_GBDT_GRAPH")[0] == '0');
+  if (graph_on && r1 - r0 >= 2 && !qmem) {
+    GraphCache& gc = graph_cache();
+    GbdtGraphKey key;
+    std::memset(&key, 0, sizeof(key));
+    key.p[0] = bins; key.p[1] = Y; key.p[2] = foff_d; key.p[3] = margin; key.p[4] = g; key.p[5] = h;
+    key.p[6] = node; key.p[7] = partial; key.p[8] = Gs; key.p[9] = Hs; key.p[10] = mpart; key.p[11] = status;
+    key.p[12] = feat; key.p[13] = sbin; key.p[14] = leaf; key.p[15] = gainv; key.p[16] = cover; key.p[17] = hist_out;
+    for (int e = 0; e < n_evals && e < 4; ++e) {
+      key.ev[e][0] = evals[e].bins; key.ev[e][1] = evals[e].Y; key.ev[e][2] = evals[e].margin;
+      key.evn[e] = evals[e].n;
+    }
+    key.i[0] = n; key.i[1] = F; key.i[2] = T; key.i[3] = n_evals; key.i[4] = max_depth; key.i[5] = obj;
+    key.i[6] = metric; key.i[7] = quant_bits; key.i[8] = (int)seed;
+    key.f[0] = eta; key.f[1] = lam; key.f[2] = gamma; key.f[3] = mcw; key.f[4] = subsample;
+    key.pd = partial_doubles;
+    for (int f = 0; f <= F && f < 320; ++f) key.foff[f] = foff_h[f];
+    if (n_evals <= 4 && F < 320) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (!gc.exec || gc.dev != dev || std::memcmp(&gc.key, &key, sizeof(key)) != 0) {
+        gc.reset();
+        if (!gc.rd) {
+          if (hipError_t e = hipMalloc(&gc.rd, sizeof(int))) return (int)e;
+          if (hipError_t e = hipStreamCreateWithFlags(&gc.cap, hipStreamNonBlocking)) return (int)e;
+        }
+        hipGraph_t graph = nullptr;
+        if (hipError_t e = hipStreamBeginCapture(gc.cap, hipStreamCaptureModeThreadLocal)) return (int)e;
+        const int rc = enqueue_round(0, gc.rd, gc.cap);
+        const hipError_t ec = hipStreamEndCapture(gc.cap, &graph);
+        if (rc) return rc;
+        if (ec != hipSuccess) return (int)ec;
+        const hipError_t ei = hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return (int)ei;
+        gc.key = key;
+        gc.dev = dev;
+      }
+      hipLaunchKernelGGL(gbdt_round_set, dim3(1), dim3(64), 0, stream, gc.rd, r0);
+      for (int round = r0; round < r1; ++round)
+        if (hipError_t e = hipGraphLaunch(gc.exec, stream)) return (int)e;
+      EM_CHECK_LAUNCH();
+      return 0;
+    }
   }
+  for (int round = r0; round < r1; ++round)
+    if (int rc = enqueue_round(round, nullptr, stream)) return rc;
   return 0;
 }
 
@@ -1088,7 +1223,7 @@ EM_API int em_gbdt_predict(const uint8_t* bins, float* margin, int T, int n, int
   if (n == 0) return 0;
   const int NN = (1 << (max_depth + 1)) - 1;
   hipLaunchKernelGGL(gbdt_predict, dim3(grid_for((int64_t)T * n)), dim3(256), 0, stream, bins, margin, T, n, F, NN, k0,
-                     k1, status, feat, sbin, leaf);
+                     k1, status, feat, sbin, leaf, (const int*)nullptr);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1105,9 +1240,9 @@ EM_API int em_gbdt_dp_round_begin(int round, int T, int n, int max_depth, const 
   const int NN = (1 << (max_depth + 1)) - 1;
   const int64_t TN = (int64_t)T * n;
   hipLaunchKernelGGL(gbdt_round_init, dim3(grid_for((int64_t)T * NN)), dim3(256), 0, stream, status, feat, sbin, gainv,
-                     T * NN, NN);
+                     T * NN, NN, (const int*)nullptr);
   hipLaunchKernelGGL(gbdt_grad, dim3(grid_for(TN)), dim3(256), 0, stream, margin, Y, g, h, node, T, n, obj, subsample,
-                     seed, round);
+                     seed, round, (const int*)nullptr);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1139,9 +1274,9 @@ EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* 
   const int64_t TN = (int64_t)T * n;
   const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
   hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C,
-                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0);
+                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, (const int*)nullptr);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
-                     sbin, level);
+                     sbin, level, (const int*)nullptr);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1153,8 +1288,9 @@ EM_API int em_gbdt_dp_round_end(int T, int n, int max_depth, float* margin, cons
   const int NN = (1 << (max_depth + 1)) - 1;
   const int64_t TN = (int64_t)T * n;
   hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, stream, T, NN, max_depth, status, feat, gainv,
-                     Gs, Hs, leaf, cover, (double)lam, gamma, (double)eta);
-  hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, stream, margin, node, T, n, NN, status, leaf);
+                     Gs, Hs, leaf, cover, (double)lam, gamma, (double)eta, (const int*)nullptr);
+  hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, stream, margin, node, T, n, NN, status, leaf,
+                     (const int*)nullptr);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -218,19 +218,40 @@ EM_DEVICE bf16x8 nib_xfrag(const char* smem, uint32_t w, int q) {
 // unrolled over the ring slots (spills), XCD-major stream numbering (-0.5 %).
 //
 // slot: H0 4K | H1 4K | D2 4K | X image 4K
+#ifndef FUSED_V7
+#define FUSED_V7 0
+#endif
+// FUSED_SHARED: one tile stream per workgroup, 4 forward waves (tiles f, f + 4, ...) and 4 backward
+// waves (hidden half rho x tile parity pi) sharing one ring; 0: two independent units of 2 + 2 waves
+#ifndef FUSED_SHARED
+#define FUSED_SHARED 1
+#endif
+#ifndef FUSED_RECYCLE
+#define FUSED_RECYCLE 1
+#endif
 constexpr int V6_SLOT = 16384;
-constexpr int V6_RSLOTS = 3;               // slots per unit in the ring area
-constexpr int V6_NSLOT = V6_RSLOTS + 1;    // + the recycled weight-image slot
-static_assert(2 * V6_SLOT <= IMG_W2Q, "recycled slots must fit below the W2Q image");
+constexpr int V6_NSTREAM = FUSED_SHARED ? 1 : 2;  // tile streams (rings) per workgroup
+constexpr int V6_NF = FUSED_SHARED ? 4 : 2;       // forward waves per stream
+constexpr int V6_NBP = FUSED_SHARED ? 2 : 1;      // backward waves per hidden half (tile parities)
+constexpr int V6_RSLOTS = FUSED_SHARED ? 6 : 3;   // slots per stream in the ring area
+// + the recycled weight-image slots (v6: the W1ᵀ / W2ᵀ images are dead once the forward waves hold
+// their weights in registers).  v7's forward waves read them every tile, so they stay.
+constexpr int V6_NREC = (FUSED_V7 || !FUSED_RECYCLE) ? 0 : 2 / V6_NSTREAM;
+constexpr int V6_NSLOT = V6_RSLOTS + V6_NREC;
+static_assert(V6_NREC == 0 || 2 * V6_SLOT <= IMG_W2Q, "recycled slots must fit below the W2Q image");
+static_assert(V6_NSLOT % V6_NBP == 0, "a slot's tiles share one parity");
 constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
-constexpr int V6_FLAGS = V6_YLUT + 256;  // [2 units][16 ints]: full[N] | done0[N] | done1[N]
-constexpr int V6_RING = V6_FLAGS + 128;  // [2 units][3 slots][16 KB]
-constexpr int V6_LOOP_LDS = V6_RING + 2 * V6_RSLOTS * V6_SLOT;
-// byte offset of ring slot `slot` of unit `unit`
-EM_DEVICE uint32_t v6_slot(int unit, int slot) {
-  return slot < V6_RSLOTS ? V6_RING + (unit * V6_RSLOTS + slot) * V6_SLOT : unit * V6_SLOT;
+constexpr int V6_FLAGS = V6_YLUT + 256;  // [streams][32 / streams ints]: full[N] | done0[N] | done1[N]
+constexpr int V6_FLAG_STRIDE = 128 / V6_NSTREAM;
+static_assert(3 * V6_NSLOT * 4 <= V6_FLAG_STRIDE, "flag words");
+constexpr int V6_RING = V6_FLAGS + 128;  // [streams][ring slots][16 KB]
+constexpr int V6_LOOP_LDS = V6_RING + V6_NSTREAM * V6_RSLOTS * V6_SLOT;
+// byte offset of slot `slot` of stream `st`
+EM_DEVICE uint32_t v6_slot(int st, int slot) {
+  return slot < V6_RSLOTS ? V6_RING + (st * V6_RSLOTS + slot) * V6_SLOT
+                          : (FUSED_SHARED ? slot - V6_RSLOTS : st) * V6_SLOT;
 }
 constexpr int V6_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below, DB2S [2][64] + LOSSS [8] above
 constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 2048);
@@ -254,34 +275,34 @@ EM_DEVICE void v6_wait(const char* smem, uint32_t off, int target, bool& ok) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// stream index U of unit `unit` of this block (tiles U, U + nunits, ...)
-EM_DEVICE int v6_unit_id(int unit) { return blockIdx.x * 2 + unit; }
+// tile stream `st` of this block: global stream U, tiles U, U + nunits, ...
+EM_DEVICE int v6_unit_id(int st) { return blockIdx.x * V6_NSTREAM + st; }
 
 EM_DEVICE int v6_ntiles_of_unit(int B, int U, int nunits) {
   const int ntiles = (B + 31) / 32;
   return U < ntiles ? (ntiles - U + nunits - 1) / nunits : 0;
 }
 
-// forward wave F (0/1) of unit `unit`: tiles k = F, F + 2, ... of the unit's stream
-template <int LOSS, int F>
+// forward wave f of stream `unit`: tiles k = f, f + V6_NF, ... of the stream
+template <int LOSS, bool SIDX>
 EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                          int offset, int unit, int lane, float& loss_acc, bool& ok, Stamps& st) {
+                          int offset, int unit, int f, int lane, float& loss_acc, bool& ok, Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
-  const int nunits = gridDim.x * 2, U = v6_unit_id(unit);
+  const int nunits = gridDim.x * V6_NSTREAM, U = v6_unit_id(unit);
   const int K = v6_ntiles_of_unit(B, U, nunits);
-  const uint32_t FL = V6_FLAGS + unit * 64;
+  const uint32_t FL = V6_FLAGS + unit * V6_FLAG_STRIDE;
+  // Branch-free prefetch of the next tile's masks: samples past the stream read sample 0 (valid when
+  // K > 0) and are masked at use.  An exec-masked load here made the compiler wait vmcnt(0) right
+  // after issuing it -- one HBM round trip (~900 cycles) per forward tile, round 3's "F wait slot".
   auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {
     const int s = (U + k * nunits) * 32 + r;
-    mi = 0;
-    mt = 0;
-    if (k < K && s < B) {
-      const int idx = sidx ? sidx[s] : (offset + s);
-      mi = masks[idx];
-      mt = masks[idx + 1];
-    }
+    const int sc = (k < K && s < B) ? s : 0;
+    const int idx = SIDX ? sidx[sc] : (offset + sc);
+    mi = masks[idx];
+    mt = masks[idx + 1];
   };
   uint64_t nin = 0, ntg = 0;
-  fetch(F, nin, ntg);
+  if (K > 0) fetch(f, nin, ntg);
   // the forward wave's weight fragments (W1ᵀ 4 x 4, W2ᵀ 2 x 8: 128 VGPRs) stay in registers for the
   // whole launch: no LDS read stands between the tile's operands and its 32 MFMAs
   bf16x8 w1r[4][4], w2r[2][8];
@@ -394,25 +415,376 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     lds_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
   };
-  for (int k = F; k < K; k += 2) ftile(k, k % V6_NSLOT, k + 2);
+  for (int k = f; k < K; k += V6_NF) ftile(k, k % V6_NSLOT, k + V6_NF);
+}
+
+// ============================================================================================
+// v7 forward wave: a two-tile software pipeline.  v6's forward wave ran one tile's chain
+// X -> F1 -> relu -> F2 -> softmax -> dZ2 alone, and phase stamps put it at ~4.2 k active cycles per
+// tile with the matrix pipe idle beside the softmax (profiles/r3/fused_timeline_stamps.txt).  Here one
+// iteration finishes tile k's grouped softmax + dZ2 on the VALU while the same wave's 32 MFMAs run
+// tile k + 2's F1 and F2 (the two tiles share nothing, so every VALU step has a whole MFMA slot to
+// issue into; cdna_hip_programming.md T15).  The program order is pinned by sched_barrier fences:
+// 32 slots = {one MFMA, the LDS read of the weight fragment four slots ahead, one softmax step or one
+// relu/pack of F1's output}.  The weights come from the LDS images every tile (32 ds_read_b128): the
+// registers hold two tiles' state instead, and the W1ᵀ / W2ᵀ images stay (3 ring slots per unit).
+// H / X images of tile k + 2 are written into its ring slot at the end of the iteration that staged
+// it (hT / xf stay in registers until then), dZ2 at the end of the next one, then FULL.
+//
+// MFMA slot schedule (F1 hidden tile t = 4 MFMAs over the 64 features; F2 step kk = 16 hidden rows
+// for both output tiles u):
+//   0-3 F1 t0 | 4-7 F1 t1 | 8-11 F2 kk0,1 | 12-15 F1 t2 | 16-19 F2 kk2,3 | 20-23 F1 t3 | 24-31 F2 kk4-7
+// relu/pack of hidden tile t two slots after its last MFMA (slots 5,6 / 9,10 / 17,18 / 25,26).
+template <int N, typename Fn>
+EM_DEVICE void static_for(Fn&& fn) {  // fn(integral_constant<0>) ... fn(integral_constant<N - 1>), in order
+  if constexpr (N > 0) {
+    static_for<N - 1>(fn);
+    fn(std::integral_constant<int, N - 1>{});
+  }
+}
+struct V7Mfma {
+  int kind, a, b;  // kind 0: F1 (t, q), 1: F2 (u, kk)
+};
+EM_DEVICE constexpr V7Mfma v7_mfma(int m) {
+  return m < 8 ? V7Mfma{0, m >> 2, m & 3}
+       : m < 12 ? V7Mfma{1, m & 1, (m - 8) >> 1}
+       : m < 16 ? V7Mfma{0, 2, m & 3}
+       : m < 20 ? V7Mfma{1, m & 1, 2 + ((m - 16) >> 1)}
+       : m < 24 ? V7Mfma{0, 3, m & 3}
+                : V7Mfma{1, m & 1, 4 + ((m - 24) >> 1)};
+}
+// relu/pack placed at slot m: hidden tile t, fragment q (-1 = none)
+EM_DEVICE constexpr int v7_relu(int m) {
+  return m == 5 ? 0 : m == 6 ? 1 : m == 9 ? 2 : m == 10 ? 3 : m == 17 ? 4 : m == 18 ? 5 : m == 25 ? 6
+       : m == 26 ? 7 : -1;
+}
+// softmax step j placed at slot m (-1 = none): the 24 slots without a relu
+EM_DEVICE constexpr int v7_sm_step(int m) {
+  return m < 5 ? m : m < 7 ? -1 : m < 9 ? m - 2 : m < 11 ? -1 : m < 17 ? m - 4 : m < 19 ? -1 : m < 25 ? m - 6
+       : m < 27 ? -1 : m - 8;
+}
+constexpr int V7_LEAD = 4;  // weight fragments are read this many MFMA slots ahead
+
+template <int LOSS, bool SIDX>
+EM_DEVICE void v7_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                          int offset, int unit, int f, int lane, float& loss_acc, bool& ok, Stamps& st) {
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  const int r = lane & 31, h = lane >> 5;
+  const bool h0 = h == 0;
+  const int nunits = gridDim.x * V6_NSTREAM, U = v6_unit_id(unit);
+  const int K = v6_ntiles_of_unit(B, U, nunits);
+  const uint32_t FL = V6_FLAGS + unit * V6_FLAG_STRIDE;
+  // branch-free prefetch (an exec-masked load made the compiler wait for it at once): samples past the
+  // stream read sample 0 (valid whenever K > 0); the caller masks them by validity
+  auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {
+    const int s = (U + k * nunits) * 32 + r;
+    const int sc = (k < K && s < B) ? s : 0;
+    const int idx = SIDX ? sidx[sc] : (offset + sc);
+    mi = masks[idx];
+    mt = masks[idx + 1];
+  };
+  // keep a step's results where the step computes them: without it LLVM sinks the dZ2 work into the
+  // `if (has_c)` image write after the MFMA slots (sched_barrier orders only within a block)
+  auto pin = [](auto& x) { asm volatile("" : "+v"(x)); };
+  const uint32_t w1a = w1t_off(r, h), w2a = w2p_off(r, h);
+  auto wfrag = [&](int m) {  // the weight (A) fragment of MFMA slot m
+    const V7Mfma x = v7_mfma(m);
+    return x.kind == 0 ? lds_frag(smem, w1a + x.a * 32 * W1T_RS + x.b * 32)
+                       : lds_frag(smem, w2a + x.a * 32 * W2P_RS + x.b * 32);
+  };
+  __syncthreads();  // matches the backward waves' barrier
+  st.start();
+  uint64_t nin = 0, ntg = 0, tmn = 0;
+  bf16x8 xfn[4], wfn[V7_LEAD];
+  // stage-1 operands of tile kn (X fragments from its mask, the first weight fragments), read at the
+  // end of the previous iteration so that the first MFMA slot finds them in registers
+  auto stage_in = [&](int kn) {
+    const bool validn = kn < K && (U + kn * nunits) * 32 + r < B;
+    const uint64_t imask = validn ? (nin | BIAS_BIT) : 0ull;
+    tmn = validn ? ntg : 0ull;
+    fetch(kn + V6_NF, nin, ntg);
+    const uint32_t wlo = (uint32_t)imask >> (8 * h), whi = (uint32_t)(imask >> 32) >> (8 * h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xfn[q] = nib_xfrag<V6_XLUT>(smem, q < 2 ? wlo : whi, q);
+      wfn[q] = wfrag(q);
+    }
+  };
+  auto stage_pin = [&]() {  // the reads above complete here (else LLVM sinks them to the first MFMA)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pin(xfn[q]);
+      pin(wfn[q]);
+    }
+  };
+  static_assert(V7_LEAD == 4, "stage_in reads the first V7_LEAD weight fragments");
+  if (K > 0) {
+    fetch(f, nin, ntg);
+    stage_in(f);
+    stage_pin();
+  }
+  f32x16 zc[2] = {f32x16{}, f32x16{}};  // logits of the tile being finished (zeros before the first)
+  uint64_t tmc = 0;
+  int kc = -1;
+  for (int kn = f;; kn += V6_NF) {
+    const bool has_c = kc >= 0, has_n = kn < K;
+    if (!has_c && !has_n) break;
+    bf16x8 xf[4], wf[32];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xf[q] = xfn[q];
+      wf[q] = wfn[q];
+    }
+    f32x16 a1[2], z2n[2], b2i[2];
+    bf16x8 hT[4][2];
+
+    // ---- softmax state of tile kc ----
+    const uint32_t tlo = (uint32_t)tmc, thi = (uint32_t)(tmc >> 32);
+    const f32x2 L2E2 = {L2E, L2E};
+    auto zpair = [&](int u, int i) { return f32x2{zc[u][i], zc[u][i + 1]}; };
+    auto exp2p = [](f32x2 t) { return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)}; };
+    float mxa[4], mm = 0.f, ms = 0.f, yb[2][16];
+    f32x2 nmL2 = {0.f, 0.f}, nsL2 = {0.f, 0.f};
+    f32x2 sm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, ss = {0.f, 0.f};
+    f32x2 tdm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, tds = {0.f, 0.f};
+    int nm = 0, ns = 0;
+    float inv_m = 0.f, inv_s = 0.f, S = 1.f, Ss = 1.f, fm = 0.f, fs = 0.f;
+    u32x4 dpk[2][2];
+    auto targets = [&](int u) {
+      const uint32_t tmh = (u == 0 ? tlo : thi) >> (4 * h);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + V6_YLUT + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+        yb[u][4 * g + 0] = y4[0]; yb[u][4 * g + 1] = y4[1]; yb[u][4 * g + 2] = y4[2]; yb[u][4 * g + 3] = y4[3];
+      }
+    };
+    // dz of element (u, i) from its exp e (stored in zc) and target
+    auto dzv = [&](int u, int i) {
+      const int c0 = out_cls(u, i, 0), c1 = out_cls(u, i, 1);
+      const float e = zc[u][i], y = yb[u][i];
+      if (c0 == c1) {
+        if (c0 == 0) return __builtin_fmaf(e, fm, y * -inv_m);
+        if (c0 == 1) return __builtin_fmaf(e, fs, y * -inv_s);
+        return 0.f;
+      }
+      if (c0 == 0) return __builtin_fmaf(e, h0 ? fm : fs, y * (h0 ? -inv_m : -inv_s));
+      return __builtin_fmaf(e, fs, y * -inv_s);  // star (h = 0) / pad (h = 1): the pad's e and y are 0
+    };
+    auto sm_step = [&](auto J) {
+      constexpr int j = decltype(J)::value;
+      if constexpr (LOSS != 0) return;
+      if constexpr (j == 0) {  // main max over output tile 0 (all main); targets of tile 0
+        mxa[0] = zc[0][0]; mxa[1] = zc[0][1]; mxa[2] = zc[0][2]; mxa[3] = zc[0][3];
+#pragma unroll
+        for (int i = 4; i < 16; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], zc[0][i]);
+        targets(0);
+        for (int k = 0; k < 4; ++k) pin(mxa[k]);
+      } else if constexpr (j == 1) {  // tile 1: 32..49 main (elements 0..7, and 8, 9 for h = 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], zc[1][i]);
+        mxa[0] = h0 ? fmaxf(mxa[0], zc[1][8]) : mxa[0];
+        mxa[1] = h0 ? fmaxf(mxa[1], zc[1][9]) : mxa[1];
+        for (int k = 0; k < 4; ++k) pin(mxa[k]);
+      } else if constexpr (j == 2) {
+        mm = xhalf_max(fmaxf(fmaxf(mxa[0], mxa[1]), fmaxf(mxa[2], mxa[3])));
+        nmL2 = f32x2{-mm * L2E, -mm * L2E};
+        pin(nmL2);
+      } else if constexpr (j == 3) {  // star max: elements 10..13 both halves, 14/15 (h = 0) or 8/9 (h = 1)
+        const float a = fmaxf(fmaxf(zc[1][10], zc[1][11]), fmaxf(zc[1][12], zc[1][13]));
+        const float b = fmaxf(h0 ? zc[1][14] : zc[1][8], h0 ? zc[1][15] : zc[1][9]);
+        ms = xhalf_max(fmaxf(a, b));
+        nsL2 = f32x2{-ms * L2E, -ms * L2E};
+        targets(1);
+        pin(nsL2);
+      } else if constexpr (j == 4) {
+        nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
+        ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
+        inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
+        inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
+        pin(inv_m);
+        pin(inv_s);
+      } else if constexpr (j < 9) {  // exps of tile 0 (main), two pairs per step
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int i = 4 * (j - 5) + 2 * q;
+          const f32x2 zz = zpair(0, i);
+          f32x2 e = exp2p(pfma(zz, L2E2, nmL2));
+          sm[q] += e;
+          tdm[q] = pfma(f32x2{yb[0][i], yb[0][i + 1]}, zz, tdm[q]);
+          pin(e);
+          zc[0][i] = e.x;
+          zc[0][i + 1] = e.y;
+        }
+        pin(sm[0]);
+        pin(sm[1]);
+        pin(tdm[0]);
+        pin(tdm[1]);
+      } else if constexpr (j < 13) {  // exps of tile 1 (outputs 32..63: main / star / pad by element)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int i = 4 * (j - 9) + 2 * q;
+          const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
+          const f32x2 zz = zpair(1, i), yy = {yb[1][i], yb[1][i + 1]};
+          f32x2 e;
+          if (c0 == c1 && c0 == 0) {
+            e = exp2p(pfma(zz, L2E2, nmL2));
+            sm[q] += e;
+            tdm[q] = pfma(yy, zz, tdm[q]);
+          } else if (c0 == c1 && c0 == 1) {
+            e = exp2p(pfma(zz, L2E2, nsL2));
+            ss += e;
+            tds = pfma(yy, zz, tds);
+          } else if (c0 == 0) {  // main (h = 0) / star (h = 1): outputs 48/49 | 52/53
+            e = exp2p(pfma(zz, L2E2, h0 ? nmL2 : nsL2));
+            const f32x2 ty = yy * zz;
+            sm[q] = h0 ? sm[q] + e : sm[q];
+            ss = h0 ? ss : ss + e;
+            tdm[q] = h0 ? tdm[q] + ty : tdm[q];
+            tds = h0 ? tds : tds + ty;
+          } else {  // star (h = 0) / pad (h = 1): outputs 58/59 | 62/63
+            const f32x2 ex = exp2p(pfma(zz, L2E2, nsL2));
+            e = h0 ? ex : f32x2{0.f, 0.f};
+            ss += e;
+            tds = h0 ? pfma(yy, zz, tds) : tds;
+          }
+          pin(e);
+          zc[1][i] = e.x;
+          zc[1][i + 1] = e.y;
+        }
+        pin(sm[0]);
+        pin(sm[1]);
+        pin(ss);
+        pin(tdm[0]);
+        pin(tdm[1]);
+        pin(tds);
+      } else if constexpr (j == 13) {
+        S = xhalf_sum((sm[0].x + sm[0].y) + (sm[1].x + sm[1].y));
+        Ss = xhalf_sum(ss.x + ss.y);
+        fm = nm ? __builtin_amdgcn_rcpf(S) : 0.f;
+        fs = ns ? __builtin_amdgcn_rcpf(Ss) : 0.f;
+        pin(fm);
+        pin(fs);
+      } else if constexpr (j < 22) {  // dZ2 = p - y / |y| and its bf16 packing, 4 elements per step
+        const int u = (j - 14) >> 2, i = 4 * ((j - 14) & 3);
+        dpk[u][i >> 3][(i & 7) >> 1] = pack2(dzv(u, i), dzv(u, i + 1));
+        dpk[u][i >> 3][((i & 7) >> 1) + 1] = pack2(dzv(u, i + 2), dzv(u, i + 3));
+        pin(dpk[u][i >> 3]);
+      } else if constexpr (j == 22) {
+        float l = -(((tdm[0].x + tdm[0].y) + (tdm[1].x + tdm[1].y)) * inv_m + (tds.x + tds.y) * inv_s);
+        const float lz = (nm ? mm + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? ms + __builtin_amdgcn_logf(Ss) * LN2 : 0.f);
+        l += h0 ? lz : 0.f;
+        loss_acc += l;
+        pin(loss_acc);
+      }
+    };
+    if (LOSS != 0) {  // sigmoid-BCE: not interleaved (the headline loss is the softmax)
+      float dz[2][16], lt = 0.f;
+      bce_tile_loss<V6_YLUT>(smem, zc, tmc, tmc != 0, h, dz, lt);
+      loss_acc += lt;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          dpk[u][q] = __builtin_bit_cast(u32x4, pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2],
+                                                      dz[u][8 * q + 3], dz[u][8 * q + 4], dz[u][8 * q + 5],
+                                                      dz[u][8 * q + 6], dz[u][8 * q + 7]));
+    }
+    st.mark(0);
+
+    // ---- 32 MFMA slots ----
+    static_for<32>([&](auto M) {
+      constexpr int m = decltype(M)::value;
+      constexpr V7Mfma x = v7_mfma(m);
+      if constexpr (x.kind == 0) {
+        const int t = x.a, q = x.b;
+        a1[t & 1] = mfma32(wf[m], xf[q], q == 0 ? f32x16{} : a1[t & 1]);
+      } else {
+        const int u = x.a, kk = x.b;
+        z2n[u] = mfma32(wf[m], hT[kk >> 1][kk & 1], kk == 0 ? b2i[u] : z2n[u]);
+      }
+      if constexpr (m + V7_LEAD < 32) wf[m + V7_LEAD] = wfrag(m + V7_LEAD);
+      if constexpr (m == 4) {  // b2 as F2's initial accumulator
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
+            b2i[u][4 * g + 0] = b[0]; b2i[u][4 * g + 1] = b[1]; b2i[u][4 * g + 2] = b[2]; b2i[u][4 * g + 3] = b[3];
+          }
+      }
+      constexpr int rq = v7_relu(m);
+      if constexpr (rq >= 0) hT[rq >> 1][rq & 1] = relu_pack(a1[(rq >> 1) & 1], rq & 1);
+      constexpr int j = v7_sm_step(m);
+      if constexpr (j >= 0) sm_step(std::integral_constant<int, j>{});
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    st.mark(1);
+
+    // ---- tile kc: dZ2 image, FULL ----
+    if (has_c) {
+      const uint32_t SB = v6_slot(unit, kc % V6_NSLOT);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const u32x4 fq = dpk[u][q];
+          *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 4 * h)) =
+              u32x2{fq[0], fq[1]};
+          *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
+              u32x2{fq[2], fq[3]};
+        }
+      lds_signal(smem, FL + (kc % V6_NSLOT) * 4, kc + 1);  // FULL
+    }
+    st.mark(2);
+    zc[0] = z2n[0];
+    zc[1] = z2n[1];
+    tmc = tmn;
+    stage_in(kn + V6_NF);  // issued before the slot wait and the image stores, which cover their latency
+    // ---- tile kn: H and X images into its slot once both backward waves released it ----
+    if (has_n) {
+      const int slot = kn % V6_NSLOT;
+      const uint32_t SB = v6_slot(unit, slot);
+      if (kn >= V6_NSLOT) {
+        v6_wait(smem, FL + (V6_NSLOT + slot) * 4, kn - V6_NSLOT + 1, ok);
+        v6_wait(smem, FL + (2 * V6_NSLOT + slot) * 4, kn - V6_NSLOT + 1, ok);
+      }
+      st.mark(3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<bf16x8*>(smem + tile_img<false>(SB + V6_SX, r, 16 * q + 8 * h)) = xf[q];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t HB = SB + V6_SH + (t >> 1) * 4096;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const u32x4 d = __builtin_bit_cast(u32x4, hT[t][q]);
+          *reinterpret_cast<u32x2*>(smem + tile_img<true>(HB, r, 32 * (t & 1) + 16 * q + 4 * h)) = u32x2{d[0], d[1]};
+          *reinterpret_cast<u32x2*>(smem + tile_img<true>(HB, r, 32 * (t & 1) + 16 * q + 8 + 4 * h)) = u32x2{d[2], d[3]};
+        }
+      }
+    }
+    stage_pin();
+    kc = has_n ? kn : -1;
+    st.mark(4);
+  }
 }
 
 // backward wave of hidden half RHO: every tile of the unit's stream.  Every LDS read of the tile
 // (dZ2 A fragments, H / dZ2 / X transposes, W2ᵀ fragments: ~96 VGPRs) is issued at once right after
 // FULL, the slot is released as soon as they have landed, and the 26 MFMAs then run from registers.
 template <int RHO>
-EM_DEVICE void v6_backward(char* smem, int B, int unit, int lane, f32x16 (&dW2)[2][2], f32x16 (&dW1T)[2][2],
+EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f32x16 (&dW2)[2][2], f32x16 (&dW1T)[2][2],
                            f32x16& db2, bool& ok, Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
-  const int nunits = gridDim.x * 2, U = v6_unit_id(unit);
+  const int nunits = gridDim.x * V6_NSTREAM, U = v6_unit_id(unit);
   const int K = v6_ntiles_of_unit(B, U, nunits);
-  const uint32_t FL = V6_FLAGS + unit * 64;
+  const uint32_t FL = V6_FLAGS + unit * V6_FLAG_STRIDE;
   const uint32_t MYDONE = FL + ((1 + RHO) * V6_NSLOT) * 4;
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   __syncthreads();  // matches the forward waves' barrier (recycled images)
   st.start();
-  for (int k = 0; k < K; ++k) {
+  for (int k = parity; k < K; k += V6_NBP) {
     const int slot = k % V6_NSLOT;
     const uint32_t SB = v6_slot(unit, slot), D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
     v6_wait(smem, FL + slot * 4, k + 1, ok);
@@ -489,14 +861,18 @@ EM_DEVICE int v6_red_slot(int T, int g, int L, int h) {
 }
 
 // one role's loop + its share of the epilogue (the same two barriers in every role instantiation)
-template <int LOSS, int ROLE>  // ROLE 0/1 = forward f, 2/3 = backward rho
+// ROLE 0 = forward wave sub (its first tile), 2/3 = backward wave of hidden half rho = ROLE - 2 and
+// tile parity sub
+template <int LOSS, bool SIDX, int ROLE>
 EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                       int offset, int unit, int wave, int lane, float* slab_spare) {
+                       int offset, int unit, int sub, int wave, int lane, float* slab_spare) {
   const int r = lane & 31, h = lane >> 5;
   bool ok = true;
   Stamps st;
-  float* RED = reinterpret_cast<float*>(smem);  // [unit][16 tiles][4 g][64 lanes][4]: 0..7 dW2, 8..15 dW1T
-  float* DB2S = reinterpret_cast<float*>(smem + V6_RED);          // [2 units][64]
+  // per part (stream, or tile parity in the shared layout): [16 tiles][4 g][64 lanes][4] f32, 0..7 dW2,
+  // 8..15 dW1T
+  float* RED = reinterpret_cast<float*>(smem);
+  float* DB2S = reinterpret_cast<float*>(smem + V6_RED);          // [2 parts][64]
   float* LOSSS = reinterpret_cast<float*>(smem + V6_RED + 512);   // [8]
   auto dump = [&]() {
     if (FUSED_STAMPS && lane < 10) {  // phase cycles of this wave -> spare slab floats
@@ -509,7 +885,10 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   if (ROLE < 2) {
     float loss_acc = 0.f;
     __builtin_amdgcn_s_setprio(FUSED_FPRIO);  // forward waves bound the pipeline (+3 % at 1)
-    v6_forward<LOSS, ROLE>(smem, masks, sidx, B, offset, unit, lane, loss_acc, ok, st);
+    if (FUSED_V7)
+      v7_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, unit, sub, lane, loss_acc, ok, st);
+    else
+      v6_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, unit, sub, lane, loss_acc, ok, st);
     float lsum = wave_sum(loss_acc);
     if (!ok) lsum = __builtin_nanf("");
     dump();
@@ -527,10 +906,11 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
         dW1T[t][u] = f32x16{};
       }
     f32x16 db2 = f32x16{};
-    v6_backward<RHO>(smem, B, unit, lane, dW2, dW1T, db2, ok, st);
+    v6_backward<RHO>(smem, B, unit, sub, lane, dW2, dW1T, db2, ok, st);
+    const int part = FUSED_SHARED ? sub : unit;
     dump();
     __syncthreads();
-    if (h == 0) DB2S[unit * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
+    if (h == 0) DB2S[part * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
@@ -542,7 +922,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
           const int T = 8 * which + 2 * (2 * RHO + tt) + u;
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<f32x4*>(RED + unit * 16384 + v6_red_slot(T, g, r, h) * 4) =
+            *reinterpret_cast<f32x4*>(RED + part * 16384 + v6_red_slot(T, g, r, h) * 4) =
                 f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
         }
     __syncthreads();
@@ -552,7 +932,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
 // Slabs only: em_adam_slab reduces them (or the DP paths all-reduce them first).  A one-launch form
 // with the slab reduction and Adam inside this kernel was measured 4.3 us per step slower (round 3,
 // docs/DESIGN.md §6b) and removed in round 4.
-template <int LOSS>
+template <int LOSS, bool SIDX>
 __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                                          int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                                          float* __restrict__ loss_slabs, int* __restrict__ step) {
@@ -589,21 +969,28 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
   }
   if (tid < 32) reinterpret_cast<int*>(smem + V6_FLAGS)[tid] = 0;
   __syncthreads();
-  // wave w runs on SIMD w % 4.  unit 0 = waves 0-3 (F0 F1 B0 B1), unit 1 = waves 4-7 (B0 B1 F0 F1):
-  // every SIMD hosts one forward and one backward wave
-  // (pairing F and B of the same unit on a SIMD measured 1.5 % slower)
-  const int unit = wave >> 2, wl = wave & 3;
-  const int role = unit == 0 ? wl : (wl ^ 2);  // 0/1 forward f, 2/3 backward rho
+  // wave w runs on SIMD w % 4, and every SIMD hosts one forward and one backward wave.
+  //   shared ring: waves 0-3 forward (first tile w), waves 4-7 backward (rho = (w >> 1) & 1, parity w & 1)
+  //   two units: unit 0 = waves 0-3 (F0 F1 B0 B1), unit 1 = waves 4-7 (B0 B1 F0 F1) (pairing F and B of
+  //   the same unit on a SIMD measured 1.5 % slower)
+  int unit = 0, role, sub;
+  if (FUSED_SHARED) {
+    role = wave < 4 ? 0 : 2 + ((wave >> 1) & 1);
+    sub = wave < 4 ? wave : (wave & 1);
+  } else {
+    unit = wave >> 2;
+    const int r0 = unit == 0 ? (wave & 3) : ((wave & 3) ^ 2);  // 0/1 forward f, 2/3 backward rho
+    role = r0 < 2 ? 0 : r0;
+    sub = r0 < 2 ? r0 : 0;
+  }
   float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
   if (FUSED_STAMPS) ts[1] = __builtin_amdgcn_s_memrealtime();
   if (role == 0)
-    v6_body<LOSS, 0>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
-  else if (role == 1)
-    v6_body<LOSS, 1>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+    v6_body<LOSS, SIDX, 0>(smem, masks, sidx, B, offset, unit, sub, wave, lane, slab_spare);
   else if (role == 2)
-    v6_body<LOSS, 2>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+    v6_body<LOSS, SIDX, 2>(smem, masks, sidx, B, offset, unit, sub, wave, lane, slab_spare);
   else
-    v6_body<LOSS, 3>(smem, masks, sidx, B, offset, unit, wave, lane, slab_spare);
+    v6_body<LOSS, SIDX, 3>(smem, masks, sidx, B, offset, unit, sub, wave, lane, slab_spare);
   if (FUSED_STAMPS) ts[2] = __builtin_amdgcn_s_memrealtime();
 
   const float* RED = reinterpret_cast<const float*>(smem);
@@ -644,12 +1031,13 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
   }
 }
 
-template <int LOSS>
+// SIDX: samples addressed through sidx (shuffled epochs) instead of offset + s
+template <int LOSS, bool SIDX>
 __global__ void __launch_bounds__(512, 1)
 mlp_fused_train_v6_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
                           const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                           float* __restrict__ loss_slabs, int* __restrict__ step) {
-  train_v6<LOSS>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step);
+  train_v6<LOSS, SIDX>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step);
 }
 
 // Forward only: logits [B, 64] fp32 (cols 62/63 padding).  F1+F2 of the train kernel.
@@ -725,8 +1113,10 @@ EM_API int em_mlp_fused_lds_bytes() { return V6_LDS; }
 namespace {
 template <int LOSS>
 void set_lds_attr() {
-  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            V6_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
 }
 int check_train_args(const uint64_t*& draws, const int32_t* sidx, int64_t B, int64_t& offset, const void* wimg,
                      float* slabs, float* loss_slabs, int nslab) {
@@ -756,12 +1146,13 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
   if (int e = check_train_args(draws, sidx, B, offset, wimg, slabs, loss_slabs, nslab)) return e;
   const int Bi = (int)B, oi = (int)offset;
   const uint8_t* w = (const uint8_t*)wimg;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
+  };
   if (loss_kind == 0)
-    hipLaunchKernelGGL(mlp_fused_train_v6_kernel<0>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, step);
+    sidx ? go(mlp_fused_train_v6_kernel<0, true>) : go(mlp_fused_train_v6_kernel<0, false>);
   else
-    hipLaunchKernelGGL(mlp_fused_train_v6_kernel<1>, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w,
-                       slabs, loss_slabs, step);
+    sidx ? go(mlp_fused_train_v6_kernel<1, true>) : go(mlp_fused_train_v6_kernel<1, false>);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -248,13 +248,19 @@ class FusedSmallMLP:
 
     # ------------------------------------------------------------------ inference / eval
     def logits(self, draws: torch.Tensor, B: int, offset: int = 0, sidx=None) -> torch.Tensor:
-        if self.dtype == "fp32":  # evaluation in fp32 as well (torch fp32 GEMMs on the master weights)
+        if self.dtype == "fp32":
+            # evaluation in fp32 as well: the exact-fp32 MFMA GEMM (csrc/gemm_f32.hip) on the master
+            # weights, bias + relu in its epilogue; W1 / W2 are read as [K, N] operands in place
+            from ..ops import linear_f32 as LF
+
             FM = self.FM
-            x = FM.onehot(draws, B, offset=offset, which=0, sidx=sidx).float()
+            x = LF.onehot(draws, B, offset=offset, which=0, sidx=sidx)  # [B, 64], no bias column
             W1 = self.params[FM.P_W1:FM.P_W2].view(64, 128)
             W2 = self.params[FM.P_W2:FM.P_B2].view(128, 64)
-            h = torch.relu(x @ W1 + W1[62])
-            return h @ W2 + self.params[FM.P_B2:FM.P_TOTAL]
+            h = torch.empty(B, 128, dtype=torch.float32, device=self.device)
+            LF.gemm_f32(x, True, W1, False, h, B, 128, 64, bias=W1[62], act="relu")
+            z = torch.empty(B, 64, dtype=torch.float32, device=self.device)
+            return LF.gemm_f32(h, True, W2, False, z, B, 64, 128, bias=self.params[FM.P_B2:FM.P_TOTAL])
         return self.FM.forward_logits(draws, B, self.img, offset=offset, sidx=sidx)
 
     def evaluate(self, draws: torch.Tensor, B: int, offset: int = 0, sidx=None, chunk: int = 1 << 22) -> dict:

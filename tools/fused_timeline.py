@@ -17,6 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 NAMES = ["F wait slot", "F X+F1+H", "F F2", "F loss", "F D2+signal",
          "B wait full", "B reads", "B B1+dW2+db2", "B mask", "B dW1T"]
+if os.environ.get("TL_V7", "0") == "1":  # v7 forward marks (csrc/mlp_fused.hip v7_forward)
+    NAMES[:5] = ["F bce", "F 32 slots", "F D2+full", "F wait slot", "F HX+stage"]
 
 
 def main():
@@ -57,7 +59,10 @@ def main():
         xcd = np.arange(nslab) % 8
         print("   loop median per blockIdx%8:", " ".join("%.1f" % np.median(loop[xcd == k]) for k in range(8)))
         st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
-        for nm, ws in (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5])):  # wave -> role map of the kernel
+        shared = os.environ.get("TL_SHARED", "1") == "1"  # FUSED_SHARED layout: waves 0-3 forward
+        roles = (("forward", [0, 1, 2, 3]), ("backward", [4, 5, 6, 7])) if shared else \
+            (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5]))
+        for nm, ws in roles:  # wave -> role map of the kernel
             v = st[:, ws, :].reshape(-1, 10).mean(0)
             tot = v.sum()
             print(f"   {nm}: {tot / 1e3:.1f} k cycles/wave; " +
