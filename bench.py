@@ -136,7 +136,10 @@ def _parse():
     ap.add_argument("--device-data-gb", type=float, default=0.0,
                     help="HBM-resident dataset: this many GiB of draw masks per GPU (replaces --draws-per-gpu); "
                          "the timed steps are spread over the whole training shard (no hipGraph: offsets "
-                         "change per step)")
+                         "change per step).  -1 = fill the GPU: free HBM (torch.cuda.mem_get_info) minus "
+                         "--headroom-gb")
+    ap.add_argument("--headroom-gb", type=float, default=10.0,
+                    help="--device-data-gb -1: GiB left free for the model, slabs and the evaluation")
     ap.add_argument("--accum", type=int, default=1,
                     help="mlp-wide: micro-batches of --batch per optimizer step (gradient accumulation; "
                          "the per-GPU batch of the step is batch * accum)")
@@ -216,6 +219,9 @@ def main():
         import torch.distributed as dist
 
         if a.dist_backend == "nccl":
+            from euromillioner_amd.parallel.dist import high_priority_comm
+
+            high_priority_comm()
             dist.init_process_group("nccl", timeout=datetime.timedelta(minutes=10), device_id=dev)
         else:
             dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
@@ -226,6 +232,15 @@ def main():
     from euromillioner_amd.data.device_gen import gb_to_draws
     from euromillioner_amd.models.mlp import FusedSmallMLP
 
+    if a.device_data_gb < 0:  # fill the GPU: what is free now, minus the headroom, on every rank
+        free_b, _ = torch.cuda.mem_get_info(dev)
+        # the training shard (70 % of the sequence) is what stays resident while training
+        gb = max(1.0, (free_b / 2**30 - a.headroom_gb) / 0.7)
+        if world > 1:  # every rank the same shard size (the smallest free memory)
+            t = torch.tensor([gb], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            gb = float(t.item())
+        a.device_data_gb = gb
     n_loc = gb_to_draws(a.device_data_gb) if a.device_data_gb > 0 else a.draws_per_gpu
     n_loc = -(-n_loc // SEG) * SEG
     sh = _Shards(n_loc, rank, world)
@@ -234,6 +249,7 @@ def main():
     draws, tr_skip = sh.materialize(sh.train, a.seed, a.planted, dev)
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - tg
+    resident_gb = draws.numel() * draws.element_size() / 2**30
     if a.device_data_gb > 0:
         a.graph = 0  # per-step offsets walk the whole training shard
 
@@ -437,8 +453,9 @@ def main():
             "train_loss_last": loss,
             "val": ev,
             "val_iid": ev_iid,
-            "datagen": {"draws": n_loc, "seconds": gen_s, "gb_per_s": n_loc * 8 / max(gen_s, 1e-9) / 1e9,
-                        "steps_spread": spread},
+            "datagen": {"draws": n_loc, "seconds": gen_s, "gb_per_s": resident_gb * 2**30 / max(gen_s, 1e-9) / 1e9,
+                        "steps_spread": spread, "resident_train_gb": resident_gb,
+                        "device_data_gb": a.device_data_gb},
             **extra,
         }
         print(json.dumps(out), flush=True)

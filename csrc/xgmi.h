@@ -110,4 +110,6 @@ struct XgmiComm {
   XgmiDesc desc{};
   int device = 0;
   bool connected = false;
+  bool local_proxy = false;   // em_xgmi_connect_local: peers are this process's buffers (no IPC)
+  void* peer_ptrs = nullptr;  // em_xgmi_emulate_peers: device array of the peers' header / data pointers
 };

@@ -30,6 +30,33 @@ __global__ void __launch_bounds__(XG_BLOCK) xgmi_reduce_kernel(XgmiDesc d, float
   xg_finish(d, s);
 }
 
+// One-process proxy of the N-rank exchange (tools/xgmi_budget.py): stands in for the peers of rank
+// d.rank.  After `delay_ticks` of wall clock (the peers reaching the exchange later than this rank:
+// publication skew) every emulated peer's slot gets this rank's staged gradient and its flag the
+// step's sequence number, as the peers' own consumers would publish them.
+__global__ void __launch_bounds__(XG_BLOCK)
+xgmi_emulate_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, float* const* __restrict__ peer_data, int n,
+                          long long delay_ticks) {
+  __shared__ int s_sh;
+  if (threadIdx.x == 0) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < delay_ticks) __builtin_amdgcn_s_sleep(2);
+    s_sh = xg_next_seq(d.my_hdr);
+  }
+  __syncthreads();
+  const int s = s_sh;
+  const float* src = d.my_data + (size_t)(s & 1) * d.cap;
+  for (int q = 0; q < d.world; ++q) {
+    if (q == d.rank) continue;
+    float* dst = peer_data[q] + (size_t)(s & 1) * d.cap;
+    for (int i = threadIdx.x; i < n; i += XG_BLOCK) dst[i] = src[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // slot data before the flags (system scope)
+  __syncthreads();
+  if (threadIdx.x < (unsigned)d.world && (int)threadIdx.x != d.rank)
+    __hip_atomic_store(&peer_hdr[threadIdx.x][XG_FLAG], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // consumer blocks spin on peer flags, so keep the grid well inside one wave of residency
 int grid_for(int n) {
   int nb = (n + XG_BLOCK - 1) / XG_BLOCK;
@@ -139,9 +166,10 @@ EM_API int em_xgmi_destroy(void* h) {
   XgmiComm* c = static_cast<XgmiComm*>(h);
   if (!c) return 0;
   (void)hipDeviceSynchronize();
-  if (c->connected)
+  if (c->connected && !c->local_proxy)
     for (int q = 0; q < c->desc.world; ++q)
       if (q != c->desc.rank && c->peers[q]) (void)hipIpcCloseMemHandle(c->peers[q]);
+  if (c->peer_ptrs) (void)hipFree(c->peer_ptrs);
   if (c->own) (void)hipFree(c->own);
   delete c;
   return 0;
@@ -162,6 +190,50 @@ EM_API int em_xgmi_reduce(void* h, float* out, int n, float scale, hipStream_t s
   XgmiComm* c = static_cast<XgmiComm*>(h);
   if (!c || !out || n <= 0 || n > c->desc.cap || !c->connected) return EM_ERR_ARG;
   hipLaunchKernelGGL(xgmi_reduce_kernel, dim3(grid_for(n)), dim3(XG_BLOCK), 0, stream, c->desc, out, n, scale);
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- one-process proxy of an N-rank exchange (tools/xgmi_budget.py; never used for training) ----
+// Connects `h` as rank `rank` of `world` whose peers are the buffers of other comms created in THIS
+// process on the same device (`others[q]`, q != rank; no IPC, no peer access): the consumer kernels
+// then read 7 peer slots and poll 7 flags exactly as on a node, with the peers played by
+// em_xgmi_emulate_peers.
+EM_API int em_xgmi_connect_local(void* h, int world, int rank, void* const* others) {
+  XgmiComm* c = static_cast<XgmiComm*>(h);
+  if (!c || !others || world < 1 || world > XG_MAXW || rank < 0 || rank >= world || c->connected) return EM_ERR_ARG;
+  for (int q = 0; q < world; ++q) {
+    XgmiComm* o = q == rank ? c : static_cast<XgmiComm*>(others[q]);
+    if (!o || o->desc.cap != c->desc.cap) return EM_ERR_ARG;
+    c->desc.peer_hdr[q] = o->desc.my_hdr;
+    c->desc.peer_data[q] = o->desc.my_data;
+  }
+  c->desc.world = world;
+  c->desc.rank = rank;
+  c->local_proxy = true;  // peers are not IPC mappings: nothing to close
+  c->connected = true;
+  return 0;
+}
+
+// the emulated peers of a connect_local'ed comm publish n floats + their flags after delay_us
+EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t stream) {
+  XgmiComm* c = static_cast<XgmiComm*>(h);
+  if (!c || !c->local_proxy || n <= 0 || n > c->desc.cap || delay_us < 0) return EM_ERR_ARG;
+  if (!c->peer_ptrs) {  // device copies of the peers' header / data pointers
+    if (hipMalloc(&c->peer_ptrs, 2 * XG_MAXW * sizeof(void*)) != hipSuccess) return EM_ERR_ARG;
+    void* host[2 * XG_MAXW];
+    for (int q = 0; q < XG_MAXW; ++q) {
+      host[q] = q < c->desc.world ? (void*)c->desc.peer_hdr[q] : nullptr;
+      host[XG_MAXW + q] = q < c->desc.world ? (void*)c->desc.peer_data[q] : nullptr;
+    }
+    if (hipMemcpy(c->peer_ptrs, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess) return EM_ERR_ARG;
+  }
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
+  int* const* hdr = reinterpret_cast<int* const*>(c->peer_ptrs);
+  float* const* data = reinterpret_cast<float* const*>(c->peer_ptrs) + XG_MAXW;
+  hipLaunchKernelGGL(xgmi_emulate_peers_kernel, dim3(1), dim3(XG_BLOCK), 0, stream, c->desc, hdr, data, n,
+                     (long long)(delay_us * 1e-3 * khz));
   EM_CHECK_LAUNCH();
   return 0;
 }

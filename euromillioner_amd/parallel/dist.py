@@ -39,6 +39,14 @@ class DistInfo:
         return dist.group.WORLD if self.is_dist else None
 
 
+def high_priority_comm() -> None:
+    """RCCL's stream at high priority (before the process group is created): the bucketed gradient
+    all-reduces of the wide trainer are issued while the backward GEMMs fill the chip, and a
+    normal-priority collective queues behind them until the backward ends (the exposed tail in
+    profiles/wide_dp_overlap.md).  An explicit TORCH_NCCL_HIGH_PRIORITY in the environment wins."""
+    os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
+
+
 def init(backend: str = "auto", timeout_s: float = 300.0, device: str = "auto") -> DistInfo:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -55,6 +63,7 @@ def init(backend: str = "auto", timeout_s: float = 300.0, device: str = "auto") 
         kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
         if be == "nccl":
             kw["device_id"] = dev
+            high_priority_comm()
         dist.init_process_group(be, **kw)
     return DistInfo(rank, world, local, be, dev)
 

@@ -76,10 +76,12 @@ def test_gloo_data_parallel_rehearsal():
     _check(_run(2, "gloo"), expect_xgmi=None)
 
 
-@pytest.mark.parametrize("world,backend", [(1, "gloo"), (2, "nccl"), (4, "nccl"), (8, "nccl")])
+@pytest.mark.parametrize("world,backend", [(1, "gloo"), (2, "gloo"), (2, "nccl"), (4, "nccl"), (8, "nccl")])
 def test_wide_dp_panels_bf16_wire(world, backend):
     """Wide GEMM trainer (62->1024->1024->62) with the bf16 gradient wire and 4 async wgrad panels on
-    the 1024x1024 layer: ranks bit-identical, tracking the single-process run on the concatenated batch."""
+    the 1024x1024 layer: ranks bit-identical, tracking the single-process run on the concatenated batch.
+    (2, gloo) runs two ranks on a one-GPU box (sharing the device): the GPU panel path with a real
+    two-term bf16 all-reduce, which world 1 cannot exercise."""
     if backend == "nccl" and _ndev() < world:
         pytest.skip(f"RCCL world {world} needs {world} GPUs (this box has {_ndev()})")
     res = _run(world, backend, case="wide")

@@ -61,12 +61,17 @@ def run(steps: int = 20, B: int = 1 << 16, bucket_mb: float = 25.0):
     draws = generate_masks(B * 4 + 16, seed=3, planted=0.9, device=dev)
     m = GemmMLPTrainer((62, 8192, 8192, 62), dev, lr=1e-3, seed=0, bucket_mb=bucket_mb)
     side = torch.cuda.Stream()
+    # the RCCL stream under TORCH_NCCL_HIGH_PRIORITY=1 (set by parallel.dist for the GEMM trainer): its
+    # kernels are dispatched ahead of the GEMMs' when CUs free up, so the bucket queue does not back up
+    side_hi = torch.cuda.Stream(priority=-1)
     peer = torch.randn(m.P + 1, device=dev)
     out = torch.empty_like(peer)
-    for mode in ("none", "sidecopy", "serial", "none"):
+    modes = os.environ.get("WO_MODES", "none,sidecopy,sidecopy_hi,serial,none").split(",")
+    for mode in modes:
         m.last_buckets = []
         m.comm_emulator = None if mode == "none" else (
-            lambda flat, be, s=(mode == "serial"): SideCopy(flat, be, side, peer, out, serial=s))
+            lambda flat, be, s=(mode == "serial"), st=(side_hi if mode == "sidecopy_hi" else side):
+            SideCopy(flat, be, st, peer, out, serial=s))
         for i in range(3):
             m.step(draws, B, offset=(i % 4) * B)
         torch.cuda.synchronize()
@@ -102,9 +107,10 @@ def report(path: str):
             cur = []
         cur.append(k)
     phases.append(cur)
-    phases = [p for p in phases if len(p) > 50][-4:]  # the four modes (setup kernels dropped)
-    modes = ["none", "sidecopy", "serial", "none(again)"]
+    modes = os.environ.get("WO_MODES", "none,sidecopy,sidecopy_hi,serial,none").split(",")
+    phases = [p for p in phases if len(p) > 50][-len(modes):]  # one phase per mode (setup kernels dropped)
     main = max(set(k[3] for k in ks), key=lambda s: sum(1 for k in ks if k[3] == s))
+    
 
     def per_kernel(ph):  # compute-stream time per kernel name per optimizer step (Adam launches = steps)
         d = {}
