@@ -53,6 +53,13 @@ EM_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 // same kernel sequence; the eager paths pass rd = nullptr and pre-offset pointers.
 EM_DEVICE int64_t rd_off(const int* rd, int64_t stride) { return rd ? (int64_t)(*rd) * stride : 0; }
 
+EM_DEVICE void round_init_elem(int i, int8_t* st, int16_t* fe, uint8_t* sb, float* gn, int NN) {
+  st[i] = (i % NN) == 0 ? 2 : 0;
+  fe[i] = -1;
+  sb[i] = 0;
+  gn[i] = 0.f;
+}
+
 // per-round tree reset: status/feature/bin/gain cleared, every task's root opened (status 2)
 __global__ void gbdt_round_init(int8_t* __restrict__ st, int16_t* __restrict__ fe, uint8_t* __restrict__ sb,
                                 float* __restrict__ gn, int total, int NN, const int* __restrict__ rd) {
@@ -61,12 +68,8 @@ __global__ void gbdt_round_init(int8_t* __restrict__ st, int16_t* __restrict__ f
   fe += o;
   sb += o;
   gn += o;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    st[i] = (i % NN) == 0 ? 2 : 0;
-    fe[i] = -1;
-    sb[i] = 0;
-    gn[i] = 0.f;
-  }
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
+    round_init_elem(i, st, fe, sb, gn, NN);
 }
 
 __global__ void gbdt_init_margin(float* __restrict__ margin, int64_t total, float base) {
@@ -75,34 +78,59 @@ __global__ void gbdt_init_margin(float* __restrict__ margin, int64_t total, floa
 }
 
 // margin/g/h/node: [T][n]; Y: [n][T]
+EM_DEVICE void grad_elem(int64_t i, const float* __restrict__ margin, const float* __restrict__ Y,
+                         float* __restrict__ g, float* __restrict__ h, int16_t* __restrict__ node, int T, int n,
+                         int obj, float subsample, uint32_t seed, int round) {
+  const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
+  const float m = margin[i], y = Y[(int64_t)r * T + t];
+  float gg, hh;
+  if (obj == OBJ_LOGISTIC) {
+    const float p = 1.f / (1.f + expf(-m));
+    gg = p - y;
+    hh = fmaxf(p * (1.f - p), 1e-16f);
+  } else if (obj == OBJ_SOFTMAX) {  // XGBoost SoftmaxMultiClassObj: g = p - y, h = max(2p(1-p), eps)
+    const float p = softmax_p(margin, T, n, r, t);
+    gg = p - y;
+    hh = fmaxf(2.f * p * (1.f - p), 1e-16f);
+  } else {
+    gg = m - y;
+    hh = 1.f;
+  }
+  if (subsample < 1.f) {
+    const float u = (hash3(seed, (uint32_t)round * 131071u + t, r) >> 8) * (1.f / 16777216.f);
+    if (u >= subsample) gg = hh = 0.f;
+  }
+  g[i] = gg;
+  h[i] = hh;
+  node[i] = 0;
+}
+
 __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restrict__ Y, float* __restrict__ g,
                           float* __restrict__ h, int16_t* __restrict__ node, int T, int n, int obj, float subsample,
                           uint32_t seed, int round, const int* __restrict__ rd) {
   if (rd) round = *rd;
   const int64_t total = (int64_t)T * n;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
-    const float m = margin[i], y = Y[(int64_t)r * T + t];
-    float gg, hh;
-    if (obj == OBJ_LOGISTIC) {
-      const float p = 1.f / (1.f + expf(-m));
-      gg = p - y;
-      hh = fmaxf(p * (1.f - p), 1e-16f);
-    } else if (obj == OBJ_SOFTMAX) {  // XGBoost SoftmaxMultiClassObj: g = p - y, h = max(2p(1-p), eps)
-      const float p = softmax_p(margin, T, n, r, t);
-      gg = p - y;
-      hh = fmaxf(2.f * p * (1.f - p), 1e-16f);
-    } else {
-      gg = m - y;
-      hh = 1.f;
-    }
-    if (subsample < 1.f) {
-      const float u = (hash3(seed, (uint32_t)round * 131071u + t, r) >> 8) * (1.f / 16777216.f);
-      if (u >= subsample) gg = hh = 0.f;
-    }
-    g[i] = gg;
-    h[i] = hh;
-    node[i] = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+    grad_elem(i, margin, Y, g, h, node, T, n, obj, subsample, seed, round);
+}
+
+// round_init + grad in one launch (independent element spaces; the reference-size fit is launch-bound)
+__global__ void gbdt_round_start(int8_t* __restrict__ st, int16_t* __restrict__ fe, uint8_t* __restrict__ sb,
+                                 float* __restrict__ gn, int TNN, int NN, const float* __restrict__ margin,
+                                 const float* __restrict__ Y, float* __restrict__ g, float* __restrict__ h,
+                                 int16_t* __restrict__ node, int T, int n, int obj, float subsample, uint32_t seed,
+                                 int round, const int* __restrict__ rd) {
+  if (rd) round = *rd;
+  const int64_t o = rd_off(rd, TNN);
+  st += o;
+  fe += o;
+  sb += o;
+  gn += o;
+  const int64_t total = (int64_t)T * n;
+  const int64_t all = total > TNN ? total : TNN;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < all; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < TNN) round_init_elem((int)i, st, fe, sb, gn, NN);
+    if (i < total) grad_elem(i, margin, Y, g, h, node, T, n, obj, subsample, seed, round);
   }
 }
 
@@ -219,6 +247,13 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
 // scale), rint rounds half to even like numpy's np.rint, and the int64 conversion of an integral
 // double is exact
 EM_DEVICE long long quantise(float x, double scale) { return (long long)__builtin_rint((double)x * scale); }
+// hessians: a positive h never rounds to 0 (the 1e-16 floor of a saturated row would at s < 53, and a
+// node of such rows would then have H = 0 exactly where the exact form keeps H > 0: with
+// min_child_weight = lambda = 0 its gain and leaf divide by zero).  models/gbdt.py _quantise_h agrees.
+EM_DEVICE long long quantise_h(float x, double scale) {
+  const long long q = quantise(x, scale);
+  return (x > 0.f && q < 1) ? 1 : q;
+}
 
 // LDS layout of the fixed-point form: two planes (g sums, then h sums) of 8-byte cells, so a lane's
 // atomic touches one 8-byte word, and one pad cell after every feature's bins: with the compact
@@ -286,7 +321,7 @@ gbdt_hist_q(const uint8_t* __restrict__ bins, const float* __restrict__ g, const
     }
     for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
       sq[2 * (r - r0)] = quantise(g[base + r], qscale);
-      sq[2 * (r - r0) + 1] = quantise(h[base + r], qscale);
+      sq[2 * (r - r0) + 1] = quantise_h(h[base + r], qscale);
       sn[r - r0] = (int16_t)(node[base + r] - first - n0);
     }
     __syncthreads();
@@ -409,7 +444,7 @@ gbdt_hist_qb(const uint64_t* __restrict__ bmask, int WB, const int* __restrict__
 #pragma unroll
     for (int u = 0; u < QB_ROWS; ++u) {
       if ((unsigned)nd[u] >= (unsigned)NTn) continue;
-      const long long qg = quantise(gv[u], qscale), qh = quantise(hv[u], qscale);
+      const long long qg = quantise(gv[u], qscale), qh = quantise_h(hv[u], qscale);
       long long* pn = hist + nd[u] * NW;
       long long* pl = pn + rep * W;
       __hip_atomic_fetch_add(pl + nb, qg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -734,6 +769,29 @@ __global__ void gbdt_predict(const uint8_t* __restrict__ bins, float* __restrict
   }
 }
 
+// per-element term of the elementwise metrics (logloss / rmse / error) of one (task, row) margin
+EM_DEVICE double metric_term(float m, float y, int obj, int metric) {
+  const float p = obj == OBJ_LOGISTIC ? 1.f / (1.f + expf(-m)) : m;
+  if (metric == MET_LOGLOSS) {
+    const double pc = fmin(fmax((double)p, 1e-16), 1.0 - 1e-16);
+    return -(y * log(pc) + (1.0 - y) * log(1.0 - pc));
+  }
+  if (metric == MET_RMSE) return (double)(p - y) * (double)(p - y);
+  return ((p > 0.5f ? 1.f : 0.f) != y) ? 1.0 : 0.0;
+}
+
+// fixed-order tree sum over the 256 threads of a block (thread 0 gets the result)
+EM_DEVICE double block_tree_sum(double acc) {
+  __shared__ double red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  return red[0];
+}
+
 // K13: partial sums per block of the metric over (task,row); Y [n][T], margin [T][n]
 __global__ void __launch_bounds__(256)
 gbdt_metric(const float* __restrict__ margin, const float* __restrict__ Y, int T, int n, int obj, int metric,
@@ -758,27 +816,10 @@ gbdt_metric(const float* __restrict__ margin, const float* __restrict__ Y, int T
       continue;
     }
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
-    const float m = margin[i], y = Y[(int64_t)r * T + t];
-    const float p = obj == OBJ_LOGISTIC ? 1.f / (1.f + expf(-m)) : m;
-    double v;
-    if (metric == MET_LOGLOSS) {
-      const double pc = fmin(fmax((double)p, 1e-16), 1.0 - 1e-16);
-      v = -(y * log(pc) + (1.0 - y) * log(1.0 - pc));
-    } else if (metric == MET_RMSE) {
-      v = (double)(p - y) * (double)(p - y);
-    } else {
-      v = ((p > 0.5f ? 1.f : 0.f) != y) ? 1.0 : 0.0;
-    }
-    acc += v;
+    acc += metric_term(margin[i], Y[(int64_t)r * T + t], obj, metric);
   }
-  __shared__ double red[256];
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+  const double bs = block_tree_sum(acc);
+  if (threadIdx.x == 0) partial[blockIdx.x] = bs;
 }
 
 // fixed-order block reduction of the per-block metric partials (256 threads: strided sequential
@@ -806,6 +847,92 @@ gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int
     if (metric == MET_RMSE) v = sqrt(v);
     out[0] = (float)v;
   }
+}
+
+// The last-arriving block of a fused metric launch: every block stores its partial write-through (sc1)
+// and drains it before its single arrival add; the block whose add completes the count sums the
+// partials (sc1 loads) exactly as gbdt_metric_final does, writes the mean, re-arms the counter and,
+// in a replayed round, advances the round counter (every block read it at entry).
+EM_DEVICE void metric_arrive_final(double bs, double* __restrict__ partial, int* __restrict__ ctr, int64_t count,
+                                   int metric, float* __restrict__ out, int* __restrict__ rd_adv) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partial + blockIdx.x, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256)
+    s += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double v = red[0] / (double)(count > 0 ? count : 1);
+    if (metric == MET_RMSE) v = sqrt(v);
+    out[0] = (float)v;
+    __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rd_adv) *rd_adv += 1;
+  }
+}
+
+// gbdt_update + gbdt_metric + gbdt_metric_final (elementwise metrics) in one launch: same grid, same
+// elements per thread, same partial and final sums -> bit-identical to the three launches
+__global__ void __launch_bounds__(256)
+gbdt_update_metric(float* __restrict__ margin, const int16_t* __restrict__ node, int T, int n, int NN,
+                   const int8_t* __restrict__ status, const float* __restrict__ leaf, const int* __restrict__ rd,
+                   const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial, int* __restrict__ ctr,
+                   float* __restrict__ out, int ostride, int* __restrict__ rd_adv) {
+  status += rd_off(rd, (int64_t)T * NN);
+  leaf += rd_off(rd, (int64_t)T * NN);
+  out += rd_off(rd, ostride);
+  const int64_t total = (int64_t)T * n;
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
+    const int8_t* st = status + (int64_t)t * NN;
+    const float m = margin[i] + leaf[(int64_t)t * NN + leaf_ancestor(st, node[i])];
+    margin[i] = m;
+    acc += metric_term(m, Y[(int64_t)r * T + t], obj, metric);
+  }
+  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv);
+}
+
+// gbdt_predict (one round's trees) + gbdt_metric + gbdt_metric_final of an eval set in one launch
+__global__ void __launch_bounds__(256)
+gbdt_predict_metric(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F, int NN, int k0,
+                    int k1, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
+                    const uint8_t* __restrict__ sbin, const float* __restrict__ leaf, const int* __restrict__ rd,
+                    const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial,
+                    int* __restrict__ ctr, float* __restrict__ out, int ostride, int* __restrict__ rd_adv) {
+  if (rd) {
+    k0 += *rd * T;
+    k1 += *rd * T;
+  }
+  out += rd_off(rd, ostride);
+  const int64_t total = (int64_t)T * n;
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
+    const uint8_t* row = bins + (int64_t)r * F;
+    float tacc = 0.f;
+    for (int k = k0 + ((t - k0 % T) % T + T) % T; k < k1; k += T) {
+      const int64_t o = (int64_t)k * NN;
+      int nd = 0;
+      while (status[o + nd] == 1) nd = 2 * nd + 1 + (row[feat[o + nd]] > sbin[o + nd] ? 1 : 0);
+      tacc += leaf[o + nd];
+    }
+    const float m = margin[i] + tacc;
+    margin[i] = m;
+    acc += metric_term(m, Y[(int64_t)r * T + t], obj, metric);
+  }
+  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv);
 }
 
 __global__ void __launch_bounds__(256)
@@ -1002,6 +1129,21 @@ GraphCache& graph_cache() {
   static GraphCache c;
   return c;
 }
+// one zeroed device int per process (per device in use): the fused metric launches' arrival counter
+int* metric_counter() {
+  static int* ctr = nullptr;
+  static int dev = -1;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  if (!ctr || dev != d) {
+    int* p = nullptr;
+    if (hipMalloc(&p, 64) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    ctr = p;
+    dev = d;
+  }
+  return ctr;
+}
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
@@ -1043,6 +1185,8 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   if (quant_bits && (obj == OBJ_SQERR || (int64_t)n >= (1ll << (61 - quant_bits)))) return EM_ERR_ARG;
   const double qscale = quant_bits ? ldexp(1.0, quant_bits) : 0.0, qinv = quant_bits ? ldexp(1.0, -quant_bits) : 0.0;
   const int NN = (1 << (max_depth + 1)) - 1;
+  int* mctr = metric_counter();  // arrival counter of the fused metric launches (re-armed by each)
+  if (!mctr) return EM_ERR_ARG;
   const int C = foff_h[F];
   const int64_t TN = (int64_t)T * n;
   // fixed point with >= 8 one-hot features: the sparse form (QuantAux); EM_GBDT_SPARSE=0 disables it
@@ -1107,10 +1251,8 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     float* lf = leaf + ro;
     float* gn = gainv + ro;
     float* cv = cover + ro;
-    hipLaunchKernelGGL(gbdt_round_init, dim3(grid_for((int64_t)T * NN)), dim3(256), 0, s, st, fe, sb, gn, T * NN, NN,
-                       rd);
-    hipLaunchKernelGGL(gbdt_grad, dim3(grid_for(TN)), dim3(256), 0, s, margin, Y, g, h, node, T, n, obj, subsample,
-                       seed, round, rd);
+    hipLaunchKernelGGL(gbdt_round_start, dim3(grid_for(TN > (int64_t)T * NN ? TN : (int64_t)T * NN)), dim3(256), 0, s,
+                       st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round, rd);
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
       int nch = 1;
@@ -1132,26 +1274,41 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     }
     hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, s, T, NN, max_depth, st, fe, gn, Gs, Hs, lf,
                        cv, (double)lam, gamma, (double)eta, rd);
-    hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd);
-    // metrics (train + evals) into hist_out[round]
+    // metrics (train + evals) into hist_out[round].  Elementwise metrics: the leaf update / eval
+    // prediction, the metric partials and the final sum are one launch each (last-arriving block);
+    // the round counter of a replayed round advances in the round's last launch
     const int hs = 1 + n_evals;
     float* ho = hist_out + (int64_t)round * hs;
     const int mb_train = grid_for(TN);
-    hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, s, margin, Y, T, n, obj, metric, mpart);
-    hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb_train,
-                       metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, ho, rd, hs);
+    const bool fused_metric = metric < MET_MLOGLOSS;
+    int* adv = const_cast<int*>(rd);
+    if (fused_metric) {
+      hipLaunchKernelGGL(gbdt_update_metric, dim3(mb_train), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd, Y,
+                         obj, metric, mpart, mctr, ho, hs, n_evals == 0 ? adv : nullptr);
+    } else {
+      hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd);
+      hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, s, margin, Y, T, n, obj, metric, mpart);
+      hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb_train,
+                         metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, ho, rd, hs);
+    }
     for (int e = 0; e < n_evals; ++e) {
       const int64_t TE = (int64_t)T * evals[e].n;
       const int k0 = round * T;
+      const int mb = grid_for(TE);
+      if (fused_metric) {
+        hipLaunchKernelGGL(gbdt_predict_metric, dim3(mb), dim3(256), 0, s, evals[e].bins, evals[e].margin, T,
+                           evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf, rd, evals[e].Y, obj, metric, mpart,
+                           mctr, ho + 1 + e, hs, e == n_evals - 1 ? adv : nullptr);
+        continue;
+      }
       hipLaunchKernelGGL(gbdt_predict, dim3(grid_for(TE)), dim3(256), 0, s, evals[e].bins, evals[e].margin, T,
                          evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf, rd);
-      const int mb = grid_for(TE);
       hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, s, evals[e].margin, evals[e].Y, T, evals[e].n, obj,
                          metric, mpart);
       hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb,
                          metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric, ho + 1 + e, rd, hs);
     }
-    if (rd) hipLaunchKernelGGL(gbdt_round_advance, dim3(1), dim3(64), 0, s, const_cast<int*>(rd));
+    if (rd && !fused_metric) hipLaunchKernelGGL(gbdt_round_advance, dim3(1), dim3(64), 0, s, adv);
     EM_CHECK_LAUNCH();
     return 0;
   };

@@ -45,14 +45,17 @@ xgmi_emulate_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, float* 
   }
   __syncthreads();
   const int s = s_sh;
-  const float* src = d.my_data + (size_t)(s & 1) * d.cap;
-  for (int q = 0; q < d.world; ++q) {
-    if (q == d.rank) continue;
-    float* dst = peer_data[q] + (size_t)(s & 1) * d.cap;
-    for (int i = threadIdx.x; i < n; i += XG_BLOCK) dst[i] = src[i];
+  if (n > 0) {  // optional: the peers' slots get this rank's gradient (one block: ~30 us for 7 x 64 KB,
+                // so the budget runs use n = 0 and the peers' slots keep what em_xgmi_stage left there)
+    const float* src = d.my_data + (size_t)(s & 1) * d.cap;
+    for (int q = 0; q < d.world; ++q) {
+      if (q == d.rank) continue;
+      float* dst = peer_data[q] + (size_t)(s & 1) * d.cap;
+      for (int i = threadIdx.x; i < n; i += XG_BLOCK) dst[i] = src[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // slot data before the flags (system scope)
+    __syncthreads();
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // slot data before the flags (system scope)
-  __syncthreads();
   if (threadIdx.x < (unsigned)d.world && (int)threadIdx.x != d.rank)
     __hip_atomic_store(&peer_hdr[threadIdx.x][XG_FLAG], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -215,10 +218,10 @@ EM_API int em_xgmi_connect_local(void* h, int world, int rank, void* const* othe
   return 0;
 }
 
-// the emulated peers of a connect_local'ed comm publish n floats + their flags after delay_us
+// the emulated peers of a connect_local'ed comm publish their flags (and n floats, if n > 0) after delay_us
 EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t stream) {
   XgmiComm* c = static_cast<XgmiComm*>(h);
-  if (!c || !c->local_proxy || n <= 0 || n > c->desc.cap || delay_us < 0) return EM_ERR_ARG;
+  if (!c || !c->local_proxy || n < 0 || n > c->desc.cap || delay_us < 0) return EM_ERR_ARG;
   if (!c->peer_ptrs) {  // device copies of the peers' header / data pointers
     if (hipMalloc(&c->peer_ptrs, 2 * XG_MAXW * sizeof(void*)) != hipSuccess) return EM_ERR_ARG;
     void* host[2 * XG_MAXW];

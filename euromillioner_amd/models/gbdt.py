@@ -255,6 +255,23 @@ def _quantise(x: np.ndarray, s: int) -> np.ndarray:
     return np.rint(x.astype(np.float64) * (2.0 ** s)).astype(np.int64)
 
 
+def _quantise_h(h: np.ndarray, s: int) -> np.ndarray:
+    """Hessians: a positive h never rounds to 0 (== csrc/gbdt.hip quantise_h).  The 1e-16 floor of a
+    saturated row would, and a node of such rows would get H = 0 where the exact form keeps H > 0."""
+    q = _quantise(h, s)
+    return np.where((h > 0) & (q < 1), 1, q)
+
+
+def _segment_cumsum(hist: np.ndarray, off: np.ndarray) -> np.ndarray:
+    """Left sums "bins <= b" within each feature's cell segment [off[f], off[f+1]).  Per segment, so
+    an int64 intermediate never exceeds one node's total (a cumsum over every feature's cells reaches
+    F x the node total and would wrap past 2^63 near quant_bits' bound)."""
+    out = np.empty_like(hist)
+    for f in range(len(off) - 1):
+        np.cumsum(hist[off[f]:off[f + 1]], axis=0, out=out[off[f]:off[f + 1]])
+    return out
+
+
 def _int_hist(onehot: np.ndarray, Zq: np.ndarray) -> np.ndarray:
     """Exact onehot.T @ Zq for int64 Zq (|entries| <= 2^s, n rows, quant_bits' bound n * 2^s < 2^61,
     n < 2^26): two float64 GEMMs of the 26-bit halves, whose partial sums are integers below 2^53 in
@@ -491,7 +508,7 @@ class GBDT:
                 keep = (rng.random((n, T)) < self.subsample).astype(np.float32)
                 g, h = g * keep, h * keep
             if qs:  # fixed point: integer sums, exact in any order (== gbdt_hist_q)
-                g64, h64 = _quantise(g, qs), _quantise(h, qs)
+                g64, h64 = _quantise(g, qs), _quantise_h(h, qs)
             else:
                 g64, h64 = g.astype(np.float64), h.astype(np.float64)
             node = np.zeros((n, T), dtype=np.int64)
@@ -520,14 +537,17 @@ class GBDT:
                     HG = red(onehot.T @ Zg)  # [sum bins, T*nl]; C4: all-reduced under DP
                     HH = red(onehot.T @ Zh)
                 # segmented prefix sums: left sums for "bin <= b" of feature f, all columns at once
-                CG, CH = np.cumsum(HG, axis=0), np.cumsum(HH, axis=0)
-                baseg = np.where(rowseg_start[:, None] > 0, CG[np.maximum(rowseg_start - 1, 0)], 0)
-                baseh = np.where(rowseg_start[:, None] > 0, CH[np.maximum(rowseg_start - 1, 0)], 0)
-                GL, HL = CG - baseg, CH - baseh
+                if qs:  # integers: per feature segment (no intermediate beyond one node's total)
+                    GL, HL = _segment_cumsum(HG, off), _segment_cumsum(HH, off)
+                else:
+                    CG, CH = np.cumsum(HG, axis=0), np.cumsum(HH, axis=0)
+                    baseg = np.where(rowseg_start[:, None] > 0, CG[np.maximum(rowseg_start - 1, 0)], 0)
+                    baseh = np.where(rowseg_start[:, None] > 0, CH[np.maximum(rowseg_start - 1, 0)], 0)
+                    GL, HL = CG - baseg, CH - baseh
                 cols_t = np.repeat(tix, nl)
                 cols_i = np.tile(np.arange(nl), T) + first
                 if qs:  # node totals = feature 0's cells; every sum converted to double once
-                    Gnq, Hnq = CG[off[1] - 1], CH[off[1] - 1]
+                    Gnq, Hnq = GL[off[1] - 1], HL[off[1] - 1]
                     GR, HR = (Gnq[None, :] - GL).astype(np.float64) * inv, (Hnq[None, :] - HL).astype(np.float64) * inv
                     GL, HL = GL.astype(np.float64) * inv, HL.astype(np.float64) * inv
                     Gn, Hn = Gnq.astype(np.float64) * inv, Hnq.astype(np.float64) * inv

@@ -324,6 +324,58 @@ def test_quantised_sums_are_order_free():
     assert np.array_equal(a.trees.leaf, b.trees.leaf)
 
 
+def _saturating_data(n=3000, seed=5):
+    """Labels a function of one feature; fitted from base_score = 1 - 2^-53 (SAT_KW), i.e. a margin of
+    ~36.7 where float32 p == 1 and every row sits at the logistic hessian floor (1e-16)."""
+    rng = np.random.default_rng(seed)
+    X = rng.integers(0, 8, size=(n, 4)).astype(float)
+    return X, (X[:, 0] >= 4).astype(float)
+
+
+SAT_KW = dict(nround=3, max_depth=3, eta=1.0, gamma=0.0, min_child_weight=0.0, reg_lambda=0.0,
+              base_score=1 - 2 ** -53)
+
+
+def test_quantised_hessian_floor_keeps_nodes_positive():
+    """with fixed-point sums a row at the 1e-16 hessian floor quantises to q = 0 at
+    s < 53, so a node of saturated rows had H == 0 where the exact form keeps H > 0, and with
+    min_child_weight = reg_lambda = 0 its gain and leaf were 0/0.  A positive h now quantises to at
+    least one quantum (oracle and csrc/gbdt.hip quantise_h): every leaf stays finite."""
+    X, y = _saturating_data()
+    m = G.GBDT(hist_mode="quant", backend="numpy", **SAT_KW).fit(X, y)  # (without the fix: -inf leaves)
+    assert m.quant_bits_used > 0
+    assert np.isfinite(m.trees.leaf).all() and np.isfinite(m.trees.gain).all()
+    assert (m.trees.cover[m.trees.status != 0] > 0).all()
+    assert np.isfinite(m.predict(X)).all()
+    q = G._quantise_h(np.array([1e-16, 0.0, 0.25], np.float32), 40)
+    assert q.tolist() == [1, 0, 1 << 38]
+
+
+def test_segment_cumsum_has_no_cross_feature_intermediate():
+    """the fixed-point left sums are per feature segment, so no int64 intermediate grows
+    with the feature count: 62 one-hot features whose cells all sit near the per-node bound (a
+    cumsum over all of them would exceed 2^63) give the exact per-feature left sums."""
+    F, big = 62, (1 << 60) // 2
+    off = np.arange(0, 2 * F + 1, 2)
+    hist = np.full((2 * F, 3), big, dtype=np.int64)
+    got = G._segment_cumsum(hist, off)
+    want = np.tile(np.array([[big], [2 * big]], dtype=np.int64), (F, 3))
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_hip_quantised_saturated_matches_oracle():
+    """The device's quantise_h (fixed-point hessians never round to 0) reproduces the oracle on the
+    saturating case: identical trees, finite leaves."""
+    X, y = _saturating_data()
+    a = G.GBDT(backend="numpy", hist_mode="quant", **SAT_KW).fit(X, y)
+    b = G.GBDT(backend="hip", hist_mode="quant", **SAT_KW).fit(X, y)
+    assert np.array_equal(a.trees.status, b.trees.status) and np.array_equal(a.trees.feat, b.trees.feat)
+    assert np.array_equal(a.trees.sbin, b.trees.sbin)
+    assert np.isfinite(b.trees.leaf).all()
+    assert np.allclose(a.trees.leaf, b.trees.leaf, rtol=1e-6, atol=1e-9)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("obj", ["reg:logistic", "multi:softprob"])
 def test_hip_quantised_matches_oracle(obj):

@@ -7,7 +7,8 @@ reduce into the own xGMI slot -> ``em_adam_xgmi``: publish the flag, poll 7 peer
 rank order, Adam), hipGraph-replayed like bench.py.  The 7 peers are buffers of this process on the
 same device (``em_xgmi_connect_local``), played by ``em_xgmi_emulate_peers``: a one-block kernel on a
 side stream that starts when rank 0 finishes its slab reduction, waits ``skew`` microseconds (the
-peers reaching the exchange later than rank 0), writes the peers' slots and publishes their flags.
+peers reaching the exchange later than rank 0) and publishes their flags.  The peers' slots keep the
+gradient staged into them once at setup (the consumer's reads and sums do not depend on the values).
 
 What it measures: the device cost of the 8-way exchange on top of the single-GPU step (7 extra slot
 reads and flag polls inside the consumer, the side kernel), and how a late peer propagates into the
@@ -58,6 +59,11 @@ def main():
     arr = (ctypes.c_void_p * world)(*[c.value for c in comms])
     N.call("em_xgmi_connect_local", comms[0], world, 0, arr)
     h0 = comms[0].value
+    g0 = torch.randn(P + 1, device=dev) * 1e-3
+    for c in comms:  # both slots of every rank hold a plausible gradient
+        for _ in range(2):
+            N.call("em_xgmi_stage", c.value, g0.data_ptr(), P + 1, N.stream_handle(dev))
+    torch.cuda.synchronize()
 
     def make_step(m, mode, skew_us, side):
         scale = 1.0 / (B * world)
@@ -74,7 +80,7 @@ def main():
             ev.record()
             side.wait_event(ev)
             with torch.cuda.stream(side):
-                N.call("em_xgmi_emulate_peers", h0, P + 1, float(skew_us), N.stream_handle(dev))
+                N.call("em_xgmi_emulate_peers", h0, 0, float(skew_us), N.stream_handle(dev))
             FM.adam_xgmi(h0, m.params, m.m, m.v, m.hp, m.state, img=m.img, loss_out=m.loss_out, pre=True)
             torch.cuda.current_stream().wait_stream(side)
         return step
