@@ -514,6 +514,12 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
             log.info(f"step {step + 1}/{steps} loss {loss:.5f} val_acc {ev.get('acc', float('nan')):.4f} "
                      f"hits {ev.get('hits_main', float('nan')):.3f}+{ev.get('hits_star', float('nan')):.3f}")
         if ckpt_path and cfg.ckpt.every and (step + 1) % cfg.ckpt.every == 0 and not last:
+            # --avg-frequency: rank 0's local parameters and moments are not the model every rank
+            # resumes from after a restart, so a checkpoint between averaging points averages first
+            # (collective; at fixed steps, so a restarted run and an uninterrupted one take the same
+            # averages and stay bit-identical)
+            if engine.avg_k > 0 and engine.n_local % engine.avg_k != 0 and info.is_dist:
+                engine.average_parameters()
             if info.rank == 0:
                 save_mlp_checkpoint(ckpt_path, engine, cfg, sizes, step + 1)
             D.barrier(info)

@@ -174,6 +174,24 @@ def test_elastic_restart_resumes_bit_identical(tmp_path):
         assert np.array_equal(x, y), np.abs(x - y).max()
 
 
+def test_elastic_restart_with_parameter_averaging(tmp_path):
+    """ADVICE r3: --avg-frequency 3 with --ckpt-every 2 takes checkpoints between averaging points;
+    each averages first, so the restart from the step-4 checkpoint continues the interrupted run and
+    the final parameters equal an uninterrupted run's, bit for bit."""
+    ref, got = str(tmp_path / "ref.zip"), str(tmp_path / "restarted.zip")
+    common = ["--steps", "9", "--batch", "128", "--lr", "0.01", "--dp", "2", "--ckpt-every", "2",
+              "--avg-frequency", "3"]
+    r = _cli(_train_argv(common + ["--ckpt", ref]))
+    assert r.returncode == 0, r.stdout[-3000:]
+    r = _cli(_train_argv(common + ["--ckpt", got, "--fault-at-step", "5", "--fault-rank", "1",
+                                   "--max-restarts", "1", "--timeout", "60"]))
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "restart 1/1" in r.stdout
+    a, b = _params(ref), _params(got)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y), np.abs(x - y).max()
+
+
 def test_no_restart_fails_loudly(tmp_path):
     """The same fault with --max-restarts 0: the job exits non-zero (rank 1's code 17)."""
     r = _cli(_train_argv(["--steps", "9", "--batch", "128", "--dp", "2", "--ckpt", str(tmp_path / "x.zip"),
