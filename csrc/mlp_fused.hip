@@ -218,9 +218,6 @@ EM_DEVICE bf16x8 nib_xfrag(const char* smem, uint32_t w, int q) {
 // unrolled over the ring slots (spills), XCD-major stream numbering (-0.5 %).
 //
 // slot: H0 4K | H1 4K | D2 4K | X image 4K
-#ifndef FUSED_V7
-#define FUSED_V7 0
-#endif
 // FUSED_SHARED: one tile stream per workgroup, 4 forward waves (tiles f, f + 4, ...) and 4 backward
 // waves (hidden half rho x tile parity pi) sharing one ring; 0: two independent units of 2 + 2 waves
 #ifndef FUSED_SHARED
@@ -234,9 +231,9 @@ constexpr int V6_NSTREAM = FUSED_SHARED ? 1 : 2;  // tile streams (rings) per wo
 constexpr int V6_NF = FUSED_SHARED ? 4 : 2;       // forward waves per stream
 constexpr int V6_NBP = FUSED_SHARED ? 2 : 1;      // backward waves per hidden half (tile parities)
 constexpr int V6_RSLOTS = FUSED_SHARED ? 6 : 3;   // slots per stream in the ring area
-// + the recycled weight-image slots (v6: the W1ᵀ / W2ᵀ images are dead once the forward waves hold
-// their weights in registers).  v7's forward waves read them every tile, so they stay.
-constexpr int V6_NREC = (FUSED_V7 || !FUSED_RECYCLE) ? 0 : 2 / V6_NSTREAM;
+// + the recycled weight-image slots (the W1ᵀ / W2ᵀ images are dead once the forward waves hold their
+// weights in registers)
+constexpr int V6_NREC = FUSED_RECYCLE ? 2 / V6_NSTREAM : 0;
 constexpr int V6_NSLOT = V6_RSLOTS + V6_NREC;
 static_assert(V6_NREC == 0 || 2 * V6_SLOT <= IMG_W2Q, "recycled slots must fit below the W2Q image");
 static_assert(V6_NSLOT % V6_NBP == 0, "a slot's tiles share one parity");
@@ -418,357 +415,6 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
   for (int k = f; k < K; k += V6_NF) ftile(k, k % V6_NSLOT, k + V6_NF);
 }
 
-// ============================================================================================
-// v7 forward wave: a two-tile software pipeline.  v6's forward wave ran one tile's chain
-// X -> F1 -> relu -> F2 -> softmax -> dZ2 alone, and phase stamps put it at ~4.2 k active cycles per
-// tile with the matrix pipe idle beside the softmax (profiles/r3/fused_timeline_stamps.txt).  Here one
-// iteration finishes tile k's grouped softmax + dZ2 on the VALU while the same wave's 32 MFMAs run
-// tile k + 2's F1 and F2 (the two tiles share nothing, so every VALU step has a whole MFMA slot to
-// issue into; cdna_hip_programming.md T15).  The program order is pinned by sched_barrier fences:
-// 32 slots = {one MFMA, the LDS read of the weight fragment four slots ahead, one softmax step or one
-// relu/pack of F1's output}.  The weights come from the LDS images every tile (32 ds_read_b128): the
-// registers hold two tiles' state instead, and the W1ᵀ / W2ᵀ images stay (3 ring slots per unit).
-// H / X images of tile k + 2 are written into its ring slot at the end of the iteration that staged
-// it (hT / xf stay in registers until then), dZ2 at the end of the next one, then FULL.
-//
-// MFMA slot schedule (F1 hidden tile t = 4 MFMAs over the 64 features; F2 step kk = 16 hidden rows
-// for both output tiles u):
-//   0-3 F1 t0 | 4-7 F1 t1 | 8-11 F2 kk0,1 | 12-15 F1 t2 | 16-19 F2 kk2,3 | 20-23 F1 t3 | 24-31 F2 kk4-7
-// relu/pack of hidden tile t two slots after its last MFMA (slots 5,6 / 9,10 / 17,18 / 25,26).
-template <int N, typename Fn>
-EM_DEVICE void static_for(Fn&& fn) {  // fn(integral_constant<0>) ... fn(integral_constant<N - 1>), in order
-  if constexpr (N > 0) {
-    static_for<N - 1>(fn);
-    fn(std::integral_constant<int, N - 1>{});
-  }
-}
-struct V7Mfma {
-  int kind, a, b;  // kind 0: F1 (t, q), 1: F2 (u, kk)
-};
-EM_DEVICE constexpr V7Mfma v7_mfma(int m) {
-  return m < 8 ? V7Mfma{0, m >> 2, m & 3}
-       : m < 12 ? V7Mfma{1, m & 1, (m - 8) >> 1}
-       : m < 16 ? V7Mfma{0, 2, m & 3}
-       : m < 20 ? V7Mfma{1, m & 1, 2 + ((m - 16) >> 1)}
-       : m < 24 ? V7Mfma{0, 3, m & 3}
-                : V7Mfma{1, m & 1, 4 + ((m - 24) >> 1)};
-}
-// relu/pack placed at slot m: hidden tile t, fragment q (-1 = none)
-EM_DEVICE constexpr int v7_relu(int m) {
-  return m == 5 ? 0 : m == 6 ? 1 : m == 9 ? 2 : m == 10 ? 3 : m == 17 ? 4 : m == 18 ? 5 : m == 25 ? 6
-       : m == 26 ? 7 : -1;
-}
-// softmax step j placed at slot m (-1 = none): the 24 slots without a relu
-EM_DEVICE constexpr int v7_sm_step(int m) {
-  return m < 5 ? m : m < 7 ? -1 : m < 9 ? m - 2 : m < 11 ? -1 : m < 17 ? m - 4 : m < 19 ? -1 : m < 25 ? m - 6
-       : m < 27 ? -1 : m - 8;
-}
-constexpr int V7_LEAD = 4;  // weight fragments are read this many MFMA slots ahead
-
-template <int LOSS, bool SIDX>
-EM_DEVICE void v7_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                          int offset, int unit, int f, int lane, float& loss_acc, bool& ok, Stamps& st) {
-  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
-  const int r = lane & 31, h = lane >> 5;
-  const bool h0 = h == 0;
-  const int nunits = gridDim.x * V6_NSTREAM, U = v6_unit_id(unit);
-  const int K = v6_ntiles_of_unit(B, U, nunits);
-  const uint32_t FL = V6_FLAGS + unit * V6_FLAG_STRIDE;
-  // branch-free prefetch (an exec-masked load made the compiler wait for it at once): samples past the
-  // stream read sample 0 (valid whenever K > 0); the caller masks them by validity
-  auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {
-    const int s = (U + k * nunits) * 32 + r;
-    const int sc = (k < K && s < B) ? s : 0;
-    const int idx = SIDX ? sidx[sc] : (offset + sc);
-    mi = masks[idx];
-    mt = masks[idx + 1];
-  };
-  // keep a step's results where the step computes them: without it LLVM sinks the dZ2 work into the
-  // `if (has_c)` image write after the MFMA slots (sched_barrier orders only within a block)
-  auto pin = [](auto& x) { asm volatile("" : "+v"(x)); };
-  const uint32_t w1a = w1t_off(r, h), w2a = w2p_off(r, h);
-  auto wfrag = [&](int m) {  // the weight (A) fragment of MFMA slot m
-    const V7Mfma x = v7_mfma(m);
-    return x.kind == 0 ? lds_frag(smem, w1a + x.a * 32 * W1T_RS + x.b * 32)
-                       : lds_frag(smem, w2a + x.a * 32 * W2P_RS + x.b * 32);
-  };
-  __syncthreads();  // matches the backward waves' barrier
-  st.start();
-  uint64_t nin = 0, ntg = 0, tmn = 0;
-  bf16x8 xfn[4], wfn[V7_LEAD];
-  // stage-1 operands of tile kn (X fragments from its mask, the first weight fragments), read at the
-  // end of the previous iteration so that the first MFMA slot finds them in registers
-  auto stage_in = [&](int kn) {
-    const bool validn = kn < K && (U + kn * nunits) * 32 + r < B;
-    const uint64_t imask = validn ? (nin | BIAS_BIT) : 0ull;
-    tmn = validn ? ntg : 0ull;
-    fetch(kn + V6_NF, nin, ntg);
-    const uint32_t wlo = (uint32_t)imask >> (8 * h), whi = (uint32_t)(imask >> 32) >> (8 * h);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      xfn[q] = nib_xfrag<V6_XLUT>(smem, q < 2 ? wlo : whi, q);
-      wfn[q] = wfrag(q);
-    }
-  };
-  auto stage_pin = [&]() {  // the reads above complete here (else LLVM sinks them to the first MFMA)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      pin(xfn[q]);
-      pin(wfn[q]);
-    }
-  };
-  static_assert(V7_LEAD == 4, "stage_in reads the first V7_LEAD weight fragments");
-  if (K > 0) {
-    fetch(f, nin, ntg);
-    stage_in(f);
-    stage_pin();
-  }
-  f32x16 zc[2] = {f32x16{}, f32x16{}};  // logits of the tile being finished (zeros before the first)
-  uint64_t tmc = 0;
-  int kc = -1;
-  for (int kn = f;; kn += V6_NF) {
-    const bool has_c = kc >= 0, has_n = kn < K;
-    if (!has_c && !has_n) break;
-    bf16x8 xf[4], wf[32];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      xf[q] = xfn[q];
-      wf[q] = wfn[q];
-    }
-    f32x16 a1[2], z2n[2], b2i[2];
-    bf16x8 hT[4][2];
-
-    // ---- softmax state of tile kc ----
-    const uint32_t tlo = (uint32_t)tmc, thi = (uint32_t)(tmc >> 32);
-    const f32x2 L2E2 = {L2E, L2E};
-    auto zpair = [&](int u, int i) { return f32x2{zc[u][i], zc[u][i + 1]}; };
-    auto exp2p = [](f32x2 t) { return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)}; };
-    float mxa[4], mm = 0.f, ms = 0.f, yb[2][16];
-    f32x2 nmL2 = {0.f, 0.f}, nsL2 = {0.f, 0.f};
-    f32x2 sm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, ss = {0.f, 0.f};
-    f32x2 tdm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, tds = {0.f, 0.f};
-    int nm = 0, ns = 0;
-    float inv_m = 0.f, inv_s = 0.f, S = 1.f, Ss = 1.f, fm = 0.f, fs = 0.f;
-    u32x4 dpk[2][2];
-    auto targets = [&](int u) {
-      const uint32_t tmh = (u == 0 ? tlo : thi) >> (4 * h);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + V6_YLUT + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
-        yb[u][4 * g + 0] = y4[0]; yb[u][4 * g + 1] = y4[1]; yb[u][4 * g + 2] = y4[2]; yb[u][4 * g + 3] = y4[3];
-      }
-    };
-    // dz of element (u, i) from its exp e (stored in zc) and target
-    auto dzv = [&](int u, int i) {
-      const int c0 = out_cls(u, i, 0), c1 = out_cls(u, i, 1);
-      const float e = zc[u][i], y = yb[u][i];
-      if (c0 == c1) {
-        if (c0 == 0) return __builtin_fmaf(e, fm, y * -inv_m);
-        if (c0 == 1) return __builtin_fmaf(e, fs, y * -inv_s);
-        return 0.f;
-      }
-      if (c0 == 0) return __builtin_fmaf(e, h0 ? fm : fs, y * (h0 ? -inv_m : -inv_s));
-      return __builtin_fmaf(e, fs, y * -inv_s);  // star (h = 0) / pad (h = 1): the pad's e and y are 0
-    };
-    auto sm_step = [&](auto J) {
-      constexpr int j = decltype(J)::value;
-      if constexpr (LOSS != 0) return;
-      if constexpr (j == 0) {  // main max over output tile 0 (all main); targets of tile 0
-        mxa[0] = zc[0][0]; mxa[1] = zc[0][1]; mxa[2] = zc[0][2]; mxa[3] = zc[0][3];
-#pragma unroll
-        for (int i = 4; i < 16; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], zc[0][i]);
-        targets(0);
-        for (int k = 0; k < 4; ++k) pin(mxa[k]);
-      } else if constexpr (j == 1) {  // tile 1: 32..49 main (elements 0..7, and 8, 9 for h = 0)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], zc[1][i]);
-        mxa[0] = h0 ? fmaxf(mxa[0], zc[1][8]) : mxa[0];
-        mxa[1] = h0 ? fmaxf(mxa[1], zc[1][9]) : mxa[1];
-        for (int k = 0; k < 4; ++k) pin(mxa[k]);
-      } else if constexpr (j == 2) {
-        mm = xhalf_max(fmaxf(fmaxf(mxa[0], mxa[1]), fmaxf(mxa[2], mxa[3])));
-        nmL2 = f32x2{-mm * L2E, -mm * L2E};
-        pin(nmL2);
-      } else if constexpr (j == 3) {  // star max: elements 10..13 both halves, 14/15 (h = 0) or 8/9 (h = 1)
-        const float a = fmaxf(fmaxf(zc[1][10], zc[1][11]), fmaxf(zc[1][12], zc[1][13]));
-        const float b = fmaxf(h0 ? zc[1][14] : zc[1][8], h0 ? zc[1][15] : zc[1][9]);
-        ms = xhalf_max(fmaxf(a, b));
-        nsL2 = f32x2{-ms * L2E, -ms * L2E};
-        targets(1);
-        pin(nsL2);
-      } else if constexpr (j == 4) {
-        nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
-        ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
-        inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
-        inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
-        pin(inv_m);
-        pin(inv_s);
-      } else if constexpr (j < 9) {  // exps of tile 0 (main), two pairs per step
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int i = 4 * (j - 5) + 2 * q;
-          const f32x2 zz = zpair(0, i);
-          f32x2 e = exp2p(pfma(zz, L2E2, nmL2));
-          sm[q] += e;
-          tdm[q] = pfma(f32x2{yb[0][i], yb[0][i + 1]}, zz, tdm[q]);
-          pin(e);
-          zc[0][i] = e.x;
-          zc[0][i + 1] = e.y;
-        }
-        pin(sm[0]);
-        pin(sm[1]);
-        pin(tdm[0]);
-        pin(tdm[1]);
-      } else if constexpr (j < 13) {  // exps of tile 1 (outputs 32..63: main / star / pad by element)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int i = 4 * (j - 9) + 2 * q;
-          const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
-          const f32x2 zz = zpair(1, i), yy = {yb[1][i], yb[1][i + 1]};
-          f32x2 e;
-          if (c0 == c1 && c0 == 0) {
-            e = exp2p(pfma(zz, L2E2, nmL2));
-            sm[q] += e;
-            tdm[q] = pfma(yy, zz, tdm[q]);
-          } else if (c0 == c1 && c0 == 1) {
-            e = exp2p(pfma(zz, L2E2, nsL2));
-            ss += e;
-            tds = pfma(yy, zz, tds);
-          } else if (c0 == 0) {  // main (h = 0) / star (h = 1): outputs 48/49 | 52/53
-            e = exp2p(pfma(zz, L2E2, h0 ? nmL2 : nsL2));
-            const f32x2 ty = yy * zz;
-            sm[q] = h0 ? sm[q] + e : sm[q];
-            ss = h0 ? ss : ss + e;
-            tdm[q] = h0 ? tdm[q] + ty : tdm[q];
-            tds = h0 ? tds : tds + ty;
-          } else {  // star (h = 0) / pad (h = 1): outputs 58/59 | 62/63
-            const f32x2 ex = exp2p(pfma(zz, L2E2, nsL2));
-            e = h0 ? ex : f32x2{0.f, 0.f};
-            ss += e;
-            tds = h0 ? pfma(yy, zz, tds) : tds;
-          }
-          pin(e);
-          zc[1][i] = e.x;
-          zc[1][i + 1] = e.y;
-        }
-        pin(sm[0]);
-        pin(sm[1]);
-        pin(ss);
-        pin(tdm[0]);
-        pin(tdm[1]);
-        pin(tds);
-      } else if constexpr (j == 13) {
-        S = xhalf_sum((sm[0].x + sm[0].y) + (sm[1].x + sm[1].y));
-        Ss = xhalf_sum(ss.x + ss.y);
-        fm = nm ? __builtin_amdgcn_rcpf(S) : 0.f;
-        fs = ns ? __builtin_amdgcn_rcpf(Ss) : 0.f;
-        pin(fm);
-        pin(fs);
-      } else if constexpr (j < 22) {  // dZ2 = p - y / |y| and its bf16 packing, 4 elements per step
-        const int u = (j - 14) >> 2, i = 4 * ((j - 14) & 3);
-        dpk[u][i >> 3][(i & 7) >> 1] = pack2(dzv(u, i), dzv(u, i + 1));
-        dpk[u][i >> 3][((i & 7) >> 1) + 1] = pack2(dzv(u, i + 2), dzv(u, i + 3));
-        pin(dpk[u][i >> 3]);
-      } else if constexpr (j == 22) {
-        float l = -(((tdm[0].x + tdm[0].y) + (tdm[1].x + tdm[1].y)) * inv_m + (tds.x + tds.y) * inv_s);
-        const float lz = (nm ? mm + __builtin_amdgcn_logf(S) * LN2 : 0.f) + (ns ? ms + __builtin_amdgcn_logf(Ss) * LN2 : 0.f);
-        l += h0 ? lz : 0.f;
-        loss_acc += l;
-        pin(loss_acc);
-      }
-    };
-    if (LOSS != 0) {  // sigmoid-BCE: not interleaved (the headline loss is the softmax)
-      float dz[2][16], lt = 0.f;
-      bce_tile_loss<V6_YLUT>(smem, zc, tmc, tmc != 0, h, dz, lt);
-      loss_acc += lt;
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          dpk[u][q] = __builtin_bit_cast(u32x4, pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2],
-                                                      dz[u][8 * q + 3], dz[u][8 * q + 4], dz[u][8 * q + 5],
-                                                      dz[u][8 * q + 6], dz[u][8 * q + 7]));
-    }
-    st.mark(0);
-
-    // ---- 32 MFMA slots ----
-    static_for<32>([&](auto M) {
-      constexpr int m = decltype(M)::value;
-      constexpr V7Mfma x = v7_mfma(m);
-      if constexpr (x.kind == 0) {
-        const int t = x.a, q = x.b;
-        a1[t & 1] = mfma32(wf[m], xf[q], q == 0 ? f32x16{} : a1[t & 1]);
-      } else {
-        const int u = x.a, kk = x.b;
-        z2n[u] = mfma32(wf[m], hT[kk >> 1][kk & 1], kk == 0 ? b2i[u] : z2n[u]);
-      }
-      if constexpr (m + V7_LEAD < 32) wf[m + V7_LEAD] = wfrag(m + V7_LEAD);
-      if constexpr (m == 4) {  // b2 as F2's initial accumulator
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
-            b2i[u][4 * g + 0] = b[0]; b2i[u][4 * g + 1] = b[1]; b2i[u][4 * g + 2] = b[2]; b2i[u][4 * g + 3] = b[3];
-          }
-      }
-      constexpr int rq = v7_relu(m);
-      if constexpr (rq >= 0) hT[rq >> 1][rq & 1] = relu_pack(a1[(rq >> 1) & 1], rq & 1);
-      constexpr int j = v7_sm_step(m);
-      if constexpr (j >= 0) sm_step(std::integral_constant<int, j>{});
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    st.mark(1);
-
-    // ---- tile kc: dZ2 image, FULL ----
-    if (has_c) {
-      const uint32_t SB = v6_slot(unit, kc % V6_NSLOT);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const u32x4 fq = dpk[u][q];
-          *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 4 * h)) =
-              u32x2{fq[0], fq[1]};
-          *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
-              u32x2{fq[2], fq[3]};
-        }
-      lds_signal(smem, FL + (kc % V6_NSLOT) * 4, kc + 1);  // FULL
-    }
-    st.mark(2);
-    zc[0] = z2n[0];
-    zc[1] = z2n[1];
-    tmc = tmn;
-    stage_in(kn + V6_NF);  // issued before the slot wait and the image stores, which cover their latency
-    // ---- tile kn: H and X images into its slot once both backward waves released it ----
-    if (has_n) {
-      const int slot = kn % V6_NSLOT;
-      const uint32_t SB = v6_slot(unit, slot);
-      if (kn >= V6_NSLOT) {
-        v6_wait(smem, FL + (V6_NSLOT + slot) * 4, kn - V6_NSLOT + 1, ok);
-        v6_wait(smem, FL + (2 * V6_NSLOT + slot) * 4, kn - V6_NSLOT + 1, ok);
-      }
-      st.mark(3);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<bf16x8*>(smem + tile_img<false>(SB + V6_SX, r, 16 * q + 8 * h)) = xf[q];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t HB = SB + V6_SH + (t >> 1) * 4096;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const u32x4 d = __builtin_bit_cast(u32x4, hT[t][q]);
-          *reinterpret_cast<u32x2*>(smem + tile_img<true>(HB, r, 32 * (t & 1) + 16 * q + 4 * h)) = u32x2{d[0], d[1]};
-          *reinterpret_cast<u32x2*>(smem + tile_img<true>(HB, r, 32 * (t & 1) + 16 * q + 8 + 4 * h)) = u32x2{d[2], d[3]};
-        }
-      }
-    }
-    stage_pin();
-    kc = has_n ? kn : -1;
-    st.mark(4);
-  }
-}
-
 // backward wave of hidden half RHO: every tile of the unit's stream.  Every LDS read of the tile
 // (dZ2 A fragments, H / dZ2 / X transposes, W2ᵀ fragments: ~96 VGPRs) is issued at once right after
 // FULL, the slot is released as soon as they have landed, and the 26 MFMAs then run from registers.
@@ -885,10 +531,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   if (ROLE < 2) {
     float loss_acc = 0.f;
     __builtin_amdgcn_s_setprio(FUSED_FPRIO);  // forward waves bound the pipeline (+3 % at 1)
-    if (FUSED_V7)
-      v7_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, unit, sub, lane, loss_acc, ok, st);
-    else
-      v6_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, unit, sub, lane, loss_acc, ok, st);
+    v6_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, unit, sub, lane, loss_acc, ok, st);
     float lsum = wave_sum(loss_acc);
     if (!ok) lsum = __builtin_nanf("");
     dump();

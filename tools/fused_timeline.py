@@ -17,8 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 NAMES = ["F wait slot", "F X+F1+H", "F F2", "F loss", "F D2+signal",
          "B wait full", "B reads", "B B1+dW2+db2", "B mask", "B dW1T"]
-if os.environ.get("TL_V7", "0") == "1":  # v7 forward marks (csrc/mlp_fused.hip v7_forward)
-    NAMES[:5] = ["F bce", "F 32 slots", "F D2+full", "F wait slot", "F HX+stage"]
+
 
 
 def main():
