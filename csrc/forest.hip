@@ -99,7 +99,6 @@ struct RfParams {
 // per candidate), hist[k][64] (sum of w*x_f*y_j) -- exact, so block partials merge with atomics in
 // any order and the split decision is independent of row order and of the block count
 __host__ __device__ inline int rec_words(int k) { return 68 + ((k + 3) & ~3) + 64 * k; }
-
 // Root row lists: rows with non-zero bootstrap weight, compacted per tree by (blocks x tree)
 // workgroups; each 256-row chunk reserves its output range with one atomic (row order inside a list
 // is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
@@ -168,9 +167,42 @@ EM_DEVICE void rf_node_cands(const RfParams& p, int t, int node, int16_t* __rest
   }
 }
 
+// rf_node_cands by one whole wave (all 64 lanes call it): the identity array lives in registers,
+// element e in lane e & 63, register e >> 6 (F <= 256), so the partial Fisher-Yates needs no
+// private array (rf_node_cands' int[256] is scratch memory).  Same hash stream and swaps.
+EM_DEVICE void rf_node_cands_wave(const RfParams& p, int t, int node, int16_t* __restrict__ co) {
+  const int lane = threadIdx.x & 63;
+  int v[RF_MAXF / 64];
+#pragma unroll
+  for (int q = 0; q < RF_MAXF / 64; ++q) v[q] = lane + 64 * q;
+  auto get = [&](int e) {  // arr[e] (e uniform)
+    const int q = e >> 6;
+    const int src = q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+    return __shfl(src, e & 63);
+  };
+  auto put = [&](int e, int val) {  // arr[e] = val (e uniform)
+    if (lane == (e & 63)) {
+      const int q = e >> 6;
+      if (q == 0) v[0] = val;
+      else if (q == 1) v[1] = val;
+      else if (q == 2) v[2] = val;
+      else v[3] = val;
+    }
+  };
+  const int kk = p.k_feat < p.F ? p.k_feat : p.F;
+  for (int i = 0; i < kk; ++i) {
+    const uint64_t h = hash3(p.seed ^ 0x5EEDF00Dull, ((uint64_t)(t + p.t_off) << 32) | (uint64_t)node, (uint64_t)i);
+    const int j = i + (int)(h % (uint64_t)(p.F - i));
+    const int ai = get(i), aj = get(j);
+    put(i, aj);
+    put(j, ai);
+    if (lane == 0) co[i] = (int16_t)aj;
+  }
+}
+
 // One thread per (tree, node of this level): child segments from the parent's partition counters,
 // then the node's candidate features (partial Fisher-Yates on a hashed stream, as the oracle).
-__global__ void rf_level_prep(RfParams p, int level, int have_cands) {
+__global__ void rf_level_prep(RfParams p, int level) {
   const int nodesL = 1 << level, first = nodesL - 1;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)p.T * nodesL) return;
@@ -191,19 +223,8 @@ __global__ void rf_level_prep(RfParams p, int level, int have_cands) {
   }
   sg[0] = start;
   sg[1] = count;
-  if (count < 0 || level >= p.max_depth || have_cands) return;  // have_cands: rf_level_cands drew them
+  if (count < 0 || level >= p.max_depth) return;
   rf_node_cands(p, t, node, p.cand + ((int64_t)t * nodesL + nd) * p.k_feat);
-}
-
-// Candidates of every node of `level` into cand_out (present or not): the fused partition of level - 1
-// accumulates the children's histograms before rf_level_prep(level) runs, so they are drawn here (they
-// depend on (seed, tree, node) only) and rf_level_prep(level) skips them.
-__global__ void rf_level_cands(RfParams p, int level, int16_t* __restrict__ cand_out) {
-  const int nodesL = 1 << level, first = nodesL - 1;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)p.T * nodesL) return;
-  const int t = (int)(gid / nodesL), nd = (int)(gid - (int64_t)t * nodesL);
-  rf_node_cands(p, t, first + nd, cand_out + ((int64_t)t * nodesL + nd) * p.k_feat);
 }
 
 // Level work lists.  Deep levels are very unbalanced (a one-hot split sends ~90 % of a node's rows to
@@ -231,6 +252,83 @@ EM_DEVICE bool rf_work(const int32_t* __restrict__ wl, int nitems, int nodesL, R
 
 __global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32_t* __restrict__ wl) {
   const int nodesL = 1 << level, first = nodesL - 1, n = p.T * nodesL;
+  __shared__ int part[1024];
+  const int per = (n + 1023) / 1024, a = threadIdx.x * per, b = min(n, a + per);
+  auto blocks = [&](int i) {
+    const int t = i / nodesL, nd = i - t * nodesL;
+    const int cnt = p.seg[((int64_t)t * p.nodes + first + nd) * 2 + 1];
+    return cnt < 0 ? 0 : max(1, (cnt + RF_CHUNK - 1) / RF_CHUNK);
+  };
+  int sum = 0;
+  for (int i = a; i < b; ++i) sum += blocks(i);
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = part[threadIdx.x] - sum;
+  for (int i = a; i < b; ++i) {
+    wl[i] = run;
+    run += blocks(i);
+  }
+  if (threadIdx.x == 1023) wl[n] = part[1023];
+}
+
+// The fused driver's level start in ONE workgroup: rf_level_prep (child segments; candidates at the
+// root only: deeper levels' are drawn by the parent's rf_split), then -- after every segment is
+// written and every parent counter read -- this level's partition counters zeroed (and, at the root,
+// the root records), then rf_worklist's scan.  Replaces 2 kernels and 1-2 memsets per level.
+__global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, int32_t* __restrict__ wl) {
+  const int nodesL = 1 << level, first = nodesL - 1, n = p.T * nodesL;
+  // items in batches of 8 per thread: the batch's parent loads are all issued before its stores
+  constexpr int PB = 8;
+  for (int g0 = 0; g0 < n; g0 += PB * 1024) {
+    int ps0[PB], ps1[PB], pf[PB], lc[PB];
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const int gid = g0 + u * 1024 + (int)threadIdx.x;
+      ps0[u] = 0;
+      ps1[u] = -1;
+      pf[u] = -1;
+      lc[u] = 0;
+      if (gid >= n) continue;
+      const int t = gid / nodesL, nd = gid - t * nodesL, node = first + nd;
+      if (level == 0) {
+        lc[u] = p.lrc[(int64_t)t * 2];
+      } else {
+        const int parent = (node - 1) >> 1, pnd = parent - ((nodesL >> 1) - 1);
+        ps0[u] = p.seg[((int64_t)t * p.nodes + parent) * 2];
+        ps1[u] = p.seg[((int64_t)t * p.nodes + parent) * 2 + 1];
+        pf[u] = p.feat[(int64_t)t * p.nodes + parent];
+        lc[u] = p.lrc[((int64_t)t * (nodesL >> 1) + pnd) * 2];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const int gid = g0 + u * 1024 + (int)threadIdx.x;
+      if (gid >= n) continue;
+      const int t = gid / nodesL, nd = gid - t * nodesL, node = first + nd;
+      int start = 0, count = -1;
+      if (level == 0) {
+        count = lc[u];
+      } else if (ps1[u] >= 0 && pf[u] >= 0) {
+        const bool left = ((node - 1) & 1) == 0;
+        start = left ? ps0[u] : ps0[u] + lc[u];
+        count = left ? lc[u] : ps1[u] - lc[u];
+      }
+      int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
+      sg[0] = start;
+      sg[1] = count;
+      if (level == 0 && count >= 0 && p.max_depth > 0) rf_node_cands(p, t, node, p.cand + (int64_t)t * p.k_feat);
+    }
+  }
+  __syncthreads();  // segments written, the parents' counters read
+  for (int i = threadIdx.x; i < 2 * n; i += 1024) p.lrc[i] = 0;
+  if (level == 0)
+    for (int i = threadIdx.x; i < n * rec_words(p.k_feat); i += 1024) p.acc[i] = 0u;
   __shared__ int part[1024];
   const int per = (n + 1023) / 1024, a = threadIdx.x * per, b = min(n, a + per);
   auto blocks = [&](int i) {
@@ -494,7 +592,12 @@ __global__ void __launch_bounds__(RF_NT) rf_hist_mfma(RfParams p, const RfRec* _
 
 // K9: one wavefront per (tree, node): node record (weighted mean outputs, cover) and the split scan
 // over the candidates (lane j = output j): gain = SL2/nL + SR2/nR - S2/n from exact integers.
-__global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
+// child_acc (the fused driver, derived totals): a node that splits also writes its two children's
+// records for level + 1 -- node totals S / n (right = the histogram of the split candidate, left =
+// parent - right: rf_child_totals' arithmetic), every other word zeroed for the partition's histogram
+// atomics -- and, with child_cand, draws the children's candidate features (rf_node_cands).
+__global__ void __launch_bounds__(64) rf_split(RfParams p, int level, uint32_t* __restrict__ child_acc,
+                                               int16_t* __restrict__ child_cand) {
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.y, nd = blockIdx.x, node = first + nd;
   const int lane = threadIdx.x;
@@ -545,6 +648,20 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level) {
     p.gain[(int64_t)t * p.nodes + node] = bf >= 0 ? best : 0.0;
     A[65] = bf >= 0 ? (uint32_t)bc : 0u;  // candidate slot of the split (rf_child_totals)
   }
+  if (bf < 0 || !child_acc) return;
+  const uint32_t sr = A[68 + kp + bc * 64 + lane], nr = A[68 + bc];
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {  // sd 0: x_f = 0 child (2 node + 1), 1: x_f = 1 child
+    uint32_t* dst = child_acc + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * rec;
+    dst[lane] = sd ? sr : A[lane] - sr;
+    // words 68.. are the partition's: it stores them when one block owns this node (rf_worklist:
+    // ceil(count / RF_CHUNK) blocks) and adds into zeroed words otherwise
+    const int hi = (sg[1] + RF_CHUNK - 1) / RF_CHUNK > 1 ? rec : 68;
+    for (int i = 64 + lane; i < hi; i += 64) dst[i] = i == 64 ? (sd ? nr : n - nr) : 0u;
+  }
+  if (child_cand)
+    for (int sd = 0; sd < 2; ++sd)
+      rf_node_cands_wave(p, t, 2 * node + 1 + sd, child_cand + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * k);
 }
 
 // K10: children row lists, (blocks x nodes x trees) workgroups: left rows (x_f = 0) fill the parent
@@ -678,8 +795,12 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
 #pragma unroll
     for (int sd = 0; sd < 2; ++sd) {
       uint32_t* dst = acc_next + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * rec;
-      for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x)
-        if (chl[sd * rec + i]) atomicAdd(&dst[i], chl[sd * rec + i]);
+      if (B == 1) {  // the node's only block: plain stores (rf_split did not zero these words)
+        for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x) dst[i] = chl[sd * rec + i];
+      } else {
+        for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x)
+          if (chl[sd * rec + i]) atomicAdd(&dst[i], chl[sd * rec + i]);
+      }
     }
   }
 }
@@ -814,6 +935,42 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   void* rin = rows_a;
   void* rout = rows_b;
   const int64_t kept = bootstrap ? (N * 632) / 1000 : N;  // expected rows per tree (Poisson(1): 1 - 1/e)
+  if (fuse) {
+    // per level: rf_level_begin (segments, counters, work list), the root's histogram pass (level 0
+    // only), rf_split (also the children's totals, zeroed records and candidates), the partition
+    // (also the children's histograms while a next level still splits) -- 3 launches per level
+    for (int level = 0; level <= max_depth; ++level) {
+      const int nodesL = 1 << level;
+      int B, nt;
+      rf_shape(kept, level, B, nt);
+      (void)B;
+      const int64_t tn = (int64_t)T * nodesL;
+      p.acc = accs[level & 1];
+      p.cand = cands[level & 1];
+      hipLaunchKernelGGL(rf_level_begin, dim3(1), dim3(1024), 0, stream, p, level, wl);
+      const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;
+      const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
+      if (level == 0)
+        hipLaunchKernelGGL((rf_hist<true, false>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level,
+                           (const int32_t*)wl);
+      uint32_t* an = level < max_depth ? accs[(level + 1) & 1] : nullptr;
+      int16_t* cn = level + 1 < max_depth ? cands[(level + 1) & 1] : nullptr;
+      hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level, an, cn);
+      EM_CHECK_LAUNCH();
+      if (level == max_depth) break;
+      if (level + 1 < max_depth)
+        hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), 2 * lds, stream, p, (const void*)rin, rout,
+                           level, (const int32_t*)wl, an, (const int16_t*)cn);
+      else
+        hipLaunchKernelGGL((rf_partition<true, false>), dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
+                           (const int32_t*)wl, (uint32_t*)nullptr, (const int16_t*)nullptr);
+      EM_CHECK_LAUNCH();
+      void* tmp = rin;
+      rin = rout;
+      rout = tmp;
+    }
+    return 0;
+  }
   for (int level = 0; level <= max_depth; ++level) {
     const int nodesL = 1 << level;
     int B, nt;
@@ -821,20 +978,16 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     const int64_t tn = (int64_t)T * nodesL;
     p.acc = accs[level & 1];  // this level's node records and candidate lists (double-buffered)
     p.cand = cands[level & 1];
-    const bool fused_prev = fuse && level >= 1 && level < max_depth;  // built by partition(level - 1)
-    hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level,
-                       (int)fused_prev);
+    hipLaunchKernelGGL(rf_level_prep, dim3((unsigned)((tn + 127) / 128)), dim3(128), 0, stream, p, level);
     hipLaunchKernelGGL(rf_worklist, dim3(1), dim3(1024), 0, stream, p, level, wl);
     // grid: an upper bound of the work list (the kernels exit past wl[tn])
     const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;  // kept rows per tree <= N
     const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
     (void)B;
-    if (!fused_prev) (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
+    (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
     const bool dl = derive && level > 0;
     if (dl) hipLaunchKernelGGL(rf_child_totals, dim3(nodesL, T), dim3(64), 0, stream, p, accs[(level - 1) & 1], level);
-    if (fused_prev)
-      ;  // cnt / hist words were accumulated by the fused partition of the previous level
-    else if (use_mfma)
+    if (use_mfma)
       hipLaunchKernelGGL(rf_hist_mfma, dim3(G), dim3(nt), lds_mfma, stream, p, (const RfRec*)rin, level, (const int32_t*)wl);
     else if (dl && level == max_depth)
       ;  // the last level needs node totals only: all derived
@@ -846,19 +999,12 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
       hipLaunchKernelGGL((rf_hist<false, true>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
     else
       hipLaunchKernelGGL((rf_hist<false, false>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
-    hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level);
+    hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level, (uint32_t*)nullptr,
+                       (int16_t*)nullptr);
     EM_CHECK_LAUNCH();
     if (level == max_depth) break;
     (void)hipMemsetAsync(lrc, 0, (size_t)tn * 2 * sizeof(int32_t), stream);
-    if (fuse && level + 1 < max_depth) {
-      const int64_t tn2 = 2 * tn;
-      int16_t* cn = cands[(level + 1) & 1];
-      hipLaunchKernelGGL(rf_level_cands, dim3((unsigned)((tn2 + 127) / 128)), dim3(128), 0, stream, p, level + 1, cn);
-      uint32_t* an = accs[(level + 1) & 1];  // = the records of level - 1, already read by rf_child_totals(level)
-      (void)hipMemsetAsync(an, 0, (size_t)tn2 * rec * sizeof(uint32_t), stream);
-      hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), 2 * lds, stream, p, (const void*)rin, rout,
-                         level, (const int32_t*)wl, an, (const int16_t*)cn);
-    } else if (rec_rows) {
+    if (rec_rows) {
       hipLaunchKernelGGL((rf_partition<true, false>), dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
                          (const int32_t*)wl, (uint32_t*)nullptr, (const int16_t*)nullptr);
     } else {

@@ -941,438 +941,6 @@ gbdt_metric_sum(const double* __restrict__ partial, int nb, double* __restrict__
   if (threadIdx.x == 0) out[0] = s;
 }
 
-// ---------------------------------------------------------------- small fits: one block per task
-// Reference-sized fits (Main.java:113-141: 62 boosters, ~930 draws, depth 3, 500 rounds) are bound
-// by launch latency on the level-by-level path: 13-19 launches per round, each a few microseconds
-// of mostly idle CUs for ~60 k (row, feature) updates.  Here ONE 1024-thread block per task keeps its
-// rows resident in LDS (a packed bin record per row, margin, label, g, h, node) and runs every round
-// of the call: grad -> per level: histogram, split scan (one wave per node), partition -> prune +
-// leaves -> margin update and eval prediction.  The T blocks never communicate.
-// Bit-identical to the level path (em_gbdt_fit with EM_GBDT_SMALL=0, eager or graph-replayed):
-//  * histograms use the level plan's own summation structure (plan_hist: chunk, P row phases,
-//    pieces): unit (chunk c, phase p) sums its rows in row order from 0, a chunk is 0 + unit p=0 +
-//    p=1 + ..., the level's cell is chunk 0 + chunk 1 + ... in chunk order.  Units run Gc chunks at
-//    a time in private LDS slots and fold into the running total between groups.
-//  * split scan, pruning, leaves and margins are gbdt_split / gbdt_finalize / gbdt_update /
-//    gbdt_predict's arithmetic.
-//  * metrics: every element's term goes to HBM, and gbdt_small_metric_blocks + gbdt_small_metric_final
-//    reduce them exactly as the fused update/predict-metric launches' blocks and last block do.
-constexpr int SM_NT = 1024, SM_NW = SM_NT / 64;
-constexpr int SM_LDS = 160 * 1024;
-constexpr int SM_MAX_EVALS = 4, SM_MAX_DEPTH = 6;
-
-struct SmEval {
-  const uint8_t* bins;  // [n][F]
-  const float* Y;       // [n][T]
-  float* margin;        // [T][n]
-  int n;
-};
-struct SmLevel {
-  int chunk, nchunks, P, piece, Gc;  // the level plan's chunking; Gc chunks' units per group
-};
-struct SmLayout {  // byte offsets into the block's dynamic LDS (doubles first)
-  int hist, G, H, rec, desc, marg, y, g, h, em, ey, lf, gn, fe, st, sb, node;
-};
-struct SmArgs {
-  const uint8_t* bins;
-  const float* Y;
-  float* margin;
-  const int* foff;
-  int n, F, T, C, NN, max_depth, obj, metric, r0, r1, n_evals;
-  int RW, WBW;  // packed record: u32 words per row, words of one-hot bits before the byte features
-  float eta, lam, gamma, mcw, subsample;
-  uint32_t seed;
-  int8_t* status;
-  int16_t* feat;
-  uint8_t* sbin;
-  float* leaf;
-  float* gain;
-  float* cover;
-  double* terms;     // [r1 - r0][sum over sets of T * n_set]: per-element metric terms
-  int64_t tstride;   // doubles per round in `terms`
-  SmLevel lv[SM_MAX_DEPTH];
-  SmLayout L;
-  SmEval ev[SM_MAX_EVALS];
-};
-
-__host__ __device__ inline int sm_align(int x, int a) { return (x + a - 1) / a * a; }
-// LDS of everything but the histogram slots, which take the rest (from L.hist to SM_LDS)
-__host__ __device__ inline SmLayout sm_layout(int n, int F, int NN, int RW, int ne_tot) {
-  SmLayout L;
-  int o = 0;
-  L.G = o;
-  o += sm_align(NN * 8, 16);
-  L.H = o;
-  o += sm_align(NN * 8, 16);
-  L.rec = o;
-  o += sm_align(n * RW * 4, 16);
-  L.desc = o;
-  o += sm_align(F * 4, 16);
-  L.marg = o;
-  o += sm_align(n * 4, 16);
-  L.y = o;
-  o += sm_align(n * 4, 16);
-  L.g = o;
-  o += sm_align(n * 4, 16);
-  L.h = o;
-  o += sm_align(n * 4, 16);
-  L.em = o;
-  o += sm_align(ne_tot * 4, 16);
-  L.ey = o;
-  o += sm_align(ne_tot * 4, 16);
-  L.lf = o;
-  o += sm_align(NN * 4, 16);
-  L.gn = o;
-  o += sm_align(NN * 4, 16);
-  L.fe = o;
-  o += sm_align(NN * 2, 16);
-  L.st = o;
-  o += sm_align(NN, 16);
-  L.sb = o;
-  o += sm_align(NN, 16);
-  L.node = o;
-  o += sm_align(n, 16);
-  L.hist = o;
-  return L;
-}
-
-// bin of row r, feature with descriptor d (word | shift << 16 | byte-feature << 24) from the packed records
-EM_DEVICE int sm_bin(const uint32_t* rec, int RW, int r, uint32_t d) {
-  return (int)((rec[r * RW + (d & 0xFFFF)] >> ((d >> 16) & 31)) & ((d >> 24) ? 0xFFu : 1u));
-}
-
-__global__ void __launch_bounds__(SM_NT)
-gbdt_fit_small(const SmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const SmLayout& L = a.L;
-  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = a.n, F = a.F, T = a.T, C = a.C, NN = a.NN, RW = a.RW;
-  double* hist = reinterpret_cast<double*>(smem + L.hist);
-  double* G = reinterpret_cast<double*>(smem + L.G);
-  double* H = reinterpret_cast<double*>(smem + L.H);
-  uint32_t* rec = reinterpret_cast<uint32_t*>(smem + L.rec);
-  uint32_t* desc = reinterpret_cast<uint32_t*>(smem + L.desc);
-  float* marg = reinterpret_cast<float*>(smem + L.marg);
-  float* ys = reinterpret_cast<float*>(smem + L.y);
-  float* gs = reinterpret_cast<float*>(smem + L.g);
-  float* hs = reinterpret_cast<float*>(smem + L.h);
-  float* em = reinterpret_cast<float*>(smem + L.em);
-  float* ey = reinterpret_cast<float*>(smem + L.ey);
-  float* lf = reinterpret_cast<float*>(smem + L.lf);
-  float* gn = reinterpret_cast<float*>(smem + L.gn);
-  int16_t* fe = reinterpret_cast<int16_t*>(smem + L.fe);
-  int8_t* st = reinterpret_cast<int8_t*>(smem + L.st);
-  uint8_t* sb = reinterpret_cast<uint8_t*>(smem + L.sb);
-  uint8_t* node = reinterpret_cast<uint8_t*>(smem + L.node);
-  const double lam = a.lam, mcw = a.mcw;
-
-  // ---- residency.  Feature descriptors: a 2-bin feature is one bit of the row record (bit index =
-  // its rank among the 2-bin features), any other a byte after the bit words.
-  for (int f = tid; f < F; f += SM_NT) {
-    int nb = 0;
-    for (int k = 0; k < f; ++k) nb += (a.foff[k + 1] - a.foff[k]) == 2;
-    const bool bit = (a.foff[f + 1] - a.foff[f]) == 2;
-    const int kb = f - nb;  // byte index of a byte feature
-    desc[f] = bit ? (uint32_t)((nb >> 5) | ((nb & 31) << 16))
-                  : (uint32_t)((a.WBW + (kb >> 2)) | ((8 * (kb & 3)) << 16) | (1u << 24));
-  }
-  for (int i = tid; i < n * RW; i += SM_NT) rec[i] = 0u;
-  for (int r = tid; r < n; r += SM_NT) {
-    marg[r] = a.margin[(int64_t)t * n + r];
-    ys[r] = a.Y[(int64_t)r * T + t];
-  }
-  {
-    int eo = 0;
-    for (int e = 0; e < a.n_evals; ++e) {
-      const SmEval& ev = a.ev[e];
-      for (int r = tid; r < ev.n; r += SM_NT) {
-        em[eo + r] = ev.margin[(int64_t)t * ev.n + r];
-        ey[eo + r] = ev.Y[(int64_t)r * T + t];
-      }
-      eo += ev.n;
-    }
-  }
-  __syncthreads();
-  for (int r = tid; r < n; r += SM_NT) {  // each row's record is built by one thread
-    const uint8_t* row = a.bins + (int64_t)r * F;
-    for (int f = 0; f < F; ++f) {
-      const uint32_t d = desc[f];
-      rec[r * RW + (d & 0xFFFF)] |= (uint32_t)row[f] << ((d >> 16) & 31);
-    }
-  }
-  // (the first round's barrier orders the records before any read)
-  const int nthF = F < SM_NT ? F : SM_NT;  // feature lanes of one unit
-  for (int round = a.r0; round < a.r1; ++round) {
-    // ---- round start: tree reset, g / h, every row at the root, level 0's unit slots zeroed
-    for (int i = tid; i < NN; i += SM_NT) {
-      st[i] = i == 0 ? 2 : 0;
-      fe[i] = -1;
-      sb[i] = 0;
-      gn[i] = 0.f;
-    }
-    for (int r = tid; r < n; r += SM_NT) {
-      const float m = marg[r], y = ys[r];
-      float gg, hh;
-      if (a.obj == OBJ_LOGISTIC) {
-        const float p = 1.f / (1.f + expf(-m));
-        gg = p - y;
-        hh = fmaxf(p * (1.f - p), 1e-16f);
-      } else {
-        gg = m - y;
-        hh = 1.f;
-      }
-      if (a.subsample < 1.f) {
-        const float u = (hash3(a.seed, (uint32_t)round * 131071u + t, r) >> 8) * (1.f / 16777216.f);
-        if (u >= a.subsample) gg = hh = 0.f;
-      }
-      gs[r] = gg;
-      hs[r] = hh;
-      node[r] = 0;
-    }
-    for (int i = tid; i < a.lv[0].Gc * a.lv[0].P * C * 2; i += SM_NT) hist[i] = 0.0;
-    __syncthreads();
-    for (int level = 0; level < a.max_depth; ++level) {
-      const int nodesL = 1 << level, first = nodesL - 1, last = 2 * nodesL - 1;
-      const SmLevel lv = a.lv[level];
-      const int P = lv.P, units = lv.Gc * lv.P;
-      const int per = nodesL * C * 2;      // doubles per slot
-      double* total = hist + (size_t)units * per;  // the level's folded histogram
-      for (int g0 = 0; g0 < lv.nchunks; g0 += lv.Gc) {
-        // ---- units (chunk g0 + u / P, phase u % P) x feature lanes: rows in row order into the unit's slot
-        {
-          const int u = tid / nthF, fl = tid - u * nthF;
-          const int c = g0 + u / P, p = u - (u / P) * P;
-          if (u < units && c < lv.nchunks) {
-            const int rb = c * lv.chunk, re = min(n, rb + lv.chunk);
-            for (int f = fl; f < F; f += nthF) {
-              double* my = hist + (size_t)u * per + 2 * a.foff[f];
-              const uint32_t d = desc[f];
-              for (int r0 = rb; r0 < re; r0 += lv.piece) {
-                const int len = min(re, r0 + lv.piece) - r0, sub = (len + P - 1) / P;
-                const int a0 = r0 + min(len, p * sub), a1 = r0 + min(len, min(len, p * sub) + sub);
-                int r = a0;
-                for (; r + 8 <= a1; r += 8) {  // 8 rows' inputs, then their updates in row order
-                  int b[8], nd[8];
-                  float gv[8], hv[8];
-#pragma unroll
-                  for (int k = 0; k < 8; ++k) {
-                    b[k] = sm_bin(rec, RW, r + k, d);
-                    nd[k] = (int)node[r + k] - first;
-                    gv[k] = gs[r + k];
-                    hv[k] = hs[r + k];
-                  }
-#pragma unroll
-                  for (int k = 0; k < 8; ++k) {
-                    if ((unsigned)nd[k] >= (unsigned)nodesL) continue;
-                    double* e = my + (nd[k] * C + b[k]) * 2;
-                    e[0] += (double)gv[k];
-                    e[1] += (double)hv[k];
-                  }
-                }
-                for (; r < a1; ++r) {
-                  const int nd = (int)node[r] - first;
-                  if ((unsigned)nd >= (unsigned)nodesL) continue;
-                  double* e = my + (nd * C + sm_bin(rec, RW, r, d)) * 2;
-                  e[0] += (double)gs[r];
-                  e[1] += (double)hs[r];
-                }
-              }
-            }
-          }
-        }
-        __syncthreads();
-        // ---- fold: chunk = 0 + its phases in order; total = chunk 0, then + each chunk in order.
-        // The unit slots are re-zeroed for the next group (a cell is read and cleared by one thread).
-        const int gc = min(lv.Gc, lv.nchunks - g0);
-        for (int i = tid; i < per; i += SM_NT) {
-          double tot = g0 ? total[i] : 0.0;
-          for (int cl = 0; cl < gc; ++cl) {
-            double v = 0.0;
-            for (int q = 0; q < P; ++q) {
-              double* s = hist + (size_t)(cl * P + q) * per + i;
-              v += *s;
-              *s = 0.0;
-            }
-            tot = (g0 + cl) ? tot + v : v;
-          }
-          total[i] = tot;
-        }
-        __syncthreads();
-      }
-      // ---- split scan: one wave per node (gbdt_split's arithmetic and tie rule)
-      for (int nd = w; nd < nodesL; nd += SM_NW) {
-        const int i = first + nd;
-        if (st[i] != 2) continue;  // wave-uniform
-        const double* hn = total + (size_t)nd * C * 2;
-        double Gn, Hn;
-        if (level == 0) {  // node totals: feature 0's cells in bin order
-          Gn = 0.0;
-          Hn = 0.0;
-          for (int c = a.foff[0]; c < a.foff[1]; ++c) {
-            Gn += hn[2 * c];
-            Hn += hn[2 * c + 1];
-          }
-        } else {
-          Gn = G[i];
-          Hn = H[i];
-        }
-        const double root = Gn * Gn / (Hn + lam);
-        double best = -INFINITY, bGL = 0.0, bHL = 0.0;
-        int bf = 0x7fffffff, bb = 0;
-        for (int f = lane; f < F; f += 64) {
-          const int ca = a.foff[f], cb = a.foff[f + 1];
-          double GL = 0.0, HL = 0.0;
-          for (int c = ca; c < cb - 1; ++c) {
-            GL += hn[2 * c];
-            HL += hn[2 * c + 1];
-            const double GR = Gn - GL, HR = Hn - HL;
-            if (HL >= mcw && HR >= mcw) {
-              const double gv = GL * GL / (HL + lam) + GR * GR / (HR + lam) - root;
-              if (gv > best) {
-                best = gv;
-                bf = f;
-                bb = c - ca;
-                bGL = GL;
-                bHL = HL;
-              }
-            }
-          }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const double ov = __shfl_xor(best, o), ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
-          const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o);
-          if (ov > best || (ov == best && of < bf)) {
-            best = ov;
-            bf = of;
-            bb = ob;
-            bGL = ogl;
-            bHL = ohl;
-          }
-        }
-        if (lane == 0) {
-          if (level == 0) {
-            G[0] = Gn;
-            H[0] = Hn;
-          }
-          if (bf < F && best > KRT_EPS) {
-            st[i] = 1;
-            fe[i] = (int16_t)bf;
-            sb[i] = (uint8_t)bb;
-            gn[i] = (float)best;
-            const int l = 2 * i + 1, rr = 2 * i + 2;
-            st[l] = 2;
-            st[rr] = 2;
-            G[l] = bGL;
-            H[l] = bHL;
-            G[rr] = Gn - bGL;
-            H[rr] = Hn - bHL;
-          }
-        }
-      }
-      __syncthreads();
-      // ---- partition; the next level's unit slots zeroed alongside (its total is written, not added)
-      for (int r = tid; r < n; r += SM_NT) {
-        const int nd = node[r];
-        if (nd < first || nd >= last || st[nd] != 1) continue;
-        node[r] = (uint8_t)(2 * nd + 1 + (sm_bin(rec, RW, r, desc[fe[nd]]) > sb[nd] ? 1 : 0));
-      }
-      if (level + 1 < a.max_depth)
-        for (int i = tid; i < a.lv[level + 1].Gc * a.lv[level + 1].P * 2 * per; i += SM_NT) hist[i] = 0.0;
-      __syncthreads();
-    }
-    // ---- prune (gamma, bottom-up) and leaves: gbdt_finalize
-    if (tid == 0) {
-      for (int i = (1 << a.max_depth) - 2; i >= 0; --i)
-        if (st[i] == 1 && st[2 * i + 1] == 2 && st[2 * i + 2] == 2 && gn[i] < a.gamma) {
-          st[i] = 2;
-          st[2 * i + 1] = 0;
-          st[2 * i + 2] = 0;
-          fe[i] = -1;
-        }
-      for (int i = 0; i < NN; ++i) lf[i] = st[i] == 2 ? (float)(-G[i] / (H[i] + lam) * (double)a.eta) : 0.f;
-    }
-    __syncthreads();
-    {
-      const int64_t o = ((int64_t)round * T + t) * NN;
-      for (int i = tid; i < NN; i += SM_NT) {
-        a.status[o + i] = st[i];
-        a.feat[o + i] = fe[i];
-        a.sbin[o + i] = sb[i];
-        a.gain[o + i] = gn[i];
-        a.leaf[o + i] = lf[i];
-        a.cover[o + i] = st[i] ? (float)H[i] : 0.f;
-      }
-    }
-    // ---- train margins (gbdt_update), then each eval set's one-tree prediction (gbdt_predict);
-    // metric terms of element i = t * n_set + r to HBM
-    double* tm = a.terms + (int64_t)(round - a.r0) * a.tstride;
-    for (int r = tid; r < n; r += SM_NT) {
-      const float m = marg[r] + lf[leaf_ancestor(st, node[r])];
-      marg[r] = m;
-      tm[(int64_t)t * n + r] = metric_term(m, ys[r], a.obj, a.metric);
-    }
-    tm += (int64_t)T * n;
-    int eo = 0;
-    for (int e = 0; e < a.n_evals; ++e) {
-      const SmEval& ev = a.ev[e];
-      for (int r = tid; r < ev.n; r += SM_NT) {
-        const uint8_t* row = ev.bins + (int64_t)r * F;
-        int nd = 0;
-        while (st[nd] == 1) nd = 2 * nd + 1 + (row[fe[nd]] > sb[nd] ? 1 : 0);
-        float tacc = 0.f;
-        tacc += lf[nd];
-        const float m = em[eo + r] + tacc;
-        em[eo + r] = m;
-        tm[(int64_t)t * ev.n + r] = metric_term(m, ey[eo + r], a.obj, a.metric);
-      }
-      tm += (int64_t)T * ev.n;
-      eo += ev.n;
-    }
-    __syncthreads();  // the tree is re-initialised by the next round
-  }
-  // ---- margins back to HBM (the next call, and predict, continue from them)
-  for (int r = tid; r < n; r += SM_NT) a.margin[(int64_t)t * n + r] = marg[r];
-  int eo = 0;
-  for (int e = 0; e < a.n_evals; ++e) {
-    const SmEval& ev = a.ev[e];
-    for (int r = tid; r < ev.n; r += SM_NT) ev.margin[(int64_t)t * ev.n + r] = em[eo + r];
-    eo += ev.n;
-  }
-}
-
-// The metric reductions of the fused launches, replayed over stored terms.  Set s of a round has
-// total_s = T * n_s terms and mb_s = grid_for(total_s) virtual blocks; virtual block b sums its grid-
-// stride elements in order and tree-reduces them (block_tree_sum), the final sum is
-// block_sum_partials over the mb_s block sums (= metric_arrive_final).
-struct SmMetricSets {
-  int64_t total[1 + SM_MAX_EVALS];
-  int64_t off[1 + SM_MAX_EVALS];  // offset of the set's terms within a round
-  int mb[1 + SM_MAX_EVALS];
-};
-__global__ void __launch_bounds__(256)
-gbdt_small_metric_blocks(const double* __restrict__ terms, int64_t tstride, SmMetricSets ms,
-                         double* __restrict__ bpart) {
-  const int b = blockIdx.x, s = blockIdx.y, rd = blockIdx.z;
-  const int mb = ms.mb[s];
-  if (b >= mb) return;  // block-uniform
-  const double* tp = terms + (int64_t)rd * tstride + ms.off[s];
-  double acc = 0.0;
-  for (int64_t i = (int64_t)b * 256 + threadIdx.x; i < ms.total[s]; i += (int64_t)mb * 256) acc += tp[i];
-  const double bs = block_tree_sum(acc);
-  if (threadIdx.x == 0) bpart[((int64_t)rd * gridDim.y + s) * 4096 + b] = bs;
-}
-__global__ void __launch_bounds__(256)
-gbdt_small_metric_final(const double* __restrict__ bpart, SmMetricSets ms, int metric, float* __restrict__ out) {
-  const int s = blockIdx.x, rd = blockIdx.y, hsz = gridDim.x;
-  const double v0 = block_sum_partials(bpart + ((int64_t)rd * hsz + s) * 4096, ms.mb[s]);
-  if (threadIdx.x == 0) {
-    double v = v0 / (double)(ms.total[s] > 0 ? ms.total[s] : 1);
-    if (metric == MET_RMSE) v = sqrt(v);
-    out[(int64_t)rd * hsz + s] = (float)v;
-  }
-}
-
 inline int grid_for(int64_t total, int bs = 256) {
   int64_t g = (total + bs - 1) / bs;
   if (g > 4096) g = 4096;
@@ -1561,11 +1129,6 @@ GraphCache& graph_cache() {
   static GraphCache c;
   return c;
 }
-// 1 when the last em_gbdt_fit call ran gbdt_fit_small (em_gbdt_last_fit_small; tests)
-int& last_fit_small() {
-  static int v = 0;
-  return v;
-}
 // one zeroed device int per process (per device in use): the fused metric launches' arrival counter
 int* metric_counter() {
   static int* ctr = nullptr;
@@ -1624,131 +1187,6 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   const int NN = (1 << (max_depth + 1)) - 1;
   const int C = foff_h[F];
   const int64_t TN = (int64_t)T * n;
-  // Small fits (the packed bin records, per-row state and the histogram units of every level fit one
-  // block's LDS): gbdt_fit_small runs every round of the call, one block per task, then two small
-  // launches reduce the metric terms.  Bit-identical to the level path below.  Exact fp64 sums,
-  // per-task objectives and elementwise metrics only; EM_GBDT_SMALL=0 disables it.
-  {
-    const char* sv = getenv("EM_GBDT_SMALL");
-    bool ok = !(sv && sv[0] == '0') && quant_bits == 0 && (obj == OBJ_LOGISTIC || obj == OBJ_SQERR) &&
-              metric < MET_MLOGLOSS && max_depth <= SM_MAX_DEPTH && n_evals >= 0 && n_evals <= SM_MAX_EVALS &&
-              r1 > r0 && n <= SM_LDS;
-    int64_t ne_tot = 0, per_round = TN;
-    for (int e = 0; ok && e < n_evals; ++e) {
-      ok = evals[e].bins && evals[e].Y && evals[e].margin && evals[e].n > 0;
-      ne_tot += ok ? evals[e].n : 0;
-      per_round += ok ? (int64_t)T * evals[e].n : 0;
-    }
-    int nbit = 0;
-    for (int f = 0; f < F; ++f) nbit += (foff_h[f + 1] - foff_h[f]) == 2;
-    const int WBW = (nbit + 31) / 32, RW = WBW + (F - nbit + 3) / 4;
-    ok = ok && ne_tot <= SM_LDS && (int64_t)n * RW * 4 <= SM_LDS;
-    SmArgs sa;
-    std::memset(&sa, 0, sizeof(sa));
-    if (ok) {
-      sa.L = sm_layout(n, F, NN, RW, (int)ne_tot);
-      const int64_t avail = SM_LDS - sa.L.hist;
-      const int nthF = F < SM_NT ? F : SM_NT;
-      for (int l = 0; ok && l < max_depth; ++l) {
-        HistPlan pl;
-        ok = plan_hist(l, n, T, F, foff_h, false, pl);
-        if (!ok) break;
-        const int64_t slots = avail > 0 ? avail / ((int64_t)(1 << l) * C * 16) : 0;  // units + the total
-        int64_t gc = (slots - 1) / pl.P;
-        gc = gc < (SM_NT / nthF) / pl.P ? gc : (SM_NT / nthF) / pl.P;
-        gc = gc < pl.nchunks ? gc : pl.nchunks;
-        sa.lv[l] = SmLevel{pl.chunk, pl.nchunks, pl.P, pl.piece, (int)gc};
-        ok = gc >= 1;
-      }
-    }
-    // HBM scratch: the call's metric terms + the virtual blocks' sums (grown on demand, kept)
-    double* terms = nullptr;
-    const int hsz = 1 + n_evals;
-    const int64_t scratch = (int64_t)(r1 - r0) * per_round + (int64_t)(r1 - r0) * hsz * 4096;
-    if (ok) {
-      static double* buf = nullptr;
-      static int64_t cap = 0;
-      static int dev = -1;
-      int d = 0;
-      (void)hipGetDevice(&d);
-      if (scratch > cap || d != dev) {
-        if (buf) {
-          (void)hipDeviceSynchronize();
-          (void)hipFree(buf);
-        }
-        buf = nullptr;
-        cap = 0;
-        if (hipError_t e = hipMalloc(&buf, scratch * sizeof(double))) return (int)e;
-        cap = scratch;
-        dev = d;
-      }
-      terms = buf;
-    }
-    if (ok) {
-      sa.bins = bins;
-      sa.Y = Y;
-      sa.margin = margin;
-      sa.foff = foff_d;
-      sa.n = n;
-      sa.F = F;
-      sa.T = T;
-      sa.C = C;
-      sa.NN = NN;
-      sa.max_depth = max_depth;
-      sa.obj = obj;
-      sa.metric = metric;
-      sa.r0 = r0;
-      sa.r1 = r1;
-      sa.n_evals = n_evals;
-      sa.RW = RW;
-      sa.WBW = WBW;
-      sa.eta = eta;
-      sa.lam = lam;
-      sa.gamma = gamma;
-      sa.mcw = mcw;
-      sa.subsample = subsample;
-      sa.seed = seed;
-      sa.status = status;
-      sa.feat = feat;
-      sa.sbin = sbin;
-      sa.leaf = leaf;
-      sa.gain = gainv;
-      sa.cover = cover;
-      sa.terms = terms;
-      sa.tstride = per_round;
-      SmMetricSets ms;
-      std::memset(&ms, 0, sizeof(ms));
-      ms.total[0] = TN;
-      ms.mb[0] = grid_for(TN);
-      int64_t off = TN;
-      for (int e = 0; e < n_evals; ++e) {
-        sa.ev[e] = SmEval{evals[e].bins, evals[e].Y, evals[e].margin, evals[e].n};
-        ms.off[1 + e] = off;
-        ms.total[1 + e] = (int64_t)T * evals[e].n;
-        ms.mb[1 + e] = grid_for(ms.total[1 + e]);
-        off += ms.total[1 + e];
-      }
-      static bool attr = false;
-      if (!attr) {
-        if (hipError_t e = hipFuncSetAttribute((const void*)gbdt_fit_small,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, SM_LDS))
-          return (int)e;
-        attr = true;
-      }
-      int mbmax = 1;
-      for (int s = 0; s < hsz; ++s) mbmax = ms.mb[s] > mbmax ? ms.mb[s] : mbmax;
-      double* bpart = terms + (int64_t)(r1 - r0) * per_round;
-      hipLaunchKernelGGL(gbdt_fit_small, dim3(T), dim3(SM_NT), SM_LDS, stream, sa);
-      hipLaunchKernelGGL(gbdt_small_metric_blocks, dim3(mbmax, hsz, r1 - r0), dim3(256), 0, stream, terms,
-                         per_round, ms, bpart);
-      hipLaunchKernelGGL(gbdt_small_metric_final, dim3(hsz, r1 - r0), dim3(256), 0, stream, bpart, ms, metric,
-                         hist_out + (int64_t)r0 * hsz);
-      EM_CHECK_LAUNCH();
-      last_fit_small() = 1;
-      return 0;
-    }
-  }
-  last_fit_small() = 0;
   int* mctr = metric_counter();  // arrival counter of the fused metric launches (re-armed by each)
   if (!mctr) return EM_ERR_ARG;
   // fixed point with >= 8 one-hot features: the sparse form (QuantAux); EM_GBDT_SPARSE=0 disables it
@@ -1927,8 +1365,6 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     if (int rc = enqueue_round(round, nullptr, stream)) return rc;
   return 0;
 }
-
-EM_API int em_gbdt_last_fit_small() { return last_fit_small(); }
 
 EM_API int em_gbdt_init_margin(float* margin, int64_t total, float base, hipStream_t stream) {
   if (!margin || total < 0) return EM_ERR_ARG;

@@ -145,9 +145,13 @@ class TreeArrays:
         return self.feat.shape[0]
 
     def set_split_values(self, cuts):
-        for t in range(self.n_trees):
-            for i in np.nonzero(self.status[t] == 1)[0]:
-                self.split_value[t, i] = cuts[self.feat[t, i]][self.sbin[t, i]]
+        """split_value = cuts[feat][sbin] at every split node (one gather over a flattened cut table)."""
+        t, i = np.nonzero(self.status == 1)
+        if t.size == 0:
+            return
+        off = np.concatenate([[0], np.cumsum([len(c) for c in cuts])]).astype(np.int64)
+        flat = np.concatenate([np.asarray(c, np.float64) for c in cuts] + [np.zeros(1)])
+        self.split_value[t, i] = flat[off[self.feat[t, i]] + self.sbin[t, i]]
 
 
 def predict_margin_values(trees: TreeArrays, X: np.ndarray, tree_task: np.ndarray, n_tasks: int,

@@ -32,7 +32,6 @@ N.register_signatures({
     "em_gbdt_dp_level_split": (_i, [_i, _v, _v, _i, _i, _i, _v, _i, _i, _v, _v, _v, _v, _v, _v, _v, _f, _f, _v]),
     "em_gbdt_dp_round_end": (_i, [_i, _i, _i, _v, _v, _v, _v, _v, _v, _v, _v, _v, _f, _f, _f, _v]),
     "em_gbdt_metric_sum": (_i, [_v, _v, _i, _i, _i, _i, _v, _v, _v]),
-    "em_gbdt_last_fit_small": (_i, []),
 })
 
 OBJ = {"reg:logistic": 0, "binary:logistic": 0, "reg:squarederror": 1, "multi:softprob": 2, "multi:softmax": 2}

@@ -1,6 +1,4 @@
 """GBDT with XGBoost semantics: formulas, pruning, exact-vs-hist equivalence, persistence."""
-import os
-
 import numpy as np
 import pytest
 
@@ -210,11 +208,7 @@ def test_hip_dp_primitives_match_single_call():
     X, Y, _ = gbdt_dataset(ds, C.RunConfig())
     Y = Y[:, :5]
     kw = dict(eta=0.7, max_depth=3, gamma=0.5, min_child_weight=0.5, nround=12, backend="hip")
-    os.environ["EM_GBDT_SMALL"] = "0"  # the level-by-level driver (same kernels as the DP primitives)
-    try:
-        ref = GBDT(**kw).fit(X[:600], Y[:600], evals={"test": (X[600:], Y[600:])})
-    finally:
-        del os.environ["EM_GBDT_SMALL"]
+    ref = GBDT(**kw).fit(X[:600], Y[:600], evals={"test": (X[600:], Y[600:])})
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -227,37 +221,6 @@ def test_hip_dp_primitives_match_single_call():
     assert np.array_equal(dp.trees.feat, ref.trees.feat) and np.array_equal(dp.trees.sbin, ref.trees.sbin)
     assert np.array_equal(dp.trees.leaf, ref.trees.leaf)
     assert np.allclose([h["test"] for h in dp.history], [h["test"] for h in ref.history], rtol=1e-6)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("obj,sub", [("reg:logistic", 1.0), ("reg:squarederror", 1.0), ("reg:logistic", 0.7)])
-def test_hip_small_fit_matches_level_path(obj, sub):
-    """gbdt_fit_small (one block per task, every round of a call in one launch) is bit-identical to
-    the level-by-level driver (EM_GBDT_SMALL=0) on a reference-sized calendar fit: trees, leaves,
-    covers, the per-round watch metrics and the predictions."""
-    from euromillioner_amd import config as C
-    from euromillioner_amd.data.draws import DrawSet
-    from euromillioner_amd.models.gbdt_hip import N as NH
-    from euromillioner_amd.pipeline import gbdt_dataset
-
-    ds = DrawSet.synthetic(n=None, seed=3, planted=0.5)
-    X, Y, _ = gbdt_dataset(ds, C.RunConfig())
-    m = int(0.7 * len(X))
-    kw = dict(eta=1.0 if obj == "reg:logistic" else 0.3, max_depth=3, gamma=1.0, nround=60, objective=obj,
-              eval_metric="logloss" if obj == "reg:logistic" else "rmse", subsample=sub, backend="hip")
-    ev = {"test": (X[m:], Y[m:]), "train": (X[:m], Y[:m])}
-    a = G.GBDT(**kw).fit(X[:m], Y[:m], evals=ev)
-    assert NH.query("em_gbdt_last_fit_small") == 1
-    os.environ["EM_GBDT_SMALL"] = "0"
-    try:
-        b = G.GBDT(**kw).fit(X[:m], Y[:m], evals=ev)
-        assert NH.query("em_gbdt_last_fit_small") == 0
-    finally:
-        del os.environ["EM_GBDT_SMALL"]
-    for k in ("status", "feat", "sbin", "leaf", "gain", "cover"):
-        assert np.array_equal(getattr(a.trees, k), getattr(b.trees, k)), k
-    assert a.history == b.history
-    assert np.array_equal(a.predict(X[m:], backend="hip"), b.predict(X[m:], backend="hip"))
 
 
 def test_native_hist_plan_bounds():

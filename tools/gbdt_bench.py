@@ -54,9 +54,6 @@ def main():
             res[f"{key}_test_logloss"] = g.history[-1]["test"]
             res[f"{key}_trees_per_s"] = round(rounds * Y.shape[1] / dt, 1)
             res[f"{key}_quant_bits"] = int(getattr(g, "quant_bits_used", 0))
-            if be == "hip":  # 1: one-block-per-task fit (gbdt_fit_small), 0: level-by-level driver
-                from euromillioner_amd.models.gbdt_hip import N as NH
-                res[f"{key}_small_path"] = int(NH.query("em_gbdt_last_fit_small"))
         print(json.dumps(res), flush=True)
 
 
