@@ -53,6 +53,26 @@ EM_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 // same kernel sequence; the eager paths pass rd = nullptr and pre-offset pointers.
 EM_DEVICE int64_t rd_off(const int* rd, int64_t stride) { return rd ? (int64_t)(*rd) * stride : 0; }
 
+// GBDT_STAMPS=1 builds (tools/build_variant.sh): block 0's wall clock at phase boundaries of the round
+// kernels, slot = kernel base + phase (em_gbdt_stamps copies them out); compiled out otherwise
+#ifndef GBDT_STAMPS
+#define GBDT_STAMPS 0
+#endif
+#if GBDT_STAMPS
+__device__ unsigned long long g_stamp[512];  // [0, 256): 100 MHz wall clock, [256, 512): shader clock
+#define GSTAMP(slot) \
+  do { \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) { \
+      g_stamp[(slot) & 255] = wall_clock64(); \
+      g_stamp[256 + ((slot) & 255)] = __builtin_amdgcn_s_memtime(); \
+    } \
+  } while (0)
+#else
+#define GSTAMP(slot) \
+  do { \
+  } while (0)
+#endif
+
 EM_DEVICE void round_init_elem(int i, int8_t* st, int16_t* fe, uint8_t* sb, float* gn, int NN) {
   st[i] = (i % NN) == 0 ? 2 : 0;
   fe[i] = -1;
@@ -155,14 +175,27 @@ __global__ void gbdt_round_start(int8_t* __restrict__ st, int16_t* __restrict__ 
 constexpr int HIST_MAX_CHUNK = 1024;             // rows staged in LDS per piece
 constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // 8-byte words of per-chunk partials (1 GiB) per level
 constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (+ staged rows)
+// exact form: up to 4 private copies in a 256-thread block.  (8 copies in 512-thread blocks halved a
+// block's serial read-modify-write chain but measured slower per level on the reference fit: the CUs
+// then run fewer, longer blocks and the level is bound by LDS throughput, not by one block's chain.)
+constexpr int HIST_EXACT_LDS_BUDGET = HIST_LDS_BUDGET;
+constexpr int HIST_EXACT_THREADS = 256;
 constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(HIST_EXACT_THREADS)
 gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
-          int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece) {
+          int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, int stage_rows,
+          int16_t* __restrict__ node_out, const int8_t* __restrict__ pst, const int16_t* __restrict__ pfe,
+          const uint8_t* __restrict__ psb, int NN, const int* __restrict__ rd) {
+  // stage_rows > 0: each piece's bin rows are staged in LDS with 16-B loads (one round trip instead of
+  // one per 8 rows of byte loads); the host sets it when a piece's rows fit (stage_rows * F <= 16 KB).
+  // node_out != nullptr (level >= 1): the rows' nodes are the previous level's partition, applied here
+  // (gbdt_partition's rule on the round's split arrays pst / pfe / psb, staged in LDS), and the
+  // (chunk, task)'s first tile block writes them to node_out for the next level -- one launch less per level
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
+  GSTAMP(64 + 16 * level);
   const int c = blockIdx.x, t = blockIdx.y;
   const int nft = (F + FT - 1) / FT;
   const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
@@ -174,11 +207,21 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   float* sg = reinterpret_cast<float*>(smem + (size_t)P * per * sizeof(double));
   float* sh = sg + piece;
   int16_t* sn = reinterpret_cast<int16_t*>(sh + piece);
+  // the previous level's split arrays of this task (nodes pf .. first - 1): int32 {status | sbin << 8 | feat << 16}
+  int32_t* ptree = reinterpret_cast<int32_t*>(smem + (((size_t)P * per * 8 + (size_t)piece * 10 + 15) & ~(size_t)15));
+  const int pf = (first - 1) >> 1, npn = node_out ? first - pf : 0;
+  u32x4* sbw = reinterpret_cast<u32x4*>(reinterpret_cast<char*>(ptree) + (((size_t)npn * 4 + 15) & ~(size_t)15));
+  if (npn) {
+    const int64_t k0 = rd_off(rd, (int64_t)T * NN) + (int64_t)t * NN + pf;
+    for (int i = threadIdx.x; i < npn; i += blockDim.x)
+      ptree[i] = (int32_t)(uint8_t)pst[k0 + i] | ((int32_t)psb[k0 + i] << 8) | ((int32_t)pfe[k0 + i] << 16);
+  }
   const int64_t base = (int64_t)t * n;
   const int nth = f1 - f0;
   const int p = threadIdx.x / nth, fl = threadIdx.x - p * nth;
   const int f = f0 + (p < P ? fl : 0);
   double* my = hist + (size_t)(p < P ? p : 0) * per + (foff[f] - c0) * 2;
+  const int64_t nbytes = (int64_t)n * F;
   // the block's rows [c*chunk, +chunk) in staged pieces of <= piece rows: per piece the rows'
   // (node, g, h) go to LDS once, shared by every feature thread, then thread (p, fl) adds the p-th
   // contiguous part of the piece to its copy in row order
@@ -186,16 +229,53 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   for (int r0 = rb; r0 < re; r0 += piece) {
     const int r1 = min(re, r0 + piece);
     __syncthreads();  // the previous piece's staging is consumed
+    // the piece's bin rows: bytes [r0 F, r1 F) as 16-B words (range-checked buffer loads; a word running
+    // past the array's end is assembled bytewise), row r's byte f at rowb[(r - r0) F + f]
+    const uint8_t* rowb = bins + (int64_t)r0 * F;
+    if (stage_rows) {
+      const int64_t w0 = ((int64_t)r0 * F) >> 4;
+      const int boff = (int)(((int64_t)r0 * F) & 15);
+      const int nw = (int)((((int64_t)r1 * F + 15) >> 4) - w0);
+      const int64_t left = nbytes - w0 * 16;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(bins + w0 * 16), 0, (int)(left < 0x7FFFFFF0 ? left : 0x7FFFFFF0), 0x00020000);
+      const bool tail = (w0 + nw) * 16 > nbytes;
+      for (int i = threadIdx.x; i < nw - (tail ? 1 : 0); i += blockDim.x)
+        sbw[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, i * 16, 0, 0));
+      if (tail && threadIdx.x == 0) {
+        uint8_t* wb = reinterpret_cast<uint8_t*>(sbw + nw - 1);
+        for (int k = 0; k < 16; ++k) {
+          const int64_t q = (w0 + nw - 1) * 16 + k;
+          wb[k] = q < nbytes ? bins[q] : 0;
+        }
+      }
+      rowb = reinterpret_cast<const uint8_t*>(sbw) + boff;
+    }
     for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
       sg[r - r0] = g[base + r];
       sh[r - r0] = h[base + r];
-      sn[r - r0] = (int16_t)(node[base + r] - first - n0);  // tile-relative node (outside -> skipped)
+      const int nd = node[base + r];
+      sn[r - r0] = (int16_t)(npn ? nd : nd - first - n0);  // tile-relative node (outside -> skipped)
     }
     __syncthreads();
+    GSTAMP(64 + 16 * level + 1);
+    if (npn) {  // the previous level's partition on the staged rows
+      for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
+        int nd = sn[r - r0];
+        if (nd >= pf && nd < first) {
+          const int32_t e = ptree[nd - pf];
+          if ((e & 0xFF) == 1) nd = 2 * nd + 1 + ((int)rowb[(int64_t)(r - r0) * F + (e >> 16)] > ((e >> 8) & 0xFF) ? 1 : 0);
+        }
+        if (blockIdx.z == 0) node_out[base + r] = (int16_t)nd;
+        sn[r - r0] = (int16_t)(nd - first - n0);
+      }
+      __syncthreads();
+      GSTAMP(64 + 16 * level + 2);
+    }
     if (p < P) {
       const int len = r1 - r0, sub = (len + P - 1) / P;
       const int a0 = min(len, p * sub), a1 = min(len, a0 + sub);
-      const uint8_t* col = bins + (int64_t)r0 * F + f;
+      const uint8_t* col = rowb + f;
       int r = a0;
       // 8 rows' inputs first, then their 8 updates in row order (sums bitwise = the plain loop)
       for (; r + 8 <= a1; r += 8) {
@@ -226,6 +306,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
     }
   }
   __syncthreads();
+  GSTAMP(64 + 16 * level + 3);
   // fold the P copies (p order) and write this chunk's cells: partial [nchunks][T][nodesL][C][2]
   double* out = partial + ((int64_t)c * T + t) * (int64_t)nodesL * C * 2;
   const int nn = min(NTn, nodesL - n0);
@@ -241,6 +322,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
     o[0] = sgv;
     o[1] = shv;
   }
+  GSTAMP(64 + 16 * level + 4);
 }
 
 // fixed-point value of x * 2^s (x a float, |x * 2^s| < 2^62): the product is exact (power-of-two
@@ -530,148 +612,282 @@ __global__ void gbdt_chunk_reduce(A* __restrict__ partial, int nchunks, int64_t 
 // A = double (exact form) or long long (fixed point, value = q * qinv): the fixed-point form keeps
 // the left sums and the node totals (feature 0's cells, every level) in integers and converts each
 // to double once, so GR = (Gn - GL) is exact as well.
+// Finalize (tf != nullptr, the last level): each (task, node) block arrives on the task's counter after
+// its decision (release); the task's last block (acquire) runs gbdt_finalize's prune and leaves for the
+// task and re-arms the counter -- one launch less per round.
+struct SplitFinal {
+  int* tctr = nullptr;  // [T] zeroed arrival counters (left zeroed)
+  float* leaf = nullptr;
+  float* cover = nullptr;
+  float gamma = 0.f;
+  double eta = 0.0;
+  int max_depth = 0;
+};
+EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma);
+constexpr int SPLIT_FINAL_MAX_DEPTH = 8;
+constexpr int SPLIT_ONESHOT_LDS = 48 * 1024;  // chunk partials staged at once up to this many bytes (+ the
+                                              // finalize's <= 12 KB: within the default 64 KB)  // the fused finalize stages NN <= 511 nodes (23 B each) in LDS
+
 template <typename A>
 __global__ void __launch_bounds__(256)
 gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
            int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
            int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
-           double qinv, const int* __restrict__ rd) {
+           double qinv, const int* __restrict__ rd, SplitFinal fin, int oneshot, int pscan) {
   constexpr bool Q = std::is_same<A, long long>::value;
-  {
-    const int64_t o = rd_off(rd, (int64_t)T * NN);
-    status += o;
-    feat += o;
-    sbin += o;
-    gain += o;
-  }
+  const int64_t ro = rd_off(rd, (int64_t)T * NN);
+  status += ro;
+  feat += ro;
+  sbin += ro;
+  gain += ro;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
+  GSTAMP(16 * level);
   int8_t* st = status + (int64_t)t * NN;
-  if (st[i] != 2) return;  // block-uniform
-  const A* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
-  if (nchunks > 1) {  // per-chunk partials: fold this node's cells into LDS in chunk order (== gbdt_chunk_reduce)
-    A* fold = reinterpret_cast<A*>(smem);
-    for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
-      A acc = hs[e];
-      int c = 1;
-      for (; c + 8 <= nchunks; c += 8) {  // 8 independent loads in flight, added in chunk order
-        A v[8];
+  // the thread's feature cells and feature 0's, loaded before the partials (one round trip for all)
+  const int fa0 = foff[0], fb0 = foff[1];
+  const int myca = (int)threadIdx.x < F ? foff[threadIdx.x] : 0, mycb = (int)threadIdx.x < F ? foff[threadIdx.x + 1] : 0;
+  if (st[i] == 2) {  // block-uniform: an open node
+    const A* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
+    if (nchunks > 1 && oneshot) {
+      // every chunk's cells staged at once (32 loads per thread in flight: one round trip, where the
+      // per-element chunk loop took 2-3), then folded in chunk order (== gbdt_chunk_reduce)
+      A* stg = reinterpret_cast<A*>(smem);
+      const int tot = nchunks * 2 * C;
+      for (int b0 = threadIdx.x; b0 < tot; b0 += 32 * blockDim.x) {
+        A v[32];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = hs[(int64_t)(c + u) * cstride + e];
+        for (int u = 0; u < 32; ++u) {
+          const int idx = b0 + u * blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
+          v[u] = idx < tot ? hs[(int64_t)c * cstride + e] : A(0);
+        }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u];
+        for (int u = 0; u < 32; ++u) {
+          const int idx = b0 + u * blockDim.x;
+          if (idx < tot) stg[idx] = v[u];
+        }
       }
-      for (; c < nchunks; ++c) acc += hs[(int64_t)c * cstride + e];
-      fold[e] = acc;
+      __syncthreads();
+      for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
+        A acc = stg[e];
+        for (int c = 1; c < nchunks; ++c) acc += stg[c * 2 * C + e];
+        stg[e] = acc;
+      }
+      __syncthreads();
+      GSTAMP(16 * level + 1);
+      hs = stg;
+    } else if (nchunks > 1) {  // per-chunk partials: fold this node's cells into LDS in chunk order (== gbdt_chunk_reduce)
+      A* fold = reinterpret_cast<A*>(smem);
+      for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
+        A acc = hs[e];
+        int c = 1;
+        for (; c + 8 <= nchunks; c += 8) {  // 8 independent loads in flight, added in chunk order
+          A v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = hs[(int64_t)(c + u) * cstride + e];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; c < nchunks; ++c) acc += hs[(int64_t)c * cstride + e];
+        fold[e] = acc;
+      }
+      __syncthreads();
+      hs = fold;
+    }
+    auto val = [qinv](A x) -> double {
+      if constexpr (Q)
+        return (double)x * qinv;
+      else
+        return x;
+    };
+    __shared__ A sGn[2];
+    __shared__ double rv[4];
+    __shared__ int rf[4], rb[4];
+    __shared__ A rgl[4], rhl[4];
+    if (threadIdx.x == 0) {
+      A Gn, Hn;
+      if (Q || level == 0) {  // node totals: feature 0's cells in bin order
+        Gn = 0;
+        Hn = 0;
+        for (int c = fa0; c < fb0; ++c) {
+          Gn += hs[2 * c];
+          Hn += hs[2 * c + 1];
+        }
+        if (level == 0) {
+          G[(int64_t)t * NN] = val(Gn);
+          H[(int64_t)t * NN] = val(Hn);
+        }
+      } else {
+        Gn = G[(int64_t)t * NN + i];
+        Hn = H[(int64_t)t * NN + i];
+      }
+      sGn[0] = Gn;
+      sGn[1] = Hn;
     }
     __syncthreads();
-    hs = fold;
-  }
-  auto val = [qinv](A x) -> double {
-    if constexpr (Q)
-      return (double)x * qinv;
-    else
-      return x;
-  };
-  __shared__ A sGn[2];
-  __shared__ double rv[4];
-  __shared__ int rf[4], rb[4];
-  __shared__ A rgl[4], rhl[4];
-  if (threadIdx.x == 0) {
-    A Gn, Hn;
-    if (Q || level == 0) {  // node totals: feature 0's cells in bin order
-      Gn = 0;
-      Hn = 0;
-      for (int c = foff[0]; c < foff[1]; ++c) {
-        Gn += hs[2 * c];
-        Hn += hs[2 * c + 1];
-      }
-      if (level == 0) {
-        G[(int64_t)t * NN] = val(Gn);
-        H[(int64_t)t * NN] = val(Hn);
-      }
-    } else {
-      Gn = G[(int64_t)t * NN + i];
-      Hn = H[(int64_t)t * NN + i];
-    }
-    sGn[0] = Gn;
-    sGn[1] = Hn;
-  }
-  __syncthreads();
-  const A Gna = sGn[0], Hna = sGn[1];
-  const double Gn = val(Gna), Hn = val(Hna);
-  const double root = Gn * Gn / (Hn + lam);
-  double best = -INFINITY;
-  A bGL = 0, bHL = 0;
-  int bf = 0x7fffffff, bb = 0;
-  for (int f = threadIdx.x; f < F; f += blockDim.x) {
-    const int ca = foff[f], cb = foff[f + 1];
-    A GLa = 0, HLa = 0;
-    for (int c = ca; c < cb - 1; ++c) {  // the last bin is never a candidate (nothing to its right)
-      GLa += hs[2 * c];
-      HLa += hs[2 * c + 1];
+    GSTAMP(16 * level + 2);
+    const A Gna = sGn[0], Hna = sGn[1];
+    const double Gn = val(Gna), Hn = val(Hna);
+    const double root = Gn * Gn / (Hn + lam);
+    double best = -INFINITY;
+    A bGL = 0, bHL = 0;
+    int bf = 0x7fffffff, bb = 0;
+    auto cand = [&](int f, int b, A GLa, A HLa) {  // candidate "bin <= b" of feature f
       const double GL = val(GLa), HL = val(HLa);
       const double GR = val(Gna - GLa), HR = val(Hna - HLa);
       if (HL >= mcw && HR >= mcw) {
         const double gn = GL * GL / (HL + lam) + GR * GR / (HR + lam) - root;
-        if (gn > best) {  // strict: the lower bin of this feature keeps ties
+        if (gn > best) {  // strict: candidates come in ascending (feature, bin) order per thread
           best = gn;
           bf = f;
-          bb = c - ca;
+          bb = b;
           bGL = GLa;
           bHL = HLa;
         }
       }
-    }
-  }
-  // block arg-max: larger gain, then lower feature (a thread's features ascend with its loop)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    };
+    if (pscan) {
+      // two passes: thread f writes its feature's left sums in bin order (the same sequential sums),
+      // then thread c evaluates candidate cell c -- the divisions of a 31-bin feature no longer
+      // run one after another on one lane
+      char* sa = smem + (nchunks > 1 ? (((oneshot ? nchunks : 1) * 2 * C * (int)sizeof(A) + 15) & ~15) : 0);
+      A* cGL = reinterpret_cast<A*>(sa);
+      A* cHL = cGL + C;
+      int16_t* cfe = reinterpret_cast<int16_t*>(cHL + C);  // feature of a candidate cell, -1: a last bin
+      int16_t* cbn = cfe + C;                              // its bin
+      for (int f = threadIdx.x; f < F; f += blockDim.x) {
+        const int ca = f == (int)threadIdx.x ? myca : foff[f], cb = f == (int)threadIdx.x ? mycb : foff[f + 1];
+        A GLa = 0, HLa = 0;
+        int c = ca;
+        for (; c + 8 <= cb - 1; c += 8) {  // 8 cells' loads in flight, then their left sums in bin order
+          A vg[8], vh[8];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double ov = __shfl_xor(best, o);
-    const A ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
-    const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o);
-    if (ov > best || (ov == best && of < bf)) {
-      best = ov;
-      bf = of;
-      bb = ob;
-      bGL = ogl;
-      bHL = ohl;
+          for (int u = 0; u < 8; ++u) {
+            vg[u] = hs[2 * (c + u)];
+            vh[u] = hs[2 * (c + u) + 1];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            GLa += vg[u];
+            HLa += vh[u];
+            cGL[c + u] = GLa;
+            cHL[c + u] = HLa;
+            cfe[c + u] = (int16_t)f;
+            cbn[c + u] = (int16_t)(c + u - ca);
+          }
+        }
+        for (; c < cb - 1; ++c) {
+          GLa += hs[2 * c];
+          HLa += hs[2 * c + 1];
+          cGL[c] = GLa;
+          cHL[c] = HLa;
+          cfe[c] = (int16_t)f;
+          cbn[c] = (int16_t)(c - ca);
+        }
+        cfe[cb - 1] = -1;
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const int f = cfe[c];
+        if (f >= 0) cand(f, cbn[c], cGL[c], cHL[c]);
+      }
+    } else {
+      for (int f = threadIdx.x; f < F; f += blockDim.x) {
+        const int ca = f == (int)threadIdx.x ? myca : foff[f], cb = f == (int)threadIdx.x ? mycb : foff[f + 1];
+        A GLa = 0, HLa = 0;
+        for (int c = ca; c < cb - 1; ++c) {  // the last bin is never a candidate (nothing to its right)
+          GLa += hs[2 * c];
+          HLa += hs[2 * c + 1];
+          cand(f, c - ca, GLa, HLa);
+        }
+      }
+    }
+    // block arg-max: larger gain, then lower feature (a thread's features ascend with its loop)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(best, o);
+      const A ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
+      const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o);
+      if (ov > best || (ov == best && (of < bf || (of == bf && ob < bb)))) {
+        best = ov;
+        bf = of;
+        bb = ob;
+        bGL = ogl;
+        bHL = ohl;
+      }
+    }
+    if (lane == 0) {
+      rv[w] = best;
+      rf[w] = bf;
+      rb[w] = bb;
+      rgl[w] = bGL;
+      rhl[w] = bHL;
+    }
+    __syncthreads();
+    GSTAMP(16 * level + 3);
+    if (threadIdx.x == 0) {
+      const int nw = (blockDim.x + 63) >> 6;
+      for (int k = 1; k < nw; ++k)
+        if (rv[k] > best || (rv[k] == best && (rf[k] < bf || (rf[k] == bf && rb[k] < bb)))) {
+          best = rv[k];
+          bf = rf[k];
+          bb = rb[k];
+          bGL = rgl[k];
+          bHL = rhl[k];
+        }
+      if (bf < F && best > KRT_EPS) {
+        st[i] = 1;
+        feat[(int64_t)t * NN + i] = (int16_t)bf;
+        sbin[(int64_t)t * NN + i] = (uint8_t)bb;
+        gain[(int64_t)t * NN + i] = (float)best;
+        const int l = 2 * i + 1, r = 2 * i + 2;
+        st[l] = 2;
+        st[r] = 2;
+        G[(int64_t)t * NN + l] = val(bGL);
+        H[(int64_t)t * NN + l] = val(bHL);
+        G[(int64_t)t * NN + r] = val(Gna - bGL);
+        H[(int64_t)t * NN + r] = val(Hna - bHL);
+      }
     }
   }
-  if (lane == 0) {
-    rv[w] = best;
-    rf[w] = bf;
-    rb[w] = bb;
-    rgl[w] = bGL;
-    rhl[w] = bHL;
+  GSTAMP(16 * level + 4);
+  if (!fin.tctr) return;
+  __shared__ int last;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(fin.tctr + t, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nodesL - 1;
+  __syncthreads();
+  if (!last) return;  // block-uniform
+  // the task's tree staged in LDS (after the fold area), pruned by one thread, leaves by all
+  char* fa = smem + (nchunks > 1 ? (((oneshot ? nchunks : 1) * 2 * C * (int)sizeof(A) + 15) & ~15) : 0) +
+             (pscan ? ((C * (2 * (int)sizeof(A) + 4) + 15) & ~15) : 0);
+  double* sG = reinterpret_cast<double*>(fa);
+  double* sH = sG + NN;
+  float* sgn = reinterpret_cast<float*>(sH + NN);
+  int16_t* sfe = reinterpret_cast<int16_t*>(sgn + NN);
+  int8_t* sst = reinterpret_cast<int8_t*>(sfe + NN);
+  const int64_t o = (int64_t)t * NN;
+  for (int k = threadIdx.x; k < NN; k += blockDim.x) {
+    sst[k] = st[k];
+    sfe[k] = feat[o + k];
+    sgn[k] = gain[o + k];
+    sG[k] = G[o + k];
+    sH[k] = H[o + k];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int nw = (blockDim.x + 63) >> 6;
-    for (int k = 1; k < nw; ++k)
-      if (rv[k] > best || (rv[k] == best && rf[k] < bf)) {
-        best = rv[k];
-        bf = rf[k];
-        bb = rb[k];
-        bGL = rgl[k];
-        bHL = rhl[k];
-      }
-    if (bf < F && best > KRT_EPS) {
-      st[i] = 1;
-      feat[(int64_t)t * NN + i] = (int16_t)bf;
-      sbin[(int64_t)t * NN + i] = (uint8_t)bb;
-      gain[(int64_t)t * NN + i] = (float)best;
-      const int l = 2 * i + 1, r = 2 * i + 2;
-      st[l] = 2;
-      st[r] = 2;
-      G[(int64_t)t * NN + l] = val(bGL);
-      H[(int64_t)t * NN + l] = val(bHL);
-      G[(int64_t)t * NN + r] = val(Gna - bGL);
-      H[(int64_t)t * NN + r] = val(Hna - bHL);
-    }
+    fin.tctr[t] = 0;  // re-armed for the next round (the kernel boundary orders it)
+    prune_task(sst, sfe, sgn, fin.max_depth, fin.gamma);
   }
+  __syncthreads();
+  for (int k = threadIdx.x; k < NN; k += blockDim.x) {
+    st[k] = sst[k];
+    feat[o + k] = sfe[k];
+    fin.leaf[ro + o + k] = sst[k] == 2 ? (float)(-sG[k] / (sH[k] + lam) * fin.eta) : 0.f;
+    fin.cover[ro + o + k] = sst[k] ? (float)sH[k] : 0.f;
+  }
+  GSTAMP(16 * level + 5);
 }
 
 __global__ void gbdt_partition(const uint8_t* __restrict__ bins, int16_t* __restrict__ node, int T, int n, int F,
@@ -711,19 +927,25 @@ __global__ void gbdt_finalize(int T, int NN, int max_depth, int8_t* __restrict__
     leaf += ro;
     cover += ro;
   }
-  int8_t* st = status + (int64_t)t * NN;
   const int64_t o = (int64_t)t * NN;
-  for (int i = (1 << max_depth) - 2; i >= 0; --i) {
-    if (st[i] == 1 && st[2 * i + 1] == 2 && st[2 * i + 2] == 2 && gain[o + i] < gamma) {
-      st[i] = 2;
-      st[2 * i + 1] = 0;
-      st[2 * i + 2] = 0;
-      feat[o + i] = -1;
-    }
-  }
+  int8_t* st = status + o;
+  prune_task(st, feat + o, gain + o, max_depth, gamma);
   for (int i = 0; i < NN; ++i) {
     leaf[o + i] = st[i] == 2 ? (float)(-G[o + i] / (H[o + i] + lam) * eta) : 0.f;
     cover[o + i] = st[i] ? (float)H[o + i] : 0.f;
+  }
+}
+
+// TreePruner: a split whose children are both leaves and whose gain is below gamma becomes a leaf
+// (bottom-up over the internal slots; arrays at the task's base)
+EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma) {
+  for (int i = (1 << max_depth) - 2; i >= 0; --i) {
+    if (st[i] == 1 && st[2 * i + 1] == 2 && st[2 * i + 2] == 2 && gn[i] < gamma) {
+      st[i] = 2;
+      st[2 * i + 1] = 0;
+      st[2 * i + 2] = 0;
+      fe[i] = -1;
+    }
   }
 }
 
@@ -853,19 +1075,20 @@ gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int
 // and drains it before its single arrival add; the block whose add completes the count sums the
 // partials (sc1 loads) exactly as gbdt_metric_final does, writes the mean, re-arms the counter and,
 // in a replayed round, advances the round counter (every block read it at entry).
+// (b, nb: this block's index among the nb blocks of its metric set; a fused launch runs several sets)
 EM_DEVICE void metric_arrive_final(double bs, double* __restrict__ partial, int* __restrict__ ctr, int64_t count,
-                                   int metric, float* __restrict__ out, int* __restrict__ rd_adv) {
+                                   int metric, float* __restrict__ out, int* __restrict__ rd_adv, int b, int nb) {
   __shared__ int last;
   if (threadIdx.x == 0) {
-    __hip_atomic_store(partial + blockIdx.x, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partial + b, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
   }
   __syncthreads();
   if (!last) return;
   __shared__ double red[256];
   double s = 0.0;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256)
+  for (int i = threadIdx.x; i < nb; i += 256)
     s += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   red[threadIdx.x] = s;
   __syncthreads();
@@ -882,43 +1105,100 @@ EM_DEVICE void metric_arrive_final(double bs, double* __restrict__ partial, int*
   }
 }
 
+// The next round's start inside the current round's update (eager driver): its tree arrays reset and,
+// from each element's freshly updated margin, its g / h with every row back at the root
+// (gbdt_round_start's work for per-task objectives) -- one launch less per round.
+EM_DEVICE void predict_metric_body(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F,
+                                   int NN, int k0, int k1, const int8_t* __restrict__ status,
+                                   const int16_t* __restrict__ feat, const uint8_t* __restrict__ sbin,
+                                   const float* __restrict__ leaf, const float* __restrict__ Y, int obj, int metric,
+                                   double* __restrict__ partial, int* __restrict__ ctr, float* __restrict__ out,
+                                   int* __restrict__ rd_adv, int b, int nb);
+// eval sets handled by the update launch's trailing blocks (eager rounds): set s gets mb blocks, its own
+// partial region (partial + (1 + s) * 4096) and arrival counter (ctr + 1 + s)
+struct EvalSets {
+  const uint8_t* bins[4];
+  float* margin[4];
+  const float* Y[4];
+  int n[4];
+  int mb[4];
+  int count = 0;
+};
+struct NextRound {
+  int round = -1;  // < 0: none
+  float* g = nullptr;
+  float* h = nullptr;
+  int16_t* node = nullptr;  // the next round's level-0 node buffer
+  int8_t* st = nullptr;     // the next round's tree arrays (host-offset)
+  int16_t* fe = nullptr;
+  uint8_t* sb = nullptr;
+  float* gn = nullptr;
+  float subsample = 1.f;
+  uint32_t seed = 0;
+};
+
 // gbdt_update + gbdt_metric + gbdt_metric_final (elementwise metrics) in one launch: same grid, same
-// elements per thread, same partial and final sums -> bit-identical to the three launches
+// elements per thread, same partial and final sums -> bit-identical to the three launches.
+// plevel >= 0: the rows' nodes are before the last level's partition, applied here (gbdt_partition's
+// rule: a node of level plevel that still splits after pruning sends the row to a child; a pruned one
+// is a leaf, where the partition-then-ancestor walk of the separate launches ends as well).
 __global__ void __launch_bounds__(256)
 gbdt_update_metric(float* __restrict__ margin, const int16_t* __restrict__ node, int T, int n, int NN,
                    const int8_t* __restrict__ status, const float* __restrict__ leaf, const int* __restrict__ rd,
                    const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial, int* __restrict__ ctr,
-                   float* __restrict__ out, int ostride, int* __restrict__ rd_adv) {
-  status += rd_off(rd, (int64_t)T * NN);
-  leaf += rd_off(rd, (int64_t)T * NN);
+                   float* __restrict__ out, int ostride, int* __restrict__ rd_adv, const uint8_t* __restrict__ bins,
+                   int F, int plevel, const int16_t* __restrict__ feat, const uint8_t* __restrict__ sbin,
+                   NextRound nx, int nbu, EvalSets evs) {
+  if ((int)blockIdx.x >= nbu) {  // an eval set's prediction + metric (eager rounds: rd == nullptr)
+    int b = (int)blockIdx.x - nbu, s = 0;
+    while (s < evs.count - 1 && b >= evs.mb[s]) b -= evs.mb[s++];
+    // (status / feat / sbin / leaf are this round's arrays: its trees are 0 .. T - 1 of them)
+    predict_metric_body(evs.bins[s], evs.margin[s], T, evs.n[s], F, NN, 0, T, status, feat, sbin, leaf, evs.Y[s], obj,
+                        metric, partial + (int64_t)(1 + s) * 4096, ctr + 1 + s, out + 1 + s, nullptr, b, evs.mb[s]);
+    return;
+  }
+  const int64_t ro = rd_off(rd, (int64_t)T * NN);
+  status += ro;
+  leaf += ro;
+  feat += ro;
+  sbin += ro;
   out += rd_off(rd, ostride);
   const int64_t total = (int64_t)T * n;
+  const int pf = plevel >= 0 ? (1 << plevel) - 1 : 0, pl = plevel >= 0 ? 2 * pf + 1 : 0;
+  GSTAMP(128);
   double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)nbu * blockDim.x) {
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
     const int8_t* st = status + (int64_t)t * NN;
-    const float m = margin[i] + leaf[(int64_t)t * NN + leaf_ancestor(st, node[i])];
+    int nd = node[i];
+    if (nd >= pf && nd < pl && st[nd] == 1) {
+      const int64_t k = (int64_t)t * NN + nd;
+      nd = 2 * nd + 1 + (bins[(int64_t)r * F + feat[k]] > sbin[k] ? 1 : 0);
+    }
+    const float m = margin[i] + leaf[(int64_t)t * NN + leaf_ancestor(st, nd)];
     margin[i] = m;
     acc += metric_term(m, Y[(int64_t)r * T + t], obj, metric);
+    if (nx.round >= 0) grad_elem(i, margin, Y, nx.g, nx.h, nx.node, T, n, obj, nx.subsample, nx.seed, nx.round);
   }
-  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv);
+  if (nx.round >= 0)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)T * NN;
+         i += (int64_t)nbu * blockDim.x)
+      round_init_elem((int)i, nx.st, nx.fe, nx.sb, nx.gn, NN);
+  GSTAMP(129);
+  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv, blockIdx.x, nbu);
+  GSTAMP(130);
 }
 
 // gbdt_predict (one round's trees) + gbdt_metric + gbdt_metric_final of an eval set in one launch
-__global__ void __launch_bounds__(256)
-gbdt_predict_metric(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F, int NN, int k0,
-                    int k1, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
-                    const uint8_t* __restrict__ sbin, const float* __restrict__ leaf, const int* __restrict__ rd,
-                    const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial,
-                    int* __restrict__ ctr, float* __restrict__ out, int ostride, int* __restrict__ rd_adv) {
-  if (rd) {
-    k0 += *rd * T;
-    k1 += *rd * T;
-  }
-  out += rd_off(rd, ostride);
+EM_DEVICE void predict_metric_body(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F,
+                                   int NN, int k0, int k1, const int8_t* __restrict__ status,
+                                   const int16_t* __restrict__ feat, const uint8_t* __restrict__ sbin,
+                                   const float* __restrict__ leaf, const float* __restrict__ Y, int obj, int metric,
+                                   double* __restrict__ partial, int* __restrict__ ctr, float* __restrict__ out,
+                                   int* __restrict__ rd_adv, int b, int nb) {
   const int64_t total = (int64_t)T * n;
   double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < total; i += (int64_t)nb * blockDim.x) {
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
     const uint8_t* row = bins + (int64_t)r * F;
     float tacc = 0.f;
@@ -932,7 +1212,20 @@ gbdt_predict_metric(const uint8_t* __restrict__ bins, float* __restrict__ margin
     margin[i] = m;
     acc += metric_term(m, Y[(int64_t)r * T + t], obj, metric);
   }
-  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv);
+  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv, b, nb);
+}
+__global__ void __launch_bounds__(256)
+gbdt_predict_metric(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F, int NN, int k0,
+                    int k1, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
+                    const uint8_t* __restrict__ sbin, const float* __restrict__ leaf, const int* __restrict__ rd,
+                    const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial,
+                    int* __restrict__ ctr, float* __restrict__ out, int ostride, int* __restrict__ rd_adv) {
+  if (rd) {
+    k0 += *rd * T;
+    k1 += *rd * T;
+  }
+  predict_metric_body(bins, margin, T, n, F, NN, k0, k1, status, feat, sbin, leaf, Y, obj, metric, partial, ctr,
+                      out + rd_off(rd, ostride), rd_adv, blockIdx.x, gridDim.x);
 }
 
 __global__ void __launch_bounds__(256)
@@ -974,11 +1267,14 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
       }
       const int lanes = FT + (quant ? 1 : 0);  // fixed point: + the total lane per phase
       const int W = maxC + (quant ? FT + 1 : 0);  // fixed point: + a pad cell per feature + the total cell
-      int P = 256 / lanes;  // row phases: the exact form keeps P private copies (<= 4), the fixed-point
-      const int Pmax = quant ? 64 : 4;  // form one shared copy, so a few-feature tile fills the block with phases
+      // row phases: the exact form keeps P private copies (<= 8 in a 512-thread block: each copy's serial
+      // read-modify-write chain is a P-th of the chunk), the fixed-point form one shared copy, so a
+      // few-feature tile fills its 256-thread block with phases
+      int P = (quant ? 256 : HIST_EXACT_THREADS) / lanes;
+      const int Pmax = quant ? 64 : 4;
       P = P > Pmax ? Pmax : (P < 1 ? 1 : P);
       for (; P >= 1; --P)
-        if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= HIST_LDS_BUDGET) break;
+        if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= (quant ? HIST_LDS_BUDGET : HIST_EXACT_LDS_BUDGET)) break;
       if (P >= 1) {
         pl.FT = FT;
         pl.NTn = NTn;
@@ -1003,6 +1299,9 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
         pl.piece = quant ? ((HIST_QBIN_LDS / RB) & ~15) : HIST_MAX_CHUNK;
         if (pl.piece > HIST_MAX_CHUNK) pl.piece = HIST_MAX_CHUNK;
         if (pl.piece < 16) pl.piece = 16;
+        // exact form: no staging beyond the chunk (a 64-row chunk staged 1024 rows' worth of LDS, which
+        // cut the blocks per CU from 4 to 3 at depth 2 of the reference fit: two rounds of blocks)
+        if (!quant && pl.piece > pl.chunk) pl.piece = (pl.chunk + 15) & ~15;
         pl.lds = (size_t)(quant ? 1 : P) * NTn * pl.ldsC * 16 + (size_t)pl.piece * (quant ? 18 : 10) + 4 +
                  (quant ? ((size_t)pl.piece * RB + 32 + 15) / 16 * 16 : 0);
         return true;
@@ -1040,9 +1339,18 @@ struct QuantAux {
   const int* fmap_d = nullptr;        // [Fm] sub-feature -> bin-row column
 };
 
+struct HistPartition {  // the previous level's partition fused into the exact-form histogram (gbdt_hist)
+  int16_t* node_out = nullptr;
+  const int8_t* st = nullptr;
+  const int16_t* fe = nullptr;
+  const uint8_t* sb = nullptr;
+  int NN = 0;
+  const int* rd = nullptr;
+};
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
-                      bool fold, double qscale, int* nchunks_out, hipStream_t stream, const QuantAux* qa = nullptr) {
+                      bool fold, double qscale, int* nchunks_out, hipStream_t stream, const QuantAux* qa = nullptr,
+                      const HistPartition& hp = HistPartition()) {
   const bool quant = qscale != 0.0;
   const int C = foff_h[F];
   const int nodesL = 1 << level;
@@ -1075,8 +1383,24 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
                          (const int*)nullptr, foff_d, qpart, T, n, F, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
                          pl.ldsC, pl.piece, qscale);
     else
-      hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d, partial, T, n,
-                         F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece);
+    {
+      // exact form: the previous level's split arrays (partition fused in) and, when a piece's bin rows
+      // fit 16 KB, the rows themselves are staged in LDS after the (g, h, node) staging
+      const int srows = pl.piece < pl.chunk ? pl.piece : pl.chunk;
+      const int npn = hp.node_out ? (1 << level) - (1 << (level - 1)) : 0;
+      size_t lds = ((pl.lds + 15) & ~(size_t)15) + (((size_t)npn * 4 + 15) & ~(size_t)15);
+      const size_t sbytes = (((size_t)srows * F + 32 + 15) & ~(size_t)15);
+      const int stage = ((int64_t)srows * F <= 16 * 1024 && lds + sbytes <= 160 * 1024) ? srows : 0;
+      if (stage) lds += sbytes;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gbdt_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
+                         C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece, stage, hp.node_out, hp.st, hp.fe,
+                         hp.sb, hp.NN, hp.rd);
+    }
   }
   const bool split_folds = !fold && nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
   if (nchunks > 1 && !split_folds) {
@@ -1106,10 +1430,10 @@ __global__ void gbdt_round_advance(int* rd) {
 
 // every argument a captured round depends on (compared bytewise: zero-filled before use)
 struct GbdtGraphKey {
-  const void* p[18];
+  const void* p[19];
   const void* ev[4][3];
   int evn[4];
-  int i[9];
+  int i[10];
   float f[5];
   int64_t pd;
   int foff[320];
@@ -1128,6 +1452,29 @@ struct GraphCache {
 GraphCache& graph_cache() {
   static GraphCache c;
   return c;
+}
+// [T] zeroed device ints (grown on demand; left zeroed by every use): gbdt_split's per-task arrival
+// counters of the fused finalize
+int* task_counters(int T) {
+  static int* ctr = nullptr;
+  static int cap = 0, dev = -1;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  if (!ctr || dev != d || T > cap) {
+    if (ctr && dev == d) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(ctr);
+    }
+    ctr = nullptr;
+    int* p = nullptr;
+    const int want = T > 1024 ? T : 1024;
+    if (hipMalloc(&p, (size_t)want * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, (size_t)want * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    ctr = p;
+    cap = want;
+    dev = d;
+  }
+  return ctr;
 }
 // one zeroed device int per process (per device in use): the fused metric launches' arrival counter
 int* metric_counter() {
@@ -1169,14 +1516,14 @@ EM_API int64_t em_gbdt_partial_doubles(int n, int T, int F, const int* foff, int
 // Trains rounds [r0, r1).  Tree arrays hold ALL rounds: [R*T][NN] (tree k = round*T + task).
 // foff_h / foff_d: feature -> first compact histogram cell, [F+1] (host copy for the plan, device copy
 // for the kernels); feature f has foff[f+1]-foff[f] bins.
-// scratch: g, h [T][n]; node int16 [T][n]; partial (em_gbdt_partial_doubles); G, H [T][NN]; mpart double[4096]
+// scratch: g, h [T][n]; node, node2 int16 [T][n]; partial (em_gbdt_partial_doubles); G, H [T][NN]; mpart double[5 * 4096]
 // hist_out: float [R][1 + n_evals] (metric of train + each eval set after each round)
 EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const int* foff_h, const int* foff_d, int T,
                        float* margin, const EmGbdtEval* evals, int n_evals, int r0, int r1, int max_depth, int obj,
                        int metric, float eta, float lam, float gamma, float mcw, float subsample, uint32_t seed,
-                       float* g, float* h, int16_t* node, double* partial, int64_t partial_doubles, double* Gs,
-                       double* Hs, double* mpart, int8_t* status, int16_t* feat, uint8_t* sbin, float* leaf,
-                       float* gainv, float* cover, float* hist_out, int quant_bits, hipStream_t stream) {
+                       float* g, float* h, int16_t* node, int16_t* node2, double* partial, int64_t partial_doubles,
+                       double* Gs, double* Hs, double* mpart, int8_t* status, int16_t* feat, uint8_t* sbin,
+                       float* leaf, float* gainv, float* cover, float* hist_out, int quant_bits, hipStream_t stream) {
   if (!bins || !Y || !margin || n <= 0 || F <= 0 || !valid_foff(foff_h, F) || !foff_d || T <= 0 || max_depth < 1 ||
       max_depth > 12 || r0 < 0 || r1 < r0 || quant_bits < 0 || quant_bits > 61)
     return EM_ERR_ARG;
@@ -1243,6 +1590,19 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   // one round's kernel sequence.  rd == nullptr: the arrays of `round` are addressed from the host;
   // rd = the device round counter: every round-dependent offset is taken in-kernel (round = 0 here),
   // so the identical sequence is captured once and replayed for every round
+  // Exact-form fits with an elementwise metric run the fused round: the previous level's partition
+  // inside each histogram pass (double-buffered nodes), the prune / leaves in the last level's split
+  // (last-arriving block per task), the last partition in the update, and -- eager rounds of per-task
+  // objectives -- the next round's start in the update too: 8 launches per depth-3 round instead of 13.
+  // Bit-identical to the separate launches (same arithmetic on the same values).
+  // EM_GBDT_FUSE=0: the separate launches (A/B, tests)
+  int* tctr = nullptr;
+  const char* fz = getenv("EM_GBDT_FUSE");
+  const bool fuse = !(fz && fz[0] == '0') && !quant_bits && metric < MET_MLOGLOSS &&
+                    max_depth <= SPLIT_FINAL_MAX_DEPTH && node2 && (tctr = task_counters(T)) != nullptr;
+  // one round's kernel sequence.  rd == nullptr: the arrays of `round` are addressed from the host;
+  // rd = the device round counter: every round-dependent offset is taken in-kernel (round = 0 here),
+  // so the identical sequence is captured once and replayed for every round
   auto enqueue_round = [&](int round, const int* rd, hipStream_t s) -> int {
     const int64_t ro = (int64_t)round * T * NN;
     int8_t* st = status + ro;
@@ -1251,29 +1611,60 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     float* lf = leaf + ro;
     float* gn = gainv + ro;
     float* cv = cover + ro;
-    hipLaunchKernelGGL(gbdt_round_start, dim3(grid_for(TN > (int64_t)T * NN ? TN : (int64_t)T * NN)), dim3(256), 0, s,
-                       st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round, rd);
+    const bool next_in_update = fuse && !rd && obj != OBJ_SOFTMAX;  // eager: round + 1 started by this update
+    int16_t* nb[2] = {node, fuse ? node2 : node};
+    if (!next_in_update || round == r0)
+      hipLaunchKernelGGL(gbdt_round_start, dim3(grid_for(TN > (int64_t)T * NN ? TN : (int64_t)T * NN)), dim3(256), 0,
+                         s, st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round, rd);
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
       int nch = 1;
-      const int rc = launch_level_hist(level, bins, g, h, node, T, n, F, foff_h, foff_d, partial, partial_doubles,
-                                       false, qscale, &nch, s, qa.nb ? &qa : nullptr);
+      HistPartition hp;
+      const int16_t* nin = node;
+      if (fuse && level >= 1) {
+        nin = nb[(level - 1) & 1];
+        hp.node_out = nb[level & 1];
+        hp.st = st;
+        hp.fe = fe;
+        hp.sb = sb;
+        hp.NN = NN;
+        hp.rd = rd;
+      }
+      const int rc = launch_level_hist(level, bins, g, h, nin, T, n, F, foff_h, foff_d, partial, partial_doubles,
+                                       false, qscale, &nch, s, qa.nb ? &qa : nullptr, hp);
       if (rc) return rc;
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
       const int64_t cstride = (int64_t)T * nodesL * C * 2;
-      const size_t slds = nch > 1 ? (size_t)C * 16 : 0;
+      const int oneshot = nch > 1 && (int64_t)nch * C * 16 <= SPLIT_ONESHOT_LDS;
+      size_t slds = nch > 1 ? (((size_t)(oneshot ? nch : 1) * C * 16 + 15) & ~(size_t)15) : 0;
+      const size_t scan_b = ((size_t)C * 20 + 15) & ~(size_t)15;
+      const int pscan = slds + scan_b + (size_t)NN * 24 <= 60 * 1024;  // (+ the finalize area: < 64 KB)
+      if (pscan) slds += scan_b;
+      SplitFinal fin;
+      if (fuse && level == max_depth - 1) {
+        fin.tctr = tctr;
+        fin.leaf = lf;
+        fin.cover = cv;
+        fin.gamma = gamma;
+        fin.eta = (double)eta;
+        fin.max_depth = max_depth;
+        slds += (size_t)NN * 24;
+      }
       if (quant_bits)
         hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, s,
                            reinterpret_cast<const long long*>(partial), nch, cstride, foff_d, T, F, C, level, NN, Gs,
-                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, rd);
+                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, rd, fin, oneshot, pscan);
       else
         hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, s, partial, nch, cstride,
-                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, rd);
-      hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, s, bins, node, T, n, F, NN, st, fe, sb,
-                         level, rd);
+                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, rd, fin,
+                           oneshot, pscan);
+      if (!fuse)
+        hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, s, bins, node, T, n, F, NN, st, fe, sb,
+                           level, rd);
     }
-    hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, s, T, NN, max_depth, st, fe, gn, Gs, Hs, lf,
-                       cv, (double)lam, gamma, (double)eta, rd);
+    if (!fuse)
+      hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, s, T, NN, max_depth, st, fe, gn, Gs, Hs, lf,
+                         cv, (double)lam, gamma, (double)eta, rd);
     // metrics (train + evals) into hist_out[round].  Elementwise metrics: the leaf update / eval
     // prediction, the metric partials and the final sum are one launch each (last-arriving block);
     // the round counter of a replayed round advances in the round's last launch
@@ -1283,8 +1674,41 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     const bool fused_metric = metric < MET_MLOGLOSS;
     int* adv = const_cast<int*>(rd);
     if (fused_metric) {
-      hipLaunchKernelGGL(gbdt_update_metric, dim3(mb_train), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd, Y,
-                         obj, metric, mpart, mctr, ho, hs, n_evals == 0 ? adv : nullptr);
+      NextRound nx;
+      if (next_in_update && round + 1 < r1) {
+        const int64_t rn = ro + (int64_t)T * NN;
+        nx.round = round + 1;
+        nx.g = g;
+        nx.h = h;
+        nx.node = node;
+        nx.st = st + (int64_t)T * NN;
+        nx.fe = fe + (int64_t)T * NN;
+        nx.sb = sb + (int64_t)T * NN;
+        nx.gn = gainv + rn;
+        nx.subsample = subsample;
+        nx.seed = seed;
+      }
+      // eager rounds: the eval sets' predictions ride in the same launch (trailing blocks)
+      EvalSets evs;
+      int grid = mb_train;
+      if (!rd && n_evals <= 4) {
+        for (int e = 0; e < n_evals; ++e) {
+          evs.bins[e] = evals[e].bins;
+          evs.margin[e] = evals[e].margin;
+          evs.Y[e] = evals[e].Y;
+          evs.n[e] = evals[e].n;
+          evs.mb[e] = grid_for((int64_t)T * evals[e].n);
+          grid += evs.mb[e];
+        }
+        evs.count = n_evals;
+      }
+      hipLaunchKernelGGL(gbdt_update_metric, dim3(grid), dim3(256), 0, s, margin,
+                         fuse ? nb[(max_depth - 1) & 1] : node, T, n, NN, st, lf, rd, Y, obj, metric, mpart, mctr, ho,
+                         hs, n_evals == 0 ? adv : nullptr, bins, F, fuse ? max_depth - 1 : -1, fe, sb, nx, mb_train, evs);
+      if (evs.count == n_evals) {
+        EM_CHECK_LAUNCH();
+        return 0;
+      }
     } else {
       hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd);
       hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, s, margin, Y, T, n, obj, metric, mpart);
@@ -1312,11 +1736,14 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     EM_CHECK_LAUNCH();
     return 0;
   };
-  // Launch-bound fits (the reference's ~1k rows: ~20 tiny kernels per round) replay one captured
-  // round instead: host enqueue cost per round drops from ~20 launches to one graph launch.  The
-  // graph is cached across calls with the same arguments (the Python driver calls per 25 rounds);
-  // EM_GBDT_GRAPH=0 keeps the eager loop.  Same kernels and arguments: bit-identical trees.
-  static const bool graph_on = !(getenv("EM_GBDT_GRAPH") && getenv("EM_GBDT_GRAPH")[0] == '0');
+  // EM_GBDT_GRAPH=1: replay one captured round per round (the graph is cached across calls with the
+  // same arguments; the Python driver calls per 100 rounds).  Opt-in: on the reference fit the replayed
+  // rounds measured slower than the eager stream (0.056-0.057 vs 0.049-0.050 s for 500 rounds) -- the
+  // device, not the host enqueue, bounds a round, a graph's nodes start a little later than
+  // back-to-back launches, and a replayed round cannot carry the next round's start in its update
+  // (the eager round does: one launch less).  Same kernels and arguments: bit-identical trees.
+  const char* gv = getenv("EM_GBDT_GRAPH");
+  const bool graph_on = gv && gv[0] == '1';
   if (graph_on && r1 - r0 >= 2 && !qmem) {
     GraphCache& gc = graph_cache();
     GbdtGraphKey key;
@@ -1324,12 +1751,13 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     key.p[0] = bins; key.p[1] = Y; key.p[2] = foff_d; key.p[3] = margin; key.p[4] = g; key.p[5] = h;
     key.p[6] = node; key.p[7] = partial; key.p[8] = Gs; key.p[9] = Hs; key.p[10] = mpart; key.p[11] = status;
     key.p[12] = feat; key.p[13] = sbin; key.p[14] = leaf; key.p[15] = gainv; key.p[16] = cover; key.p[17] = hist_out;
+    key.p[18] = node2;
     for (int e = 0; e < n_evals && e < 4; ++e) {
       key.ev[e][0] = evals[e].bins; key.ev[e][1] = evals[e].Y; key.ev[e][2] = evals[e].margin;
       key.evn[e] = evals[e].n;
     }
     key.i[0] = n; key.i[1] = F; key.i[2] = T; key.i[3] = n_evals; key.i[4] = max_depth; key.i[5] = obj;
-    key.i[6] = metric; key.i[7] = quant_bits; key.i[8] = (int)seed;
+    key.i[6] = metric; key.i[7] = quant_bits; key.i[8] = (int)seed; key.i[9] = fuse ? 1 : 0;
     key.f[0] = eta; key.f[1] = lam; key.f[2] = gamma; key.f[3] = mcw; key.f[4] = subsample;
     key.pd = partial_doubles;
     for (int f = 0; f <= F && f < 320; ++f) key.foff[f] = foff_h[f];
@@ -1364,6 +1792,17 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   for (int round = r0; round < r1; ++round)
     if (int rc = enqueue_round(round, nullptr, stream)) return rc;
   return 0;
+}
+
+// GBDT_STAMPS builds: the 256 phase stamps (100 MHz ticks) and the matching 256 shader-clock counts
+// to host memory (512 values); -1 in other builds
+EM_API int em_gbdt_stamps(unsigned long long* out) {
+#if GBDT_STAMPS
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(g_stamp));
+#else
+  (void)out;
+  return -1;
+#endif
 }
 
 EM_API int em_gbdt_init_margin(float* margin, int64_t total, float base, hipStream_t stream) {
@@ -1431,7 +1870,8 @@ EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* 
   const int64_t TN = (int64_t)T * n;
   const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
   hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C,
-                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, (const int*)nullptr);
+                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, (const int*)nullptr,
+                     SplitFinal(), 0, 0);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
                      sbin, level, (const int*)nullptr);
   EM_CHECK_LAUNCH();

@@ -23,7 +23,7 @@ class _Eval(ctypes.Structure):
 
 N.register_signatures({
     "em_gbdt_fit": (_i, [_v, _v, _i, _i, _v, _v, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f,
-                         _f, _f, _u32, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _i, _v]),
+                         _f, _f, _u32, _v, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _i, _v]),
     "em_gbdt_partial_doubles": (_i64, [_i, _i, _i, _v, _i]),
     "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
     "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
@@ -63,7 +63,7 @@ class _Cells:
         return self.host.ctypes.data
 
 
-def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
+def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 100, dp=None):
     dev = _dev()
     n, F = bins.shape
     T = Y.shape[1]
@@ -90,13 +90,14 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
     g = torch.empty(T * n, dtype=torch.float32, device=dev)
     h = torch.empty_like(g)
     node = torch.empty(T * n, dtype=torch.int16, device=dev)
+    node2 = torch.empty_like(node)  # the fused round's double-buffered level nodes
     pdoubles = N.query("em_gbdt_partial_doubles", n, T, F, cells.hp, D)
     if pdoubles < 0:
         raise PlanUnsupported(f"GPU GBDT: no histogram plan for depth {D} x {cells.C} bins x {T} tasks")
     partial = torch.empty(max(pdoubles, 1), dtype=torch.float64, device=dev)
     Gs = torch.zeros(T * NN, dtype=torch.float64, device=dev)
     Hs = torch.zeros_like(Gs)
-    mpart = torch.zeros(4096, dtype=torch.float64, device=dev)
+    mpart = torch.zeros(5 * 4096, dtype=torch.float64, device=dev)  # train + up to 4 eval sets (fused launch)
     status = torch.zeros(R * T * NN, dtype=torch.int8, device=dev)
     feat = torch.zeros(R * T * NN, dtype=torch.int16, device=dev)
     sbin = torch.zeros(R * T * NN, dtype=torch.uint8, device=dev)
@@ -117,7 +118,7 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 25, dp=None):
                margin.data_ptr(), ev_structs,
                len(ev_names), r0, r1, D, OBJ[model.objective], MET[model.eval_metric], model.eta, model.lam,
                model.gamma, model.mcw, model.subsample, model.seed & 0xFFFFFFFF, g.data_ptr(), h.data_ptr(),
-               node.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
+               node.data_ptr(), node2.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
                status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), gain.data_ptr(),
                cover.data_ptr(), hist.data_ptr(), qbits, stream)
         hh = hist.view(R, 1 + len(ev_names))[r0:r1].cpu().numpy()

@@ -1,4 +1,6 @@
 """GBDT with XGBoost semantics: formulas, pruning, exact-vs-hist equivalence, persistence."""
+import os
+
 import numpy as np
 import pytest
 
@@ -221,6 +223,43 @@ def test_hip_dp_primitives_match_single_call():
     assert np.array_equal(dp.trees.feat, ref.trees.feat) and np.array_equal(dp.trees.sbin, ref.trees.sbin)
     assert np.array_equal(dp.trees.leaf, ref.trees.leaf)
     assert np.allclose([h["test"] for h in dp.history], [h["test"] for h in ref.history], rtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obj", ["reg:logistic", "reg:squarederror"])
+def test_hip_fused_round_and_graph_bit_identical(obj):
+    """The fused round (partition inside the histogram pass, prune/leaves in the last split, last
+    partition and next round start in the update), the separate launches (EM_GBDT_FUSE=0) and the
+    hipGraph-replayed rounds (EM_GBDT_GRAPH=1) give bit-identical trees, margins and histories."""
+    from euromillioner_amd import config as C
+    from euromillioner_amd.pipeline import gbdt_dataset
+
+    ds = DrawSet.synthetic(n=None, seed=3, planted=0.5)
+    X, Y, _ = gbdt_dataset(ds, C.RunConfig())
+    m = int(0.7 * len(X))
+    kw = dict(eta=1.0 if obj == "reg:logistic" else 0.3, max_depth=3, gamma=1.0, nround=60, objective=obj,
+              eval_metric="logloss" if obj == "reg:logistic" else "rmse", subsample=0.8, backend="hip")
+    ev = {"test": (X[m:], Y[m:])}
+    fits = {}
+    for name, env in (("fused", {"EM_GBDT_GRAPH": "0"}), ("separate", {"EM_GBDT_GRAPH": "0", "EM_GBDT_FUSE": "0"}),
+                      ("graph", {"EM_GBDT_GRAPH": "1"})):
+        old = {k: os.environ.get(k) for k in ("EM_GBDT_GRAPH", "EM_GBDT_FUSE")}
+        os.environ.update(env)
+        try:
+            fits[name] = G.GBDT(**kw).fit(X[:m], Y[:m], evals=ev)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    a = fits["fused"]
+    for name in ("separate", "graph"):
+        b = fits[name]
+        for k in ("status", "feat", "sbin", "leaf", "gain", "cover"):
+            assert np.array_equal(getattr(a.trees, k), getattr(b.trees, k)), (name, k)
+        assert a.history == b.history, name
+        assert np.array_equal(a.predict(X[m:], backend="hip"), b.predict(X[m:], backend="hip")), name
 
 
 def test_native_hist_plan_bounds():
