@@ -140,6 +140,15 @@ class TreeArrays:
         self.gain = np.zeros((n_trees, nn), dtype=np.float64)
         self.cover = np.zeros((n_trees, nn), dtype=np.float64)
 
+    @classmethod
+    def from_arrays(cls, max_depth: int, status, feat, sbin, leaf, gain, cover) -> "TreeArrays":
+        """Wrap existing [n_trees, nn] arrays (int8 / int32 / int32 / float64 x 3) without copying."""
+        t = cls.__new__(cls)
+        t.max_depth = max_depth
+        t.status, t.feat, t.sbin, t.leaf, t.gain, t.cover = status, feat, sbin, leaf, gain, cover
+        t.split_value = np.zeros(feat.shape, dtype=np.float64)
+        return t
+
     @property
     def n_trees(self):
         return self.feat.shape[0]

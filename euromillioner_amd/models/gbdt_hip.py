@@ -130,13 +130,19 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 100, dp=None):
             history.append(rec)
             model._log_round(rec)
         r0 = r1
-    trees = TreeArrays(R * T, D)
-    trees.status[:] = status.view(R * T, NN).cpu().numpy()
-    trees.feat[:] = feat.view(R * T, NN).cpu().numpy().astype(np.int32)
-    trees.sbin[:] = sbin.view(R * T, NN).cpu().numpy().astype(np.int32)
-    trees.leaf[:] = leaf.view(R * T, NN).cpu().numpy().astype(np.float64)
-    trees.gain[:] = gain.view(R * T, NN).cpu().numpy().astype(np.float64)
-    trees.cover[:] = cover.view(R * T, NN).cpu().numpy().astype(np.float64)
+    # the host copy of the ensemble: dtypes converted on the device, one packed device-to-host copy,
+    # numpy views of it (per-array host conversions of ~0.5 M nodes cost several ms)
+    # (widest dtypes first: every view starts aligned)
+    parts = [leaf.to(torch.float64), gain.to(torch.float64), cover.to(torch.float64), feat.to(torch.int32),
+             sbin.to(torch.int32), status]
+    host = torch.cat([t.reshape(-1).view(torch.uint8) for t in parts]).cpu().numpy()
+    arrs, o = [], 0
+    for t, dt in zip(parts, (np.float64, np.float64, np.float64, np.int32, np.int32, np.int8)):
+        nb = t.numel() * t.element_size()
+        arrs.append(host[o:o + nb].view(dt).reshape(R * T, NN))
+        o += nb
+    lf, gn, cv, fe, sb, st = arrs
+    trees = TreeArrays.from_arrays(D, st, fe, sb, lf, gn, cv)
     model._device_trees = (status, feat, sbin, leaf)
     return trees, history
 
