@@ -99,6 +99,54 @@ struct RfParams {
 // per candidate), hist[k][64] (sum of w*x_f*y_j) -- exact, so block partials merge with atomics in
 // any order and the split decision is independent of row order and of the block count
 __host__ __device__ inline int rec_words(int k) { return 68 + ((k + 3) & ~3) + 64 * k; }
+// The fused partition's LDS image of a child's cnt / hist words, replicated by lane so the lanes of one
+// atomic mostly hit distinct words: cnt [RF_REP_CNT][kp + 1] (lane & 15), hist [RF_REP_HIST][k * 64 + 16]
+// (lane & 3; the +16 pad moves a replica's output j to another bank).  Summed at the merge.
+#ifndef RF_REP_CNT
+#define RF_REP_CNT 16
+#endif
+#ifndef RF_REP_HIST
+#define RF_REP_HIST 4
+#endif
+__host__ __device__ inline int rf_rep_cnt_stride(int k) { return ((k + 3) & ~3) + 1; }
+__host__ __device__ inline int rf_rep_hist_stride(int k) { return 64 * k + 16; }
+__host__ __device__ inline int rf_chl_words(int k) {
+  return RF_REP_CNT * rf_rep_cnt_stride(k) + RF_REP_HIST * rf_rep_hist_stride(k);
+}
+
+// A row's output bits, extracted once per row: the first 8 positions (-1 = none) + the rest (rows with
+// more than 8 set outputs; a drawn row has 7).  Every candidate bit of the row then adds to its output
+// words with 8 branch-free atomics (an absent position adds 0 to pad word 63: exact integers) instead
+// of a divergent bit-walk loop per candidate -- the loop's ~13 instructions per output were the
+// histogram's cost, not the atomics.
+#ifndef RF_YBITS
+#define RF_YBITS 1
+#endif
+// RF_CNT62: the fused partition counts a candidate's rows (cnt) as output word 62 of its histogram row
+// (no output uses it), so a drawn row's 7 outputs + its count are exactly the 8 unrolled atomics
+#ifndef RF_CNT62
+#define RF_CNT62 1
+#endif
+struct RfYBits {
+  int j[8];
+  uint64_t rest;
+};
+EM_DEVICE RfYBits rf_ybits(uint64_t y) {
+  RfYBits b;
+  uint64_t yy = y;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    b.j[q] = yy ? (int)__builtin_ctzll(yy) : -1;
+    yy &= yy - 1;
+  }
+  b.rest = yy;
+  return b;
+}
+EM_DEVICE void rf_add_ybits(uint32_t* __restrict__ row, const RfYBits& b, uint32_t w) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) atomicAdd(&row[b.j[q] & 63], b.j[q] >= 0 ? w : 0u);
+  for (uint64_t r = b.rest; r; r &= r - 1) atomicAdd(&row[__builtin_ctzll(r)], w);
+}
 // Root row lists: rows with non-zero bootstrap weight, compacted per tree by (blocks x tree)
 // workgroups; each 256-row chunk reserves its output range with one atomic (row order inside a list
 // is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
@@ -413,12 +461,17 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restr
       w = packed ? (uint32_t)e >> RF_WSHIFT : (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
       y = p.Y[r] & RF_M62;
     }
+    const RfYBits yb = rf_ybits(y);
     if (!DERIVE) {
       my_n += w;
-      uint64_t yy = y;
-      while (yy) {
-        atomicAdd(&S[__builtin_ctzll(yy)], w);
-        yy &= yy - 1;
+      if (RF_YBITS) {
+        rf_add_ybits(S, yb, w);
+      } else {
+        uint64_t yy = y;
+        while (yy) {
+          atomicAdd(&S[__builtin_ctzll(yy)], w);
+          yy &= yy - 1;
+        }
       }
     }
     if (!split) continue;
@@ -428,10 +481,14 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restr
         const int sl = slot[wd * 64 + __builtin_ctzll(xx)];
         xx &= xx - 1;
         atomicAdd(&cnt[sl], w);
-        uint64_t y2 = y;
-        while (y2) {
-          atomicAdd(&hist[sl * 64 + __builtin_ctzll(y2)], w);
-          y2 &= y2 - 1;
+        if (RF_YBITS) {
+          rf_add_ybits(hist + sl * 64, yb, w);
+        } else {
+          uint64_t y2 = y;
+          while (y2) {
+            atomicAdd(&hist[sl * 64 + __builtin_ctzll(y2)], w);
+            y2 &= y2 - 1;
+          }
         }
       }
     }
@@ -691,8 +748,10 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
   __shared__ int8_t cslot[2][64];
   __shared__ uint64_t cmk[2];
   const int kf = p.k_feat, rec = rec_words(kf), kp = (kf + 3) & ~3;
+  const int chw = rf_chl_words(kf), cst = rf_rep_cnt_stride(kf), hst = rf_rep_hist_stride(kf);
+  const int lane_c = (threadIdx.x & 63) % RF_REP_CNT, lane_h = (threadIdx.x & 63) % RF_REP_HIST;
   if (HIST) {
-    for (int i = threadIdx.x; i < 2 * rec; i += blockDim.x) chl[i] = 0u;
+    for (int i = threadIdx.x; i < 2 * chw; i += blockDim.x) chl[i] = 0u;
     if (threadIdx.x < 2) {
       const int s = threadIdx.x;
       const int16_t* co = cand_next + ((int64_t)t * (2 * nodesL) + 2 * nd + s) * kf;
@@ -775,9 +834,18 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
         const uint32_t w = rf_rec_w(r[k2]);
         const uint64_t y = r[k2].y & RF_M62;
         uint64_t xx = r[k2].x & RF_M62 & cmk[sd];
-        uint32_t* cnt = chl + sd * rec + 68;
-        uint32_t* hist = cnt + kp;
-        while (xx) {
+        uint32_t* cnt = chl + sd * chw + lane_c * cst;
+        uint32_t* hist = chl + sd * chw + RF_REP_CNT * cst + lane_h * hst;
+        if (RF_YBITS && xx) {
+          const RfYBits yb = rf_ybits(RF_CNT62 ? (y | (1ull << 62)) : y);
+          while (xx) {
+            const int sl = cslot[sd][__builtin_ctzll(xx)];
+            xx &= xx - 1;
+            if (!RF_CNT62) atomicAdd(&cnt[sl], w);
+            rf_add_ybits(hist + sl * 64, yb, w);
+          }
+        }
+        while (!RF_YBITS && xx) {
           const int sl = cslot[sd][__builtin_ctzll(xx)];
           xx &= xx - 1;
           atomicAdd(&cnt[sl], w);
@@ -795,11 +863,24 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
 #pragma unroll
     for (int sd = 0; sd < 2; ++sd) {
       uint32_t* dst = acc_next + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * rec;
-      if (B == 1) {  // the node's only block: plain stores (rf_split did not zero these words)
-        for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x) dst[i] = chl[sd * rec + i];
-      } else {
-        for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x)
-          if (chl[sd * rec + i]) atomicAdd(&dst[i], chl[sd * rec + i]);
+      const uint32_t* src = chl + sd * chw;
+      for (int i = 68 + threadIdx.x; i < rec; i += blockDim.x) {
+        uint32_t v = 0;
+        if (i < 68 + kp) {  // cnt[sl]: its replicas (RF_CNT62: word 62 of the slot's histogram row)
+          if (RF_YBITS && RF_CNT62) {
+            if (i - 68 < kf)
+              for (int q = 0; q < RF_REP_HIST; ++q) v += src[RF_REP_CNT * cst + q * hst + (i - 68) * 64 + 62];
+          } else {
+            for (int q = 0; q < RF_REP_CNT; ++q) v += src[q * cst + (i - 68)];
+          }
+        } else if (!(RF_YBITS && RF_CNT62) || ((i - 68 - kp) & 63) < 62) {  // hist[sl][j]: its replicas
+          const int o = i - 68 - kp;
+          for (int q = 0; q < RF_REP_HIST; ++q) v += src[RF_REP_CNT * cst + q * hst + o];
+        }
+        if (B == 1)  // the node's only block: plain stores (rf_split did not zero these words)
+          dst[i] = v;
+        else if (v)
+          atomicAdd(&dst[i], v);
       }
     }
   }
@@ -919,7 +1000,8 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   uint32_t* accs[2] = {acc, acc + (int64_t)T * (1ll << max_depth) * rec};
   int16_t* cands[2] = {cand, reinterpret_cast<int16_t*>(acc + 2 * (int64_t)T * (1ll << max_depth) * rec)};
   const bool derive = derive_env && !use_mfma;
-  const bool fuse = derive && fuse_env && rec_rows;
+  // (the fused partition's replicated child images must fit the LDS: k <= ~70 candidates)
+  const bool fuse = derive && fuse_env && rec_rows && (size_t)2 * rf_chl_words(k_feat) * 4 <= 160 * 1024 - 8192;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
              cover, cand, accs[0], lrc};
   (void)hipMemsetAsync(lrc, 0, (size_t)T * 2 * sizeof(int32_t), stream);
@@ -959,7 +1041,8 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
       EM_CHECK_LAUNCH();
       if (level == max_depth) break;
       if (level + 1 < max_depth)
-        hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), 2 * lds, stream, p, (const void*)rin, rout,
+        hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), (size_t)2 * rf_chl_words(k_feat) * 4, stream,
+                           p, (const void*)rin, rout,
                            level, (const int32_t*)wl, an, (const int16_t*)cn);
       else
         hipLaunchKernelGGL((rf_partition<true, false>), dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,

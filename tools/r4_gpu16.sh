@@ -6,7 +6,7 @@ timeout -k 10 300 python -u -m pytest tests/test_forest.py -m gpu -x -v --timeou
 tail -2 $O/pytest_rf.log
 for rnd in 1 2; do
   timeout -k 10 120 python tools/rf_bench.py > $O/rf_ybits_$rnd.jsonl 2>&1 || { tail $O/rf_ybits_$rnd.jsonl; exit 7; }
-  EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/rf_ybits_norep.so timeout -k 10 120 python tools/rf_bench.py > $O/rf_ybitsnorep_$rnd.jsonl 2>&1 || { tail $O/rf_ybitsnorep_$rnd.jsonl; exit 8; }
+  EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/rf_ybits_cntsep.so timeout -k 10 120 python tools/rf_bench.py > $O/rf_ybitscntsep_$rnd.jsonl 2>&1 || { tail $O/rf_ybitscntsep_$rnd.jsonl; exit 8; }
   EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/rf_noybits.so timeout -k 10 120 python tools/rf_bench.py > $O/rf_noybits_$rnd.jsonl 2>&1 || { tail $O/rf_noybits_$rnd.jsonl; exit 8; }
 done
 for f in $O/rf_*_?.jsonl; do echo "$f $(grep -o '"fit_s": [0-9.]*' $f | tr '\n' ' ')"; done
