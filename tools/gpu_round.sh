@@ -7,6 +7,12 @@
 #   bash tools/gpu_round.sh gbdt            GBDT GPU tests, kernel trace of the 183k-row case, gbdt_bench
 #   bash tools/gpu_round.sh fp32            bench.py --dtype fp32 + kernel trace
 #   bash tools/gpu_round.sh wide            wide-MLP bench + kernel trace, one-GPU overlap rehearsal
+#   bash tools/gpu_round.sh gbdt-ref        round-4 GBDT reference fit: GPU tests, eager vs graph bench, phase
+#                                           stamps (needs lib/ab/gbdt_stamps.so: build_variant.sh -DGBDT_STAMPS=1)
+#   bash tools/gpu_round.sh rf-ab           RF tests + rf_bench against lib/ab/rf_head.so (the committed
+#                                           forest.hip: SRC=... build_variant.sh rf_head), kernel stats
+#   bash tools/gpu_round.sh dp-proxy        one-GPU DP=8 small-MLP exchange proxy (tools/xgmi_budget.py)
+#   bash tools/gpu_round.sh hbm-fill        HBM-filling 256M-sample runs on p = 0.9 and p = 0.7
 # Several stages run in order: bash tools/gpu_round.sh gbdt fp32
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -51,6 +57,41 @@ for stage in "$@"; do
     summ $O/bench.json wide || exit 20
     timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/overlap -o run -- python tools/wide_overlap.py > $O/overlap.jsonl 2> $O/overlap.err || { tail $O/overlap.err; exit 21; }
     python tools/wide_overlap.py report $O/overlap/run_kernel_trace.csv > $O/overlap_report.jsonl && cat $O/overlap.jsonl
+    ;;
+  gbdt-ref)
+    timeout -k 10 400 python -u -m pytest tests/test_gbdt.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 22; }
+    tail -1 $O/pytest.log
+    for rnd in 1 2; do
+      timeout -k 10 200 python tools/gbdt_bench.py reference > $O/eager_$rnd.jsonl 2>&1 || { tail $O/eager_$rnd.jsonl; exit 23; }
+      EM_GBDT_GRAPH=1 timeout -k 10 200 python tools/gbdt_bench.py reference > $O/graph_$rnd.jsonl 2>&1 || { tail $O/graph_$rnd.jsonl; exit 23; }
+    done
+    grep -h -o '"hip_s": [0-9.]*' $O/eager_?.jsonl $O/graph_?.jsonl
+    if [ -f euromillioner_amd/lib/ab/gbdt_stamps.so ]; then
+      EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/gbdt_stamps.so timeout -k 10 120 python tools/gbdt_stamps.py > $O/stamps.jsonl 2>&1 || { tail $O/stamps.jsonl; exit 24; }
+      cat $O/stamps.jsonl
+    fi
+    ;;
+  rf-ab)
+    timeout -k 10 300 python -u -m pytest tests/test_forest.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 25; }
+    tail -1 $O/pytest.log
+    for rnd in 1 2; do
+      timeout -k 10 120 python tools/rf_bench.py > $O/new_$rnd.jsonl 2>&1 || { tail $O/new_$rnd.jsonl; exit 26; }
+      if [ -f euromillioner_amd/lib/ab/rf_head.so ]; then
+        EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/rf_head.so timeout -k 10 120 python tools/rf_bench.py > $O/head_$rnd.jsonl 2>&1 || { tail $O/head_$rnd.jsonl; exit 26; }
+      fi
+    done
+    for f in $O/*_?.jsonl; do echo "$f $(grep -o '"fit_s": [0-9.]*' $f)"; done
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python tools/rf_bench.py --repeat 2 > $O/trace.log 2>&1 || { tail $O/trace.log; exit 27; }
+    ;;
+  dp-proxy)
+    timeout -k 10 240 python tools/xgmi_budget.py > $O/xgmi_budget.jsonl 2>&1 || { tail -20 $O/xgmi_budget.jsonl; exit 28; }
+    grep round $O/xgmi_budget.jsonl
+    ;;
+  hbm-fill)
+    for pl in 0.9 0.7; do
+      timeout -k 10 300 python bench.py --device-data-gb -1 --batch 268435456 --steps 10 --warmup 2 --planted $pl > $O/fill_$pl.json 2> $O/fill_$pl.err || { tail $O/fill_$pl.err; exit 29; }
+      summ $O/fill_$pl.json fill_$pl || exit 30
+    done
     ;;
   *) echo "unknown stage $stage"; exit 2;;
   esac
