@@ -150,7 +150,11 @@ EM_DEVICE void rf_add_ybits(uint32_t* __restrict__ row, const RfYBits& b, uint32
 // Root row lists: rows with non-zero bootstrap weight, compacted per tree by (blocks x tree)
 // workgroups; each 256-row chunk reserves its output range with one atomic (row order inside a list
 // is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
-template <bool REC>
+// ROOTH (record rows, the fused driver): the root's histogram record (S, n, candidate cnt / hist) is
+// accumulated while the rows are listed -- the root histogram pass re-read every record (700 MB at
+// 700 k rows x 100 trees) -- in an LDS image per block, added to the zeroed root record at the end.
+EM_DEVICE void rf_node_cands_wave(const RfParams& p, int t, int node, int16_t* __restrict__ co);
+template <bool REC, bool ROOTH = false>
 __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restrict__ rows_v) {
   // chunks of RR x RF_NT rows: every thread hashes RR rows (all hashes / loads in flight), one count
   // exchange and one atomic reservation per chunk; the count arrays are double-buffered, so a chunk
@@ -160,6 +164,28 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ int wcnt[2][RR][4];
   __shared__ int base[2];
+  extern __shared__ __attribute__((aligned(16))) uint32_t rlds[];  // ROOTH: [rec] image
+  __shared__ int8_t rslot[64];
+  __shared__ uint64_t rmask;
+  __shared__ int16_t rco[RF_MAXF];
+  const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
+  uint32_t my_n = 0;
+  if constexpr (ROOTH) {
+    for (int i = threadIdx.x; i < rec; i += blockDim.x) rlds[i] = 0u;
+    if (threadIdx.x < 64) rslot[threadIdx.x] = -1;
+    if (wv == 0) rf_node_cands_wave(p, t, 0, rco);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t m = 0;
+      const int kk = k < p.F ? k : p.F;
+      for (int i = 0; i < kk; ++i) {
+        rslot[rco[i]] = (int8_t)i;
+        m |= 1ull << rco[i];
+      }
+      rmask = p.max_depth > 0 ? m : 0ull;
+    }
+    __syncthreads();
+  }
   int32_t* out = static_cast<int32_t*>(rows_v) + (int64_t)t * p.N;
   RfRec* outr = static_cast<RfRec*>(rows_v) + (int64_t)t * p.N;
   const int64_t r0 = p.N * blockIdx.x / B, r1 = p.N * (blockIdx.x + 1) / B;
@@ -192,10 +218,42 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
       for (int i = 0; i < wv; ++i) o += wcnt[par][k][i];
       if (w[k] > 0) {
         const int64_t r = c + k * RF_NT + threadIdx.x;
-        if constexpr (REC) outr[o + pre[k]] = rf_make_rec(p.X[r], p.Y[r], (uint32_t)w[k]);
-        else out[o + pre[k]] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w[k] << RF_WSHIFT)) : (int32_t)r;
+        if constexpr (REC) {
+          const uint64_t xv = p.X[r], yv = p.Y[r];
+          outr[o + pre[k]] = rf_make_rec(xv, yv, (uint32_t)w[k]);
+          if constexpr (ROOTH) {
+            const uint32_t wk = (uint32_t)w[k];
+            const uint64_t y = yv & RF_M62;
+            my_n += wk;
+            for (uint64_t yy = y; yy; yy &= yy - 1) atomicAdd(&rlds[__builtin_ctzll(yy)], wk);
+            uint64_t xx = xv & RF_M62 & rmask;
+            if (xx) {  // candidate bits: outputs once, the count as output word 62 (as rf_hist)
+              const RfYBits yb = rf_ybits(y | (1ull << 62));
+              while (xx) {
+                const int sl = rslot[__builtin_ctzll(xx)];
+                xx &= xx - 1;
+                rf_add_ybits(rlds + 68 + kp + sl * 64, yb, wk);
+              }
+            }
+          }
+        } else {
+          out[o + pre[k]] = rf_packed(p.N) ? (int32_t)(r | ((int64_t)w[k] << RF_WSHIFT)) : (int32_t)r;
+        }
       }
       off += wcnt[par][k][0] + wcnt[par][k][1] + wcnt[par][k][2] + wcnt[par][k][3];
+    }
+  }
+  if constexpr (ROOTH) {
+    for (int o = 32; o > 0; o >>= 1) my_n += __shfl_xor(my_n, o);
+    if (lane == 0) atomicAdd(&rlds[64], my_n);
+    __syncthreads();
+    uint32_t* dst = p.acc + (int64_t)t * rec;  // the root record of tree t (zeroed by the driver)
+    for (int i = threadIdx.x; i < rec; i += blockDim.x) {
+      uint32_t v;
+      if (i < 68) v = rlds[i];
+      else if (i < 68 + kp) v = i - 68 < k ? rlds[68 + kp + (i - 68) * 64 + 62] : 0u;
+      else v = ((i - 68 - kp) & 63) < 62 ? rlds[i] : 0u;
+      if (v) atomicAdd(&dst[i], v);
     }
   }
 }
@@ -329,7 +387,8 @@ __global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32
 // root only: deeper levels' are drawn by the parent's rf_split), then -- after every segment is
 // written and every parent counter read -- this level's partition counters zeroed (and, at the root,
 // the root records), then rf_worklist's scan.  Replaces 2 kernels and 1-2 memsets per level.
-__global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, int32_t* __restrict__ wl) {
+__global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, int32_t* __restrict__ wl,
+                                                       int zero_root) {
   const int nodesL = 1 << level, first = nodesL - 1, n = p.T * nodesL;
   // items in batches of 8 per thread: the batch's parent loads are all issued before its stores
   constexpr int PB = 8;
@@ -375,7 +434,7 @@ __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, in
   }
   __syncthreads();  // segments written, the parents' counters read
   for (int i = threadIdx.x; i < 2 * n; i += 1024) p.lrc[i] = 0;
-  if (level == 0)
+  if (level == 0 && zero_root)
     for (int i = threadIdx.x; i < n * rec_words(p.k_feat); i += 1024) p.acc[i] = 0u;
   __shared__ int part[1024];
   const int per = (n + 1023) / 1024, a = threadIdx.x * per, b = min(n, a + per);
@@ -461,29 +520,30 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restr
       w = packed ? (uint32_t)e >> RF_WSHIFT : (uint32_t)row_weight(p.bootstrap, p.seed, t + p.t_off, r);
       y = p.Y[r] & RF_M62;
     }
-    const RfYBits yb = rf_ybits(y);
-    if (!DERIVE) {
+    if (!DERIVE) {  // (every row: the uniform 7-output walk is already branch-coherent)
       my_n += w;
-      if (RF_YBITS) {
-        rf_add_ybits(S, yb, w);
-      } else {
-        uint64_t yy = y;
-        while (yy) {
-          atomicAdd(&S[__builtin_ctzll(yy)], w);
-          yy &= yy - 1;
-        }
+      uint64_t yy = y;
+      while (yy) {
+        atomicAdd(&S[__builtin_ctzll(yy)], w);
+        yy &= yy - 1;
       }
     }
     if (!split) continue;
     for (int wd = 0; wd < p.W; ++wd) {
       uint64_t xx = (REC ? xr : p.X[r * p.W + wd]) & cmask[wd];
-      while (xx) {
+      if (RF_YBITS && xx) {  // candidate rows: outputs extracted once, the count as output word 62
+        const RfYBits yb = rf_ybits(y | (1ull << 62));
+        while (xx) {
+          const int sl = slot[wd * 64 + __builtin_ctzll(xx)];
+          xx &= xx - 1;
+          rf_add_ybits(hist + sl * 64, yb, w);
+        }
+      }
+      while (!RF_YBITS && xx) {
         const int sl = slot[wd * 64 + __builtin_ctzll(xx)];
         xx &= xx - 1;
         atomicAdd(&cnt[sl], w);
-        if (RF_YBITS) {
-          rf_add_ybits(hist + sl * 64, yb, w);
-        } else {
+        {
           uint64_t y2 = y;
           while (y2) {
             atomicAdd(&hist[sl * 64 + __builtin_ctzll(y2)], w);
@@ -501,11 +561,18 @@ __global__ void __launch_bounds__(RF_NT) rf_hist(RfParams p, const void* __restr
   uint32_t* dst = p.acc + ((int64_t)t * nodesL + nd) * rec;
   const int used = split ? rec : 68;
   const int lo = DERIVE ? 68 : 0;  // S / n (words 0..67) already hold the derived totals
+  auto word = [&](int i) -> uint32_t {  // RF_YBITS: cnt[c] was counted in hist[c][62]
+    if (!RF_YBITS || i < 68) return lds[i];
+    if (i < 68 + kp) return i - 68 < k ? lds[68 + kp + (i - 68) * 64 + 62] : 0u;
+    return ((i - 68 - kp) & 63) < 62 ? lds[i] : 0u;
+  };
   if (B == 1) {
-    for (int i = lo + threadIdx.x; i < used; i += blockDim.x) dst[i] = lds[i];
+    for (int i = lo + threadIdx.x; i < used; i += blockDim.x) dst[i] = word(i);
   } else {
-    for (int i = lo + threadIdx.x; i < used; i += blockDim.x)
-      if (lds[i]) atomicAdd(&dst[i], lds[i]);
+    for (int i = lo + threadIdx.x; i < used; i += blockDim.x) {
+      const uint32_t v = word(i);
+      if (v) atomicAdd(&dst[i], v);
+    }
   }
 }
 
@@ -653,15 +720,22 @@ __global__ void __launch_bounds__(RF_NT) rf_hist_mfma(RfParams p, const RfRec* _
 // records for level + 1 -- node totals S / n (right = the histogram of the split candidate, left =
 // parent - right: rf_child_totals' arithmetic), every other word zeroed for the partition's histogram
 // atomics -- and, with child_cand, draws the children's candidate features (rf_node_cands).
-__global__ void __launch_bounds__(64) rf_split(RfParams p, int level, uint32_t* __restrict__ child_acc,
-                                               int16_t* __restrict__ child_cand) {
+// (launched with 128 threads when child_cand is set: the second wave draws the children's candidates
+// -- they depend on (seed, tree, node) only -- while the first runs the split scan)
+__global__ void __launch_bounds__(128) rf_split(RfParams p, int level, uint32_t* __restrict__ child_acc,
+                                                int16_t* __restrict__ child_cand) {
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.y, nd = blockIdx.x, node = first + nd;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
   int16_t* fo = p.feat + (int64_t)t * p.nodes + node;
   if (sg[1] < 0) {
-    if (lane == 0) *fo = -2;
+    if (threadIdx.x == 0) *fo = -2;
+    return;
+  }
+  if (threadIdx.x >= 64) {  // wave 1: the children's candidates (unused if this node ends as a leaf)
+    for (int sd = 0; sd < 2; ++sd)
+      rf_node_cands_wave(p, t, 2 * node + 1 + sd, child_cand + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * p.k_feat);
     return;
   }
   const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
@@ -716,9 +790,6 @@ __global__ void __launch_bounds__(64) rf_split(RfParams p, int level, uint32_t* 
     const int hi = (sg[1] + RF_CHUNK - 1) / RF_CHUNK > 1 ? rec : 68;
     for (int i = 64 + lane; i < hi; i += 64) dst[i] = i == 64 ? (sd ? nr : n - nr) : 0u;
   }
-  if (child_cand)
-    for (int sd = 0; sd < 2; ++sd)
-      rf_node_cands_wave(p, t, 2 * node + 1 + sd, child_cand + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * k);
 }
 
 // K10: children row lists, (blocks x nodes x trees) workgroups: left rows (x_f = 0) fill the parent
@@ -1008,7 +1079,16 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   {
     int B, nt;
     rf_shape(N, 0, B, nt);
-    if (rec_rows)
+    if (fuse) {  // the root records are accumulated by the listing pass
+      (void)hipMemsetAsync(accs[0], 0, (size_t)T * rec * sizeof(uint32_t), stream);
+      static bool ra = false;
+      if (!ra) {
+        (void)hipFuncSetAttribute((const void*)rf_init_rows<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024 - 8192);
+        ra = true;
+      }
+      hipLaunchKernelGGL((rf_init_rows<true, true>), dim3(B, T), dim3(RF_NT), lds, stream, p, (void*)rows_a);
+    } else if (rec_rows)
       hipLaunchKernelGGL(rf_init_rows<true>, dim3(B, T), dim3(RF_NT), 0, stream, p, (void*)rows_a);
     else
       hipLaunchKernelGGL(rf_init_rows<false>, dim3(B, T), dim3(RF_NT), 0, stream, p, (void*)rows_a);
@@ -1018,9 +1098,9 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   void* rout = rows_b;
   const int64_t kept = bootstrap ? (N * 632) / 1000 : N;  // expected rows per tree (Poisson(1): 1 - 1/e)
   if (fuse) {
-    // per level: rf_level_begin (segments, counters, work list), the root's histogram pass (level 0
-    // only), rf_split (also the children's totals, zeroed records and candidates), the partition
-    // (also the children's histograms while a next level still splits) -- 3 launches per level
+    // per level: rf_level_begin (segments, counters, work list), rf_split (also the children's totals,
+    // zeroed records and candidates), the partition (also the children's histograms while a next
+    // level still splits) -- 3 launches per level; the root's record came with the row lists
     for (int level = 0; level <= max_depth; ++level) {
       const int nodesL = 1 << level;
       int B, nt;
@@ -1029,15 +1109,12 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
       const int64_t tn = (int64_t)T * nodesL;
       p.acc = accs[level & 1];
       p.cand = cands[level & 1];
-      hipLaunchKernelGGL(rf_level_begin, dim3(1), dim3(1024), 0, stream, p, level, wl);
+      hipLaunchKernelGGL(rf_level_begin, dim3(1), dim3(1024), 0, stream, p, level, wl, 0);
       const int64_t gmax = (int64_t)T * ((N + RF_CHUNK - 1) / RF_CHUNK + 1) + tn;
       const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
-      if (level == 0)
-        hipLaunchKernelGGL((rf_hist<true, false>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level,
-                           (const int32_t*)wl);
       uint32_t* an = level < max_depth ? accs[(level + 1) & 1] : nullptr;
       int16_t* cn = level + 1 < max_depth ? cands[(level + 1) & 1] : nullptr;
-      hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(64), 0, stream, p, level, an, cn);
+      hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(cn ? 128 : 64), 0, stream, p, level, an, cn);
       EM_CHECK_LAUNCH();
       if (level == max_depth) break;
       if (level + 1 < max_depth)
