@@ -715,8 +715,8 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
           Hn += hs[2 * c + 1];
         }
         if (level == 0) {
-          G[(int64_t)t * NN] = val(Gn);
-          H[(int64_t)t * NN] = val(Hn);
+          __hip_atomic_store(G + (int64_t)t * NN, val(Gn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(H + (int64_t)t * NN, val(Hn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       } else {
         Gn = G[(int64_t)t * NN + i];
@@ -838,25 +838,30 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
           bHL = rhl[k];
         }
       if (bf < F && best > KRT_EPS) {
-        st[i] = 1;
-        feat[(int64_t)t * NN + i] = (int16_t)bf;
-        sbin[(int64_t)t * NN + i] = (uint8_t)bb;
-        gain[(int64_t)t * NN + i] = (float)best;
+        // write-through (agent-scope) stores: the fused finalize's last block reads them back without
+        // an acq_rel arrival, which would write back every arriving block's L2
+        auto wt = [](auto* ptr, auto v) { __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        wt(st + i, (int8_t)1);
+        wt(feat + (int64_t)t * NN + i, (int16_t)bf);
+        wt(sbin + (int64_t)t * NN + i, (uint8_t)bb);
+        wt(gain + (int64_t)t * NN + i, (float)best);
         const int l = 2 * i + 1, r = 2 * i + 2;
-        st[l] = 2;
-        st[r] = 2;
-        G[(int64_t)t * NN + l] = val(bGL);
-        H[(int64_t)t * NN + l] = val(bHL);
-        G[(int64_t)t * NN + r] = val(Gna - bGL);
-        H[(int64_t)t * NN + r] = val(Hna - bHL);
+        wt(st + l, (int8_t)2);
+        wt(st + r, (int8_t)2);
+        wt(G + (int64_t)t * NN + l, val(bGL));
+        wt(H + (int64_t)t * NN + l, val(bHL));
+        wt(G + (int64_t)t * NN + r, val(Gna - bGL));
+        wt(H + (int64_t)t * NN + r, val(Hna - bHL));
       }
     }
   }
   GSTAMP(16 * level + 4);
   if (!fin.tctr) return;
   __shared__ int last;
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(fin.tctr + t, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nodesL - 1;
+  if (threadIdx.x == 0) {  // (this block's write-through stores have completed before its arrival)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(fin.tctr + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nodesL - 1;
+  }
   __syncthreads();
   if (!last) return;  // block-uniform
   // the task's tree staged in LDS (after the fold area), pruned by one thread, leaves by all
@@ -868,12 +873,12 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
   int16_t* sfe = reinterpret_cast<int16_t*>(sgn + NN);
   int8_t* sst = reinterpret_cast<int8_t*>(sfe + NN);
   const int64_t o = (int64_t)t * NN;
-  for (int k = threadIdx.x; k < NN; k += blockDim.x) {
-    sst[k] = st[k];
-    sfe[k] = feat[o + k];
-    sgn[k] = gain[o + k];
-    sG[k] = G[o + k];
-    sH[k] = H[o + k];
+  for (int k = threadIdx.x; k < NN; k += blockDim.x) {  // (agent-scope loads: the siblings' stores)
+    sst[k] = __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sfe[k] = __hip_atomic_load(feat + o + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sgn[k] = __hip_atomic_load(gain + o + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sG[k] = __hip_atomic_load(G + o + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sH[k] = __hip_atomic_load(H + o + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
