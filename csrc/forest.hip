@@ -781,6 +781,23 @@ __global__ void __launch_bounds__(128) rf_split(RfParams p, int level, uint32_t*
   }
   if (bf < 0 || !child_acc) return;
   const uint32_t sr = A[68 + kp + bc * 64 + lane], nr = A[68 + bc];
+  if (level + 1 == p.max_depth) {
+    // the children are leaves of the last level: their outputs straight from the derived totals (what
+    // rf_split of that level would compute from the records written below), so the fused driver needs
+    // no last partition, level start or split
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      const uint32_t cs = sd ? sr : A[lane] - sr, cn = sd ? nr : n - nr;
+      const int64_t c = (int64_t)t * p.nodes + 2 * node + 1 + sd;
+      p.value[c * 64 + lane] = (cn > 0 && lane < 62) ? (float)((double)cs / (double)cn) : 0.f;
+      if (lane == 0) {
+        p.cover[c] = (float)cn;
+        p.feat[c] = -1;
+        p.gain[c] = 0.0;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int sd = 0; sd < 2; ++sd) {  // sd 0: x_f = 0 child (2 node + 1), 1: x_f = 1 child
     uint32_t* dst = child_acc + ((int64_t)t * (2 * nodesL) + 2 * nd + sd) * rec;
@@ -1116,14 +1133,11 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
       int16_t* cn = level + 1 < max_depth ? cands[(level + 1) & 1] : nullptr;
       hipLaunchKernelGGL(rf_split, dim3(nodesL, T), dim3(cn ? 128 : 64), 0, stream, p, level, an, cn);
       EM_CHECK_LAUNCH();
-      if (level == max_depth) break;
-      if (level + 1 < max_depth)
-        hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), (size_t)2 * rf_chl_words(k_feat) * 4, stream,
-                           p, (const void*)rin, rout,
-                           level, (const int32_t*)wl, an, (const int16_t*)cn);
-      else
-        hipLaunchKernelGGL((rf_partition<true, false>), dim3(G), dim3(nt), 0, stream, p, (const void*)rin, rout, level,
-                           (const int32_t*)wl, (uint32_t*)nullptr, (const int16_t*)nullptr);
+      // rf_split of the level before the last wrote the last level's leaves (their rows are never read)
+      if (level + 1 >= max_depth) break;
+      hipLaunchKernelGGL((rf_partition<true, true>), dim3(G), dim3(nt), (size_t)2 * rf_chl_words(k_feat) * 4, stream,
+                         p, (const void*)rin, rout,
+                         level, (const int32_t*)wl, an, (const int16_t*)cn);
       EM_CHECK_LAUNCH();
       void* tmp = rin;
       rin = rout;
