@@ -39,14 +39,16 @@ __host__ __device__ inline uint64_t mix64(uint64_t x) {
 __host__ __device__ inline uint64_t hash3(uint64_t seed, uint64_t a, uint64_t b) { return mix64(mix64(seed ^ mix64(a)) ^ b); }
 
 // Poisson(1) inverse CDF on a 53-bit uniform (literals shared with models/forest.py)
+// u = m * 2^-53 with m = h >> 11 < 2^53, so u >= cdf[k] <=> m >= cdf[k] * 2^53, an exact integer for
+// every cdf[k] below: the same weights from 9 integer compares (no fp64 conversion or compares)
 __device__ inline int poisson1(uint64_t h) {
-  const double u = (double)(h >> 11) * 0x1.0p-53;
-  const double cdf[9] = {0.36787944117144233, 0.7357588823428847, 0.9196986029286058, 0.9810118431238463,
-                         0.9963401531726563, 0.9994058151824183, 0.999916758850712, 0.9999897508033253,
-                         0.999998874797402};
+  const uint64_t m = h >> 11;
+  const uint64_t th[9] = {0xbc5ab1b16779cull,  0x178b56362cef38ull, 0x1d6e2bc3b82b06ull,
+                          0x1f6472f2e6944bull, 0x1fe204beb22e9cull, 0x1ffb21e77480acull,
+                          0x1fff516e3f8e59ull, 0x1fffea81812296ull, 0x1ffffda3e9551eull};
   int w = 0;
 #pragma unroll
-  for (int k = 0; k < 9; ++k) w += u >= cdf[k] ? 1 : 0;
+  for (int k = 0; k < 9; ++k) w += m >= th[k] ? 1 : 0;
   return w;
 }
 
@@ -93,6 +95,7 @@ struct RfParams {
   int16_t* cand;  // [T][2^max_depth][k] candidate features of the current level's nodes
   uint32_t* acc;  // [T][2^max_depth][rec] per-node integer sums of the current level (see rec_words)
   int32_t* lrc;   // [T][2^max_depth][2] partition counters (left, right) of the current level
+  const int32_t* yover;  // fused driver: 0 = every row has <= 7 outputs (position-form records), else 1
 };
 
 // per-node record of integer sums: S[64] (sum of w*y_j), n (sum of w), 3 pad, cnt[kp] (sum of w*x_f
@@ -147,6 +150,55 @@ EM_DEVICE void rf_add_ybits(uint32_t* __restrict__ row, const RfYBits& b, uint32
   for (int q = 0; q < 8; ++q) atomicAdd(&row[b.j[q] & 63], b.j[q] >= 0 ? w : 0u);
   for (uint64_t r = b.rest; r; r &= r - 1) atomicAdd(&row[__builtin_ctzll(r)], w);
 }
+
+// Position-form records (the fused driver, when no row has more than 7 outputs -- a draw has 5 + 2):
+// the y word holds the row's output positions instead of its output mask, extracted once by
+// rf_init_rows -- p0..p4 in bits 0..29, p5, p6 in bits 32..43 (6 bits each, absent = 63: the pad
+// word), w_lo in bits 62..63 as before.  Every level's histogram then reads the positions with 7 bit-field
+// extracts instead of re-extracting them from the mask (~11 VALU per output per row per level: the
+// partition was VALU-issue bound).  rf_ycheck decides the form on the device (no host sync).
+constexpr int RF_NPOS = 7;
+struct RfPos {
+  uint32_t o[RF_NPOS];  // output positions (63 = none)
+};
+EM_DEVICE RfPos rf_pos_extract(uint64_t y) {  // y: the output mask (bits 0..61)
+  RfPos p;
+  uint64_t yy = y | (1ull << 63);  // sentinel: an exhausted mask yields 63
+#pragma unroll
+  for (int q = 0; q < RF_NPOS; ++q) {
+    p.o[q] = (uint32_t)__builtin_ctzll(yy);
+    yy = (yy & (yy - 1)) | (1ull << 63);
+  }
+  return p;
+}
+EM_DEVICE uint64_t rf_pos_pack(const RfPos& p) {
+  const uint32_t lo = p.o[0] | p.o[1] << 6 | p.o[2] << 12 | p.o[3] << 18 | p.o[4] << 24;
+  const uint32_t hi = p.o[5] | p.o[6] << 6;
+  return (uint64_t)lo | (uint64_t)hi << 32;
+}
+EM_DEVICE RfPos rf_pos_unpack(uint64_t yw) {
+  const uint32_t lo = (uint32_t)yw, hi = (uint32_t)(yw >> 32);
+  RfPos p;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) p.o[q] = (lo >> (6 * q)) & 63u;
+  p.o[5] = hi & 63u;
+  p.o[6] = (hi >> 6) & 63u;
+  return p;
+}
+// a candidate bit's histogram row: the 7 outputs + the row count as output word 62 (RF_CNT62 layout)
+EM_DEVICE void rf_add_pos(uint32_t* __restrict__ row, const RfPos& p, uint32_t w) {
+#pragma unroll
+  for (int q = 0; q < RF_NPOS; ++q) atomicAdd(&row[p.o[q]], w);
+  atomicAdd(&row[62], w);
+}
+static_assert(RF_YBITS && RF_CNT62, "position-form records assume the count-as-word-62 layout");
+
+__global__ void __launch_bounds__(256) rf_ycheck(const uint64_t* __restrict__ Y, int64_t N, int32_t* __restrict__ over) {
+  int o = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x)
+    o |= __builtin_popcountll(Y[i] & RF_M62) > RF_NPOS ? 1 : 0;
+  if (__ballot(o) && (threadIdx.x & 63) == 0) atomicOr(over, 1);
+}
 // Root row lists: rows with non-zero bootstrap weight, compacted per tree by (blocks x tree)
 // workgroups; each 256-row chunk reserves its output range with one atomic (row order inside a list
 // is irrelevant: every sum is an exact integer).  Root count -> lrc[t][0][0].
@@ -169,6 +221,7 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
   __shared__ uint64_t rmask;
   __shared__ int16_t rco[RF_MAXF];
   const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
+  const bool pos = ROOTH && p.yover && *p.yover == 0;
   uint32_t my_n = 0;
   if constexpr (ROOTH) {
     for (int i = threadIdx.x; i < rec; i += blockDim.x) rlds[i] = 0u;
@@ -220,9 +273,21 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
         const int64_t r = c + k * RF_NT + threadIdx.x;
         if constexpr (REC) {
           const uint64_t xv = p.X[r], yv = p.Y[r];
-          outr[o + pre[k]] = rf_make_rec(xv, yv, (uint32_t)w[k]);
-          if constexpr (ROOTH) {
-            const uint32_t wk = (uint32_t)w[k];
+          const uint32_t wk = (uint32_t)w[k];
+          if (ROOTH && pos) {  // position form: the outputs extracted once, for the record and the root sums
+            const RfPos ps = rf_pos_extract(yv & RF_M62);
+            RfRec e = rf_make_rec(xv, 0ull, wk);
+            e.y |= rf_pos_pack(ps);
+            outr[o + pre[k]] = e;
+            my_n += wk;
+#pragma unroll
+            for (int q = 0; q < RF_NPOS; ++q) atomicAdd(&rlds[ps.o[q]], wk);  // S (none: pad word 63)
+            for (uint64_t xx = xv & RF_M62 & rmask; xx; xx &= xx - 1)
+              rf_add_pos(rlds + 68 + kp + rslot[__builtin_ctzll(xx)] * 64, ps, wk);
+          } else {
+            outr[o + pre[k]] = rf_make_rec(xv, yv, wk);
+          }
+          if (ROOTH && !pos) {
             const uint64_t y = yv & RF_M62;
             my_n += wk;
             for (uint64_t yy = y; yy; yy &= yy - 1) atomicAdd(&rlds[__builtin_ctzll(yy)], wk);
@@ -250,7 +315,7 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
     uint32_t* dst = p.acc + (int64_t)t * rec;  // the root record of tree t (zeroed by the driver)
     for (int i = threadIdx.x; i < rec; i += blockDim.x) {
       uint32_t v;
-      if (i < 68) v = rlds[i];
+      if (i < 68) v = (i & ~1) == 62 ? 0u : rlds[i];  // (S words 62 / 63: pads)
       else if (i < 68 + kp) v = i - 68 < k ? rlds[68 + kp + (i - 68) * 64 + 62] : 0u;
       else v = ((i - 68 - kp) & 63) < 62 ? rlds[i] : 0u;
       if (v) atomicAdd(&dst[i], v);
@@ -838,6 +903,7 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
   const int kf = p.k_feat, rec = rec_words(kf), kp = (kf + 3) & ~3;
   const int chw = rf_chl_words(kf), cst = rf_rep_cnt_stride(kf), hst = rf_rep_hist_stride(kf);
   const int lane_c = (threadIdx.x & 63) % RF_REP_CNT, lane_h = (threadIdx.x & 63) % RF_REP_HIST;
+  const bool pos = HIST && REC && p.yover && *p.yover == 0;
   if (HIST) {
     for (int i = threadIdx.x; i < 2 * chw; i += blockDim.x) chl[i] = 0u;
     if (threadIdx.x < 2) {
@@ -924,6 +990,13 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
         uint64_t xx = r[k2].x & RF_M62 & cmk[sd];
         uint32_t* cnt = chl + sd * chw + lane_c * cst;
         uint32_t* hist = chl + sd * chw + RF_REP_CNT * cst + lane_h * hst;
+        if (pos) {  // position-form record: the outputs are 7 bit fields
+          if (xx) {
+            const RfPos ps = rf_pos_unpack(r[k2].y);
+            for (; xx; xx &= xx - 1) rf_add_pos(hist + cslot[sd][__builtin_ctzll(xx)] * 64, ps, w);
+          }
+          continue;
+        }
         if (RF_YBITS && xx) {
           const RfYBits yb = rf_ybits(RF_CNT62 ? (y | (1ull << 62)) : y);
           while (xx) {
@@ -1035,7 +1108,8 @@ EM_API int64_t em_rf_acc_words(int T, int max_depth, int k_feat) {
   if (T < 1 || max_depth < 0 || max_depth > 14 || k_feat < 1 || k_feat > RF_MAXF) return -1;
   // two levels' records (rf_child_totals) + a second candidate buffer (the fused partition fills the
   // next level's candidates while the current level's are still in use)
-  return 2 * (int64_t)T * (1ll << max_depth) * rec_words(k_feat) + ((int64_t)T * (1ll << max_depth) * k_feat + 1) / 2;
+  // (+1: the fused driver's rf_ycheck flag, the last word)
+  return 2 * (int64_t)T * (1ll << max_depth) * rec_words(k_feat) + ((int64_t)T * (1ll << max_depth) * k_feat + 1) / 2 + 1;
 }
 
 // Native level-wise driver: all T trees advance one level per (prep, hist, split, partition) round.
@@ -1090,14 +1164,18 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const bool derive = derive_env && !use_mfma;
   // (the fused partition's replicated child images must fit the LDS: k <= ~70 candidates)
   const bool fuse = derive && fuse_env && rec_rows && (size_t)2 * rf_chl_words(k_feat) * 4 <= 160 * 1024 - 8192;
+  int32_t* yover = reinterpret_cast<int32_t*>(acc) + em_rf_acc_words(T, max_depth, k_feat) - 1;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
-             cover, cand, accs[0], lrc};
+             cover, cand, accs[0], lrc, fuse ? yover : nullptr};
   (void)hipMemsetAsync(lrc, 0, (size_t)T * 2 * sizeof(int32_t), stream);
   {
     int B, nt;
     rf_shape(N, 0, B, nt);
     if (fuse) {  // the root records are accumulated by the listing pass
       (void)hipMemsetAsync(accs[0], 0, (size_t)T * rec * sizeof(uint32_t), stream);
+      (void)hipMemsetAsync(yover, 0, sizeof(int32_t), stream);  // record form decided on the device
+      const int64_t yb = (N + 255) / 256;
+      hipLaunchKernelGGL(rf_ycheck, dim3((unsigned)(yb < 1024 ? yb : 1024)), dim3(256), 0, stream, Y, N, yover);
       static bool ra = false;
       if (!ra) {
         (void)hipFuncSetAttribute((const void*)rf_init_rows<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -180,3 +180,32 @@ def test_hip_forest_mfma_histogram_matches_oracle():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, EM_RF_MFMA="1", PYTHONPATH=root),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "MFMA_RF_OK" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ymax", [7, 30])
+def test_hip_forest_record_forms_match_oracle(ymax):
+    """Rows with 0..7 outputs (absent positions included) take the position-form records, any row with
+    more the mask form (rf_ycheck decides on the device): both equal the oracle."""
+    rng = np.random.default_rng(ymax)
+    n = 3000
+    X = np.zeros(n, dtype=np.uint64)
+    Y = np.zeros(n, dtype=np.uint64)
+    for i in range(n):
+        for b in rng.choice(62, size=int(rng.integers(0, 12)), replace=False):
+            X[i] |= np.uint64(1) << np.uint64(b)
+        for b in rng.choice(62, size=int(rng.integers(0, ymax)), replace=False):
+            Y[i] |= np.uint64(1) << np.uint64(b)
+        if i % 3 == 0:  # a learnable output
+            Y[i] |= (X[i] & np.uint64(1)) << np.uint64(5)
+    for depth, subset, boot in ((6, "sqrt", True), (4, "all", False)):
+        g = RandomForest(n_trees=12, max_depth=depth, feature_subset=subset, bootstrap=boot, seed=7, device="cuda")
+        g.fit(X.reshape(-1, 1), Y, 62)
+        assert g.backend_used == "hip"
+        c = RandomForest(n_trees=12, max_depth=depth, feature_subset=subset, bootstrap=boot, seed=7, device="cpu")
+        c.fit(X.reshape(-1, 1), Y, 62)
+        assert np.array_equal(g.feat, c.feat)
+        live = g.feat > -2
+        assert np.array_equal(g.value[live], c.value[live])
+        assert np.array_equal(g.gain, c.gain)
+        assert np.array_equal(g.cover[live], c.cover[live])
