@@ -206,12 +206,15 @@ __global__ void __launch_bounds__(256) rf_ycheck(const uint64_t* __restrict__ Y,
 // accumulated while the rows are listed -- the root histogram pass re-read every record (700 MB at
 // 700 k rows x 100 trees) -- in an LDS image per block, added to the zeroed root record at the end.
 EM_DEVICE void rf_node_cands_wave(const RfParams& p, int t, int node, int16_t* __restrict__ co);
+#ifndef RF_INIT_RR
+#define RF_INIT_RR 4
+#endif
 template <bool REC, bool ROOTH = false>
 __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restrict__ rows_v) {
   // chunks of RR x RF_NT rows: every thread hashes RR rows (all hashes / loads in flight), one count
   // exchange and one atomic reservation per chunk; the count arrays are double-buffered, so a chunk
   // costs two barriers (was three per RF_NT rows)
-  constexpr int RR = 4;
+  constexpr int RR = RF_INIT_RR;
   const int t = blockIdx.y, B = gridDim.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ int wcnt[2][RR][4];
@@ -880,6 +883,9 @@ __global__ void __launch_bounds__(128) rf_split(RfParams p, int level, uint32_t*
 // HIST (record rows, derived node totals): while a record moves to its child, its candidate bits are
 // also added to that child's histogram (cnt / hist words of the child's record in acc_next, LDS partials
 // merged by integer atomics), so level + 1 needs no histogram pass over its rows.
+#ifndef RF_PART_RR
+#define RF_PART_RR 4
+#endif
 template <bool REC, bool HIST>
 __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __restrict__ rin_v,
                                                       void* __restrict__ rout_v, int level,
@@ -919,10 +925,10 @@ __global__ void __launch_bounds__(RF_NT) rf_partition(RfParams p, const void* __
     }
     __syncthreads();
   }
-  // chunks of 4 x blockDim rows: 4 ballots per wave (row k of the thread = c + k*blockDim + tid), one
+  // chunks of RR x blockDim rows: RR ballots per wave (row k of the thread = c + k*blockDim + tid), one
   // LDS count exchange and one atomic reservation per side per chunk (instead of per blockDim rows);
   // the small count arrays are double-buffered so a chunk needs two barriers
-  constexpr int RR = 4;
+  constexpr int RR = RF_PART_RR;
   __shared__ int lc[2][RR][4], rc[2][RR][4];
   __shared__ int lbase[2], rbase[2];
   int32_t* ctr = p.lrc + ((int64_t)t * nodesL + nd) * 2;
