@@ -209,6 +209,21 @@ EM_DEVICE void rf_node_cands_wave(const RfParams& p, int t, int node, int16_t* _
 #ifndef RF_INIT_RR
 #define RF_INIT_RR 4
 #endif
+// RF_INIT_REP: the position-form root sums go to lane-replicated LDS images (S by lane & 15, the
+// candidate histograms by lane & 3) summed at the merge: a wave's q-th smallest outputs crowd a few
+// words (the smallest drawn number), and same-word atomics serialise
+#ifndef RF_INIT_REP
+#define RF_INIT_REP 1
+#endif
+#ifndef RF_IREP_S
+#define RF_IREP_S 16
+#endif
+#ifndef RF_IREP_H
+#define RF_IREP_H 4
+#endif
+__host__ __device__ inline int rf_init_lds_words(int k) {
+  return ((rec_words(k) + 3) & ~3) + (RF_INIT_REP ? RF_IREP_S * 64 + RF_IREP_H * rf_rep_hist_stride(k) : 0);
+}
 template <bool REC, bool ROOTH = false>
 __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restrict__ rows_v) {
   // chunks of RR x RF_NT rows: every thread hashes RR rows (all hashes / loads in flight), one count
@@ -226,8 +241,11 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
   const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
   const bool pos = ROOTH && p.yover && *p.yover == 0;
   uint32_t my_n = 0;
+  uint32_t* Sr = rlds + ((rec + 3) & ~3);  // RF_INIT_REP images: S [16][64], candidate hist [4][hst]
+  uint32_t* Hr = Sr + RF_IREP_S * 64;
+  const int hst = rf_rep_hist_stride(k);
   if constexpr (ROOTH) {
-    for (int i = threadIdx.x; i < rec; i += blockDim.x) rlds[i] = 0u;
+    for (int i = threadIdx.x; i < rf_init_lds_words(k); i += blockDim.x) rlds[i] = 0u;
     if (threadIdx.x < 64) rslot[threadIdx.x] = -1;
     if (wv == 0) rf_node_cands_wave(p, t, 0, rco);
     __syncthreads();
@@ -283,10 +301,12 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
             e.y |= rf_pos_pack(ps);
             outr[o + pre[k]] = e;
             my_n += wk;
+            uint32_t* srow = RF_INIT_REP ? Sr + (lane & (RF_IREP_S - 1)) * 64 : rlds;
+            uint32_t* hrow = RF_INIT_REP ? Hr + (lane & (RF_IREP_H - 1)) * hst : rlds + 68 + kp;
 #pragma unroll
-            for (int q = 0; q < RF_NPOS; ++q) atomicAdd(&rlds[ps.o[q]], wk);  // S (none: pad word 63)
+            for (int q = 0; q < RF_NPOS; ++q) atomicAdd(&srow[ps.o[q]], wk);  // S (none: pad word 63)
             for (uint64_t xx = xv & RF_M62 & rmask; xx; xx &= xx - 1)
-              rf_add_pos(rlds + 68 + kp + rslot[__builtin_ctzll(xx)] * 64, ps, wk);
+              rf_add_pos(hrow + rslot[__builtin_ctzll(xx)] * 64, ps, wk);
           } else {
             outr[o + pre[k]] = rf_make_rec(xv, yv, wk);
           }
@@ -317,8 +337,19 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
     __syncthreads();
     uint32_t* dst = p.acc + (int64_t)t * rec;  // the root record of tree t (zeroed by the driver)
     for (int i = threadIdx.x; i < rec; i += blockDim.x) {
-      uint32_t v;
-      if (i < 68) v = (i & ~1) == 62 ? 0u : rlds[i];  // (S words 62 / 63: pads)
+      uint32_t v = 0;
+      if (RF_INIT_REP && pos) {  // sum the replicas
+        if (i < 62) {
+          for (int q = 0; q < RF_IREP_S; ++q) v += Sr[q * 64 + i];
+        } else if (i == 64) {
+          v = rlds[64];
+        } else if (i >= 68 && i < 68 + kp) {
+          if (i - 68 < k)
+            for (int q = 0; q < RF_IREP_H; ++q) v += Hr[q * hst + (i - 68) * 64 + 62];
+        } else if (i >= 68 + kp && ((i - 68 - kp) & 63) < 62) {
+          for (int q = 0; q < RF_IREP_H; ++q) v += Hr[q * hst + (i - 68 - kp)];
+        }
+      } else if (i < 68) v = (i & ~1) == 62 ? 0u : rlds[i];  // (S words 62 / 63: pads)
       else if (i < 68 + kp) v = i - 68 < k ? rlds[68 + kp + (i - 68) * 64 + 62] : 0u;
       else v = ((i - 68 - kp) & 63) < 62 ? rlds[i] : 0u;
       if (v) atomicAdd(&dst[i], v);
@@ -1169,7 +1200,8 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   int16_t* cands[2] = {cand, reinterpret_cast<int16_t*>(acc + 2 * (int64_t)T * (1ll << max_depth) * rec)};
   const bool derive = derive_env && !use_mfma;
   // (the fused partition's replicated child images must fit the LDS: k <= ~70 candidates)
-  const bool fuse = derive && fuse_env && rec_rows && (size_t)2 * rf_chl_words(k_feat) * 4 <= 160 * 1024 - 8192;
+  const bool fuse = derive && fuse_env && rec_rows && (size_t)2 * rf_chl_words(k_feat) * 4 <= 160 * 1024 - 8192 &&
+                    (size_t)rf_init_lds_words(k_feat) * 4 <= 160 * 1024 - 8192;
   int32_t* yover = reinterpret_cast<int32_t*>(acc) + em_rf_acc_words(T, max_depth, k_feat) - 1;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
              cover, cand, accs[0], lrc, fuse ? yover : nullptr};
@@ -1188,7 +1220,8 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
                                   160 * 1024 - 8192);
         ra = true;
       }
-      hipLaunchKernelGGL((rf_init_rows<true, true>), dim3(B, T), dim3(RF_NT), lds, stream, p, (void*)rows_a);
+      hipLaunchKernelGGL((rf_init_rows<true, true>), dim3(B, T), dim3(RF_NT), (size_t)rf_init_lds_words(k_feat) * 4,
+                         stream, p, (void*)rows_a);
     } else if (rec_rows)
       hipLaunchKernelGGL(rf_init_rows<true>, dim3(B, T), dim3(RF_NT), 0, stream, p, (void*)rows_a);
     else
