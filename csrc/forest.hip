@@ -439,6 +439,16 @@ __global__ void rf_level_prep(RfParams p, int level) {
 // blocks (exclusive prefix in wl[]); the level kernels run a 1-D grid and map block g to its
 // (tree, node, slice) by binary search.
 constexpr int RF_CHUNK = 8192;
+// the root level's nodes hold every kept row of their tree: their partition blocks all merge into the
+// same two child records with global atomics, so fewer, longer blocks there (RF_CHUNK0 rows)
+#ifndef RF_CHUNK0
+#define RF_CHUNK0 32768
+#endif
+#ifndef RF_CHUNK1
+#define RF_CHUNK1 8192
+#endif
+static_assert(RF_CHUNK0 >= RF_CHUNK && RF_CHUNK1 >= RF_CHUNK, "the launch bound assumes RF_CHUNK is the smallest");
+__host__ __device__ inline int rf_chunk(int level) { return level == 0 ? RF_CHUNK0 : (level == 1 ? RF_CHUNK1 : RF_CHUNK); }
 struct RfWork {
   int t, nd, j, nb;
 };
@@ -462,7 +472,7 @@ __global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32
   auto blocks = [&](int i) {
     const int t = i / nodesL, nd = i - t * nodesL;
     const int cnt = p.seg[((int64_t)t * p.nodes + first + nd) * 2 + 1];
-    return cnt < 0 ? 0 : max(1, (cnt + RF_CHUNK - 1) / RF_CHUNK);
+    return cnt < 0 ? 0 : max(1, (cnt + rf_chunk(level) - 1) / rf_chunk(level));
   };
   int sum = 0;
   for (int i = a; i < b; ++i) sum += blocks(i);
@@ -540,7 +550,7 @@ __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, in
   auto blocks = [&](int i) {
     const int t = i / nodesL, nd = i - t * nodesL;
     const int cnt = p.seg[((int64_t)t * p.nodes + first + nd) * 2 + 1];
-    return cnt < 0 ? 0 : max(1, (cnt + RF_CHUNK - 1) / RF_CHUNK);
+    return cnt < 0 ? 0 : max(1, (cnt + rf_chunk(level) - 1) / rf_chunk(level));
   };
   int sum = 0;
   for (int i = a; i < b; ++i) sum += blocks(i);
@@ -903,7 +913,7 @@ __global__ void __launch_bounds__(128) rf_split(RfParams p, int level, uint32_t*
     dst[lane] = sd ? sr : A[lane] - sr;
     // words 68.. are the partition's: it stores them when one block owns this node (rf_worklist:
     // ceil(count / RF_CHUNK) blocks) and adds into zeroed words otherwise
-    const int hi = (sg[1] + RF_CHUNK - 1) / RF_CHUNK > 1 ? rec : 68;
+    const int hi = (sg[1] + rf_chunk(level) - 1) / rf_chunk(level) > 1 ? rec : 68;
     for (int i = 64 + lane; i < hi; i += 64) dst[i] = i == 64 ? (sd ? nr : n - nr) : 0u;
   }
 }
