@@ -496,9 +496,15 @@ __global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32
 // root only: deeper levels' are drawn by the parent's rf_split), then -- after every segment is
 // written and every parent counter read -- this level's partition counters zeroed (and, at the root,
 // the root records), then rf_worklist's scan.  Replaces 2 kernels and 1-2 memsets per level.
+// partition blocks of a node with `count` rows at `level` (rf_worklist's rule)
+EM_DEVICE int rf_blocks(int count, int level) {
+  return count < 0 ? 0 : max(1, (count + rf_chunk(level) - 1) / rf_chunk(level));
+}
+constexpr int RF_BEGIN_LDS = 16384;  // rf_level_begin keeps per-node block counts in LDS up to this many nodes
 __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, int32_t* __restrict__ wl,
                                                        int zero_root) {
   const int nodesL = 1 << level, first = nodesL - 1, n = p.T * nodesL;
+  __shared__ uint16_t nblk[RF_BEGIN_LDS];
   // items in batches of 8 per thread: the batch's parent loads are all issued before its stores
   constexpr int PB = 8;
   for (int g0 = 0; g0 < n; g0 += PB * 1024) {
@@ -538,6 +544,7 @@ __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, in
       int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
       sg[0] = start;
       sg[1] = count;
+      if (gid < RF_BEGIN_LDS) nblk[gid] = (uint16_t)rf_blocks(count, level);
       if (level == 0 && count >= 0 && p.max_depth > 0) rf_node_cands(p, t, node, p.cand + (int64_t)t * p.k_feat);
     }
   }
@@ -547,10 +554,10 @@ __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, in
     for (int i = threadIdx.x; i < n * rec_words(p.k_feat); i += 1024) p.acc[i] = 0u;
   __shared__ int part[1024];
   const int per = (n + 1023) / 1024, a = threadIdx.x * per, b = min(n, a + per);
-  auto blocks = [&](int i) {
+  auto blocks = [&](int i) {  // (counts from LDS: each global re-read costs ~1 us, in series per thread)
+    if (n <= RF_BEGIN_LDS) return (int)nblk[i];
     const int t = i / nodesL, nd = i - t * nodesL;
-    const int cnt = p.seg[((int64_t)t * p.nodes + first + nd) * 2 + 1];
-    return cnt < 0 ? 0 : max(1, (cnt + rf_chunk(level) - 1) / rf_chunk(level));
+    return rf_blocks(p.seg[((int64_t)t * p.nodes + first + nd) * 2 + 1], level);
   };
   int sum = 0;
   for (int i = a; i < b; ++i) sum += blocks(i);
