@@ -249,6 +249,8 @@ __global__ void __launch_bounds__(RF_NT) rf_init_rows(RfParams p, void* __restri
     if (threadIdx.x < 64) rslot[threadIdx.x] = -1;
     if (wv == 0) rf_node_cands_wave(p, t, 0, rco);
     __syncthreads();
+    if (blockIdx.x == 0 && p.max_depth > 0)  // the root's candidates for rf_split (rf_level_begin draws none)
+      for (int i = threadIdx.x; i < (k < p.F ? k : p.F); i += blockDim.x) p.cand[(int64_t)t * k + i] = rco[i];
     if (threadIdx.x == 0) {
       uint64_t m = 0;
       const int kk = k < p.F ? k : p.F;
@@ -492,15 +494,15 @@ __global__ void __launch_bounds__(1024) rf_worklist(RfParams p, int level, int32
   if (threadIdx.x == 1023) wl[n] = part[1023];
 }
 
-// The fused driver's level start in ONE workgroup: rf_level_prep (child segments; candidates at the
-// root only: deeper levels' are drawn by the parent's rf_split), then -- after every segment is
-// written and every parent counter read -- this level's partition counters zeroed (and, at the root,
-// the root records), then rf_worklist's scan.  Replaces 2 kernels and 1-2 memsets per level.
 // partition blocks of a node with `count` rows at `level` (rf_worklist's rule)
 EM_DEVICE int rf_blocks(int count, int level) {
   return count < 0 ? 0 : max(1, (count + rf_chunk(level) - 1) / rf_chunk(level));
 }
 constexpr int RF_BEGIN_LDS = 16384;  // rf_level_begin keeps per-node block counts in LDS up to this many nodes
+// The fused driver's level start in ONE workgroup: rf_level_prep's child segments (no candidates:
+// the root's come with rf_init_rows, deeper levels' from the parent's rf_split), then -- after every
+// segment is written and every parent counter read -- this level's partition counters zeroed (and, at
+// the root, the root records), then rf_worklist's scan.  Replaces 2 kernels and 1-2 memsets per level.
 __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, int32_t* __restrict__ wl,
                                                        int zero_root) {
   const int nodesL = 1 << level, first = nodesL - 1, n = p.T * nodesL;
@@ -545,7 +547,6 @@ __global__ void __launch_bounds__(1024) rf_level_begin(RfParams p, int level, in
       sg[0] = start;
       sg[1] = count;
       if (gid < RF_BEGIN_LDS) nblk[gid] = (uint16_t)rf_blocks(count, level);
-      if (level == 0 && count >= 0 && p.max_depth > 0) rf_node_cands(p, t, node, p.cand + (int64_t)t * p.k_feat);
     }
   }
   __syncthreads();  // segments written, the parents' counters read
