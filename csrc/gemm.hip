@@ -1172,6 +1172,18 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  // the dgrad's ReLU activity words are loaded before the operands: with K = 64 the MFMA phase is one
+  // K tile, and loaded at the epilogue their round trip sat between the MFMAs and the stores (dgrad
+  // 615 -> 559 us on the wide MLP; the CROW = 0 form has no registers left for them and loads late)
+  uint32_t bw[2][2] = {{0u, 0u}, {0u, 0u}};  // ReLU activity words [32-row block i][column half j] (g_epilogue)
+  auto load_bits = [&]() {
+    const int rb = m0 + wm * 64, cw = n0 + wn * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bw[i][j] = bits[(int64_t)((rb >> 5) + i) * N + cw + 32 * j + r];
+  };
+  if (DACT && CROW && bits) load_bits();
   for (int k0 = 0; k0 < K; k0 += 64) {
     u32x4 rs[4];  // one staging set for both operands (keeps the kernel at <= 128 VGPRs, 4 blocks / CU)
     if (k0) __syncthreads();  // the previous K tile's fragments are read
@@ -1199,13 +1211,8 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   const int rowb = m0 + wm * 64, colw = n0 + wn * 64;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, gq = lane >> 4;
   constexpr bool WBITS = !DACT && FN == ACT_RELU;
-  uint32_t bw[2][2] = {{0u, 0u}, {0u, 0u}};  // ReLU activity words [32-row block i][column half j] (g_epilogue)
-  if (DACT && bits) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bw[i][j] = bits[(int64_t)((rowb >> 5) + i) * N + colw + 32 * j + r];
-  } else if (DACT) {
+  if (DACT && !CROW && bits) load_bits();
+  if (DACT && !bits) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // 512 chunks of 16 B: rows q >> 3, chunk q & 7
       const int q = lane + 64 * t, row = q >> 3, ch = q & 7;
