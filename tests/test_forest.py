@@ -94,7 +94,8 @@ def test_tree_ids_make_shards_compose(draws):
 # histogram kernel must reproduce the oracle exactly (test_hip_forest_mfma_histogram_matches_oracle
 # runs the matrix-core one)
 @pytest.mark.parametrize("depth,subset,boot,lags", [(5, "sqrt", True, 1), (3, "all", False, 1), (6, "0.3", True, 2),
-                                                   (7, "log2", False, 1), (8, "sqrt", True, 1)])
+                                                   (7, "log2", False, 1), (8, "sqrt", True, 1), (0, "sqrt", True, 1),
+                                                   (1, "sqrt", True, 1), (2, "log2", False, 1)])
 def test_hip_forest_matches_oracle(depth, subset, boot, lags):
     ds = DrawSet.synthetic(n=3000, seed=2, planted=0.7, calendar=False)
     X, Y, F = draw_features(ds.numbers, lags)
