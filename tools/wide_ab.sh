@@ -1,5 +1,8 @@
+#!/bin/bash
+# Same-box A/B of the wide-MLP step: the shipped library vs lib/ab/gemm_head.so (tools/build_variant.sh with
+# FILE=csrc/gemm.hip SRC=<old gemm.hip>), GEMM GPU tests first, then two alternating rounds and a kernel trace each.
 set -o pipefail
-cd /root/repo
+cd "$(dirname "$0")/.."
 O=gpurun_out/wab; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -20 $O/pytest.log; exit 3; }
 tail -1 $O/pytest.log
