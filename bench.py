@@ -435,10 +435,11 @@ def main():
             "vs_baseline": None,
             "dtype": a.dtype,
             "data": ("synthetic, generated on the GPU: one seeded Euromillions draw sequence of %d draws "
-                     "(%d per GPU%s), planted Markov p=%.2f, shared by all ranks; positional 70/30 split, "
-                     "contiguous shard per rank; random-init weights"
-                     % (sh.n_draws, n_loc, ", %.1f GiB HBM-resident" % a.device_data_gb if a.device_data_gb > 0
-                        else "", a.planted)),
+                     "(%d per GPU: %.1f GiB logical%s), planted Markov p=%.2f, shared by all ranks; positional "
+                     "70/30 split, contiguous shard per rank; random-init weights"
+                     % (sh.n_draws, n_loc, n_loc * 8 / 2**30,
+                        "; the %.1f GiB training shard HBM-resident, the validation span regenerated and capped "
+                        "at 16M draws" % resident_gb if a.device_data_gb > 0 else "", a.planted)),
             "config": {"model": desc,
                        "global_batch": BS * world, "seq_len": 1, "parallelism": f"dp{world}",
                        "per_gpu_batch": BS, "optimizer": "adam", "hipgraph": use_graph,
@@ -455,7 +456,7 @@ def main():
             "val_iid": ev_iid,
             "datagen": {"draws": n_loc, "seconds": gen_s, "gb_per_s": resident_gb * 2**30 / max(gen_s, 1e-9) / 1e9,
                         "steps_spread": spread, "resident_train_gb": resident_gb,
-                        "device_data_gb": a.device_data_gb},
+                        "logical_sequence_gb_per_gpu": n_loc * 8 / 2**30},
             **extra,
         }
         print(json.dumps(out), flush=True)

@@ -90,13 +90,8 @@ __global__ void __launch_bounds__(AS_P * AS_G)
 adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, float grad_scale, float* __restrict__ params,
                  float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io, const float* __restrict__ hp,
                  int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img, const float* __restrict__ loss_slabs,
-                 float* __restrict__ loss_out, float loss_scale, int* __restrict__ xg_hdr, float* __restrict__ xg_data,
-                 int xg_cap, int pre) {
+                 float* __restrict__ loss_out, float loss_scale, int pre) {
   const int tstep = (mode == 1) ? 0 : pre ? state[0] : adam_begin(state);
-  if (xg_hdr) {  // mode 1 producer for the xGMI all-reduce: [grad | loss] into this rank's next slot
-    grad_io = xg_produce_slot(xg_hdr, xg_data, xg_cap);
-    loss_out = grad_io + P;
-  }
   // hp = {lr, beta1, beta2, eps, weight_decay}; state = {step, ticket} (device ints, graph-replay safe)
   __shared__ float part[AS_G][AS_P];
   const int tx = threadIdx.x % AS_P, ty = threadIdx.x / AS_P;
@@ -141,87 +136,119 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
 // t = (slab group g = t >> 4, quad q = t & 15) sums float4 quads of slabs g, g + 16, ... with all of
 // its loads in flight (16-B loads: 4x fewer memory instructions than one float per thread), then
 // thread (quad, e) adds the 16 group sums in group order.  The fixed summation order keeps the result
-// bitwise reproducible, and the train kernel's in-launch Adam epilogue (csrc/mlp_fused.hip epi_adam)
-// replays it exactly, so the split path and the one-launch step produce bit-identical gradients.
+// bitwise reproducible; the single-GPU step (adam_slab4_kernel) and the fused xGMI DP step
+// (adam_slab_xgmi_kernel) share it, so their per-rank gradients are bit-identical.
 constexpr int A4_T = 256, A4_G = 16;
-__global__ void __launch_bounds__(A4_T)
-adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, float grad_scale,
-                  float* __restrict__ params, float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io,
-                  const float* __restrict__ hp, int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img,
-                  const float* __restrict__ loss_slabs, float* __restrict__ loss_out, float loss_scale,
-                  int* __restrict__ xg_hdr, float* __restrict__ xg_data, int xg_cap, int pre) {
-  // the step counter: only wave 0 (the 64 Adam lanes) needs it.  A plain load suffices -- the previous
-  // kernel boundary published it, and this launch writes it (ticket mode) only after every block's
-  // ticket -- whereas 1024 waves issuing an agent-scope atomic load of one word serialise on one L2 channel.
-  int tstep = 0;
-  if (mode != 1 && threadIdx.x < 64) tstep = state[0] + (pre ? 0 : 1);
-  if (xg_hdr) {
-    grad_io = xg_produce_slot(xg_hdr, xg_data, xg_cap);
-    loss_out = grad_io + P;
-  }
+struct Slab4Out {
+  float g = 0.f;                  // threads < 64: grad_scale * sum over slabs of parameter blockIdx.x * 64 + t
+  float w0 = 0.f, m0 = 0.f, v0 = 0.f;  // threads < 64 (with adam): the Adam operands, loaded under the slab loads
+  float bc1 = 1.f, bc2 = 1.f;     // threads < 64 (with adam): bias corrections of step tstep
+};
+// (slice j = parameters 64 j .. 64 j + 63; callers that loop over slices sync before the next call)
+EM_DEVICE Slab4Out slab4_reduce(int j, const float* __restrict__ slabs, int nslab, int stride, float grad_scale,
+                                bool adam, int tstep, const float* __restrict__ params, const float* __restrict__ m,
+                                const float* __restrict__ v, const float* __restrict__ hp) {
   __shared__ f32x4 part[A4_G][16];
+  Slab4Out o;
   const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int p0 = blockIdx.x * 64 + 4 * q;
-  const float* src = slabs + p0;
-  float w0 = 0.f, m0 = 0.f, v0 = 0.f;  // Adam operands, in flight during the slab reduction
-  if (mode != 1 && threadIdx.x < 64) {
-    const int p = blockIdx.x * 64 + threadIdx.x;
-    w0 = params[p];
-    m0 = m[p];
-    v0 = v[p];
+  const float* src = slabs + j * 64 + 4 * q;
+  if (adam && threadIdx.x < 64) {
+    const int p = j * 64 + threadIdx.x;
+    o.w0 = params[p];
+    o.m0 = m[p];
+    o.v0 = v[p];
   }
   f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
-  float bc1 = 1.f, bc2 = 1.f;  // bias corrections: their fp64 chain runs under the slab loads below
   int sl = g;
   for (; sl + 15 * A4_G < nslab; sl += 16 * A4_G) {
     f32x4 t[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) t[k] = *reinterpret_cast<const f32x4*>(src + (size_t)(sl + k * A4_G) * stride);
-    if (sl == g && mode != 1 && threadIdx.x < 64) {
-      bc1 = bias_correction(hp[1], tstep);
-      bc2 = bias_correction(hp[2], tstep);
+    if (sl == g && adam && threadIdx.x < 64) {  // the fp64 chain runs while the loads are in flight
+      o.bc1 = bias_correction(hp[1], tstep);
+      o.bc2 = bias_correction(hp[2], tstep);
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[k & 3] += t[k];
   }
-  if (nslab <= g + 15 * A4_G && mode != 1 && threadIdx.x < 64) {  // (no full block of slabs above)
-    bc1 = bias_correction(hp[1], tstep);
-    bc2 = bias_correction(hp[2], tstep);
+  if (nslab <= g + 15 * A4_G && adam && threadIdx.x < 64) {  // (no full block of slabs above)
+    o.bc1 = bias_correction(hp[1], tstep);
+    o.bc2 = bias_correction(hp[2], tstep);
   }
   for (; sl < nslab; sl += A4_G) acc[0] += *reinterpret_cast<const f32x4*>(src + (size_t)sl * stride);
   part[g][q] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  if (blockIdx.x == 0 && loss_slabs && loss_out && threadIdx.x >= 64 && threadIdx.x < 128) {
-    float l = 0.f;
-    for (int i = threadIdx.x - 64; i < nslab; i += 64) l += loss_slabs[i];
-    l = wave_sum(l);
-    if (threadIdx.x == 64) loss_out[0] = l * loss_scale;
-  }
   if (threadIdx.x < 64) {
-    const int pq = threadIdx.x >> 2, e = threadIdx.x & 3, p = blockIdx.x * 64 + threadIdx.x;
+    const int pq = threadIdx.x >> 2, e = threadIdx.x & 3;
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < A4_G; ++k) t += part[k][pq][e];
-    const float gsum = t * grad_scale;
-    if (mode == 1) grad_io[p] = gsum;
-    else adam_apply_bc(p, gsum, w0, m0, v0, bc1, bc2, params, m, v, hp, mlp_img);
+    o.g = t * grad_scale;
+  }
+  return o;
+}
+
+// sum of the per-workgroup loss partials (one wave)
+EM_DEVICE float loss_sum(const float* __restrict__ loss_slabs, int nslab, int lane) {
+  float l = 0.f;
+  for (int i = lane; i < nslab; i += 64) l += loss_slabs[i];
+  return wave_sum(l);
+}
+
+__global__ void __launch_bounds__(A4_T)
+adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, float grad_scale,
+                  float* __restrict__ params, float* __restrict__ m, float* __restrict__ v, float* __restrict__ grad_io,
+                  const float* __restrict__ hp, int* __restrict__ state, int mode, uint8_t* __restrict__ mlp_img,
+                  const float* __restrict__ loss_slabs, float* __restrict__ loss_out, float loss_scale, int pre) {
+  // the step counter: only wave 0 (the 64 Adam lanes) needs it.  A plain load suffices -- the previous
+  // kernel boundary published it, and this launch writes it (ticket mode) only after every block's
+  // ticket -- whereas 1024 waves issuing an agent-scope atomic load of one word serialise on one L2 channel.
+  int tstep = 0;
+  if (mode != 1 && threadIdx.x < 64) tstep = state[0] + (pre ? 0 : 1);
+  const Slab4Out o = slab4_reduce(blockIdx.x, slabs, nslab, stride, grad_scale, mode != 1, tstep, params, m, v, hp);
+  if (blockIdx.x == 0 && loss_slabs && loss_out && threadIdx.x >= 64 && threadIdx.x < 128) {
+    const float l = loss_sum(loss_slabs, nslab, threadIdx.x - 64);
+    if (threadIdx.x == 64) loss_out[0] = l * loss_scale;
+  }
+  if (threadIdx.x < 64) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (mode == 1) grad_io[p] = o.g;
+    else adam_apply_bc(p, o.g, o.w0, o.m0, o.v0, o.bc1, o.bc2, params, m, v, hp, mlp_img);
   }
   if (mode != 1 && !pre) adam_end(state, tstep);
 }
 
-// xGMI consumer (xgmi.h): g = sum over ranks of slot[s&1][p] (rank order), then the same Adam
-// update as mode 2.  Element P of the slot carries the loss.  256 threads, one parameter each.
-constexpr int AX_B = 256;
-__global__ void __launch_bounds__(AX_B)
-adam_xgmi_kernel(XgmiDesc d, int P, float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
-                 const float* __restrict__ hp, int* __restrict__ state, uint8_t* __restrict__ mlp_img,
-                 float* __restrict__ loss_out, int pre) {
+// The data-parallel step's second (and last) launch over xGMI (xgmi.h, block-flag form): slice j
+// (parameters 64j .. 64j + 63) is reduced from this rank's slabs exactly as adam_slab4_kernel does,
+// written into slice j of the own slot (system-scope write-through stores; slice 0 adds the loss as
+// element P), published with block flag j; then the block waits for block flag j of every peer, sums
+// slice j of all N slots in rank order (bit-identical on every rank) and applies Adam.  No separate
+// slab-reduction launch and no grid-wide barrier: a slice travels as soon as it is reduced.
+// One block per slice on a node (257 blocks); ranks that share a device launch fewer blocks that loop
+// over the slices, so the spinning consumer leaves CUs free for a peer's whole-CU train kernel.
+__global__ void __launch_bounds__(A4_T)
+adam_slab_xgmi_kernel(XgmiDesc d, const float* __restrict__ slabs, int nslab, int stride, float grad_scale,
+                      float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
+                      const float* __restrict__ hp, int* __restrict__ state, uint8_t* __restrict__ mlp_img,
+                      const float* __restrict__ loss_slabs, float* __restrict__ loss_out, float loss_scale,
+                      int P, int pre) {
   const int s = xg_next_seq(d.my_hdr);
-  const int tstep = pre ? state[0] : adam_begin(state);
-  if (xg_publish_and_wait(d, s)) {
-    const int p = blockIdx.x * AX_B + threadIdx.x;
-    if (p < P) adam_apply(p, xg_sum(d, s, p), tstep, params, m, v, hp, mlp_img);
-    else if (p == P && loss_out) loss_out[0] = xg_sum(d, s, P);
+  int tstep = 0;
+  if (threadIdx.x < 64) tstep = state[0] + (pre ? 0 : 1);
+  float* slot = d.my_data + (size_t)(s & 1) * d.cap;
+  for (int j = blockIdx.x; j < P / 64; j += gridDim.x) {
+    if (j != (int)blockIdx.x) __syncthreads();  // the previous slice's LDS partials are consumed
+    const Slab4Out o = slab4_reduce(j, slabs, nslab, stride, grad_scale, true, tstep, params, m, v, hp);
+    const int p = j * 64 + threadIdx.x;
+    if (threadIdx.x < 64) __hip_atomic_store(slot + p, o.g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (j == 0 && threadIdx.x >= 64 && threadIdx.x < 128) {
+      const float l = loss_sum(loss_slabs, nslab, threadIdx.x - 64);
+      if (threadIdx.x == 64) __hip_atomic_store(slot + P, l * loss_scale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (xg_publish_block_and_wait(d, s, j)) {
+      if (threadIdx.x < 64) adam_apply_bc(p, xg_sum(d, s, p), o.w0, o.m0, o.v0, o.bc1, o.bc2, params, m, v, hp, mlp_img);
+      if (j == 0 && threadIdx.x == 64 && loss_out) loss_out[0] = xg_sum(d, s, P);
+    }
   }
   xg_finish(d, s);
   if (!pre) adam_end(state, tstep);
@@ -330,42 +357,44 @@ adam_flat_kernel(float* __restrict__ params, const G* __restrict__ grad, float* 
 
 EM_API int em_adam_slab(const float* slabs, int nslab, int P, int stride, float grad_scale, float* params, float* m, float* v,
                         float* grad_io, const float* hp, int* state, int mode, void* mlp_img, const float* loss_slabs,
-                        float* loss_out, float loss_scale, void* xgmi, hipStream_t stream) {
-  XgmiComm* xc = static_cast<XgmiComm*>(xgmi);
+                        float* loss_out, float loss_scale, hipStream_t stream) {
   const int pre = (mode & EM_ADAM_PRE) ? 1 : 0;
   mode &= ~EM_ADAM_PRE;
   if (mode < 0 || mode > 2) return EM_ERR_ARG;
-  if (xc && (mode != 1 || xc->desc.cap < P + 1)) return EM_ERR_ARG;
-  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0 || stride < P)) || (mode != 0 && !grad_io && !xc)) return EM_ERR_ARG;
+  if (P <= 0 || (mode != 2 && (!slabs || nslab <= 0 || stride < P)) || (mode != 0 && !grad_io)) return EM_ERR_ARG;
   if (mode != 1 && (!params || !m || !v || !hp || !state)) return EM_ERR_ARG;
   if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
   const int nb = (P + AS_P - 1) / AS_P;
   if (mode != 2 && P % 64 == 0 && stride % 4 == 0 && ((uintptr_t)slabs & 15) == 0) {
     hipLaunchKernelGGL(adam_slab4_kernel, dim3(P / 64), dim3(A4_T), 0, stream, slabs, nslab, P, stride, grad_scale,
-                       params, m, v, grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale,
-                       xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0, pre);
+                       params, m, v, grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale, pre);
     EM_CHECK_LAUNCH();
     return 0;
   }
   hipLaunchKernelGGL(adam_slab_kernel, dim3(nb), dim3(AS_P * AS_G), 0, stream, slabs, nslab, P, stride, grad_scale, params, m, v,
-                     grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale,
-                     xc ? xc->desc.my_hdr : nullptr, xc ? xc->desc.my_data : nullptr, xc ? xc->desc.cap : 0, pre);
+                     grad_io, hp, state, mode, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale, pre);
   EM_CHECK_LAUNCH();
   return 0;
 }
 
-// Adam step whose gradient is the xGMI all-reduce of every rank's slot (see xgmi.h);
-// loss_out (optional) receives the reduced element P; pre = the step counter was already advanced
-// by this step's train kernel (EM_ADAM_PRE).
-EM_API int em_adam_xgmi(void* xgmi, int P, float* params, float* m, float* v, const float* hp, int* state, void* mlp_img,
-                        float* loss_out, int pre, hipStream_t stream) {
+// The fused DP optimizer step (adam_slab_xgmi_kernel): slab reduction into the own xGMI slot, exchange,
+// rank-order sum and Adam in ONE launch.  Needs P % 64 == 0 and a 16-B aligned slab array; max_blocks > 0
+// caps the grid (ranks sharing a device);
+// loss_out (optional) receives the reduced loss; pre = the step counter was already advanced by this
+// step's train kernel (EM_ADAM_PRE).
+EM_API int em_adam_slab_xgmi(void* xgmi, const float* slabs, int nslab, int stride, float grad_scale, int P, float* params,
+                             float* m, float* v, const float* hp, int* state, void* mlp_img, const float* loss_slabs,
+                             float* loss_out, float loss_scale, int pre, int max_blocks, hipStream_t stream) {
   XgmiComm* xc = static_cast<XgmiComm*>(xgmi);
-  if (!xc || !xc->connected || P <= 0 || xc->desc.cap < P + 1 || !params || !m || !v || !hp || !state) return EM_ERR_ARG;
+  if (!xc || !xc->connected || P <= 0 || P % 64 || xc->desc.cap < P + 1 || !slabs || nslab <= 0 || stride < P ||
+      stride % 4 || ((uintptr_t)slabs & 15) || !params || !m || !v || !hp || !state || !loss_slabs)
+    return EM_ERR_ARG;
   if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
-  const int nb = (P + 1 + AX_B - 1) / AX_B;
-  if (nb > 256) return EM_ERR_ARG;  // consumer grid must stay co-resident (blocks spin on peer flags)
-  hipLaunchKernelGGL(adam_xgmi_kernel, dim3(nb), dim3(AX_B), 0, stream, xc->desc, P, params, m, v, hp, state,
-                     (uint8_t*)mlp_img, loss_out, pre ? 1 : 0);
+  int nb = P / 64;
+  if (nb > XG_MAX_BFLAGS) return EM_ERR_ARG;  // one block flag per slice (257 blocks: co-resident at 8 per CU)
+  if (max_blocks > 0 && nb > max_blocks) nb = max_blocks;
+  hipLaunchKernelGGL(adam_slab_xgmi_kernel, dim3(nb), dim3(A4_T), 0, stream, xc->desc, slabs, nslab, stride, grad_scale,
+                     params, m, v, hp, state, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale, P, pre ? 1 : 0);
   EM_CHECK_LAUNCH();
   return 0;
 }

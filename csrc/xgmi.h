@@ -21,6 +21,14 @@
 // Slot reuse is safe with two slots: r overwrites slot[s & 1] in step s+2 only after its
 // step-(s+1) consumer saw every flag_q >= s+1, and q publishes s+1 only after finishing its
 // step-s consumer (stream order).  Flags only grow, so nothing is ever reset.
+//
+// Block-flag form (the fused DP step, adam.hip adam_slab_xgmi_kernel): the consumer itself produces
+// the slot.  Block j reduces its own slice j of the slot, writes it with system-scope (write-through)
+// stores, drains them, and publishes BLOCK flag j (header int XG_BFLAG + j); peers' block j waits for
+// block flag j of every rank only, so no grid-wide barrier stands between the slab reduction and the
+// exchange.  The reuse argument above holds per slice: q publishes block flag j = s+1 only in its
+// step-(s+1) consumer, i.e. after its step-s consumer (which read slice j of every slot) finished.
+// Both flag kinds are raised only at the start of a consumer, so the two forms may be interleaved.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,6 +39,8 @@ constexpr int XG_FLAG = 0;     // int index into the header
 constexpr int XG_ERROR = 16;   // byte 64
 constexpr int XG_SEQ = 32;     // byte 128
 constexpr int XG_TICKET = 33;  // byte 132
+constexpr int XG_BFLAG = 64;   // byte 256: block flags of the fused DP consumer
+constexpr int XG_MAX_BFLAGS = XG_HDR_BYTES / 4 - XG_BFLAG;
 
 struct XgmiDesc {
   const float* peer_data[XG_MAXW];  // slot 0 of every rank's buffer (own included), rank order
@@ -50,17 +60,14 @@ __device__ __forceinline__ float* xg_produce_slot(int* hdr, float* data, int cap
   return data + (size_t)(xg_next_seq(hdr) & 1) * cap;
 }
 
-// Consumer prologue: block 0 publishes this rank's flag; every block waits for all peers.
+// Every block waits until header int `idx` of every rank reached s (lane q polls rank q).
 // Returns false (and raises the error word) on timeout.  Must be called by all threads.
-__device__ __forceinline__ bool xg_publish_and_wait(const XgmiDesc& d, int s) {
+__device__ __forceinline__ bool xg_wait_flags(const XgmiDesc& d, int s, int idx) {
   __shared__ int xg_bad;
-  if (threadIdx.x == 0) {
-    xg_bad = 0;
-    if (blockIdx.x == 0) __hip_atomic_store(&d.my_hdr[XG_FLAG], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (threadIdx.x == 0) xg_bad = 0;
   __syncthreads();
   if (threadIdx.x < (unsigned)d.world) {
-    const int* f = &d.peer_hdr[threadIdx.x][XG_FLAG];
+    const int* f = &d.peer_hdr[threadIdx.x][idx];
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
       __builtin_amdgcn_s_sleep(1);
@@ -74,6 +81,24 @@ __device__ __forceinline__ bool xg_publish_and_wait(const XgmiDesc& d, int s) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines after the flags
   __syncthreads();
   return xg_bad == 0;
+}
+
+// Consumer prologue: block 0 publishes this rank's flag; every block waits for all peers.
+__device__ __forceinline__ bool xg_publish_and_wait(const XgmiDesc& d, int s) {
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    __hip_atomic_store(&d.my_hdr[XG_FLAG], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return xg_wait_flags(d, s, XG_FLAG);
+}
+
+// Block-flag form: slice j of the own slot is written (system-scope stores by every writing thread of
+// this block); drain them, then one lane raises block flag j and the block waits for block flag j of
+// every rank.
+__device__ __forceinline__ bool xg_publish_block_and_wait(const XgmiDesc& d, int s, int j) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slice stores have landed
+  __syncthreads();                                   // ... and every other wave's
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&d.my_hdr[XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return xg_wait_flags(d, s, XG_BFLAG + j);
 }
 
 // Sum element i of slot (s & 1) over all ranks, rank order (bitwise identical on every rank).

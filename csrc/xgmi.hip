@@ -60,6 +60,55 @@ xgmi_emulate_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, float* 
     __hip_atomic_store(&peer_hdr[threadIdx.x][XG_FLAG], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The same for the block-flag form (adam_slab_xgmi_kernel): emulated-peer block j waits until this
+// rank's block j has published its slice (own block flag j), waits `delay_ticks` more, copies the
+// slice (and, in block 0, the elements past the last full slice: the loss) into every emulated peer's
+// slot when `copy` is set, and raises the peers' block flag j.  Every wait is bounded by the
+// communicator's timeout (a missing own publication sets the error word).
+__global__ void __launch_bounds__(64)
+xgmi_emulate_block_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, float* const* __restrict__ peer_data,
+                                int n, int copy, long long delay_ticks) {
+  __shared__ int s_sh;
+  const int j = blockIdx.x;
+  if (threadIdx.x == 0) {
+    const int s = xg_next_seq(d.my_hdr);
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(&d.my_hdr[XG_BFLAG + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > d.timeout_ticks) {
+        __hip_atomic_store(&d.my_hdr[XG_ERROR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    const long long t1 = wall_clock64();
+    while (wall_clock64() - t1 < delay_ticks) __builtin_amdgcn_s_sleep(2);
+    s_sh = s;
+  }
+  __syncthreads();
+  const int s = s_sh;
+  if (copy) {
+    const size_t base = (size_t)(s & 1) * d.cap;
+    const int i = 64 * j + threadIdx.x;
+    const bool tail = j == 0 && 64 * (int)gridDim.x + (int)threadIdx.x < n;  // the loss element(s)
+    for (int q = 0; q < d.world; ++q) {
+      if (q == d.rank) continue;
+      if (i < n)
+        __hip_atomic_store(peer_data[q] + base + i,
+                           __hip_atomic_load(d.my_data + base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tail) {
+        const size_t k = base + 64 * gridDim.x + threadIdx.x;
+        __hip_atomic_store(peer_data[q] + k, __hip_atomic_load(d.my_data + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (threadIdx.x < (unsigned)d.world && (int)threadIdx.x != d.rank)
+    __hip_atomic_store(&peer_hdr[threadIdx.x][XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // consumer blocks spin on peer flags, so keep the grid well inside one wave of residency
 int grid_for(int n) {
   int nb = (n + XG_BLOCK - 1) / XG_BLOCK;
@@ -218,11 +267,10 @@ EM_API int em_xgmi_connect_local(void* h, int world, int rank, void* const* othe
   return 0;
 }
 
-// the emulated peers of a connect_local'ed comm publish their flags (and n floats, if n > 0) after delay_us
-EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t stream) {
-  XgmiComm* c = static_cast<XgmiComm*>(h);
-  if (!c || !c->local_proxy || n < 0 || n > c->desc.cap || delay_us < 0) return EM_ERR_ARG;
-  if (!c->peer_ptrs) {  // device copies of the peers' header / data pointers
+namespace {
+// device copies of a connect_local'ed comm's peer header / data pointers
+int peer_ptr_table(XgmiComm* c) {
+  if (!c->peer_ptrs) {
     if (hipMalloc(&c->peer_ptrs, 2 * XG_MAXW * sizeof(void*)) != hipSuccess) return EM_ERR_ARG;
     void* host[2 * XG_MAXW];
     for (int q = 0; q < XG_MAXW; ++q) {
@@ -231,12 +279,39 @@ EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t st
     }
     if (hipMemcpy(c->peer_ptrs, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess) return EM_ERR_ARG;
   }
+  return 0;
+}
+}  // namespace
+
+// the emulated peers of a connect_local'ed comm publish their flags (and n floats, if n > 0) after delay_us
+EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t stream) {
+  XgmiComm* c = static_cast<XgmiComm*>(h);
+  if (!c || !c->local_proxy || n < 0 || n > c->desc.cap || delay_us < 0) return EM_ERR_ARG;
+  if (int e = peer_ptr_table(c)) return e;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
   int* const* hdr = reinterpret_cast<int* const*>(c->peer_ptrs);
   float* const* data = reinterpret_cast<float* const*>(c->peer_ptrs) + XG_MAXW;
   hipLaunchKernelGGL(xgmi_emulate_peers_kernel, dim3(1), dim3(XG_BLOCK), 0, stream, c->desc, hdr, data, n,
                      (long long)(delay_us * 1e-3 * khz));
+  EM_CHECK_LAUNCH();
+  return 0;
+}
+
+// block-flag form (the fused DP consumer, em_adam_slab_xgmi over nblocks = P / 64 slices of an n-float
+// slot): run on a side stream beside the consumer; see xgmi_emulate_block_peers_kernel
+EM_API int em_xgmi_emulate_block_peers(void* h, int nblocks, int n, int copy, double delay_us, hipStream_t stream) {
+  XgmiComm* c = static_cast<XgmiComm*>(h);
+  if (!c || !c->local_proxy || nblocks <= 0 || nblocks > XG_MAX_BFLAGS || n < 0 || n > c->desc.cap ||
+      n > 64 * nblocks + 64 || delay_us < 0)
+    return EM_ERR_ARG;
+  if (int e = peer_ptr_table(c)) return e;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
+  int* const* hdr = reinterpret_cast<int* const*>(c->peer_ptrs);
+  float* const* data = reinterpret_cast<float* const*>(c->peer_ptrs) + XG_MAXW;
+  hipLaunchKernelGGL(xgmi_emulate_block_peers_kernel, dim3(nblocks), dim3(64), 0, stream, c->desc, hdr, data, n,
+                     copy ? 1 : 0, (long long)(delay_us * 1e-3 * khz));
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -93,7 +93,8 @@ class FusedSmallMLP:
     Single process: two launches per optimizer step (train kernel, then ``em_adam_slab``).  A
     one-launch form (slab reduction + Adam inside the train kernel) was bit-identical but measured
     4.3 us per step slower on MI355X (93.3 vs 89.0 us, docs/DESIGN.md §6b) and was removed in round 4.
-    Data parallel: train kernel -> all-reduce -> Adam."""
+    Data parallel over xGMI: train kernel -> ``em_adam_slab_xgmi`` (two launches); over RCCL: train
+    kernel -> slab reduce -> all-reduce -> Adam."""
 
     def __init__(self, device: str | torch.device = "cuda", loss: str = "softmax", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 0,
@@ -184,11 +185,10 @@ class FusedSmallMLP:
             FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=0,
                          img=self.img, loss_slabs=self.loss_slabs, loss_out=self.loss_out, loss_scale=lscale, pre=True)
             return self.loss_out
-        if self.xgmi is not None:  # producer -> own xGMI slot; consumer = all-reduce + Adam, no host sync
-            FM.adam_slab(self.slabs, nslab, scale, self.params, self.m, self.v, self.hp, self.state, mode=1,
-                         loss_slabs=self.loss_slabs, loss_scale=lscale, xgmi=self.xgmi.handle)
-            FM.adam_xgmi(self.xgmi.handle, self.params, self.m, self.v, self.hp, self.state, img=self.img,
-                         loss_out=self.loss_out, pre=True)
+        if self.xgmi is not None:  # one launch: slab reduce -> own slot, exchange, rank-order sum, Adam
+            FM.adam_slab_xgmi(self.xgmi.handle, self.slabs, nslab, scale, self.params, self.m, self.v, self.hp,
+                              self.state, self.loss_slabs, img=self.img, loss_out=self.loss_out, loss_scale=lscale,
+                              pre=True, max_blocks=self.xgmi.consumer_blocks)
             return self.loss_out
         import torch.distributed as dist
 
@@ -205,16 +205,16 @@ class FusedSmallMLP:
         """True when a step can be replayed from a hipGraph: single GPU, xGMI, or the RCCL path
         (an RCCL all-reduce is a stream-ordered kernel, captured like any other: the step has no
         host sync, so the fallback does not pay ~4 Python launches per 90 us step).  gloo
-        collectives run on the host and are never captured.  Captured RCCL steps have only been checked
-        against eager steps on a 1-rank group (the pool's boxes have one GPU), so replaying them is
-        opt-in: ``EUROM_RCCL_GRAPH=1``."""
+        collectives run on the host and are never captured.  The captured RCCL step is the default
+        (tests/test_train_gpu.py checks graph replay == eager on an RCCL group); ``EUROM_RCCL_GRAPH=0``
+        opts out."""
         if self.group is None or self.xgmi is not None:
             return True
         import os
 
         import torch.distributed as dist
 
-        return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "0") == "1"
+        return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "1") != "0"
 
     def check_comm(self) -> None:
         """Raise if an xGMI peer wait timed out (synchronises)."""

@@ -45,7 +45,7 @@ _SIGS = {
     "em_mlp_fused_pack": (_i32, [_c_void_p, _c_void_p, _c_void_p]),
     "em_mlp_fused_slab_stride": (_i32, []),
     "em_adam_slab": (_i32, [_c_void_p, _i32, _i32, _i32, _f32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                            _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p]),
+                            _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _f32, _c_void_p]),
     "em_adam_flat": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _f32, _c_void_p,
                             _c_void_p]),
     "em_adam_flat_bf16g": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _f32,

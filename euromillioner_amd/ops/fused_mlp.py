@@ -169,11 +169,10 @@ def forward_logits(draws: torch.Tensor, B: int, img: torch.Tensor, out: torch.Te
 def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params: torch.Tensor, m: torch.Tensor,
               v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor, mode: int = 0, grad_io: torch.Tensor | None = None,
               img: torch.Tensor | None = None, loss_slabs: torch.Tensor | None = None,
-              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0, xgmi: int | None = None,
-              pre: bool = False) -> None:
-    """mode 0: slab reduce + Adam; mode 1: slab reduce -> grad_io (or, with ``xgmi``, this rank's
-    next xGMI slot); mode 2: Adam from grad_io.  ``pre``: the step counter ``state[0]`` was already
-    advanced for this step (train_partials(step=state)), so no grid-wide ticket is drawn."""
+              loss_out: torch.Tensor | None = None, loss_scale: float = 1.0, pre: bool = False) -> None:
+    """mode 0: slab reduce + Adam; mode 1: slab reduce -> grad_io; mode 2: Adam from grad_io.
+    ``pre``: the step counter ``state[0]`` was already advanced for this step
+    (train_partials(step=state)), so no grid-wide ticket is drawn."""
     P = params.numel()
     stride = slabs.shape[1] if slabs is not None else P
     N.call("em_adam_slab", slabs.data_ptr() if slabs is not None else None, int(nslab), int(P), int(stride),
@@ -182,19 +181,24 @@ def adam_slab(slabs: torch.Tensor | None, nslab: int, grad_scale: float, params:
            hp.data_ptr(), state.data_ptr(), int(mode) | (ADAM_PRE if pre else 0),
            img.data_ptr() if img is not None else None,
            loss_slabs.data_ptr() if loss_slabs is not None else None,
-           loss_out.data_ptr() if loss_out is not None else None, float(loss_scale), xgmi,
+           loss_out.data_ptr() if loss_out is not None else None, float(loss_scale),
            N.stream_handle(params.device))
 
 
-def adam_xgmi(xgmi: int, params: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor,
-              state: torch.Tensor, img: torch.Tensor | None = None, loss_out: torch.Tensor | None = None,
-              pre: bool = False) -> None:
-    """Adam step on the xGMI all-reduce (rank-order sum) of every rank's staged [grad | loss]."""
+def adam_slab_xgmi(xgmi: int, slabs: torch.Tensor, nslab: int, grad_scale: float, params: torch.Tensor,
+                   m: torch.Tensor, v: torch.Tensor, hp: torch.Tensor, state: torch.Tensor, loss_slabs: torch.Tensor,
+                   img: torch.Tensor | None = None, loss_out: torch.Tensor | None = None, loss_scale: float = 1.0,
+                   pre: bool = False, max_blocks: int = 0) -> None:
+    """The DP optimizer step in ONE launch (csrc/adam.hip adam_slab_xgmi_kernel): this rank's slab
+    reduction into its xGMI slot (block-sliced), the exchange, the rank-order sum of every rank's
+    [grad | loss] and Adam.  ``max_blocks`` > 0 caps the grid (blocks loop over the slices)."""
     from ..parallel import xgmi as _xg  # noqa: F401  (registers the em_xgmi_* signatures)
 
-    N.call("em_adam_xgmi", xgmi, params.numel(), params.data_ptr(), m.data_ptr(), v.data_ptr(), hp.data_ptr(),
-           state.data_ptr(), img.data_ptr() if img is not None else None,
-           loss_out.data_ptr() if loss_out is not None else None, int(pre), N.stream_handle(params.device))
+    N.call("em_adam_slab_xgmi", xgmi, slabs.data_ptr(), int(nslab), int(slabs.shape[1]), float(grad_scale),
+           params.numel(), params.data_ptr(), m.data_ptr(), v.data_ptr(), hp.data_ptr(), state.data_ptr(),
+           img.data_ptr() if img is not None else None, loss_slabs.data_ptr(),
+           loss_out.data_ptr() if loss_out is not None else None, float(loss_scale), int(pre), int(max_blocks),
+           N.stream_handle(params.device))
 
 
 def cast_bf16(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:

@@ -11,6 +11,11 @@ Rules that keep the launch safe on a GPU node:
   ``exec``s — it starts N children with ``subprocess`` and waits;
 * every child gets ``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``LOCAL_WORLD_SIZE`` and a 127.0.0.1
   rendezvous (``MASTER_ADDR``/``MASTER_PORT``) plus ``EUROM_LAUNCHED=1``;
+* the rendezvous store is hosted by the parent (:func:`host_store`, as torchrun's agent does): it
+  binds port 0 and keeps the socket, and the ranks connect as clients
+  (``TORCHELASTIC_USE_AGENT_STORE=True``).  Picking a free port and letting rank 0 bind it later left
+  a window in which another process (gloo's own pairwise connections, another job) could take the
+  port; round 4's flaky 8-rank CPU test failed that way at rendezvous;
 * the first child that fails (or the whole job passing ``timeout_s``) kills the others' process
   groups; the parent returns the failing child's exit code (124 for a timeout), never 0;
 * elastic restart (``--max-restarts k``): after a rank failure the parent stops the
@@ -40,12 +45,32 @@ def free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def rank_env(rank: int, world: int, port: int, base: dict | None = None, attempt: int = 0) -> dict:
-    """Environment of rank ``rank`` of a ``world``-rank single-node job (``attempt``: restart index)."""
+def host_store(world: int, timeout_s: float = 900.0):
+    """(store, port): a TCPStore server on 127.0.0.1 owned by the caller (pure CPU: no GPU is
+    touched).  The port is bound from the start, so no other process can take it before the ranks
+    connect; keep the returned store alive until the ranks have exited."""
+    import datetime
+
+    from torch.distributed import TCPStore
+
+    store = TCPStore("127.0.0.1", 0, world, True, timeout=datetime.timedelta(seconds=timeout_s),
+                     wait_for_workers=False)
+    return store, int(store.port)
+
+
+def rank_env(rank: int, world: int, port: int, base: dict | None = None, attempt: int = 0,
+             agent_store: bool = True) -> dict:
+    """Environment of rank ``rank`` of a ``world``-rank single-node job (``attempt``: restart index).
+    ``agent_store``: the rendezvous store at ``port`` is hosted by the launcher (:func:`host_store`),
+    so rank 0 connects to it as a client instead of binding the port itself."""
     env = dict(os.environ if base is None else base)
     env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
                 "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
                 "MASTER_PORT": str(port), LAUNCHED_ENV: "1", RESTART_ENV: str(attempt)})
+    if agent_store:
+        env["TORCHELASTIC_USE_AGENT_STORE"] = "True"
+    else:
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     # dmabuf IPC is the only kind the host driver supports (RCCL / xGMI peer buffers)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return env
@@ -110,7 +135,7 @@ def spawn(argv: list[str], world: int, timeout_s: float = 3600.0, env: dict | No
 
 
 def _run_once(argv, world, t0, timeout_s, env, quiet_ranks, poll_s, attempt) -> int:
-    port = free_port()
+    store, port = host_store(world)  # a fresh store (and port) per attempt
     procs: list[subprocess.Popen] = []
     for r in range(world):
         out = subprocess.DEVNULL if (quiet_ranks and r > 0) else None
@@ -146,6 +171,7 @@ def _run_once(argv, world, t0, timeout_s, env, quiet_ranks, poll_s, attempt) -> 
             except subprocess.TimeoutExpired:
                 _kill_group(p, signal.SIGKILL)
                 p.wait()
+        del store
     return rc_final
 
 

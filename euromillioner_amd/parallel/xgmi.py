@@ -5,8 +5,9 @@ form a full xGMI mesh (7 point-to-point links per GPU), so instead of an RCCL ri
 latency-bound hops) every rank publishes its gradient in an IPC-shared, uncached HBM buffer
 and the Adam kernel of every rank reads all N buffers directly — one hop over N-1 links in
 parallel — summing them in rank order so parameters stay bit-identical across ranks.  No
-host round trip and no collective launch: the whole DP step is three kernels and replays
-from a hipGraph.
+host round trip and no collective launch: the whole DP step is two kernels (the train kernel, then
+``em_adam_slab_xgmi``: slab reduction into the own slot, exchange and Adam) and replays from a
+hipGraph.
 
 The communicator is created collectively over an existing process group (gloo or RCCL; the
 group only carries the 64-byte IPC handles and the go/no-go vote), self-tested against the
@@ -40,10 +41,19 @@ N.register_signatures({
     "em_xgmi_destroy": (ctypes.c_int, [_v]),
     "em_xgmi_stage": (ctypes.c_int, [_v, _v, ctypes.c_int, _v]),
     "em_xgmi_reduce": (ctypes.c_int, [_v, _v, ctypes.c_int, ctypes.c_float, _v]),
-    "em_adam_xgmi": (ctypes.c_int, [_v, ctypes.c_int, _v, _v, _v, _v, _v, _v, _v, ctypes.c_int, _v]),
+    "em_adam_slab_xgmi": (ctypes.c_int, [_v, _v, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, _v, _v, _v,
+                                         _v, _v, _v, _v, _v, ctypes.c_float, ctypes.c_int, ctypes.c_int, _v]),
+    "em_xgmi_connect_local": (ctypes.c_int, [_v, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_v)]),
+    "em_xgmi_emulate_peers": (ctypes.c_int, [_v, ctypes.c_int, ctypes.c_double, _v]),
+    "em_xgmi_emulate_block_peers": (ctypes.c_int, [_v, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                                   _v]),
 })
 
 MAX_WORLD = 8  # one node (XG_MAXW in xgmi.h)
+MAX_RANKS_PER_DEVICE = 2  # more ranks on one GPU: comm="auto" falls back to RCCL, comm="xgmi" raises
+# Consumer blocks of a rank sharing its GPU: each spinning block holds a CU that the peer's train kernel
+# (one 512-thread, 256-VGPR workgroup per CU) cannot use; 64 leave 192 CUs for it.
+SHARED_DEVICE_BLOCKS = 64
 DEFAULT_TIMEOUT_S = float(os.environ.get("EUROM_XGMI_TIMEOUT", "120"))
 
 
@@ -61,9 +71,18 @@ def _vote_all(ok: bool, group) -> bool:
 class XgmiComm:
     """Handle to this rank's side of the xGMI communicator (see module docstring)."""
 
-    def __init__(self, handle: int, world: int, rank: int, device: torch.device, cap: int):
+    def __init__(self, handle: int, world: int, rank: int, device: torch.device, cap: int,
+                 ranks_per_device: int = 1):
         self.handle = handle
         self.world, self.rank, self.device, self.cap = world, rank, device, cap
+        # > 1 when ranks share a GPU (tests on one-GPU boxes): the fused DP consumer then launches a
+        # smaller grid (SHARED_DEVICE_BLOCKS) so its spinning blocks leave CUs for the peer's train kernel
+        self.ranks_per_device = ranks_per_device
+
+    @property
+    def consumer_blocks(self) -> int:
+        """Grid cap for ``em_adam_slab_xgmi`` (0 = one block per 64-parameter slice)."""
+        return SHARED_DEVICE_BLOCKS if self.ranks_per_device > 1 else 0
 
     # ---------------------------------------------------------------- construction
     @classmethod
@@ -85,10 +104,19 @@ class XgmiComm:
         dist.all_gather_object(allv, me, group=group)
         hosts = {h for h, _, _ in allv}
         reasons = [r for _, _, r in allv if r]
+        per_dev = {}
+        for h, d, _ in allv:
+            per_dev[(h, d)] = per_dev.get((h, d), 0) + 1
+        crowded = max(per_dev.values())
         if reasons:
             reason = reasons[0]
         elif len(hosts) != 1:
             reason = "ranks span several hosts"
+        elif crowded > MAX_RANKS_PER_DEVICE:
+            # every consumer kernel spins on its peers' flags while holding CUs; with more than two
+            # processes on one device the peers' producers (whole-CU train kernels) are not
+            # guaranteed to be scheduled meanwhile (docs/DESIGN.md §3, "ranks sharing a device")
+            reason = f"{crowded} ranks share one device (at most {MAX_RANKS_PER_DEVICE})"
         else:
             for _, d, _ in allv:
                 if d != me[1] and not torch.cuda.can_device_access_peer(me[1], d):
@@ -116,7 +144,7 @@ class XgmiComm:
             if required:
                 raise XgmiError("xGMI all-reduce: IPC open failed on some rank")
             return None
-        comm = cls(h.value, world, rank, device, N.lib().em_xgmi_capacity(h))
+        comm = cls(h.value, world, rank, device, N.lib().em_xgmi_capacity(h), ranks_per_device=crowded)
         if verify:
             comm.set_timeout(min(t, 20.0))  # ranks are in lock-step here (just voted)
             ok = comm.self_test()

@@ -17,12 +17,19 @@ import torch.distributed as dist  # noqa: E402
 
 
 def fallback(rank, world, dev):
-    """EUROM_XGMI=0: the communicator declines collectively and comm="auto" runs the host all-reduce."""
+    """EUROM_XGMI=0, or more than two ranks per device (XGMI_CROWDED=1): the communicator declines
+    collectively, comm="xgmi" raises, and comm="auto" runs the host all-reduce."""
     from euromillioner_amd.data.device_gen import generate_masks
     from euromillioner_amd.models.mlp import FusedSmallMLP
-    from euromillioner_amd.parallel.xgmi import XgmiComm
+    from euromillioner_amd.parallel.xgmi import XgmiComm, XgmiError
 
     out = {"rank": rank, "create": XgmiComm.create(dist.group.WORLD, dev, 1024) is None}
+    try:
+        XgmiComm.create(dist.group.WORLD, dev, 1024, required=True)
+        out["required_raises"] = False
+    except XgmiError as e:
+        out["required_raises"] = True
+        out["reason"] = str(e)
     m = FusedSmallMLP(dev, loss="softmax", lr=3e-3, seed=0, process_group=dist.group.WORLD, comm="auto")
     m.broadcast_parameters()
     out["comm"] = m.comm
@@ -46,7 +53,7 @@ def main():
     dev = torch.device("cuda", rank % ndev)  # distinct devices whenever the node has >= world GPUs
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    if os.environ.get("EUROM_XGMI", "1") == "0":
+    if os.environ.get("EUROM_XGMI", "1") == "0" or os.environ.get("XGMI_CROWDED") == "1":
         return fallback(rank, world, dev)
     from euromillioner_amd.data.synthetic import generate_draws
     from euromillioner_amd.models.mlp import FusedSmallMLP

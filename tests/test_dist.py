@@ -3,33 +3,31 @@ bucketed == plain all-reduce, tree-parallel forest == single forest, fault injec
 fails loudly instead of hanging, checkpoint resume continues exactly."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
 import numpy as np
 import pytest
 
+from euromillioner_amd.parallel.launch import host_store, rank_env
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(ROOT, "tests", "_dist_worker.py")
 
 
-def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _env(rank, world, port):
-    env = dict(os.environ)
-    env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(port), OMP_NUM_THREADS="1", PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="",
-               HIP_VISIBLE_DEVICES="")
+    env = rank_env(rank, world, port)  # the rendezvous store is hosted by this process (agent store)
+    for k in ("LOCAL_WORLD_SIZE", "GROUP_RANK", "EUROM_LAUNCHED", "EUROM_RESTART"):
+        env.pop(k)
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     return env
 
 
 def _launch(argv, world, timeout=240, cwd=None):
-    port = _port()
+    # The test process hosts the TCPStore on a port it already holds (parallel/launch.py host_store): a
+    # port picked free and bound later by rank 0 could be taken in between (the round-4 flake's
+    # suspected cause).
+    store, port = host_store(world)
     procs = [subprocess.Popen(argv, env=_env(r, world, port), cwd=cwd or ROOT, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]
     outs = []
@@ -41,7 +39,16 @@ def _launch(argv, world, timeout=240, cwd=None):
                 q.kill()
             raise
         outs.append((p.returncode, out))
+    del store
     return outs
+
+
+def _ok(outs):
+    """Fail with every failing rank's exit code and output tail (a list of 8 truncated outputs in one
+    assert message hid the failing rank in round 4)."""
+    bad = [(r, rc, out) for r, (rc, out) in enumerate(outs) if rc != 0]
+    if bad:
+        pytest.fail("\n".join(f"rank {r} exited {rc}:\n{out[-2500:]}" for r, rc, out in bad), pytrace=False)
 
 
 def _train_argv(extra):
@@ -66,7 +73,7 @@ def test_dp_equals_single_process(tmp_path, world):
     outs = _launch(_train_argv(common + ["--ckpt", single]), 1)
     assert outs[0][0] == 0, outs[0][1][-2000:]
     outs = _launch(_train_argv(common + ["--ckpt", multi, "--check-sync-every", "2"]), world)
-    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    _ok(outs)
     a, b = _params(single), _params(multi)
     assert np.allclose(a[0], b[0], atol=2e-5), np.abs(a[0] - b[0]).max()  # reduction order differs
     assert np.allclose(a[1], b[1], atol=1e-6) and np.allclose(a[2], b[2], atol=1e-8)
@@ -76,7 +83,7 @@ def test_dp_equals_single_process(tmp_path, world):
 def test_bucketed_allreduce_equals_plain(tmp_path, bucket_mb):
     out = str(tmp_path / "b.json")
     res = _launch([sys.executable, WORKER, "buckets", out, bucket_mb], 2)
-    assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
+    _ok(res)
     r = json.load(open(out))
     assert r["max_err"] < 1e-6
     if bucket_mb == "0.01":
@@ -89,7 +96,7 @@ def test_tree_parallel_forest_equals_single(tmp_path):
 
     out = str(tmp_path / "f.npz")
     res = _launch([sys.executable, WORKER, "forest", out], 3)
-    assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
+    _ok(res)
     z = np.load(out, allow_pickle=False)
     ds = DrawSet.synthetic(n=900, seed=3, planted=0.5, calendar=False)
     X, Y, F = draw_features(ds.numbers)
@@ -135,7 +142,7 @@ def test_parameter_averaging_mode_stays_in_sync(tmp_path):
     p = str(tmp_path / "avg.zip")
     outs = _launch(_train_argv(["--steps", "8", "--batch", "128", "--avg-frequency", "2",
                                 "--check-sync-every", "2", "--ckpt", p]), 2)
-    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    _ok(outs)
     assert _params(p)[3]["step"] == 8
 
 
@@ -145,7 +152,7 @@ def test_parameter_averaging_final_average(tmp_path):
     p = str(tmp_path / "avg7.zip")
     outs = _launch(_train_argv(["--steps", "7", "--batch", "128", "--avg-frequency", "3",
                                 "--check-sync-every", "7", "--ckpt", p]), 2)
-    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    _ok(outs)
     assert _params(p)[3]["step"] == 7
 
 
@@ -231,7 +238,7 @@ def test_data_parallel_gbdt_equals_single(tmp_path, objective):
 
     out = str(tmp_path / "g.npz")
     res = _launch([sys.executable, WORKER, "gbdt", out, objective], 2)
-    assert all(rc == 0 for rc, _ in res), [o[-2000:] for _, o in res]
+    _ok(res)
     z = np.load(out, allow_pickle=False)
     ds = DrawSet.synthetic(n=700, seed=4, planted=0.6, calendar=True)
     X, Y, _ = gbdt_dataset(ds, C.RunConfig())
@@ -254,7 +261,7 @@ def test_cli_pipeline_data_parallel(tmp_path):
     argv = [sys.executable, "-m", "euromillioner_amd", "run", "--device", "cpu", "--n-draws", "400", "--nround", "4",
             "--workdir", str(tmp_path)]
     outs = _launch(argv, 2)
-    assert all(rc == 0 for rc, _ in outs), [o[-2000:] for _, o in outs]
+    _ok(outs)
     lines0 = [l for l in outs[0][1].splitlines() if l.strip() in ("true", "false")]
     lines1 = [l for l in outs[1][1].splitlines() if l.strip() in ("true", "false")]
     assert len(lines0) == 1 and not lines1

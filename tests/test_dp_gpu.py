@@ -3,7 +3,6 @@ with the reason on boxes with fewer GPUs, no edits needed on a full node) and a 
 that runs anywhere (ranks share the GPU).  Worker: tests/_dp_worker.py."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -22,18 +21,14 @@ def _ndev() -> int:
         return 0
 
 
-def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _run(world: int, backend: str, timeout: int = 180, case: str = ""):
-    port = _port()
+    from euromillioner_amd.parallel.launch import host_store
+
+    store, port = host_store(world)  # held by this process: rank 0 connects as a client (agent store)
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DP_BACKEND=backend, DP_CASE=case,
+                   MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True", PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DP_BACKEND=backend, DP_CASE=case,
                    HSA_ENABLE_IPC_MODE_LEGACY="0")
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_dp_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
@@ -49,6 +44,7 @@ def _run(world: int, backend: str, timeout: int = 180, case: str = ""):
         for p in procs:
             if p.poll() is None:
                 p.kill()
+        del store
     return res
 
 

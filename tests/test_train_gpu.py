@@ -93,12 +93,12 @@ def test_dp_code_path_on_one_rank_matches_local(engine):
 
 
 def test_rccl_step_replays_from_a_hipgraph(monkeypatch):
-    """The fused model's RCCL fallback (slab reduce -> RCCL all-reduce -> Adam) is graph-safe: steps
-    captured in one hipGraph and replayed equal the same steps run eagerly on a local model
-    (opt-in, EUROM_RCCL_GRAPH=1, until a multi-GPU node confirms it at world > 1)."""
+    """The fused model's RCCL fallback (slab reduce -> RCCL all-reduce -> Adam) replays from a hipGraph
+    by default (EUROM_RCCL_GRAPH=0 opts out): steps captured in one hipGraph and
+    replayed equal the same steps run eagerly, on the RCCL model and on a local model."""
     import torch
 
-    monkeypatch.setenv("EUROM_RCCL_GRAPH", "1")
+    monkeypatch.delenv("EUROM_RCCL_GRAPH", raising=False)
 
     from euromillioner_amd.data.draws import DrawSet
     from euromillioner_amd.models.mlp import FusedSmallMLP
@@ -109,6 +109,12 @@ def test_rccl_step_replays_from_a_hipgraph(monkeypatch):
     try:
         dp = FusedSmallMLP("cuda", seed=1, lr=3e-3, process_group=dist.group.WORLD, comm="rccl")
         assert dp.comm == "rccl" and dp.graph_safe
+        monkeypatch.setenv("EUROM_RCCL_GRAPH", "0")
+        assert not dp.graph_safe
+        monkeypatch.delenv("EUROM_RCCL_GRAPH")
+        eager = FusedSmallMLP("cuda", seed=1, lr=3e-3, process_group=dist.group.WORLD, comm="rccl")
+        for k in (0, 1, 2, 1, 2):  # the same RCCL step, eager, for the graph's equality check below
+            eager.step(masks, 2048, offset=1000 * k)
         dp.broadcast_parameters()
         dp.step(masks, 2048, offset=0)  # first step eager (argument checks)
         torch.cuda.synchronize()
@@ -135,6 +141,7 @@ def test_rccl_step_replays_from_a_hipgraph(monkeypatch):
     for k in (1, 2):
         ref.step(masks, 2048, offset=1000 * k)
     assert torch.allclose(dp.params, ref.params, atol=1e-6, rtol=0), float((dp.params - ref.params).abs().max())
+    assert torch.equal(dp.params, eager.params), float((dp.params - eager.params).abs().max())  # graph == eager
     assert not torch.equal(mid, dp.params)
 
 

@@ -2,17 +2,18 @@
 """One-GPU budget of the DP=8 small-MLP gradient exchange (BASELINE.json configs[2]).
 
 The pool's boxes have one GPU, so the 8-rank xGMI exchange of the fused 62->128->62 step is run as a
-one-process proxy: rank 0 is the real model and its step is the real DP step (train kernel -> slab
-reduce into the own xGMI slot -> ``em_adam_xgmi``: publish the flag, poll 7 peer flags, sum 8 slots in
-rank order, Adam), hipGraph-replayed like bench.py.  The 7 peers are buffers of this process on the
-same device (``em_xgmi_connect_local``), played by ``em_xgmi_emulate_peers``: a one-block kernel on a
-side stream that starts when rank 0 finishes its slab reduction, waits ``skew`` microseconds (the
-peers reaching the exchange later than rank 0) and publishes their flags.  The peers' slots keep the
-gradient staged into them once at setup (the consumer's reads and sums do not depend on the values).
+one-process proxy: rank 0 is the real model and its step is the real DP step, two launches (train
+kernel -> ``em_adam_slab_xgmi``: each block reduces its 64-parameter slice of the slabs into the own
+xGMI slot, raises its block flag, polls the 7 peers' block flags, sums 8 slices in rank order and
+applies Adam), hipGraph-replayed like bench.py.  The 7 peers are buffers of this process on the same
+device (``em_xgmi_connect_local``), played by ``em_xgmi_emulate_block_peers``: a kernel on a side
+stream, beside the consumer, whose block j waits for rank 0's block flag j, ``skew`` microseconds more
+(the peers reaching the exchange later than rank 0), copies the slice into the 7 peer slots and raises
+the peers' block flags j.
 
-What it measures: the device cost of the 8-way exchange on top of the single-GPU step (7 extra slot
-reads and flag polls inside the consumer, the side kernel), and how a late peer propagates into the
-step.  What it does not: xGMI link latency and bandwidth (the peer slots are local HBM here).  For
+What it measures: the device cost of the 8-way exchange on top of the single-GPU step (7 extra slice
+reads and block-flag polls inside the consumer; the emulator's copies, which real peers do in their
+own consumers), and how a late peer propagates into the step.  What it does not: xGMI link latency and bandwidth (the peer slots are local HBM here).  For
 64 KB per peer over 7 links at ~50 GB/s effective that is ~1.3 us of transfer plus one hop of
 ~1-2 us; docs/DESIGN.md adds it to the budget.
 
@@ -37,11 +38,6 @@ def main():
     from euromillioner_amd.ops import fused_mlp as FM
     from euromillioner_amd.parallel import xgmi as XG  # noqa: F401  (signatures)
 
-    N.register_signatures({
-        "em_xgmi_connect_local": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                                 ctypes.POINTER(ctypes.c_void_p)]),
-        "em_xgmi_emulate_peers": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_void_p]),
-    })
     world = int(os.environ.get("XB_WORLD", "8"))
     B = int(os.environ.get("XB_B", str(1 << 20)))
     steps = 20
@@ -59,11 +55,6 @@ def main():
     arr = (ctypes.c_void_p * world)(*[c.value for c in comms])
     N.call("em_xgmi_connect_local", comms[0], world, 0, arr)
     h0 = comms[0].value
-    g0 = torch.randn(P + 1, device=dev) * 1e-3
-    for c in comms:  # both slots of every rank hold a plausible gradient
-        for _ in range(2):
-            N.call("em_xgmi_stage", c.value, g0.data_ptr(), P + 1, N.stream_handle(dev))
-    torch.cuda.synchronize()
 
     def make_step(m, mode, skew_us, side):
         scale = 1.0 / (B * world)
@@ -74,14 +65,13 @@ def main():
                 FM.adam_slab(m.slabs, nslab, 1.0 / B, m.params, m.m, m.v, m.hp, m.state, mode=0, img=m.img,
                              loss_slabs=m.loss_slabs, loss_out=m.loss_out, loss_scale=1.0 / B, pre=True)
                 return
-            FM.adam_slab(m.slabs, nslab, scale, m.params, m.m, m.v, m.hp, m.state, mode=1,
-                         loss_slabs=m.loss_slabs, loss_scale=scale, xgmi=h0)
             ev = torch.cuda.Event()
             ev.record()
             side.wait_event(ev)
             with torch.cuda.stream(side):
-                N.call("em_xgmi_emulate_peers", h0, 0, float(skew_us), N.stream_handle(dev))
-            FM.adam_xgmi(h0, m.params, m.m, m.v, m.hp, m.state, img=m.img, loss_out=m.loss_out, pre=True)
+                N.call("em_xgmi_emulate_block_peers", h0, P // 64, P + 1, 1, float(skew_us), N.stream_handle(dev))
+            FM.adam_slab_xgmi(h0, m.slabs, nslab, scale, m.params, m.m, m.v, m.hp, m.state, m.loss_slabs, img=m.img,
+                              loss_out=m.loss_out, loss_scale=scale, pre=True)
             torch.cuda.current_stream().wait_stream(side)
         return step
 
