@@ -711,126 +711,6 @@ __global__ void __launch_bounds__(64) rf_child_totals(RfParams p, const uint32_t
   if (lane == 0) dst[64] = right ? nr : P[64] - nr;
 }
 
-// K8 on the matrix cores (binary features, W == 1, k <= 15 candidates): the node histogram is one
-// small GEMM over the node's rows, hist = (w * Xc)ᵀ · Y, with
-//   A [16 x rows]  row c < k: w_r * x_{cand c}(r); row 15: w_r (so D[15][j] = S[j], D[15][62] = n);
-//                  rows k..14: 0
-//   B [rows x 64]  y_j(r) for j < 62; column 62: 1 (so D[c][62] = cnt[c]); column 63: 0
-// on v_mfma_f32_16x16x32_bf16 (K = 32 rows per instruction, 4 output tiles).  Every operand is an
-// integer <= 15 (exact in bf16) and every per-wave sum stays < 2^24 (exact in fp32), so the record is
-// still exact integers and the trees stay bit-identical to the atomic kernel and the numpy oracle.
-// Instead of ~14 LDS atomics per row on 62 + 8x62 contended bins it costs ~3 VALU + 1/8 MFMA per row;
-// each wave keeps its 16 x 64 partial in 16 registers and folds it into the block record once.
-// Measured on the record-form row lists it is ~10 % slower than the atomic kernel (operand bits are
-// gathered one VALU op per row and column), so it is opt-in: EM_RF_MFMA=1.
-// Row data (y | w low bits, x | w high bits) are staged through a wave-private 1 KB LDS slice.
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-EM_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-__global__ void __launch_bounds__(RF_NT) rf_hist_mfma(RfParams p, const RfRec* __restrict__ rows, int level,
-                                                      const int32_t* __restrict__ wl) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const int nodesL = 1 << level, first = nodesL - 1;
-  RfWork wk;
-  if (!rf_work(wl, p.T * nodesL, nodesL, wk)) return;
-  const int t = wk.t, nd = wk.nd, B = wk.nb;
-  const int node = first + nd;
-  const int32_t* sg = p.seg + ((int64_t)t * p.nodes + node) * 2;
-  const int start = sg[0], count = sg[1];
-  if (count < 0) return;
-  const int k = p.k_feat, rec = rec_words(k), kp = (k + 3) & ~3;
-  const bool split = level < p.max_depth;
-  const int kk = split ? (k < p.F ? k : p.F) : 0;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  // LDS: [rec] record | [256] byte -> 8 bf16 {0,1} table (4 KB) | per wave 64 rows x 16 B
-  uint32_t* recd = lds;
-  const uint32_t LUT = (uint32_t)(((rec + 3) & ~3) * 4);
-  const uint32_t ROWS = LUT + 4096 + (uint32_t)wv * 1024;
-  char* smem = reinterpret_cast<char*>(lds);
-  for (int i = threadIdx.x; i < rec; i += blockDim.x) recd[i] = 0u;
-  for (int i = threadIdx.x; i < 256; i += blockDim.x)
-    *reinterpret_cast<bf16x8*>(smem + LUT + i * 16) = bits_to_bf16x8((uint32_t)i);
-  // this lane's A row: candidate slot m = lane & 15 (15 = the all-w row), its feature bit
-  const int m = lane & 15, g = lane >> 4;
-  int fbit = -1;  // -1: zero row
-  if (m < kk) fbit = p.cand[((int64_t)t * nodesL + nd) * k + m];
-  const bool wrow = m == 15;
-  __syncthreads();
-
-  const RfRec* rl = rows + (int64_t)t * p.N + start;
-  const int i0 = (int)((int64_t)count * wk.j / B), i1 = (int)((int64_t)count * (wk.j + 1) / B);
-  f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
-  for (int c0 = i0 + wv * 64; c0 < i1; c0 += nwv * 64) {
-    // stage 64 rows: lane = row
-    {  // the node's records are contiguous: one 16-B load per lane (zero record = weight 0 past the end)
-      const int i = c0 + lane;
-      const RfRec e = i < i1 ? rl[i] : RfRec{0, 0};
-      *reinterpret_cast<u32x4*>(smem + ROWS + lane * 16) =
-          u32x4{(uint32_t)e.y, (uint32_t)(e.y >> 32), (uint32_t)e.x, (uint32_t)(e.x >> 32)};
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      // this lane's 8 rows: 32 half + 8 g + j
-      uint32_t ylo[8], yhi[8], xw[8];
-      float a[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(smem + ROWS + (32 * half + 8 * g + j) * 16);
-        ylo[j] = v[0];
-        yhi[j] = v[1] & 0x3FFFFFFFu;
-        const uint32_t w = (v[1] >> 30) | ((v[3] >> 30) << 2);
-        const uint32_t xb = fbit < 0 ? 0u : ((fbit < 32 ? v[2] >> fbit : v[3] >> (fbit - 32)) & 1u);
-        a[j] = (float)(wrow ? w : xb * w);
-        xw[j] = w;
-      }
-      const bf16x8 af = pack8(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
-#pragma unroll
-      for (int tn = 0; tn < 4; ++tn) {
-        const int n = 16 * tn + m;  // output column of this lane in tile tn
-        uint32_t byte = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          uint32_t bit;
-          if (tn < 2) bit = (ylo[j] >> n) & 1u;
-          else bit = n == 62 ? (xw[j] != 0u ? 1u : 0u) : (n == 63 ? 0u : (yhi[j] >> (n - 32)) & 1u);
-          byte |= bit << j;
-        }
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(smem + LUT + byte * 16);
-        acc[tn] = mfma16(af, bfr, acc[tn]);
-      }
-    }
-    wave_lds_sync();  // the staging slice is rewritten by the next chunk
-  }
-  // fold: D[row 4g + i][col 16 tn + m] -> record (integer LDS atomics: exact, order-free)
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 4 * g + i, col = 16 * tn + m;
-      const uint32_t v = (uint32_t)acc[tn][i];
-      if (v == 0u) continue;
-      if (row == 15) {
-        if (col < 62) atomicAdd(&recd[col], v);   // S[j]
-        else if (col == 62) atomicAdd(&recd[64], v);  // n
-      } else if (row < kk) {
-        if (col < 62) atomicAdd(&recd[68 + kp + row * 64 + col], v);  // hist[c][j]
-        else if (col == 62) atomicAdd(&recd[68 + row], v);            // cnt[c]
-      }
-    }
-  __syncthreads();
-  uint32_t* dst = p.acc + ((int64_t)t * nodesL + nd) * rec;
-  const int used = split ? rec : 68;
-  if (B == 1) {
-    for (int i = threadIdx.x; i < used; i += blockDim.x) dst[i] = recd[i];
-  } else {
-    for (int i = threadIdx.x; i < used; i += blockDim.x)
-      if (recd[i]) atomicAdd(&dst[i], recd[i]);
-  }
-}
-
 // K9: one wavefront per (tree, node): node record (weighted mean outputs, cover) and the split scan
 // over the candidates (lane j = output j): gain = SL2/nL + SR2/nR - S2/n from exact integers.
 // child_acc (the fused driver, derived totals): a node that splits also writes its two children's
@@ -1159,6 +1039,144 @@ __global__ void __launch_bounds__(256) rf_predict(const uint64_t* __restrict__ X
   out[r * ldo + lane] = pr;
 }
 
+// K11, tree-streamed form (W == 1, max_depth <= 8: at most 256 leaves per tree).  Predict was bound by
+// the leaf gathers: N x T x 256 B (7.7 GB for 300 k rows x 100 trees) read from L2 / MALL, one 256-B
+// leaf vector per (row, tree).  Here each workgroup owns a block of rows for the whole launch and
+// streams the trees through LDS instead: per tree one 1-KB node table (features, leaves encoded as
+// -(slot + 1)) and the tree's compacted leaf vectors (nleaf x 256 B), double-buffered by LDS-DMA
+// (buffer_load ... lds) while the previous tree is applied.  A lane owns one row: it walks the tree in
+// LDS and adds its leaf's 16 float4 chunks into 64 accumulator registers per 64-row group.  The chunk
+// order is rotated by the lane (step c reads chunk (lane + c) & 15), so the 16 lanes of a ds_read_b128
+// phase always hit 16 different bank groups whatever leaves they read, and register set c of lane l
+// holds output chunk (l + c) & 15 (un-rotated by the store addresses).  Every output still sums its
+// trees in tree order, so the result is bit-identical to rf_predict.
+constexpr int RFP_TREE = 1024 + 256 * 256;  // bytes per prepared tree: node table + 256 leaf vectors
+
+// one workgroup per tree: node table with leaves encoded, leaf vectors compacted in level order;
+// word 511 of the node table (a padding slot: nodes <= 511) holds the leaf count
+__global__ void __launch_bounds__(64) rf_predict_prepare(const int16_t* __restrict__ feat,
+                                                         const float* __restrict__ value, int nodes, int depth,
+                                                         uint8_t* __restrict__ prep) {
+  __shared__ uint8_t reach[512];
+  __shared__ int16_t slot_of[512];
+  const int t = blockIdx.x, lane = threadIdx.x;
+  const int16_t* ft = feat + (int64_t)t * nodes;
+  int16_t* enc = reinterpret_cast<int16_t*>(prep + (int64_t)t * RFP_TREE);
+  float* vals = reinterpret_cast<float*>(prep + (int64_t)t * RFP_TREE + 1024);
+  int base = 0;
+  for (int d = 0; d <= depth; ++d) {  // level order: a node's parent is decided before it
+    const int n0 = (1 << d) - 1, n1 = (2 << d) - 1;
+    for (int c0 = n0; c0 < n1; c0 += 64) {
+      const int n = c0 + lane;
+      bool live = false, leaf = false;
+      int f = -1;
+      if (n < n1) {
+        f = ft[n];
+        live = n == 0 || (reach[(n - 1) >> 1] && ft[(n - 1) >> 1] >= 0);
+        leaf = live && (f < 0 || d == depth);
+      }
+      const uint64_t m = __ballot(leaf);
+      const int slot = base + __popcll(m & ((1ull << lane) - 1));
+      if (n < n1) {
+        reach[n] = live;
+        slot_of[n] = leaf ? (int16_t)slot : (int16_t)-1;
+        enc[n] = leaf ? (int16_t)(-(slot + 1)) : (live ? (int16_t)f : (int16_t)-1);
+      }
+      base += __popcll(m);
+      __syncthreads();
+    }
+  }
+  if (lane == 0) enc[511] = (int16_t)base;
+  for (int n = 0; n < nodes; ++n)
+    if (slot_of[n] >= 0) vals[slot_of[n] * 64 + lane] = value[((int64_t)t * nodes + n) * 64 + lane];
+}
+
+template <int G>
+__global__ void __launch_bounds__(512) rf_predict_lds(const uint64_t* __restrict__ X, int64_t N,
+                                                      const uint8_t* __restrict__ prep, int T, int rows_per_wave,
+                                                      int64_t rows_per_block, int out_logit, float* __restrict__ out,
+                                                      int ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t rw0 = (int64_t)blockIdx.x * rows_per_block + (int64_t)wave * rows_per_wave;
+  const int64_t rend = rw0 + rows_per_wave < N ? rw0 + rows_per_wave : N;
+  uint32_t xlo[G], xhi[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t r = rw0 + 64 * g + lane;
+    const uint64_t x = r < rend ? X[r] : 0ull;
+    xlo[g] = (uint32_t)x;
+    xhi[g] = (uint32_t)(x >> 32);
+  }
+  f32x4 acc[G][16];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[g][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)prep, 0, 0x7FFFFFFF, 0x00020000);
+  // tree t's node table + leaf vectors -> LDS buffer t & 1: 1 + nleaf / 4 pieces of 1 KB, over the waves
+  auto stage = [&](int t) {
+    const int nleaf = reinterpret_cast<const int16_t*>(prep + (int64_t)t * RFP_TREE)[511];
+    const int pieces = 1 + (nleaf + 3) / 4;
+    char* dst = smem + (t & 1) * RFP_TREE;
+    for (int pc = wave; pc < pieces; pc += 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (EM_LDS void*)(dst + pc * 1024), 16, (uint32_t)lane * 16,
+                                               (uint32_t)t * RFP_TREE + (uint32_t)pc * 1024, 0, 0);
+  };
+  if (T > 0) stage(0);
+  const uint32_t rot = (uint32_t)lane << 4;
+  for (int t = 0; t < T; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tree t have landed
+    __syncthreads();                                   // every wave's; and tree t - 1's buffer is free
+    if (t + 1 < T) stage(t + 1);
+    const char* buf = smem + (t & 1) * RFP_TREE;
+    const int16_t* enc = reinterpret_cast<const int16_t*>(buf);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (rw0 + 64 * g >= rend) break;  // (wave-uniform)
+      int nd = 0, f = enc[0];
+      while (f >= 0) {
+        const uint32_t w = f < 32 ? xlo[g] : xhi[g];
+        nd = 2 * nd + 1 + (int)((w >> (f & 31)) & 1u);
+        f = enc[nd];
+      }
+      const uint32_t lb = 1024u + (uint32_t)(-f - 1) * 256u;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const uint32_t off = lb | ((rot + 16u * c) & 0xF0u);
+        acc[g][c] += *reinterpret_cast<const f32x4*>(buf + off);
+      }
+    }
+  }
+  const float invT = 1.f / (float)(T > 0 ? T : 1);
+  (void)invT;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t r = rw0 + 64 * g + lane;
+    if (r >= rend) continue;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int k = (lane + c) & 15;  // output chunk held in register set c
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = 4 * k + e;
+        float pr = T > 0 ? acc[g][c][e] / (float)T : 0.f;
+        if (out_logit) {
+          const float pc = fminf(fmaxf(pr, 1e-7f), 1.f - 1e-7f);
+          pr = o < 62 ? __logf(pc / (1.f - pc)) : -30.f;
+        } else if (o >= 62) {
+          pr = 0.f;
+        }
+        v[e] = pr;
+      }
+      *reinterpret_cast<f32x4*>(out + r * ldo + 4 * k) = v;
+    }
+  }
+}
+
 }  // namespace
 
 EM_API int em_rf_nodes(int max_depth) { return (1 << (max_depth + 1)) - 1; }
@@ -1199,7 +1217,6 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   const size_t lds = (size_t)rec * 4;
   if (lds > 160 * 1024 - 8192) return EM_ERR_ARG;
   static bool attr = false;
-  static int mfma_env = -1, derive_env = 1, fuse_env = 1;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)rf_hist<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
@@ -1209,32 +1226,20 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
                               160 * 1024 - 8192);
     (void)hipFuncSetAttribute((const void*)rf_hist<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
-    (void)hipFuncSetAttribute((const void*)rf_hist_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024 - 8192);
-    // opt-in: on the record-form row lists the LDS-atomic histogram measured faster (fit 6.2 vs
-    // 7.0 ms, 700k rows x 100 trees, depth 8): the matrix-core form spends its time building
-    // operands bit by bit, not in the MFMAs
-    const char* e = std::getenv("EM_RF_MFMA");
-    mfma_env = (e && e[0] == '1') ? 1 : 0;
-    const char* d = std::getenv("EM_RF_DERIVE");  // 0: accumulate node totals at every level (A/B)
-    derive_env = (d && d[0] == '0') ? 0 : 1;
-    const char* fz = std::getenv("EM_RF_FUSE");  // 0: separate histogram pass at every level (A/B)
-    fuse_env = (fz && fz[0] == '0') ? 0 : 1;
     (void)hipFuncSetAttribute((const void*)rf_partition<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024 - 8192);
     attr = true;
   }
-  // record-form row lists for one-word features (rows_a/rows_b hold 16 B per row: em_rf_row_bytes);
-  // the matrix-core histogram on them for <= 15 candidates (bootstrap weight < 10: every operand is an
-  // exact bf16 integer)
+  // record-form row lists for one-word features (rows_a/rows_b hold 16 B per row: em_rf_row_bytes).
+  // Variants measured slower and removed in round 5 (docs/DESIGN.md §2 keeps their numbers): the
+  // matrix-core histogram (rf_hist_mfma: 7.0 vs 6.2 ms), node totals accumulated at every level instead
+  // of derived from the parent (8.45 vs 6.67 ms), a separate histogram pass at every level (6.0 vs
+  // 4.8-5.2 ms).
   const bool rec_rows = em_rf_row_bytes(W, F, N) == 16;
-  const bool use_mfma = rec_rows && mfma_env && k_feat <= 15;
-  const size_t lds_mfma = (size_t)(((rec + 3) & ~3) * 4) + 4096 + 4 * 1024;
   uint32_t* accs[2] = {acc, acc + (int64_t)T * (1ll << max_depth) * rec};
   int16_t* cands[2] = {cand, reinterpret_cast<int16_t*>(acc + 2 * (int64_t)T * (1ll << max_depth) * rec)};
-  const bool derive = derive_env && !use_mfma;
   // (the fused partition's replicated child images must fit the LDS: k <= ~70 candidates)
-  const bool fuse = derive && fuse_env && rec_rows && (size_t)2 * rf_chl_words(k_feat) * 4 <= 160 * 1024 - 8192 &&
+  const bool fuse = rec_rows && (size_t)2 * rf_chl_words(k_feat) * 4 <= 160 * 1024 - 8192 &&
                     (size_t)rf_init_lds_words(k_feat) * 4 <= 160 * 1024 - 8192;
   int32_t* yover = reinterpret_cast<int32_t*>(acc) + em_rf_acc_words(T, max_depth, k_feat) - 1;
   RfParams p{X, Y, N, W, F, T, max_depth, k_feat, min_leaf, bootstrap, t_off, nodes, seed, seg, feat, value, gain,
@@ -1310,11 +1315,9 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
     const unsigned G = (unsigned)(gmax < 0x7FFFFFFF ? gmax : 0x7FFFFFFF);
     (void)B;
     (void)hipMemsetAsync(p.acc, 0, (size_t)tn * rec * sizeof(uint32_t), stream);
-    const bool dl = derive && level > 0;
+    const bool dl = level > 0;  // node totals derived from the parent's histogram below the root
     if (dl) hipLaunchKernelGGL(rf_child_totals, dim3(nodesL, T), dim3(64), 0, stream, p, accs[(level - 1) & 1], level);
-    if (use_mfma)
-      hipLaunchKernelGGL(rf_hist_mfma, dim3(G), dim3(nt), lds_mfma, stream, p, (const RfRec*)rin, level, (const int32_t*)wl);
-    else if (dl && level == max_depth)
+    if (dl && level == max_depth)
       ;  // the last level needs node totals only: all derived
     else if (rec_rows && dl)
       hipLaunchKernelGGL((rf_hist<true, true>), dim3(G), dim3(nt), lds, stream, p, (const void*)rin, level, (const int32_t*)wl);
@@ -1344,12 +1347,51 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
   return 0;
 }
 
+// scratch bytes em_rf_predict's tree-streamed path needs (0: that path does not apply)
+EM_API int64_t em_rf_predict_scratch(int W, int T, int max_depth) {
+  return (W == 1 && max_depth <= 8 && T > 0) ? (int64_t)T * RFP_TREE : 0;
+}
+
+// prep: em_rf_predict_scratch(W, T, max_depth) bytes (16-B aligned), or null for the one-wave-per-row path
 EM_API int em_rf_predict(const uint64_t* X, int W, int64_t N, const int16_t* feat, const float* value, int T,
-                         int max_depth, int out_logit, float* out, int ldo, hipStream_t stream) {
+                         int max_depth, int out_logit, float* out, int ldo, void* prep, hipStream_t stream) {
   if (!X || !feat || !value || !out || W < 1 || N < 0 || T < 0 || ldo < 64 || max_depth < 0 || max_depth > 14)
     return EM_ERR_ARG;
   if (N == 0) return 0;
   const int nodes = (1 << (max_depth + 1)) - 1;
+  if (prep && em_rf_predict_scratch(W, T, max_depth) > 0 && ((uintptr_t)prep & 15) == 0 && (ldo & 3) == 0 &&
+      ((uintptr_t)out & 15) == 0) {
+    hipLaunchKernelGGL(rf_predict_prepare, dim3(T), dim3(64), 0, stream, feat, value, nodes, max_depth, (uint8_t*)prep);
+    EM_CHECK_LAUNCH();
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+      (void)hipFuncSetAttribute((const void*)rf_predict_lds<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * RFP_TREE);
+      (void)hipFuncSetAttribute((const void*)rf_predict_lds<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * RFP_TREE);
+      (void)hipFuncSetAttribute((const void*)rf_predict_lds<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * RFP_TREE);
+    }
+    // one workgroup per CU (the LDS double buffer), rows spread evenly; at most 3 x 64 rows per wave
+    int64_t grid = (N + 511) / 512;
+    if (grid > cus) grid = cus;
+    int64_t rpw = ((N + grid - 1) / grid + 7) / 8;
+    if (rpw > 192) {
+      rpw = 192;
+      grid = (N + 8 * rpw - 1) / (8 * rpw);
+    }
+    const int G = (int)((rpw + 63) / 64);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), 2 * RFP_TREE, stream, X, N, (const uint8_t*)prep, T,
+                         (int)rpw, 8 * rpw, out_logit, out, ldo);
+    };
+    if (G == 1) go(rf_predict_lds<1>);
+    else if (G == 2) go(rf_predict_lds<2>);
+    else go(rf_predict_lds<3>);
+    EM_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(rf_predict, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, stream, X, W, N, feat, value, T, nodes,
                      out_logit, out, ldo);
   EM_CHECK_LAUNCH();

@@ -29,16 +29,6 @@ constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand per stage
 constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;
 
-bool getenv_flag(const char* name) {
-  const char* v = std::getenv(name);
-  return v && v[0] == '1';
-}
-
-bool getenv_flag_off(const char* name) {
-  const char* v = std::getenv(name);
-  return v && v[0] == '0';
-}
-
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
 
 EM_DEVICE uint32_t kc_off(int row, int chunk) { return row * 128 + (((chunk ^ (row & 7))) << 4); }     // [128][64]
@@ -235,18 +225,11 @@ EM_DEVICE uint32_t g_off(int row, int chunk) { return row * 128 + ((chunk ^ ((ro
 // x 8192 GEMM instead of ~33 GB with whole tile-rows, whose 32 distinct B panels miss L2).
 // GM: tile-rows per group.  Measured (tools/gpurun_gemm_gm.sh, TF/s at GM = 1 / 2 / 4 / 8): without a
 // C^T output 4 is best (65536x8192x8192 forward 1353 / 1384 / 1413 / 1366, NT dgrad 1270 / 1311 /
-// 1341 / 1324); with C^T 8 is (forward+C^T 1256 / 1287 / 1314 / 1329).  EM_GEMM_GM overrides both.
-__constant__ int g_gm_c = 0;
-__constant__ int g_lead_c = 0;  // pp16 staging lead (0 or 2 slots) of G_LEAD=-1 builds; EM_GEMM_LEAD sets it
-// The lead is a compile-time constant: read at run time from g_lead_c (G_LEAD -1, the EM_GEMM_LEAD A/B
-// mode) it cost ~15 % of the kernel (fwd 1375 -> 1180 TF/s on one box, profiles/gemm_box_variance.md)
-#ifndef G_LEAD
-#define G_LEAD 0
-#endif
+// 1341 / 1324); with C^T 8 is (forward+C^T 1256 / 1287 / 1314 / 1329).
 
 template <int HAS_CT>
 EM_DEVICE void g_tile(int bid, int tiles_m, int tiles_n, int& m0, int& n0) {
-  const int GM = g_gm_c > 0 ? g_gm_c : (HAS_CT ? 8 : 4);
+  constexpr int GM = HAS_CT ? 8 : 4;
   const int per = GM * tiles_n;
   const int grp = bid / per, first = grp * GM;
   const int gm = tiles_m - first < GM ? tiles_m - first : GM;
@@ -317,185 +300,8 @@ EM_DEVICE uint32_t or_rows16(uint32_t v) {  // OR over the four 16-lane rows (sa
 }
 EM_DEVICE float bit_mul(uint32_t w, int b, float v) { return ((w >> b) & 1u) ? v : v * 0.f; }
 
-// OUT_BF16: 1 -> bf16 C (optionally + transposed C^T when HAS_CT), 0 -> fp32 C (+ beta * C_old)
-// FN: activation (DACT = 0, applied to alpha*acc + bias) or activation' (DACT = 1, multiplies
-// alpha*acc by act'(mask[m][n]))
-// Epilogue shared by the 256x256 kernels: acc[4][2] = this wave's 128x64 tile (wm, wn) of the
-// block tile at (m0, n0); LDS (>= G_EPI_LDS bytes) is free when called.
-template <int OUT_BF16, int FN, int DACT, int HAS_CT>
-EM_DEVICE void g_epilogue(f32x16 (&acc)[4][2], char* smem, int wave, int lane, int wm, int wn, int m0, int n0,
-                          void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct,
-                          const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                          float beta, float* __restrict__ colpart, int N, uint32_t* __restrict__ bits) {
-  const int r = lane & 31, h = lane >> 5;
-  // bf16 outputs go through a per-wave transposed LDS tile T[64 cols][32 rows] (ds_write_b64 of 4
-  // consecutive rows per lane), then leave as 16-B coalesced stores: C rows via ds_read_b64_tr_b16
-  // pairs (8 consecutive columns of one row), C^T rows straight from T.  DACT stages the matching
-  // 32x64 block of the saved activations with 16-B loads.
-  constexpr int TS = 80;                    // bytes per T row (32 bf16 + pad)
-  constexpr int YS = 144;                   // bytes per staged Y row (64 bf16 + pad)
-  constexpr int WEPI = 64 * TS + 32 * YS;   // per-wave epilogue bytes
-  char* tb = smem + wave * WEPI;
-  char* yb = tb + 64 * TS;
-  const int colw = n0 + wn * 64;
-  float cs[2] = {0.f, 0.f};  // column sums of the epilogue values over the wave's 128 rows (colpart)
-  constexpr bool WBITS = !DACT && FN == ACT_RELU && OUT_BF16;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // unrolled: acc[i] must stay statically indexed (no scratch)
-    const int rowb = m0 + wm * 128 + 32 * i;  // first row of this block
-    uint32_t bw[2] = {0u, 0u};  // DACT: the block's activity words of the lane's columns; WBITS: bits being built
-    if (DACT && bits) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bw[j] = bits[(int64_t)(rowb >> 5) * N + colw + 32 * j + r];
-    } else if (DACT) {
-      const __bf16* ysrc = mask + (int64_t)rowb * ldm + colw;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int q = lane + 64 * t;
-        const int row = q >> 3, ch = q & 7;
-        *reinterpret_cast<u32x4*>(yb + row * YS + ch * 16) =
-            *reinterpret_cast<const u32x4*>(ysrc + (int64_t)row * ldm + ch * 8);
-      }
-      wave_lds_sync();
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int lc = 32 * j + r;
-      const float bv = (!DACT && bias) ? bias[colw + lc] : 0.f;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float x[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int lr = 8 * g + 4 * h + e;
-          float v = alpha * acc[i][j][4 * g + e];
-          if (DACT) {
-            v = bits ? bit_mul(bw[j], lr, v) : v * g_dfn<FN>((float)*reinterpret_cast<const __bf16*>(yb + lr * YS + lc * 2));
-          } else {
-            v = g_fn<FN>(v + bv);
-            if (WBITS) bw[j] |= (v > 0.f ? 1u : 0u) << (8 * g + e);
-          }
-          x[e] = v;
-          cs[j] += v;
-          if (!OUT_BF16) {
-            float* cp = reinterpret_cast<float*>(C) + (int64_t)(rowb + lr) * ldc + colw + lc;
-            *cp = beta != 0.f ? v + beta * *cp : v;
-          }
-        }
-        if (OUT_BF16) {
-          __bf16 t4[4] = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
-          u32x2 pk;
-          __builtin_memcpy(&pk, t4, 8);
-          *reinterpret_cast<u32x2*>(tb + lc * TS + (8 * g + 4 * h) * 2) = pk;
-        }
-      }
-    }
-    if (WBITS && bits) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t w = or_xhalf(bw[j] << (4 * h));
-        if (h == 0) bits[(int64_t)(rowb >> 5) * N + colw + 32 * j + r] = w;
-      }
-    }
-    if (OUT_BF16) {
-      wave_lds_sync();
-      // C: group gg of 16 lanes covers rows 16*(gg&1)..+15, columns cb..cb+7 with cb = 8*(gg>>1) + 16*it
-      const int gg = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int cb = 8 * (gg >> 1) + 16 * it;
-        const int r0 = 16 * (gg & 1);
-        const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * TS + (r0 + 4 * p4) * 2));
-        const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * TS + (r0 + 4 * p4) * 2));
-        const bf16x8 v8 = cat_tr(lo, hi);
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + r0 + i16) * ldc + colw + cb) = v8;
-      }
-      if (HAS_CT) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = lane + 64 * k;
-          const int col = q >> 2, part = q & 3;
-          *reinterpret_cast<u32x4*>(CT + (int64_t)(colw + col) * ldct + rowb + part * 8) =
-              *reinterpret_cast<const u32x4*>(tb + col * TS + part * 16);
-        }
-      }
-    }
-    wave_lds_sync();  // T / Y blocks are rewritten by the next block
-  }
-  if (colpart) {  // bias gradient partials: row (m0 + 128 wm) / 128 of the [M / 128][N] fp32 partial array
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float t = xhalf_sum(cs[j]);
-      if (h == 0) colpart[(int64_t)((m0 >> 7) + wm) * N + colw + 32 * j + r] = t;
-    }
-  }
-}
-
-template <int OUT_BF16, int FN, int DACT, int HAS_CT>
-__global__ void __launch_bounds__(G_NT, 1)
-gemm256_nt_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
-                  void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
-                  const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta, float* __restrict__ colpart, uint32_t* __restrict__ bits) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = N / G_BN;
-  const int nwg = (M / G_BM) * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  int m0, n0;
-  g_tile<HAS_CT>(bid, M / G_BM, tiles_n, m0, n0);
-  const int ktiles = K / G_BK;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
-  g_stage(pa, 0, smem, wave_s);
-  g_stage(pb, 0, smem + G_TILE, wave_s);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int r = lane & 31, h = lane >> 5;
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const char* la = smem + (kt & 1) * 2 * G_TILE;
-    const char* lb = la + G_TILE;
-    if (kt + 1 < ktiles) {
-      char* na = smem + ((kt + 1) & 1) * 2 * G_TILE;
-      g_stage(pa, (kt + 1) * G_BK, na, wave_s);
-      g_stage(pb, (kt + 1) * G_BK, na + G_TILE, wave_s);
-    }
-#pragma unroll
-    for (int s = 0; s < G_BK / 16; ++s) {
-      bf16x8 a[4], b[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + 32 * i + r, 2 * s + h));
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + 32 * j + r, 2 * s + h));
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
-                                         alpha, beta, colpart, N, bits);
-}
-
 // ============================================================================================
-// 256x256 NT GEMM, ping-pong schedule (default large-shape path; the kernel above stays behind
-// EM_GEMM_PP=0 for A/B).  Same tile, waves, LDS image and epilogue; the K loop is restructured so
+// 256x256 NT GEMM, ping-pong schedule (the large-shape path).  The K loop is structured so
 // that the two waves sharing each SIMD alternate roles (cdna_hip_programming.md §5 "256² 8-phase
 // template", MI355X_MICROARCH.md "Two waves per SIMD"):
 //   * G0 = waves 0-3 (A rows 0-127), G1 = waves 4-7 (A rows 128-255); G1 starts one barrier late,
@@ -550,111 +356,6 @@ __device__ __forceinline__ bool pp_stage_slot(const GPanel& pa, const GPanel& pb
   return true;
 }
 
-template <int OUT_BF16, int FN, int DACT, int HAS_CT>
-__global__ void __launch_bounds__(G_NT, 1)
-gemm256_pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
-                  void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
-                  const float* __restrict__ bias, const __bf16* __restrict__ mask, int64_t ldm, float alpha,
-                  float beta, float* __restrict__ colpart, uint32_t* __restrict__ bits) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = N / G_BN;
-  const int nwg = (M / G_BM) * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  int m0, n0;
-  g_tile<HAS_CT>(bid, M / G_BM, tiles_n, m0, n0);
-  const int ktiles = K / G_BK;
-  const int nph = 4 * ktiles;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  const int wi = wave_s & 3;
-  const bool g1 = wave_s >= 4;
-  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
-  // prologue: K-tile 0 by all waves, then the K-tile-1 units of slots -4 (G1), -3 (G0), -2 (G1)
-  g_stage(pa, 0, smem, wave_s);
-  g_stage(pb, 0, smem + G_TILE, wave_s);
-  if (g1) {
-    const bool a = pp_stage_slot(pa, pb, smem, -4, ktiles, wi);
-    const bool b = pp_stage_slot(pa, pb, smem, -2, ktiles, wi);
-    if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    if (pp_stage_slot(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  const int r = lane & 31, h = lane >> 5;
-  bf16x8 fa[2][4], fb[4];
-  // load segment of phase g (slot `slot`): fragments for phase g (if any), stage, wait, barrier
-  auto load_seg = [&](int g, int slot) {
-    if (g < nph) {
-      const int kt = g >> 2, q = g & 3, qm = q & 1, qn = q >> 1;
-      const char* la = smem + (kt & 1) * 2 * G_TILE;
-      const char* lb = la + G_TILE;
-      if (qm == 0) {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) fb[ks] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + qn * 32 + r, 2 * ks + h));
-      }
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          fa[ii][ks] = *reinterpret_cast<const bf16x8*>(la + g_off(wm * 128 + qm * 64 + 32 * ii + r, 2 * ks + h));
-    }
-    if (pp_stage_slot(pa, pb, smem, slot, ktiles, wi)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  // MFMA segment of phase g: quadrant (qm, qn) += A frags x B frags over the K-tile
-  auto mfma_seg = [&](int q) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        f32x16& c = acc[2 * (q & 1) + ii][q >> 1];
-        c = mfma32(fa[ii][ks], fb[ks], c);
-      }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-  };
-
-  if (!g1) {
-    load_seg(0, -1);
-    for (int kt = 0; kt < ktiles; ++kt) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int g = 4 * kt + q;
-        mfma_seg(q);
-        load_seg(g + 1, 2 * g + 1);
-      }
-    }
-  } else {
-    __builtin_amdgcn_s_barrier();  // the stagger: G1 sits out slot -1
-    for (int kt = 0; kt < ktiles; ++kt) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int g = 4 * kt + q;
-        load_seg(g, 2 * g);
-        mfma_seg(q);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  g_epilogue<OUT_BF16, FN, DACT, HAS_CT>(acc, smem, wave, lane, wm, wn, m0, n0, C, ldc, CT, ldct, bias, mask, ldm,
-                                         alpha, beta, colpart, N, bits);
-}
-
 // --------------------------------------------------------------------------------------------
 // The same ping-pong K loop on v_mfma_f32_16x16x32_bf16 (16 cycles, 16x16 output per instruction).
 // Same LDS image, staging units, slot schedule and quadrant order; per phase a wave runs
@@ -670,6 +371,9 @@ EM_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// OUT_BF16: 1 -> bf16 C (optionally + transposed C^T when HAS_CT), 0 -> fp32 C (+ beta * C_old)
+// FN: activation (DACT = 0, applied to alpha*acc + bias) or activation' (DACT = 1, multiplies
+// alpha*acc by act'(mask[m][n]))
 // G_CROW = 1: bf16 C rows leave through a row image, 8 lanes per 128-B row (see gemm_k64_kernel)
 #ifndef G_CROW
 #define G_CROW 1
@@ -816,7 +520,7 @@ __device__ uint64_t g_gstamps[G_STAMP_BLOCKS * 8 * 8];
 #define G_MARK(t) (void)0
 #endif
 
-// BAL = 1 spreads the fragment reads evenly over the four load segments of a K-tile (at most 8
+// The fragment reads are spread evenly over the four load segments of a K-tile (at most 8
 // ds_read_b128 per wave instead of 12, 8, 4, 0): phase 3's segment reads the NEXT K-tile's A(qm 0)
 // half into fa[0] (free during phase 3, which runs on fa[1] x B(qn 1)), so phase 0 reads only
 // B(qn 0).  In phase 0 the loading group's 12 reads + the LDS-DMA unit filled the LDS array for the
@@ -824,7 +528,7 @@ __device__ uint64_t g_gstamps[G_STAMP_BLOCKS * 8 * 8];
 // A0 / A2 of K-tile kt+1 are issued in slots 8kt-2 / 8kt-1 (-10 / -9 relative to 8(kt+1)), so they are
 // readable from 8kt+5 / 8kt+6 -- exactly the slots in which G0 / G1 read phase 3 of kt; their last read
 // now sits 3 slots earlier than before, so the WAR distance to the restage only grows.
-template <int OUT_BF16, int FN, int DACT, int HAS_CT, int BAL>
+template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                     void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
@@ -859,35 +563,16 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
   g_stage(pa, 0, smem, wave_s);
   g_stage(pb, 0, smem + G_TILE, wave_s);
-  // LEAD (g_lead_c = 2): every unit is issued 2 slots earlier than its scheduled slot and waited
-  // with vmcnt(8) instead of vmcnt(6), so it has 8 slots instead of 6 to land while the slot in
-  // which it becomes readable is unchanged (RAW as above); a restage comes 2 slots closer to the
-  // last read of the unit it overwrites, which still leaves >= 2 slots (B lo: restaged exactly 2
-  // slots after its last read).  The prologue then also issues the units of slots -1 (G0) and 0 (G1).
-  const bool lead = G_LEAD < 0 ? g_lead_c != 0 : G_LEAD != 0;
+  // (issuing every unit 2 slots ahead of its schedule with vmcnt(8) -- a staging "lead" -- measured
+  // mixed, +-1.5 %, and was removed in round 5; docs/DESIGN.md §6)
   if (g1) {
     const bool a = pp_stage_slot(pa, pb, smem, -4, ktiles, wi);
     const bool b = pp_stage_slot(pa, pb, smem, -2, ktiles, wi);
-    if (lead) {
-      const bool c = pp_stage_slot(pa, pb, smem, 0, ktiles, wi);
-      if (a && b && c) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (a && b) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    const bool a = pp_stage_slot(pa, pb, smem, -3, ktiles, wi);
-    if (lead) {
-      const bool b = pp_stage_slot(pa, pb, smem, -1, ktiles, wi);
-      if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (a) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (pp_stage_slot(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
 
@@ -909,10 +594,10 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
           for (int ks = 0; ks < 2; ++ks)
             fb[jj][ks] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + (q >> 1) * 32 + 16 * jj + r16, 4 * ks + c4));
       }
-      const bool rd_a = BAL ? (q == 1 || (q == 0 && kt == 0) || (q == 3 && kt + 1 < ktiles)) : q < 2;
+      const bool rd_a = q == 1 || (q == 0 && kt == 0) || (q == 3 && kt + 1 < ktiles);
       if (rd_a) {
         const int qa = q & 1;  // q == 3 reads qm 0 of the next K-tile
-        const char* lsrc = (BAL && q == 3) ? smem + ((kt + 1) & 1) * 2 * G_TILE : la;
+        const char* lsrc = q == 3 ? smem + ((kt + 1) & 1) * 2 * G_TILE : la;
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -921,7 +606,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
                 *reinterpret_cast<const bf16x8*>(lsrc + g_off(wm * 128 + (qa ^ (q == 3)) * 64 + 16 * ii + r16, 4 * ks + c4));
       }
     }
-    const bool staged = pp_stage_slot(pa, pb, smem, lead ? slot + 2 : slot, ktiles, wi);
+    const bool staged = pp_stage_slot(pa, pb, smem, slot, ktiles, wi);
     if (G_STAMPS) {
       uint64_t t;
       G_MARK(t);
@@ -929,7 +614,6 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
       st_a = t;
     }
     if (!staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (lead) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     if (G_STAMPS) {
       uint64_t t;
@@ -1025,33 +709,12 @@ template <int OUT_BF16, int FN, int DACT, int HAS_CT>
 int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
              int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
              int64_t ldm, float alpha, float beta, float* colpart, uint32_t* bits) {
+  // (the 32x32x16 ping-pong kernel, the non-ping-pong 256 kernel and the unbalanced fragment-read
+  // schedule were measured slower and removed in round 5; docs/DESIGN.md §2 and §6 keep their numbers)
   static bool attr = false;
-  static const bool pp = !getenv_flag_off("EM_GEMM_PP");
-  static const bool m16 = !getenv_flag_off("EM_GEMM_MFMA16");
-  static const bool bal = !getenv_flag_off("EM_GEMM_BAL");
-  auto kern = pp ? (m16 ? (bal ? gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 1>
-                               : gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 0>)
-                        : gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>)
-                 : gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>;
+  auto kern = gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT>;
   if (!attr) {
-    static const char* gm_env = getenv("EM_GEMM_GM");
-    if (gm_env) {
-      const int gm = atoi(gm_env);
-      if (gm >= 1 && gm <= 64) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gm_c), &gm, sizeof(int));
-    }
-    static const char* lead_env = getenv("EM_GEMM_LEAD");
-    if (lead_env) {
-      const int ld = atoi(lead_env) ? 1 : 0;
-      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lead_c), &ld, sizeof(int));
-    }
-    (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, 0>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm256_pp_kernel<OUT_BF16, FN, DACT, HAS_CT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm256_nt_kernel<OUT_BF16, FN, DACT, HAS_CT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     attr = true;
   }
   hipLaunchKernelGGL(kern, grid, dim3(G_NT), G_LDS, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm,
@@ -1329,12 +992,9 @@ int k64_launch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, in
 int k64_dispatch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
                  __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act, const __bf16* mask,
                  int64_t ldm, int dact, float alpha, float* colpart, uint32_t* bits) {
-  static const bool crow = !getenv_flag_off("EM_K64_CROW");
-#define EM_K(FN, DA, CTV)                                                                                             \
-  return crow ? k64_launch<FN, DA, CTV, 1>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha,      \
-                                           colpart, bits)                                                              \
-              : k64_launch<FN, DA, CTV, 0>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha,      \
-                                           colpart, bits)
+  // (CROW = 0, the direct 16-B-per-line store form, measured slower: docs/DESIGN.md §6)
+#define EM_K(FN, DA, CTV) \
+  return k64_launch<FN, DA, CTV, 1>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits)
   const bool ct = CT != nullptr;
   if (mask || dact) {
     if (act != ACT_NONE) return EM_ERR_ARG;
@@ -1640,12 +1300,10 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
     attr = true;
   }
   const bool big = splits == 1 && a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
-                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && !getenv_flag("EM_GEMM_SMALL") &&
+                   (((uintptr_t)A | (uintptr_t)B) & 15) == 0 &&
                    (c_bf16 || (act == ACT_NONE && !mask));  // fp32 + act / act' epilogues: any-layout kernel
-  // skinny K (64 / 128) with a bf16 output: the store-stream kernel (see gemm_k64_kernel); EM_GEMM_K64=0
-  // keeps the 256-tile path for A/B
-  static const bool k64_on = !getenv_flag_off("EM_GEMM_K64");
-  if (big && k64_on && c_bf16 && (K == 64 || K == 128) && beta == 0.f) {
+  // skinny K (64 / 128) with a bf16 output: the store-stream kernel (see gemm_k64_kernel)
+  if (big && c_bf16 && (K == 64 || K == 128) && beta == 0.f) {
     const int rc = k64_dispatch(stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, (__bf16*)C, ldc, (__bf16*)ct,
                                 ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha, colpart, bits);
     if (rc) return rc;

@@ -19,7 +19,8 @@ N.register_signatures({
                            N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p, N._c_void_p,
                            N._c_void_p]),
     "em_rf_predict": (N._i32, [N._c_void_p, N._i32, N._i64, N._c_void_p, N._c_void_p, N._i32, N._i32, N._i32,
-                               N._c_void_p, N._i32, N._c_void_p]),
+                               N._c_void_p, N._i32, N._c_void_p, N._c_void_p]),
+    "em_rf_predict_scratch": (N._i64, [N._i32, N._i32, N._i32]),
 })
 
 
@@ -67,8 +68,11 @@ def fit(X: np.ndarray | torch.Tensor, Y: np.ndarray | torch.Tensor, F: int, t_of
     return feat.cpu().numpy(), value.cpu().numpy(), gain.cpu().numpy(), cover.cpu().numpy()
 
 
-def predict(X, feat, value, max_depth: int, out_logit: bool = False, device="cuda") -> torch.Tensor:
-    """K11: mean leaf vector per row -> [N, 64] fp32 (probabilities, or logits if out_logit)."""
+def predict(X, feat, value, max_depth: int, out_logit: bool = False, device="cuda", stream_trees: bool = True
+            ) -> torch.Tensor:
+    """K11: mean leaf vector per row -> [N, 64] fp32 (probabilities, or logits if out_logit).
+    ``stream_trees``: single-word rows and depth <= 8 stream the trees through LDS (csrc/forest.hip
+    rf_predict_lds, bit-identical); False forces the one-wave-per-row kernel."""
     dev = torch.device(device)
     Xd = X if isinstance(X, torch.Tensor) else _u64_to_device(X, dev)
     n = Xd.shape[0]
@@ -79,6 +83,8 @@ def predict(X, feat, value, max_depth: int, out_logit: bool = False, device="cud
     if fd.shape[1] != (1 << (max_depth + 1)) - 1:
         raise ValueError("feat does not match max_depth")
     out = torch.empty(n, 64, dtype=torch.float32, device=dev)
+    nb = N.lib().em_rf_predict_scratch(W, T, max_depth) if stream_trees else 0
+    prep = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev) if nb > 0 else None
     N.call("em_rf_predict", Xd.data_ptr(), W, n, fd.data_ptr(), vd.data_ptr(), T, max_depth, int(out_logit),
-           out.data_ptr(), 64, N.stream_handle(dev))
+           out.data_ptr(), 64, prep.data_ptr() if prep is not None else None, N.stream_handle(dev))
     return out

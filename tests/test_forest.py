@@ -91,8 +91,7 @@ def test_tree_ids_make_shards_compose(draws):
 
 @pytest.mark.gpu
 # one feature word: record-form row lists (sqrt / log2 / all); two words (lags 2): index form.  Every
-# histogram kernel must reproduce the oracle exactly (test_hip_forest_mfma_histogram_matches_oracle
-# runs the matrix-core one)
+# histogram kernel must reproduce the oracle exactly
 @pytest.mark.parametrize("depth,subset,boot,lags", [(5, "sqrt", True, 1), (3, "all", False, 1), (6, "0.3", True, 2),
                                                    (7, "log2", False, 1), (8, "sqrt", True, 1), (0, "sqrt", True, 1),
                                                    (1, "sqrt", True, 1), (2, "log2", False, 1)])
@@ -158,29 +157,29 @@ def test_hip_forest_predict_matches_torch_traversal(depth):
 
 
 @pytest.mark.gpu
-def test_hip_forest_mfma_histogram_matches_oracle():
-    """EM_RF_MFMA=1 (the matrix-core histogram, rf_hist_mfma) in a fresh process: trees equal the oracle's."""
-    import os
-    import subprocess
-    import sys
+@pytest.mark.parametrize("depth,trees,n", [(8, 100, 1), (8, 100, 777), (3, 37, 70001), (8, 100, 300001),
+                                           (6, 129, 600000)])
+def test_hip_forest_predict_streamed_bit_identical(depth, trees, n):
+    """The tree-streamed predict (rf_predict_lds: LDS double-buffered trees, lane = row, rotated chunk
+    order) equals the one-wave-per-row kernel bit for bit, for probabilities and logits, over row counts
+    that give 1, 2 and 3 row groups per wave (and a grid past one workgroup per CU)."""
+    import torch
 
-    code = (
-        "import numpy as np\n"
-        "from euromillioner_amd.data.draws import DrawSet\n"
-        "from euromillioner_amd.models.forest import RandomForest, draw_features\n"
-        "ds = DrawSet.synthetic(n=3000, seed=2, planted=0.7, calendar=False)\n"
-        "X, Y, F = draw_features(ds.numbers, 1)\n"
-        "for depth, subset, boot in ((5, 'sqrt', True), (7, 'log2', False)):\n"
-        "    g = RandomForest(n_trees=10, max_depth=depth, feature_subset=subset, bootstrap=boot, seed=11, device='cuda')\n"
-        "    g.fit(X, Y, F)\n"
-        "    c = RandomForest(n_trees=10, max_depth=depth, feature_subset=subset, bootstrap=boot, seed=11, device='cpu')\n"
-        "    c.fit(X, Y, F)\n"
-        "    assert np.array_equal(g.feat, c.feat) and np.array_equal(g.gain, c.gain)\n"
-        "print('MFMA_RF_OK')\n")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, EM_RF_MFMA="1", PYTHONPATH=root),
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "MFMA_RF_OK" in r.stdout, r.stderr[-2000:]
+    from euromillioner_amd.data.draws import mask_bits
+    from euromillioner_amd.data.synthetic import generate_draws
+    from euromillioner_amd.ops import forest as K
+
+    nums, _ = generate_draws(20001, seed=1, planted=0.9, native=False)
+    md = torch.from_numpy(mask_bits(nums).view(np.int64)).cuda()
+    n_tr = 14000
+    feat, value, _, _ = K.fit(md[:n_tr].reshape(-1, 1).contiguous(), md[1:n_tr + 1].contiguous(), 62, 0, trees, depth,
+                              8, 1, True, 0, return_device=True)
+    g = torch.Generator(device="cuda").manual_seed(n)
+    Xv = md[torch.randint(0, 20000, (n,), device="cuda", generator=g)].reshape(-1, 1).contiguous()
+    for logit in (False, True):
+        a = K.predict(Xv, feat, value, depth, out_logit=logit)
+        b = K.predict(Xv, feat, value, depth, out_logit=logit, stream_trees=False)
+        assert torch.equal(a, b), (logit, float((a - b).abs().max()))
 
 
 @pytest.mark.gpu
