@@ -218,7 +218,7 @@ def main():
 
         import torch.distributed as dist
 
-        if a.dist_backend == "nccl":
+        if a.dist_backend == "nccl" and a.model == "mlp-wide":  # bucketed all-reduces beside the GEMMs
             from euromillioner_amd.parallel.dist import high_priority_comm
 
             high_priority_comm()

@@ -138,7 +138,20 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
 // thread (quad, e) adds the 16 group sums in group order.  The fixed summation order keeps the result
 // bitwise reproducible; the single-GPU step (adam_slab4_kernel) and the fused xGMI DP step
 // (adam_slab_xgmi_kernel) share it, so their per-rank gradients are bit-identical.
-constexpr int A4_T = 256, A4_G = 16;
+// (compile-time A/B knobs for side builds, tools/build_variant.sh: ADAM_G slab groups per block ->
+// 16 * ADAM_G threads, 256 / ADAM_G loads in flight per thread; ADAM_NT nontemporal slab loads)
+#ifndef ADAM_G
+#define ADAM_G 16
+#endif
+#ifndef ADAM_NT
+#define ADAM_NT 0
+#endif
+constexpr int A4_G = ADAM_G, A4_T = 16 * A4_G, A4_U = 256 / A4_G;
+static_assert(A4_U >= 4 && A4_U * A4_G == 256, "slab groups");
+EM_DEVICE f32x4 slab_ld(const float* p) {
+  if (ADAM_NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return *reinterpret_cast<const f32x4*>(p);
+}
 struct Slab4Out {
   float g = 0.f;                  // threads < 64: grad_scale * sum over slabs of parameter blockIdx.x * 64 + t
   float w0 = 0.f, m0 = 0.f, v0 = 0.f;  // threads < 64 (with adam): the Adam operands, loaded under the slab loads
@@ -160,22 +173,22 @@ EM_DEVICE Slab4Out slab4_reduce(int j, const float* __restrict__ slabs, int nsla
   }
   f32x4 acc[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
   int sl = g;
-  for (; sl + 15 * A4_G < nslab; sl += 16 * A4_G) {
-    f32x4 t[16];
+  for (; sl + (A4_U - 1) * A4_G < nslab; sl += A4_U * A4_G) {
+    f32x4 t[A4_U];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t[k] = *reinterpret_cast<const f32x4*>(src + (size_t)(sl + k * A4_G) * stride);
+    for (int k = 0; k < A4_U; ++k) t[k] = slab_ld(src + (size_t)(sl + k * A4_G) * stride);
     if (sl == g && adam && threadIdx.x < 64) {  // the fp64 chain runs while the loads are in flight
       o.bc1 = bias_correction(hp[1], tstep);
       o.bc2 = bias_correction(hp[2], tstep);
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc[k & 3] += t[k];
+    for (int k = 0; k < A4_U; ++k) acc[k & 3] += t[k];
   }
-  if (nslab <= g + 15 * A4_G && adam && threadIdx.x < 64) {  // (no full block of slabs above)
+  if (nslab <= g + (A4_U - 1) * A4_G && adam && threadIdx.x < 64) {  // (no full block of slabs above)
     o.bc1 = bias_correction(hp[1], tstep);
     o.bc2 = bias_correction(hp[2], tstep);
   }
-  for (; sl < nslab; sl += A4_G) acc[0] += *reinterpret_cast<const f32x4*>(src + (size_t)sl * stride);
+  for (; sl < nslab; sl += A4_G) acc[0] += slab_ld(src + (size_t)sl * stride);
   part[g][q] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (threadIdx.x < 64) {

@@ -181,6 +181,11 @@ constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (
 constexpr int HIST_EXACT_LDS_BUDGET = HIST_LDS_BUDGET;
 constexpr int HIST_EXACT_THREADS = 256;
 constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
+// rows per histogram chunk at least HIST_MIN_CHUNK (compile-time A/B knob for side builds,
+// tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk)
+#ifndef HIST_MIN_CHUNK
+#define HIST_MIN_CHUNK 64
+#endif
 
 __global__ void __launch_bounds__(HIST_EXACT_THREADS)
 gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const float* __restrict__ h,
@@ -858,6 +863,15 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
   GSTAMP(16 * level + 4);
   if (!fin.tctr) return;
   __shared__ int last;
+  // Memory-model note: there is no release/acquire pair here.  The hand-off is the gfx950
+  // "write-through stores + drained vmcnt + relaxed arrival" form (MI355X_MICROARCH.md, Workgroup
+  // dispatch / inter-workgroup visibility, "Valid forms" table row 1): ONE lane made every store of the
+  // handed-off bytes as an agent-scope (sc1, write-through) store, waited vmcnt(0) (inline asm, so the
+  // compiler cannot drop or move it), then added to the per-task counter; the last adder's block reads
+  // them back with agent-scope (sc1, L1-bypassing) loads after a workgroup barrier.  That ordering is a
+  // property of gfx9 cache hardware measured on MI355X, not of the HIP memory model: on any other
+  // target this must become an agent-scope release add / acquire fence.  The guards are
+  // tests/test_gbdt.py (fused vs separate launches, bit-identical) and the separate-launch path.
   if (threadIdx.x == 0) {  // (this block's write-through stores have completed before its arrival)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     last = __hip_atomic_fetch_add(fin.tctr + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nodesL - 1;
@@ -1296,7 +1310,7 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
         const int64_t cap = HIST_PARTIAL_CAP / S;
         want = want > cap ? cap : want;
         int64_t chunk = (n + want - 1) / want;
-        chunk = chunk < 64 ? 64 : chunk;
+        chunk = chunk < HIST_MIN_CHUNK ? HIST_MIN_CHUNK : chunk;
         pl.chunk = (int)chunk;
         pl.nchunks = (int)((n + chunk - 1) / chunk);
         // staged rows: (g, h) floats + node id (exact); (qg, qh) int64 + node id + the piece's bin

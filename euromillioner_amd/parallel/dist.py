@@ -43,11 +43,15 @@ def high_priority_comm() -> None:
     """RCCL's stream at high priority (before the process group is created): the bucketed gradient
     all-reduces of the wide trainer are issued while the backward GEMMs fill the chip, and a
     normal-priority collective queues behind them until the backward ends (the exposed tail in
-    profiles/wide_dp_overlap.md).  An explicit TORCH_NCCL_HIGH_PRIORITY in the environment wins."""
+    profiles/wide_dp_overlap.md).  Only the GEMM engine asks for it (``init(high_priority=True)``,
+    bench.py --model mlp-wide): the fused small-MLP step and the GBDT run their collectives between
+    launches, where the priority was never measured.  An explicit TORCH_NCCL_HIGH_PRIORITY
+    in the environment wins."""
     os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
 
 
-def init(backend: str = "auto", timeout_s: float = 300.0, device: str = "auto") -> DistInfo:
+def init(backend: str = "auto", timeout_s: float = 300.0, device: str = "auto",
+         high_priority: bool = False) -> DistInfo:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -63,7 +67,8 @@ def init(backend: str = "auto", timeout_s: float = 300.0, device: str = "auto") 
         kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
         if be == "nccl":
             kw["device_id"] = dev
-            high_priority_comm()
+            if high_priority:
+                high_priority_comm()
         dist.init_process_group(be, **kw)
     return DistInfo(rank, world, local, be, dev)
 

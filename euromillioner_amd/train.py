@@ -383,7 +383,9 @@ def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
 
 def train_mlp(cfg: RunConfig) -> dict:
     log = L.get("Trainer")
-    info = D.init(cfg.dist.backend, cfg.dist.timeout_s, device=cfg.device)
+    # RCCL at high stream priority only for the GEMM engine's bucketed all-reduces (parallel/dist.py)
+    gemm_like = _mlp_sizes(cfg) != (62 * cfg.data.lags, 128, 62) or bool(cfg.dist.avg_frequency)
+    info = D.init(cfg.dist.backend, cfg.dist.timeout_s, device=cfg.device, high_priority=gemm_like)
     try:
         return _train_mlp(cfg, info, log)
     finally:
@@ -517,7 +519,11 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
             # --avg-frequency: rank 0's local parameters and moments are not the model every rank
             # resumes from after a restart, so a checkpoint between averaging points averages first
             # (collective; at fixed steps, so a restarted run and an uninterrupted one take the same
-            # averages and stay bit-identical)
+            # averages and stay bit-identical).  Limitation: that extra average is part of
+            # the trajectory, so with --avg-frequency k a run with --ckpt-every c (c not a multiple of
+            # k) differs from the same run without checkpoints; choose c a multiple of k to keep Spark
+            # ParameterAveraging's schedule exactly (tests/test_dist.py
+            # test_ckpt_at_averaging_points_keeps_trajectory)
             if engine.avg_k > 0 and engine.n_local % engine.avg_k != 0 and info.is_dist:
                 engine.average_parameters()
             if info.rank == 0:

@@ -266,3 +266,16 @@ def test_cli_pipeline_data_parallel(tmp_path):
     lines1 = [l for l in outs[1][1].splitlines() if l.strip() in ("true", "false")]
     assert len(lines0) == 1 and not lines1
     assert '"world_size": 2' in outs[0][1]
+
+
+def test_ckpt_at_averaging_points_keeps_trajectory(tmp_path):
+    """with --avg-frequency k, checkpoints taken at averaging points (--ckpt-every a multiple
+    of k) add no collective, so the run is bit-identical to the same run without intermediate
+    checkpoints (a checkpoint between averaging points averages first: documented in train.py)."""
+    a, b = str(tmp_path / "plain.zip"), str(tmp_path / "ckpt.zip")
+    common = ["--steps", "8", "--batch", "128", "--lr", "0.01", "--avg-frequency", "2"]
+    _ok(_launch(_train_argv(common + ["--ckpt", a]), 2))
+    _ok(_launch(_train_argv(common + ["--ckpt", b, "--ckpt-every", "4"]), 2))
+    pa, pb = _params(a), _params(b)
+    for x, y in zip(pa[:3], pb[:3]):
+        assert np.array_equal(x, y), np.abs(x - y).max()
