@@ -48,10 +48,9 @@ EM_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
-// Replayed rounds (em_gbdt_fit's hipGraph path): `rd` points at the device round counter and the
-// per-round tree arrays / history / predict range are offset by it in-kernel, so every round is the
-// same kernel sequence; the eager paths pass rd = nullptr and pre-offset pointers.
-EM_DEVICE int64_t rd_off(const int* rd, int64_t stride) { return rd ? (int64_t)(*rd) * stride : 0; }
+// (Round 4's hipGraph-replayed rounds, which offset every per-round array by a device round counter,
+// measured slower than the eager stream -- 0.056 vs 0.049 s on the reference fit -- and were removed
+// in round 5 together with that counter; docs/DESIGN.md §6c keeps the numbers.)
 
 // GBDT_STAMPS=1 builds (tools/build_variant.sh): block 0's wall clock at phase boundaries of the round
 // kernels, slot = kernel base + phase (em_gbdt_stamps copies them out); compiled out otherwise
@@ -82,12 +81,7 @@ EM_DEVICE void round_init_elem(int i, int8_t* st, int16_t* fe, uint8_t* sb, floa
 
 // per-round tree reset: status/feature/bin/gain cleared, every task's root opened (status 2)
 __global__ void gbdt_round_init(int8_t* __restrict__ st, int16_t* __restrict__ fe, uint8_t* __restrict__ sb,
-                                float* __restrict__ gn, int total, int NN, const int* __restrict__ rd) {
-  const int64_t o = rd_off(rd, total);
-  st += o;
-  fe += o;
-  sb += o;
-  gn += o;
+                                float* __restrict__ gn, int total, int NN) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
     round_init_elem(i, st, fe, sb, gn, NN);
 }
@@ -127,8 +121,7 @@ EM_DEVICE void grad_elem(int64_t i, const float* __restrict__ margin, const floa
 
 __global__ void gbdt_grad(const float* __restrict__ margin, const float* __restrict__ Y, float* __restrict__ g,
                           float* __restrict__ h, int16_t* __restrict__ node, int T, int n, int obj, float subsample,
-                          uint32_t seed, int round, const int* __restrict__ rd) {
-  if (rd) round = *rd;
+                          uint32_t seed, int round) {
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
     grad_elem(i, margin, Y, g, h, node, T, n, obj, subsample, seed, round);
@@ -139,13 +132,7 @@ __global__ void gbdt_round_start(int8_t* __restrict__ st, int16_t* __restrict__ 
                                  float* __restrict__ gn, int TNN, int NN, const float* __restrict__ margin,
                                  const float* __restrict__ Y, float* __restrict__ g, float* __restrict__ h,
                                  int16_t* __restrict__ node, int T, int n, int obj, float subsample, uint32_t seed,
-                                 int round, const int* __restrict__ rd) {
-  if (rd) round = *rd;
-  const int64_t o = rd_off(rd, TNN);
-  st += o;
-  fe += o;
-  sb += o;
-  gn += o;
+                                 int round) {
   const int64_t total = (int64_t)T * n;
   const int64_t all = total > TNN ? total : TNN;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < all; i += (int64_t)gridDim.x * blockDim.x) {
@@ -192,7 +179,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
           int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, int stage_rows,
           int16_t* __restrict__ node_out, const int8_t* __restrict__ pst, const int16_t* __restrict__ pfe,
-          const uint8_t* __restrict__ psb, int NN, const int* __restrict__ rd) {
+          const uint8_t* __restrict__ psb, int NN) {
   // stage_rows > 0: each piece's bin rows are staged in LDS with 16-B loads (one round trip instead of
   // one per 8 rows of byte loads); the host sets it when a piece's rows fit (stage_rows * F <= 16 KB).
   // node_out != nullptr (level >= 1): the rows' nodes are the previous level's partition, applied here
@@ -217,7 +204,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   const int pf = (first - 1) >> 1, npn = node_out ? first - pf : 0;
   u32x4* sbw = reinterpret_cast<u32x4*>(reinterpret_cast<char*>(ptree) + (((size_t)npn * 4 + 15) & ~(size_t)15));
   if (npn) {
-    const int64_t k0 = rd_off(rd, (int64_t)T * NN) + (int64_t)t * NN + pf;
+    const int64_t k0 = (int64_t)t * NN + pf;
     for (int i = threadIdx.x; i < npn; i += blockDim.x)
       ptree[i] = (int32_t)(uint8_t)pst[k0 + i] | ((int32_t)psb[k0 + i] << 8) | ((int32_t)pfe[k0 + i] << 16);
   }
@@ -630,6 +617,7 @@ struct SplitFinal {
 };
 EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma);
 constexpr int SPLIT_FINAL_MAX_DEPTH = 8;
+constexpr int EM_GBDT_SEPARATE = 1;  // em_gbdt_fit launch_flags: the separate launches instead of the fused round
 constexpr int SPLIT_ONESHOT_LDS = 48 * 1024;  // chunk partials staged at once up to this many bytes (+ the
                                               // finalize's <= 12 KB: within the default 64 KB)  // the fused finalize stages NN <= 511 nodes (23 B each) in LDS
 
@@ -638,13 +626,8 @@ __global__ void __launch_bounds__(256)
 gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
            int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
            int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
-           double qinv, const int* __restrict__ rd, SplitFinal fin, int oneshot, int pscan) {
+           double qinv, SplitFinal fin, int oneshot, int pscan) {
   constexpr bool Q = std::is_same<A, long long>::value;
-  const int64_t ro = rd_off(rd, (int64_t)T * NN);
-  status += ro;
-  feat += ro;
-  sbin += ro;
-  gain += ro;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
   const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
@@ -903,21 +886,15 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
   for (int k = threadIdx.x; k < NN; k += blockDim.x) {
     st[k] = sst[k];
     feat[o + k] = sfe[k];
-    fin.leaf[ro + o + k] = sst[k] == 2 ? (float)(-sG[k] / (sH[k] + lam) * fin.eta) : 0.f;
-    fin.cover[ro + o + k] = sst[k] ? (float)sH[k] : 0.f;
+    fin.leaf[o + k] = sst[k] == 2 ? (float)(-sG[k] / (sH[k] + lam) * fin.eta) : 0.f;
+    fin.cover[o + k] = sst[k] ? (float)sH[k] : 0.f;
   }
   GSTAMP(16 * level + 5);
 }
 
 __global__ void gbdt_partition(const uint8_t* __restrict__ bins, int16_t* __restrict__ node, int T, int n, int F,
                                int NN, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
-                               const uint8_t* __restrict__ sbin, int level, const int* __restrict__ rd) {
-  {
-    const int64_t o = rd_off(rd, (int64_t)T * NN);
-    status += o;
-    feat += o;
-    sbin += o;
-  }
+                               const uint8_t* __restrict__ sbin, int level) {
   const int first = (1 << level) - 1, last = (1 << (level + 1)) - 1;
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -934,18 +911,9 @@ __global__ void gbdt_partition(const uint8_t* __restrict__ bins, int16_t* __rest
 // one thread per task: prune (gamma) bottom-up, leaf values, cover
 __global__ void gbdt_finalize(int T, int NN, int max_depth, int8_t* __restrict__ status, int16_t* __restrict__ feat,
                               const float* __restrict__ gain, const double* __restrict__ G, const double* __restrict__ H,
-                              float* __restrict__ leaf, float* __restrict__ cover, double lam, float gamma, double eta,
-                              const int* __restrict__ rd) {
+                              float* __restrict__ leaf, float* __restrict__ cover, double lam, float gamma, double eta) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
-  {
-    const int64_t ro = rd_off(rd, (int64_t)T * NN);
-    status += ro;
-    feat += ro;
-    gain += ro;
-    leaf += ro;
-    cover += ro;
-  }
   const int64_t o = (int64_t)t * NN;
   int8_t* st = status + o;
   prune_task(st, feat + o, gain + o, max_depth, gamma);
@@ -974,10 +942,7 @@ EM_DEVICE int leaf_ancestor(const int8_t* st, int nd) {
 }
 
 __global__ void gbdt_update(float* __restrict__ margin, const int16_t* __restrict__ node, int T, int n, int NN,
-                            const int8_t* __restrict__ status, const float* __restrict__ leaf,
-                            const int* __restrict__ rd) {
-  status += rd_off(rd, (int64_t)T * NN);
-  leaf += rd_off(rd, (int64_t)T * NN);
+                            const int8_t* __restrict__ status, const float* __restrict__ leaf) {
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i / n);
@@ -989,12 +954,7 @@ __global__ void gbdt_update(float* __restrict__ margin, const int16_t* __restric
 // K11: margin[t][r] += sum over trees k in [k0, k1) (task of tree k = k % T) — traversal on bins
 __global__ void gbdt_predict(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F, int NN,
                              int k0, int k1, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
-                             const uint8_t* __restrict__ sbin, const float* __restrict__ leaf,
-                             const int* __restrict__ rd) {
-  if (rd) {  // trees of round *rd: [k0, k1) shifted by round * T
-    k0 += *rd * T;
-    k1 += *rd * T;
-  }
+                             const uint8_t* __restrict__ sbin, const float* __restrict__ leaf) {
   const int64_t total = (int64_t)T * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
@@ -1079,9 +1039,7 @@ EM_DEVICE double block_sum_partials(const double* __restrict__ partial, int nb) 
 }
 
 __global__ void __launch_bounds__(256)
-gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int metric, float* __restrict__ out,
-                  const int* __restrict__ rd = nullptr, int ostride = 0) {
-  out += rd_off(rd, ostride);
+gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int metric, float* __restrict__ out) {
   const double s = block_sum_partials(partial, nb);
   if (threadIdx.x == 0) {
     double v = s / (double)(count > 0 ? count : 1);
@@ -1092,11 +1050,10 @@ gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int
 
 // The last-arriving block of a fused metric launch: every block stores its partial write-through (sc1)
 // and drains it before its single arrival add; the block whose add completes the count sums the
-// partials (sc1 loads) exactly as gbdt_metric_final does, writes the mean, re-arms the counter and,
-// in a replayed round, advances the round counter (every block read it at entry).
+// partials (sc1 loads) exactly as gbdt_metric_final does, writes the mean and re-arms the counter.
 // (b, nb: this block's index among the nb blocks of its metric set; a fused launch runs several sets)
 EM_DEVICE void metric_arrive_final(double bs, double* __restrict__ partial, int* __restrict__ ctr, int64_t count,
-                                   int metric, float* __restrict__ out, int* __restrict__ rd_adv, int b, int nb) {
+                                   int metric, float* __restrict__ out, int b, int nb) {
   __shared__ int last;
   if (threadIdx.x == 0) {
     __hip_atomic_store(partial + b, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1120,7 +1077,6 @@ EM_DEVICE void metric_arrive_final(double bs, double* __restrict__ partial, int*
     if (metric == MET_RMSE) v = sqrt(v);
     out[0] = (float)v;
     __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (rd_adv) *rd_adv += 1;
   }
 }
 
@@ -1132,7 +1088,7 @@ EM_DEVICE void predict_metric_body(const uint8_t* __restrict__ bins, float* __re
                                    const int16_t* __restrict__ feat, const uint8_t* __restrict__ sbin,
                                    const float* __restrict__ leaf, const float* __restrict__ Y, int obj, int metric,
                                    double* __restrict__ partial, int* __restrict__ ctr, float* __restrict__ out,
-                                   int* __restrict__ rd_adv, int b, int nb);
+                                   int b, int nb);
 // eval sets handled by the update launch's trailing blocks (eager rounds): set s gets mb blocks, its own
 // partial region (partial + (1 + s) * 4096) and arrival counter (ctr + 1 + s)
 struct EvalSets {
@@ -1163,25 +1119,19 @@ struct NextRound {
 // is a leaf, where the partition-then-ancestor walk of the separate launches ends as well).
 __global__ void __launch_bounds__(256)
 gbdt_update_metric(float* __restrict__ margin, const int16_t* __restrict__ node, int T, int n, int NN,
-                   const int8_t* __restrict__ status, const float* __restrict__ leaf, const int* __restrict__ rd,
+                   const int8_t* __restrict__ status, const float* __restrict__ leaf,
                    const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial, int* __restrict__ ctr,
-                   float* __restrict__ out, int ostride, int* __restrict__ rd_adv, const uint8_t* __restrict__ bins,
+                   float* __restrict__ out, const uint8_t* __restrict__ bins,
                    int F, int plevel, const int16_t* __restrict__ feat, const uint8_t* __restrict__ sbin,
                    NextRound nx, int nbu, EvalSets evs) {
-  if ((int)blockIdx.x >= nbu) {  // an eval set's prediction + metric (eager rounds: rd == nullptr)
+  if ((int)blockIdx.x >= nbu) {  // an eval set's prediction + metric
     int b = (int)blockIdx.x - nbu, s = 0;
     while (s < evs.count - 1 && b >= evs.mb[s]) b -= evs.mb[s++];
     // (status / feat / sbin / leaf are this round's arrays: its trees are 0 .. T - 1 of them)
     predict_metric_body(evs.bins[s], evs.margin[s], T, evs.n[s], F, NN, 0, T, status, feat, sbin, leaf, evs.Y[s], obj,
-                        metric, partial + (int64_t)(1 + s) * 4096, ctr + 1 + s, out + 1 + s, nullptr, b, evs.mb[s]);
+                        metric, partial + (int64_t)(1 + s) * 4096, ctr + 1 + s, out + 1 + s, b, evs.mb[s]);
     return;
   }
-  const int64_t ro = rd_off(rd, (int64_t)T * NN);
-  status += ro;
-  leaf += ro;
-  feat += ro;
-  sbin += ro;
-  out += rd_off(rd, ostride);
   const int64_t total = (int64_t)T * n;
   const int pf = plevel >= 0 ? (1 << plevel) - 1 : 0, pl = plevel >= 0 ? 2 * pf + 1 : 0;
   GSTAMP(128);
@@ -1204,7 +1154,7 @@ gbdt_update_metric(float* __restrict__ margin, const int16_t* __restrict__ node,
          i += (int64_t)nbu * blockDim.x)
       round_init_elem((int)i, nx.st, nx.fe, nx.sb, nx.gn, NN);
   GSTAMP(129);
-  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv, blockIdx.x, nbu);
+  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, blockIdx.x, nbu);
   GSTAMP(130);
 }
 
@@ -1214,7 +1164,7 @@ EM_DEVICE void predict_metric_body(const uint8_t* __restrict__ bins, float* __re
                                    const int16_t* __restrict__ feat, const uint8_t* __restrict__ sbin,
                                    const float* __restrict__ leaf, const float* __restrict__ Y, int obj, int metric,
                                    double* __restrict__ partial, int* __restrict__ ctr, float* __restrict__ out,
-                                   int* __restrict__ rd_adv, int b, int nb) {
+                                   int b, int nb) {
   const int64_t total = (int64_t)T * n;
   double acc = 0.0;
   for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < total; i += (int64_t)nb * blockDim.x) {
@@ -1231,20 +1181,16 @@ EM_DEVICE void predict_metric_body(const uint8_t* __restrict__ bins, float* __re
     margin[i] = m;
     acc += metric_term(m, Y[(int64_t)r * T + t], obj, metric);
   }
-  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, rd_adv, b, nb);
+  metric_arrive_final(block_tree_sum(acc), partial, ctr, total, metric, out, b, nb);
 }
 __global__ void __launch_bounds__(256)
 gbdt_predict_metric(const uint8_t* __restrict__ bins, float* __restrict__ margin, int T, int n, int F, int NN, int k0,
                     int k1, const int8_t* __restrict__ status, const int16_t* __restrict__ feat,
-                    const uint8_t* __restrict__ sbin, const float* __restrict__ leaf, const int* __restrict__ rd,
+                    const uint8_t* __restrict__ sbin, const float* __restrict__ leaf,
                     const float* __restrict__ Y, int obj, int metric, double* __restrict__ partial,
-                    int* __restrict__ ctr, float* __restrict__ out, int ostride, int* __restrict__ rd_adv) {
-  if (rd) {
-    k0 += *rd * T;
-    k1 += *rd * T;
-  }
+                    int* __restrict__ ctr, float* __restrict__ out) {
   predict_metric_body(bins, margin, T, n, F, NN, k0, k1, status, feat, sbin, leaf, Y, obj, metric, partial, ctr,
-                      out + rd_off(rd, ostride), rd_adv, blockIdx.x, gridDim.x);
+                      out, blockIdx.x, gridDim.x);
 }
 
 __global__ void __launch_bounds__(256)
@@ -1364,7 +1310,6 @@ struct HistPartition {  // the previous level's partition fused into the exact-f
   const int16_t* fe = nullptr;
   const uint8_t* sb = nullptr;
   int NN = 0;
-  const int* rd = nullptr;
 };
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
@@ -1418,7 +1363,7 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
       }
       hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
                          C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece, stage, hp.node_out, hp.st, hp.fe,
-                         hp.sb, hp.NN, hp.rd);
+                         hp.sb, hp.NN);
     }
   }
   const bool split_folds = !fold && nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
@@ -1440,38 +1385,6 @@ bool valid_foff(const int* foff, int F) {
   return true;
 }
 
-__global__ void gbdt_round_set(int* rd, int v) {
-  if (threadIdx.x == 0) *rd = v;
-}
-__global__ void gbdt_round_advance(int* rd) {
-  if (threadIdx.x == 0) *rd += 1;
-}
-
-// every argument a captured round depends on (compared bytewise: zero-filled before use)
-struct GbdtGraphKey {
-  const void* p[19];
-  const void* ev[4][3];
-  int evn[4];
-  int i[10];
-  float f[5];
-  int64_t pd;
-  int foff[320];
-};
-struct GraphCache {
-  hipGraphExec_t exec = nullptr;
-  int* rd = nullptr;        // device round counter
-  hipStream_t cap = nullptr;  // capture stream (the caller's may be the legacy default stream)
-  int dev = -1;
-  GbdtGraphKey key;
-  void reset() {
-    if (exec) (void)hipGraphExecDestroy(exec);
-    exec = nullptr;
-  }
-};
-GraphCache& graph_cache() {
-  static GraphCache c;
-  return c;
-}
 // [T] zeroed device ints (grown on demand; left zeroed by every use): gbdt_split's per-task arrival
 // counters of the fused finalize
 int* task_counters(int T) {
@@ -1542,7 +1455,8 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
                        int metric, float eta, float lam, float gamma, float mcw, float subsample, uint32_t seed,
                        float* g, float* h, int16_t* node, int16_t* node2, double* partial, int64_t partial_doubles,
                        double* Gs, double* Hs, double* mpart, int8_t* status, int16_t* feat, uint8_t* sbin,
-                       float* leaf, float* gainv, float* cover, float* hist_out, int quant_bits, hipStream_t stream) {
+                       float* leaf, float* gainv, float* cover, float* hist_out, int quant_bits, int launch_flags,
+                       hipStream_t stream) {
   if (!bins || !Y || !margin || n <= 0 || F <= 0 || !valid_foff(foff_h, F) || !foff_d || T <= 0 || max_depth < 1 ||
       max_depth > 12 || r0 < 0 || r1 < r0 || quant_bits < 0 || quant_bits > 61)
     return EM_ERR_ARG;
@@ -1555,11 +1469,10 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   const int64_t TN = (int64_t)T * n;
   int* mctr = metric_counter();  // arrival counter of the fused metric launches (re-armed by each)
   if (!mctr) return EM_ERR_ARG;
-  // fixed point with >= 8 one-hot features: the sparse form (QuantAux); EM_GBDT_SPARSE=0 disables it
+  // fixed point with >= 8 one-hot features: the sparse form (QuantAux)
   QuantAux qa;
   void* qmem = nullptr;
-  static const bool sparse_on = !(getenv("EM_GBDT_SPARSE") && getenv("EM_GBDT_SPARSE")[0] == '0');
-  if (quant_bits && sparse_on) {
+  if (quant_bits) {
     std::vector<int> bcell, bfeat, fmap;
     qa.foffm_h.push_back(0);
     for (int f = 0; f < F; ++f) {
@@ -1606,23 +1519,18 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       }
     }
   } qfree{qmem, stream};
-  // one round's kernel sequence.  rd == nullptr: the arrays of `round` are addressed from the host;
-  // rd = the device round counter: every round-dependent offset is taken in-kernel (round = 0 here),
-  // so the identical sequence is captured once and replayed for every round
   // Exact-form fits with an elementwise metric run the fused round: the previous level's partition
   // inside each histogram pass (double-buffered nodes), the prune / leaves in the last level's split
-  // (last-arriving block per task), the last partition in the update, and -- eager rounds of per-task
-  // objectives -- the next round's start in the update too: 8 launches per depth-3 round instead of 13.
+  // (last-arriving block per task), the last partition in the update, and -- per-task objectives --
+  // the next round's start in the update too: 7 launches per depth-3 round instead of 13.
   // Bit-identical to the separate launches (same arithmetic on the same values).
-  // EM_GBDT_FUSE=0: the separate launches (A/B, tests)
+  // launch_flags & EM_GBDT_SEPARATE: the separate launches (the bit-identity tests; quantised fits and
+  // multi-class metrics always take them)
   int* tctr = nullptr;
-  const char* fz = getenv("EM_GBDT_FUSE");
-  const bool fuse = !(fz && fz[0] == '0') && !quant_bits && metric < MET_MLOGLOSS &&
+  const bool fuse = !(launch_flags & EM_GBDT_SEPARATE) && !quant_bits && metric < MET_MLOGLOSS &&
                     max_depth <= SPLIT_FINAL_MAX_DEPTH && node2 && (tctr = task_counters(T)) != nullptr;
-  // one round's kernel sequence.  rd == nullptr: the arrays of `round` are addressed from the host;
-  // rd = the device round counter: every round-dependent offset is taken in-kernel (round = 0 here),
-  // so the identical sequence is captured once and replayed for every round
-  auto enqueue_round = [&](int round, const int* rd, hipStream_t s) -> int {
+  // one round's kernel sequence (the arrays of `round` addressed from the host)
+  auto enqueue_round = [&](int round, hipStream_t s) -> int {
     const int64_t ro = (int64_t)round * T * NN;
     int8_t* st = status + ro;
     int16_t* fe = feat + ro;
@@ -1630,11 +1538,11 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     float* lf = leaf + ro;
     float* gn = gainv + ro;
     float* cv = cover + ro;
-    const bool next_in_update = fuse && !rd && obj != OBJ_SOFTMAX;  // eager: round + 1 started by this update
+    const bool next_in_update = fuse && obj != OBJ_SOFTMAX;  // round + 1 started by this update
     int16_t* nb[2] = {node, fuse ? node2 : node};
     if (!next_in_update || round == r0)
       hipLaunchKernelGGL(gbdt_round_start, dim3(grid_for(TN > (int64_t)T * NN ? TN : (int64_t)T * NN)), dim3(256), 0,
-                         s, st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round, rd);
+                         s, st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round);
     for (int level = 0; level < max_depth; ++level) {
       const int nodesL = 1 << level;
       int nch = 1;
@@ -1647,7 +1555,6 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         hp.fe = fe;
         hp.sb = sb;
         hp.NN = NN;
-        hp.rd = rd;
       }
       const int rc = launch_level_hist(level, bins, g, h, nin, T, n, F, foff_h, foff_d, partial, partial_doubles,
                                        false, qscale, &nch, s, qa.nb ? &qa : nullptr, hp);
@@ -1672,26 +1579,24 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       if (quant_bits)
         hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, s,
                            reinterpret_cast<const long long*>(partial), nch, cstride, foff_d, T, F, C, level, NN, Gs,
-                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, rd, fin, oneshot, pscan);
+                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, fin, oneshot, pscan);
       else
         hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, s, partial, nch, cstride,
-                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, rd, fin,
+                           foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, fin,
                            oneshot, pscan);
       if (!fuse)
         hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, s, bins, node, T, n, F, NN, st, fe, sb,
-                           level, rd);
+                           level);
     }
     if (!fuse)
       hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, s, T, NN, max_depth, st, fe, gn, Gs, Hs, lf,
-                         cv, (double)lam, gamma, (double)eta, rd);
+                         cv, (double)lam, gamma, (double)eta);
     // metrics (train + evals) into hist_out[round].  Elementwise metrics: the leaf update / eval
-    // prediction, the metric partials and the final sum are one launch each (last-arriving block);
-    // the round counter of a replayed round advances in the round's last launch
+    // prediction, the metric partials and the final sum are one launch each (last-arriving block)
     const int hs = 1 + n_evals;
     float* ho = hist_out + (int64_t)round * hs;
     const int mb_train = grid_for(TN);
     const bool fused_metric = metric < MET_MLOGLOSS;
-    int* adv = const_cast<int*>(rd);
     if (fused_metric) {
       NextRound nx;
       if (next_in_update && round + 1 < r1) {
@@ -1707,10 +1612,10 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         nx.subsample = subsample;
         nx.seed = seed;
       }
-      // eager rounds: the eval sets' predictions ride in the same launch (trailing blocks)
+      // the eval sets' predictions ride in the same launch (trailing blocks)
       EvalSets evs;
       int grid = mb_train;
-      if (!rd && n_evals <= 4) {
+      if (n_evals <= 4) {
         for (int e = 0; e < n_evals; ++e) {
           evs.bins[e] = evals[e].bins;
           evs.margin[e] = evals[e].margin;
@@ -1722,17 +1627,17 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         evs.count = n_evals;
       }
       hipLaunchKernelGGL(gbdt_update_metric, dim3(grid), dim3(256), 0, s, margin,
-                         fuse ? nb[(max_depth - 1) & 1] : node, T, n, NN, st, lf, rd, Y, obj, metric, mpart, mctr, ho,
-                         hs, n_evals == 0 ? adv : nullptr, bins, F, fuse ? max_depth - 1 : -1, fe, sb, nx, mb_train, evs);
+                         fuse ? nb[(max_depth - 1) & 1] : node, T, n, NN, st, lf, Y, obj, metric, mpart, mctr, ho,
+                         bins, F, fuse ? max_depth - 1 : -1, fe, sb, nx, mb_train, evs);
       if (evs.count == n_evals) {
         EM_CHECK_LAUNCH();
         return 0;
       }
     } else {
-      hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, s, margin, node, T, n, NN, st, lf, rd);
+      hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, s, margin, node, T, n, NN, st, lf);
       hipLaunchKernelGGL(gbdt_metric, dim3(mb_train), dim3(256), 0, s, margin, Y, T, n, obj, metric, mpart);
       hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb_train,
-                         metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, ho, rd, hs);
+                         metric >= MET_MLOGLOSS ? (int64_t)n : TN, metric, ho);
     }
     for (int e = 0; e < n_evals; ++e) {
       const int64_t TE = (int64_t)T * evals[e].n;
@@ -1740,76 +1645,22 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       const int mb = grid_for(TE);
       if (fused_metric) {
         hipLaunchKernelGGL(gbdt_predict_metric, dim3(mb), dim3(256), 0, s, evals[e].bins, evals[e].margin, T,
-                           evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf, rd, evals[e].Y, obj, metric, mpart,
-                           mctr, ho + 1 + e, hs, e == n_evals - 1 ? adv : nullptr);
+                           evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf, evals[e].Y, obj, metric, mpart,
+                           mctr, ho + 1 + e);
         continue;
       }
       hipLaunchKernelGGL(gbdt_predict, dim3(grid_for(TE)), dim3(256), 0, s, evals[e].bins, evals[e].margin, T,
-                         evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf, rd);
+                         evals[e].n, F, NN, k0, k0 + T, status, feat, sbin, leaf);
       hipLaunchKernelGGL(gbdt_metric, dim3(mb), dim3(256), 0, s, evals[e].margin, evals[e].Y, T, evals[e].n, obj,
                          metric, mpart);
       hipLaunchKernelGGL(gbdt_metric_final, dim3(1), dim3(256), 0, s, mpart, mb,
-                         metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric, ho + 1 + e, rd, hs);
+                         metric >= MET_MLOGLOSS ? (int64_t)evals[e].n : TE, metric, ho + 1 + e);
     }
-    if (rd && !fused_metric) hipLaunchKernelGGL(gbdt_round_advance, dim3(1), dim3(64), 0, s, adv);
     EM_CHECK_LAUNCH();
     return 0;
   };
-  // EM_GBDT_GRAPH=1: replay one captured round per round (the graph is cached across calls with the
-  // same arguments; the Python driver calls per 100 rounds).  Opt-in: on the reference fit the replayed
-  // rounds measured slower than the eager stream (0.056-0.057 vs 0.049-0.050 s for 500 rounds) -- the
-  // device, not the host enqueue, bounds a round, a graph's nodes start a little later than
-  // back-to-back launches, and a replayed round cannot carry the next round's start in its update
-  // (the eager round does: one launch less).  Same kernels and arguments: bit-identical trees.
-  const char* gv = getenv("EM_GBDT_GRAPH");
-  const bool graph_on = gv && gv[0] == '1';
-  if (graph_on && r1 - r0 >= 2 && !qmem) {
-    GraphCache& gc = graph_cache();
-    GbdtGraphKey key;
-    std::memset(&key, 0, sizeof(key));
-    key.p[0] = bins; key.p[1] = Y; key.p[2] = foff_d; key.p[3] = margin; key.p[4] = g; key.p[5] = h;
-    key.p[6] = node; key.p[7] = partial; key.p[8] = Gs; key.p[9] = Hs; key.p[10] = mpart; key.p[11] = status;
-    key.p[12] = feat; key.p[13] = sbin; key.p[14] = leaf; key.p[15] = gainv; key.p[16] = cover; key.p[17] = hist_out;
-    key.p[18] = node2;
-    for (int e = 0; e < n_evals && e < 4; ++e) {
-      key.ev[e][0] = evals[e].bins; key.ev[e][1] = evals[e].Y; key.ev[e][2] = evals[e].margin;
-      key.evn[e] = evals[e].n;
-    }
-    key.i[0] = n; key.i[1] = F; key.i[2] = T; key.i[3] = n_evals; key.i[4] = max_depth; key.i[5] = obj;
-    key.i[6] = metric; key.i[7] = quant_bits; key.i[8] = (int)seed; key.i[9] = fuse ? 1 : 0;
-    key.f[0] = eta; key.f[1] = lam; key.f[2] = gamma; key.f[3] = mcw; key.f[4] = subsample;
-    key.pd = partial_doubles;
-    for (int f = 0; f <= F && f < 320; ++f) key.foff[f] = foff_h[f];
-    if (n_evals <= 4 && F < 320) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (!gc.exec || gc.dev != dev || std::memcmp(&gc.key, &key, sizeof(key)) != 0) {
-        gc.reset();
-        if (!gc.rd) {
-          if (hipError_t e = hipMalloc(&gc.rd, sizeof(int))) return (int)e;
-          if (hipError_t e = hipStreamCreateWithFlags(&gc.cap, hipStreamNonBlocking)) return (int)e;
-        }
-        hipGraph_t graph = nullptr;
-        if (hipError_t e = hipStreamBeginCapture(gc.cap, hipStreamCaptureModeThreadLocal)) return (int)e;
-        const int rc = enqueue_round(0, gc.rd, gc.cap);
-        const hipError_t ec = hipStreamEndCapture(gc.cap, &graph);
-        if (rc) return rc;
-        if (ec != hipSuccess) return (int)ec;
-        const hipError_t ei = hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ei != hipSuccess) return (int)ei;
-        gc.key = key;
-        gc.dev = dev;
-      }
-      hipLaunchKernelGGL(gbdt_round_set, dim3(1), dim3(64), 0, stream, gc.rd, r0);
-      for (int round = r0; round < r1; ++round)
-        if (hipError_t e = hipGraphLaunch(gc.exec, stream)) return (int)e;
-      EM_CHECK_LAUNCH();
-      return 0;
-    }
-  }
   for (int round = r0; round < r1; ++round)
-    if (int rc = enqueue_round(round, nullptr, stream)) return rc;
+    if (int rc = enqueue_round(round, stream)) return rc;
   return 0;
 }
 
@@ -1838,7 +1689,7 @@ EM_API int em_gbdt_predict(const uint8_t* bins, float* margin, int T, int n, int
   if (n == 0) return 0;
   const int NN = (1 << (max_depth + 1)) - 1;
   hipLaunchKernelGGL(gbdt_predict, dim3(grid_for((int64_t)T * n)), dim3(256), 0, stream, bins, margin, T, n, F, NN, k0,
-                     k1, status, feat, sbin, leaf, (const int*)nullptr);
+                     k1, status, feat, sbin, leaf);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1855,9 +1706,9 @@ EM_API int em_gbdt_dp_round_begin(int round, int T, int n, int max_depth, const 
   const int NN = (1 << (max_depth + 1)) - 1;
   const int64_t TN = (int64_t)T * n;
   hipLaunchKernelGGL(gbdt_round_init, dim3(grid_for((int64_t)T * NN)), dim3(256), 0, stream, status, feat, sbin, gainv,
-                     T * NN, NN, (const int*)nullptr);
+                     T * NN, NN);
   hipLaunchKernelGGL(gbdt_grad, dim3(grid_for(TN)), dim3(256), 0, stream, margin, Y, g, h, node, T, n, obj, subsample,
-                     seed, round, (const int*)nullptr);
+                     seed, round);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1889,10 +1740,9 @@ EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* 
   const int64_t TN = (int64_t)T * n;
   const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
   hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C,
-                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, (const int*)nullptr,
-                     SplitFinal(), 0, 0);
+                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, SplitFinal(), 0, 0);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
-                     sbin, level, (const int*)nullptr);
+                     sbin, level);
   EM_CHECK_LAUNCH();
   return 0;
 }
@@ -1904,9 +1754,8 @@ EM_API int em_gbdt_dp_round_end(int T, int n, int max_depth, float* margin, cons
   const int NN = (1 << (max_depth + 1)) - 1;
   const int64_t TN = (int64_t)T * n;
   hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, stream, T, NN, max_depth, status, feat, gainv,
-                     Gs, Hs, leaf, cover, (double)lam, gamma, (double)eta, (const int*)nullptr);
-  hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, stream, margin, node, T, n, NN, status, leaf,
-                     (const int*)nullptr);
+                     Gs, Hs, leaf, cover, (double)lam, gamma, (double)eta);
+  hipLaunchKernelGGL(gbdt_update, dim3(grid_for(TN)), dim3(256), 0, stream, margin, node, T, n, NN, status, leaf);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -671,6 +671,9 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
     ts[3] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int k = 0; k < 4; ++k) slab_spare[128 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
+    uint32_t xcc;  // which XCD ran this block (HIP promises no placement: recorded, never relied on)
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    slab_spare[132] = __builtin_bit_cast(float, xcc & 15u);
   }
 }
 

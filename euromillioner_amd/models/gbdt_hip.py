@@ -23,7 +23,7 @@ class _Eval(ctypes.Structure):
 
 N.register_signatures({
     "em_gbdt_fit": (_i, [_v, _v, _i, _i, _v, _v, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f,
-                         _f, _f, _u32, _v, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _i, _v]),
+                         _f, _f, _u32, _v, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _i, _i, _v]),
     "em_gbdt_partial_doubles": (_i64, [_i, _i, _i, _v, _i]),
     "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
     "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
@@ -120,7 +120,9 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 100, dp=None):
                model.gamma, model.mcw, model.subsample, model.seed & 0xFFFFFFFF, g.data_ptr(), h.data_ptr(),
                node.data_ptr(), node2.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
                status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), gain.data_ptr(),
-               cover.data_ptr(), hist.data_ptr(), qbits, stream)
+               cover.data_ptr(), hist.data_ptr(), qbits,
+               # separate launches instead of the fused round (bit-identity tests; csrc/gbdt.hip)
+               1 if getattr(model, "separate_launches", False) else 0, stream)
         hh = hist.view(R, 1 + len(ev_names))[r0:r1].cpu().numpy()
         for i, rnd in enumerate(range(r0, r1)):
             rec = {"round": rnd}

@@ -227,10 +227,10 @@ def test_hip_dp_primitives_match_single_call():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("obj", ["reg:logistic", "reg:squarederror"])
-def test_hip_fused_round_and_graph_bit_identical(obj):
+def test_hip_fused_round_bit_identical(obj):
     """The fused round (partition inside the histogram pass, prune/leaves in the last split, last
-    partition and next round start in the update), the separate launches (EM_GBDT_FUSE=0) and the
-    hipGraph-replayed rounds (EM_GBDT_GRAPH=1) give bit-identical trees, margins and histories."""
+    partition and next round start in the update) and the separate launches give bit-identical trees,
+    margins and histories.  (Round 4's hipGraph-replayed rounds were slower and are gone.)"""
     from euromillioner_amd import config as C
     from euromillioner_amd.pipeline import gbdt_dataset
 
@@ -241,25 +241,15 @@ def test_hip_fused_round_and_graph_bit_identical(obj):
               eval_metric="logloss" if obj == "reg:logistic" else "rmse", subsample=0.8, backend="hip")
     ev = {"test": (X[m:], Y[m:])}
     fits = {}
-    for name, env in (("fused", {"EM_GBDT_GRAPH": "0"}), ("separate", {"EM_GBDT_GRAPH": "0", "EM_GBDT_FUSE": "0"}),
-                      ("graph", {"EM_GBDT_GRAPH": "1"})):
-        old = {k: os.environ.get(k) for k in ("EM_GBDT_GRAPH", "EM_GBDT_FUSE")}
-        os.environ.update(env)
-        try:
-            fits[name] = G.GBDT(**kw).fit(X[:m], Y[:m], evals=ev)
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-    a = fits["fused"]
-    for name in ("separate", "graph"):
-        b = fits[name]
-        for k in ("status", "feat", "sbin", "leaf", "gain", "cover"):
-            assert np.array_equal(getattr(a.trees, k), getattr(b.trees, k)), (name, k)
-        assert a.history == b.history, name
-        assert np.array_equal(a.predict(X[m:], backend="hip"), b.predict(X[m:], backend="hip")), name
+    for name in ("fused", "separate"):
+        g = G.GBDT(**kw)
+        g.separate_launches = name == "separate"
+        fits[name] = g.fit(X[:m], Y[:m], evals=ev)
+    a, b = fits["fused"], fits["separate"]
+    for k in ("status", "feat", "sbin", "leaf", "gain", "cover"):
+        assert np.array_equal(getattr(a.trees, k), getattr(b.trees, k)), k
+    assert a.history == b.history
+    assert np.array_equal(a.predict(X[m:], backend="hip"), b.predict(X[m:], backend="hip"))
 
 
 def test_native_hist_plan_bounds():

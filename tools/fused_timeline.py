@@ -57,6 +57,20 @@ def main():
               f" loop {q(loop)}; fold {q(us[:, 3] - us[:, 2])}; first entry -> last fold {us[:, 3].max():.1f}", flush=True)
         xcd = np.arange(nslab) % 8
         print("   loop median per blockIdx%8:", " ".join("%.1f" % np.median(loop[xcd == k]) for k in range(8)))
+        # which physical XCD ran each block (s_getreg HW_REG_XCC_ID): is the slow group a fixed XCD
+        # across launches, or a fixed blockIdx % 8?  Five more single launches.
+        for rep in range(5):
+            torch.cuda.synchronize()
+            with torch.cuda.stream(s):
+                FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
+            torch.cuda.synchronize()
+            raw = m.slabs[:nslab, FM.P_TOTAL + 128:FM.P_TOTAL + 133].contiguous().view(torch.int32).cpu().numpy()
+            t = raw[:, :4].astype(np.int64) & 0xFFFFFFFF
+            lp = (t[:, 2] - t[:, 1]) / 100.0
+            xc = raw[:, 4]
+            print(f"   launch {rep}: loop median per XCC_ID:",
+                  " ".join("%d:%.1f" % (k, np.median(lp[xc == k])) for k in range(8) if (xc == k).any()),
+                  "| blockIdx%8 -> XCC_ID:", " ".join(str(int(np.bincount(xc[xcd == k]).argmax())) for k in range(8)))
         st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
         shared = os.environ.get("TL_SHARED", "1") == "1"  # FUSED_SHARED layout: waves 0-3 forward
         roles = (("forward", [0, 1, 2, 3]), ("backward", [4, 5, 6, 7])) if shared else \

@@ -14,3 +14,5 @@ for i in 1 2; do timeout -k 10 120 python tools/rf_bench.py >> gpurun_out/g1/rf_
 cat gpurun_out/g1/rf_bench.jsonl
 timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gemm_gpu.py tests/test_gemm_accum_gpu.py tests/test_gemm_property_gpu.py tests/test_perf_guard_gpu.py > gpurun_out/g1/pytest_gemm.log 2>&1 || { tail -30 gpurun_out/g1/pytest_gemm.log; exit 8; }
 tail -2 gpurun_out/g1/pytest_gemm.log
+timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gbdt.py -m gpu > gpurun_out/g1/pytest_gbdt.log 2>&1 || { tail -30 gpurun_out/g1/pytest_gbdt.log; exit 10; }
+tail -2 gpurun_out/g1/pytest_gbdt.log

@@ -16,3 +16,5 @@ for r in 1 2; do
   done
 done
 cat gpurun_out/g2/ab_headline.jsonl
+EUROM_NATIVE_LIB=$L/stamps.so TL_B=1048576 timeout -k 10 200 python tools/fused_timeline.py > gpurun_out/g2/timeline.txt 2>&1 || { tail -20 gpurun_out/g2/timeline.txt; exit 5; }
+cat gpurun_out/g2/timeline.txt

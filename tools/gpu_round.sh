@@ -7,7 +7,7 @@
 #   bash tools/gpu_round.sh gbdt            GBDT GPU tests, kernel trace of the 183k-row case, gbdt_bench
 #   bash tools/gpu_round.sh fp32            bench.py --dtype fp32 + kernel trace
 #   bash tools/gpu_round.sh wide            wide-MLP bench + kernel trace, one-GPU overlap rehearsal
-#   bash tools/gpu_round.sh gbdt-ref        round-4 GBDT reference fit: GPU tests, eager vs graph bench, phase
+#   bash tools/gpu_round.sh gbdt-ref        GBDT reference fit: GPU tests, bench, phase
 #                                           stamps (needs lib/ab/gbdt_stamps.so: build_variant.sh -DGBDT_STAMPS=1)
 #   bash tools/gpu_round.sh rf-ab           RF tests + rf_bench against lib/ab/rf_head.so (the committed
 #                                           forest.hip: SRC=... build_variant.sh rf_head), kernel stats
@@ -63,9 +63,8 @@ for stage in "$@"; do
     tail -1 $O/pytest.log
     for rnd in 1 2; do
       timeout -k 10 200 python tools/gbdt_bench.py reference > $O/eager_$rnd.jsonl 2>&1 || { tail $O/eager_$rnd.jsonl; exit 23; }
-      EM_GBDT_GRAPH=1 timeout -k 10 200 python tools/gbdt_bench.py reference > $O/graph_$rnd.jsonl 2>&1 || { tail $O/graph_$rnd.jsonl; exit 23; }
     done
-    grep -h -o '"hip_s": [0-9.]*' $O/eager_?.jsonl $O/graph_?.jsonl
+    grep -h -o '"hip_s": [0-9.]*' $O/eager_?.jsonl
     if [ -f euromillioner_amd/lib/ab/gbdt_stamps.so ]; then
       EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/gbdt_stamps.so timeout -k 10 120 python tools/gbdt_stamps.py > $O/stamps.jsonl 2>&1 || { tail $O/stamps.jsonl; exit 24; }
       cat $O/stamps.jsonl
