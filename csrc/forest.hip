@@ -1053,42 +1053,67 @@ __global__ void __launch_bounds__(256) rf_predict(const uint64_t* __restrict__ X
 constexpr int RFP_TREE = 1024 + 256 * 256;  // bytes per prepared tree: node table + 256 leaf vectors
 
 // one workgroup per tree: node table with leaves encoded, leaf vectors compacted in level order;
-// word 511 of the node table (a padding slot: nodes <= 511) holds the leaf count
-__global__ void __launch_bounds__(64) rf_predict_prepare(const int16_t* __restrict__ feat,
-                                                         const float* __restrict__ value, int nodes, int depth,
-                                                         uint8_t* __restrict__ prep) {
+// word 511 of the node table (a padding slot: nodes <= 511) holds the leaf count.  The feature row is
+// staged into LDS by all 512 threads first (the level walk is then LDS-only), and the leaf vectors are
+// copied as float4s in batches of 4 independent loads per thread (a per-node loop of dependent
+// load -> store round trips made this kernel cost milliseconds).
+constexpr int RFP_PREP_THREADS = 512;
+__global__ void __launch_bounds__(RFP_PREP_THREADS) rf_predict_prepare(const int16_t* __restrict__ feat,
+                                                                       const float* __restrict__ value, int nodes,
+                                                                       int depth, uint8_t* __restrict__ prep) {
+  __shared__ int16_t ft[512];
   __shared__ uint8_t reach[512];
   __shared__ int16_t slot_of[512];
-  const int t = blockIdx.x, lane = threadIdx.x;
-  const int16_t* ft = feat + (int64_t)t * nodes;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   int16_t* enc = reinterpret_cast<int16_t*>(prep + (int64_t)t * RFP_TREE);
-  float* vals = reinterpret_cast<float*>(prep + (int64_t)t * RFP_TREE + 1024);
-  int base = 0;
-  for (int d = 0; d <= depth; ++d) {  // level order: a node's parent is decided before it
-    const int n0 = (1 << d) - 1, n1 = (2 << d) - 1;
-    for (int c0 = n0; c0 < n1; c0 += 64) {
-      const int n = c0 + lane;
-      bool live = false, leaf = false;
-      int f = -1;
-      if (n < n1) {
-        f = ft[n];
-        live = n == 0 || (reach[(n - 1) >> 1] && ft[(n - 1) >> 1] >= 0);
-        leaf = live && (f < 0 || d == depth);
+  f32x4* vals = reinterpret_cast<f32x4*>(prep + (int64_t)t * RFP_TREE + 1024);
+  for (int n = tid; n < nodes; n += RFP_PREP_THREADS) ft[n] = feat[(int64_t)t * nodes + n];
+  __syncthreads();
+  if (tid < 64) {
+    int base = 0;
+    for (int d = 0; d <= depth; ++d) {  // level order: a node's parent is decided before it
+      const int n0 = (1 << d) - 1, n1 = (2 << d) - 1;
+      for (int c0 = n0; c0 < n1; c0 += 64) {
+        const int n = c0 + lane;
+        bool live = false, leaf = false;
+        int f = -1;
+        if (n < n1) {
+          f = ft[n];
+          live = n == 0 || (reach[(n - 1) >> 1] && ft[(n - 1) >> 1] >= 0);
+          leaf = live && (f < 0 || d == depth);
+        }
+        const uint64_t m = __ballot(leaf);
+        const int slot = base + __popcll(m & ((1ull << lane) - 1));
+        if (n < n1) {
+          reach[n] = live;
+          slot_of[n] = leaf ? (int16_t)slot : (int16_t)-1;
+          enc[n] = leaf ? (int16_t)(-(slot + 1)) : (live ? (int16_t)f : (int16_t)-1);
+        }
+        base += __popcll(m);
+        __builtin_amdgcn_wave_barrier();  // (one wave: LDS writes above are visible to its next chunk)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       }
-      const uint64_t m = __ballot(leaf);
-      const int slot = base + __popcll(m & ((1ull << lane) - 1));
-      if (n < n1) {
-        reach[n] = live;
-        slot_of[n] = leaf ? (int16_t)slot : (int16_t)-1;
-        enc[n] = leaf ? (int16_t)(-(slot + 1)) : (live ? (int16_t)f : (int16_t)-1);
-      }
-      base += __popcll(m);
-      __syncthreads();
     }
+    if (lane == 0) enc[511] = (int16_t)base;
   }
-  if (lane == 0) enc[511] = (int16_t)base;
-  for (int n = 0; n < nodes; ++n)
-    if (slot_of[n] >= 0) vals[slot_of[n] * 64 + lane] = value[((int64_t)t * nodes + n) * 64 + lane];
+  __syncthreads();
+  const f32x4* src = reinterpret_cast<const f32x4*>(value + (int64_t)t * nodes * 64);
+  const int total = nodes * 16;  // float4s
+  constexpr int U = 4;
+  for (int i0 = tid; i0 < total; i0 += U * RFP_PREP_THREADS) {
+    f32x4 v[U];
+    int dst[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * RFP_PREP_THREADS;
+      const int sl = i < total ? slot_of[i >> 4] : -1;
+      dst[u] = sl >= 0 ? sl * 16 + (i & 15) : -1;
+      if (dst[u] >= 0) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (dst[u] >= 0) vals[dst[u]] = v[u];
+  }
 }
 
 template <int G>
@@ -1361,7 +1386,7 @@ EM_API int em_rf_predict(const uint64_t* X, int W, int64_t N, const int16_t* fea
   const int nodes = (1 << (max_depth + 1)) - 1;
   if (prep && em_rf_predict_scratch(W, T, max_depth) > 0 && ((uintptr_t)prep & 15) == 0 && (ldo & 3) == 0 &&
       ((uintptr_t)out & 15) == 0) {
-    hipLaunchKernelGGL(rf_predict_prepare, dim3(T), dim3(64), 0, stream, feat, value, nodes, max_depth, (uint8_t*)prep);
+    hipLaunchKernelGGL(rf_predict_prepare, dim3(T), dim3(RFP_PREP_THREADS), 0, stream, feat, value, nodes, max_depth, (uint8_t*)prep);
     EM_CHECK_LAUNCH();
     static int cus = 0;
     if (!cus) {

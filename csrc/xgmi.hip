@@ -109,6 +109,28 @@ xgmi_emulate_block_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, f
     __hip_atomic_store(&peer_hdr[threadIdx.x][XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Timing-only form (copy == 0, tools/xgmi_budget.py): ONE block raises every emulated peer's block
+// flags `delay_ticks` after it starts, without waiting for this rank's publications (peers that reach
+// the exchange delay_ticks after this rank's train kernel ends).  It never waits on the consumer, so a
+// graph replay that happens to run it before the consumer cannot deadlock, and it adds no polling or
+// copy traffic of its own beside the consumer being timed (the 257-block waiting form above does).
+__global__ void __launch_bounds__(256)
+xgmi_emulate_block_flags_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, int nblocks, long long delay_ticks) {
+  __shared__ int s_sh;
+  if (threadIdx.x == 0) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < delay_ticks) __builtin_amdgcn_s_sleep(2);
+    s_sh = xg_next_seq(d.my_hdr);
+  }
+  __syncthreads();
+  const int s = s_sh;
+  for (int q = 0; q < d.world; ++q) {
+    if (q == d.rank) continue;
+    for (int j = threadIdx.x; j < nblocks; j += blockDim.x)
+      __hip_atomic_store(&peer_hdr[q][XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // consumer blocks spin on peer flags, so keep the grid well inside one wave of residency
 int grid_for(int n) {
   int nb = (n + XG_BLOCK - 1) / XG_BLOCK;
@@ -310,8 +332,13 @@ EM_API int em_xgmi_emulate_block_peers(void* h, int nblocks, int n, int copy, do
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
   int* const* hdr = reinterpret_cast<int* const*>(c->peer_ptrs);
   float* const* data = reinterpret_cast<float* const*>(c->peer_ptrs) + XG_MAXW;
-  hipLaunchKernelGGL(xgmi_emulate_block_peers_kernel, dim3(nblocks), dim3(64), 0, stream, c->desc, hdr, data, n,
-                     copy ? 1 : 0, (long long)(delay_us * 1e-3 * khz));
+  const long long delay_ticks = (long long)(delay_us * 1e-3 * khz);
+  if (copy)
+    hipLaunchKernelGGL(xgmi_emulate_block_peers_kernel, dim3(nblocks), dim3(64), 0, stream, c->desc, hdr, data, n, 1,
+                       delay_ticks);
+  else
+    hipLaunchKernelGGL(xgmi_emulate_block_flags_kernel, dim3(1), dim3(256), 0, stream, c->desc, hdr, nblocks,
+                       delay_ticks);
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -67,6 +67,35 @@ def test_fused_grads_match_reference(data, loss, B, offset, kernel):
     assert float((gk * (1 - FM.pad_mask("cuda"))).abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("loss", ["softmax", "bce"])
+def test_fused_grads_match_reference_at_headline_batch(loss):
+    """The headline configuration itself (BASELINE configs[2]: B = 1,048,576 rows per step, the
+    planted synthetic draws bench.py trains on, all 256 CUs' slabs reduced): train kernel gradient
+    and loss against the fp32 PyTorch reference of the same step."""
+    from euromillioner_amd.data.device_gen import generate_masks
+    from euromillioner_amd.models.mlp import FusedSmallMLP
+    from euromillioner_amd.ops import fused_mlp as FM
+
+    B, off = 1 << 20, 5
+    draws = generate_masks(B + 16, seed=1, planted=0.9, device="cuda")
+    m = FusedSmallMLP(loss=loss, seed=3)
+    lk, gk = m.grads(draws, B, offset=off)
+    bits = torch.arange(62, device="cuda")
+    X = ((draws[off:off + B, None] >> bits) & 1).float()
+    Y = ((draws[off + 1:off + 1 + B, None] >> bits) & 1).float()
+    sd = m.state_dict()
+    rnd = lambda t: t.cuda().bfloat16().float()  # noqa: E731  (the kernel's operand rounding)
+    W1, b1, W2 = (rnd(sd[k]).requires_grad_() for k in ("l1.weight", "l1.bias", "l2.weight"))
+    b2 = sd["l2.bias"].cuda().clone().requires_grad_()
+    h = torch.relu(X @ W1.t() + b1)
+    lr_ = L.LOSSES[loss](rnd(h) @ W2.t() + b2, Y)
+    lr_.backward()
+    assert X.sum(1).min() == 7 and X.sum(1).max() == 7  # every row a draw (5 mains + 2 stars)
+    assert abs(lk - lr_.item()) <= 2e-3 * max(1.0, abs(lr_.item())), (lk, lr_.item())
+    _assert_grads_close(gk, {"l1.weight": W1.grad, "l1.bias": b1.grad, "l2.weight": W2.grad, "l2.bias": b2.grad})
+    assert float((gk * (1 - FM.pad_mask("cuda"))).abs().max()) == 0.0
+
+
 def test_fused_forward_and_metrics(data):
     from euromillioner_amd.models.mlp import FusedSmallMLP
     from euromillioner_amd.ops import fused_mlp as FM

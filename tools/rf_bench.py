@@ -52,18 +52,21 @@ def main():
         times.append(time.perf_counter() - t0)
     n_val = a.rows - n_tr
     Xv = md[n_tr:a.rows].reshape(-1, 1).contiguous()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    lg = K.predict(Xv, feat, value, a.depth, out_logit=True)
-    torch.cuda.synchronize()
-    t_pred = time.perf_counter() - t0
+    pred_times = []
+    for _ in range(1 + a.repeat):  # the first call pays one-time costs (code object load, LDS attribute)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lg = K.predict(Xv, feat, value, a.depth, out_logit=True)
+        torch.cuda.synchronize()
+        pred_times.append(time.perf_counter() - t0)
+    t_pred = min(pred_times[1:]) if len(pred_times) > 1 else pred_times[0]
     part = FM.draw_metrics(lg, md, n_val, loss="bce", offset=n_tr).double().sum(0).cpu().numpy()
     cnt = part[7]
     val = {kk: float(part[i] / cnt) for i, kk in enumerate(FM.METRIC_NAMES[:-1])}
     fit_s = min(times)
     print(json.dumps({"metric": "random forest fit (100 trees, 62 one-hot features)", "rows": n_tr,
                       "trees": a.trees, "max_depth": a.depth, "k_features": k, "fit_s": fit_s,
-                      "fit_rows_x_trees_per_s": n_tr * a.trees / fit_s, "predict_s": t_pred,
+                      "fit_rows_x_trees_per_s": n_tr * a.trees / fit_s, "predict_s": t_pred, "predict_first_call_s": pred_times[0],
                       "predict_rows_per_s": n_val / t_pred, "nodes_split": int((feat >= 0).sum().item()),
                       "val": val}))
 

@@ -6,14 +6,16 @@ one-process proxy: rank 0 is the real model and its step is the real DP step, tw
 kernel -> ``em_adam_slab_xgmi``: each block reduces its 64-parameter slice of the slabs into the own
 xGMI slot, raises its block flag, polls the 7 peers' block flags, sums 8 slices in rank order and
 applies Adam), hipGraph-replayed like bench.py.  The 7 peers are buffers of this process on the same
-device (``em_xgmi_connect_local``), played by ``em_xgmi_emulate_block_peers``: a kernel on a side
-stream, beside the consumer, whose block j waits for rank 0's block flag j, ``skew`` microseconds more
-(the peers reaching the exchange later than rank 0), copies the slice into the 7 peer slots and raises
-the peers' block flags j.
+device (``em_xgmi_connect_local``), played by ``em_xgmi_emulate_block_peers`` on a side stream beside
+the consumer.  The timed "dpN" rows use its timing-only form (copy=0): one block raises all the peers'
+block flags ``skew`` microseconds after the train kernel ends (the peers reaching the exchange later
+than rank 0) and never waits on the consumer, so it adds no traffic of its own and cannot deadlock
+when a replay runs it before the consumer.  The "dpN-copy" row uses the full form (block j waits for
+rank 0's block flag j, copies the slice into the 7 peer slots, raises the peers' flag j: the traffic
+real peers produce on their OWN GPUs), to show what that emulation costs on one device.
 
 What it measures: the device cost of the 8-way exchange on top of the single-GPU step (7 extra slice
-reads and block-flag polls inside the consumer; the emulator's copies, which real peers do in their
-own consumers), and how a late peer propagates into the step.  What it does not: xGMI link latency and bandwidth (the peer slots are local HBM here).  For
+reads and block-flag polls inside the consumer), and how a late peer propagates into the step.  What it does not: xGMI link latency and bandwidth (the peer slots are local HBM here).  For
 64 KB per peer over 7 links at ~50 GB/s effective that is ~1.3 us of transfer plus one hop of
 ~1-2 us; docs/DESIGN.md adds it to the budget.
 
@@ -40,7 +42,7 @@ def main():
 
     world = int(os.environ.get("XB_WORLD", "8"))
     B = int(os.environ.get("XB_B", str(1 << 20)))
-    steps = 20
+    steps = 100
     dev = torch.device("cuda", 0)
     draws = generate_masks(4 * B + 16, seed=1, planted=0.9, device=dev)
     P = FM.P_TOTAL
@@ -69,13 +71,15 @@ def main():
             ev.record()
             side.wait_event(ev)
             with torch.cuda.stream(side):
-                N.call("em_xgmi_emulate_block_peers", h0, P // 64, P + 1, 1, float(skew_us), N.stream_handle(dev))
+                N.call("em_xgmi_emulate_block_peers", h0, P // 64, P + 1, 1 if mode.endswith("copy") else 0,
+                       float(skew_us), N.stream_handle(dev))
             FM.adam_slab_xgmi(h0, m.slabs, nslab, scale, m.params, m.m, m.v, m.hp, m.state, m.loss_slabs, img=m.img,
                               loss_out=m.loss_out, loss_scale=scale, pre=True)
             torch.cuda.current_stream().wait_stream(side)
         return step
 
-    configs = [("single", 0.0)] + [("dp%d" % world, s) for s in (0.0, 2.0, 5.0, 10.0)]
+    configs = ([("single", 0.0)] + [("dp%d" % world, s) for s in (0.0, 2.0, 5.0, 10.0)]
+               + [("dp%d-copy" % world, 0.0)])
     for rnd in range(2):
         for mode, skew in configs:
             m = FusedSmallMLP(dev, lr=1e-3, seed=0)
