@@ -138,20 +138,17 @@ adam_slab_kernel(const float* __restrict__ slabs, int nslab, int P, int stride, 
 // thread (quad, e) adds the 16 group sums in group order.  The fixed summation order keeps the result
 // bitwise reproducible; the single-GPU step (adam_slab4_kernel) and the fused xGMI DP step
 // (adam_slab_xgmi_kernel) share it, so their per-rank gradients are bit-identical.
-// (compile-time A/B knobs for side builds, tools/build_variant.sh: ADAM_G slab groups per block ->
-// 16 * ADAM_G threads, 256 / ADAM_G loads in flight per thread; ADAM_NT nontemporal slab loads)
+// The slabs are read once, so their loads are nontemporal: same-box A/B over 3 interleaved rounds of
+// the 1M-sample step (round 5, profiles/r5/ab_headline.jsonl), 88.63 -> 87.51 us per step with
+// bit-identical parameters.  32 slab groups per block (512 threads, 8 loads in flight per thread)
+// measured 87.98 us and changes the summation order; it was not kept.
+// (compile-time A/B knob for side builds, tools/build_variant.sh: ADAM_G slab groups per block)
 #ifndef ADAM_G
 #define ADAM_G 16
 #endif
-#ifndef ADAM_NT
-#define ADAM_NT 0
-#endif
 constexpr int A4_G = ADAM_G, A4_T = 16 * A4_G, A4_U = 256 / A4_G;
 static_assert(A4_U >= 4 && A4_U * A4_G == 256, "slab groups");
-EM_DEVICE f32x4 slab_ld(const float* p) {
-  if (ADAM_NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  return *reinterpret_cast<const f32x4*>(p);
-}
+EM_DEVICE f32x4 slab_ld(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p)); }
 struct Slab4Out {
   float g = 0.f;                  // threads < 64: grad_scale * sum over slabs of parameter blockIdx.x * 64 + t
   float w0 = 0.f, m0 = 0.f, v0 = 0.f;  // threads < 64 (with adam): the Adam operands, loaded under the slab loads

@@ -1116,8 +1116,13 @@ __global__ void __launch_bounds__(RFP_PREP_THREADS) rf_predict_prepare(const int
   }
 }
 
+// RFP_WAVES waves per workgroup, at most 2 x 64 rows per wave: 3 waves per SIMD hide the walk's
+// dependent LDS reads, and 64 accumulators per row fit the 168 VGPRs a wave gets (a 3-group form at
+// 2 waves per SIMD needed 192 accumulators and spilled 576 B per lane to scratch: 2.27 ms for 300 k
+// rows x 100 trees, round 5)
+constexpr int RFP_WAVES = 12;
 template <int G>
-__global__ void __launch_bounds__(512) rf_predict_lds(const uint64_t* __restrict__ X, int64_t N,
+__global__ void __launch_bounds__(RFP_WAVES * 64) rf_predict_lds(const uint64_t* __restrict__ X, int64_t N,
                                                       const uint8_t* __restrict__ prep, int T, int rows_per_wave,
                                                       int64_t rows_per_block, int out_logit, float* __restrict__ out,
                                                       int ldo) {
@@ -1142,11 +1147,11 @@ __global__ void __launch_bounds__(512) rf_predict_lds(const uint64_t* __restrict
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)prep, 0, 0x7FFFFFFF, 0x00020000);
   // tree t's node table + leaf vectors -> LDS buffer t & 1: 1 + nleaf / 4 pieces of 1 KB, over the waves
+  // (all 65 pieces whatever the tree's leaf count: reading the count first put one dependent global load
+  // in front of every tree's DMA)
   auto stage = [&](int t) {
-    const int nleaf = reinterpret_cast<const int16_t*>(prep + (int64_t)t * RFP_TREE)[511];
-    const int pieces = 1 + (nleaf + 3) / 4;
     char* dst = smem + (t & 1) * RFP_TREE;
-    for (int pc = wave; pc < pieces; pc += 8)
+    for (int pc = wave; pc < RFP_TREE / 1024; pc += RFP_WAVES)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (EM_LDS void*)(dst + pc * 1024), 16, (uint32_t)lane * 16,
                                                (uint32_t)t * RFP_TREE + (uint32_t)pc * 1024, 0, 0);
   };
@@ -1158,20 +1163,39 @@ __global__ void __launch_bounds__(512) rf_predict_lds(const uint64_t* __restrict
     if (t + 1 < T) stage(t + 1);
     const char* buf = smem + (t & 1) * RFP_TREE;
     const int16_t* enc = reinterpret_cast<const int16_t*>(buf);
+    // the G row groups walk the tree together: their dependent node reads are independent of each
+    // other, so each step has G reads in flight instead of one
+    int nd[G], f[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      nd[g] = 0;
+      f[g] = rw0 + 64 * g < rend ? (int)enc[0] : -1;  // (wave-uniform: groups past the wave's rows stay out)
+    }
+    for (;;) {
+      bool more = false;
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (f[g] >= 0) {
+          const uint32_t w = f[g] < 32 ? xlo[g] : xhi[g];
+          nd[g] = 2 * nd[g] + 1 + (int)((w >> (f[g] & 31)) & 1u);
+          f[g] = enc[nd[g]];
+          more |= f[g] >= 0;
+        }
+      if (!__builtin_amdgcn_ballot_w64(more)) break;
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (rw0 + 64 * g >= rend) break;  // (wave-uniform)
-      int nd = 0, f = enc[0];
-      while (f >= 0) {
-        const uint32_t w = f < 32 ? xlo[g] : xhi[g];
-        nd = 2 * nd + 1 + (int)((w >> (f & 31)) & 1u);
-        f = enc[nd];
-      }
-      const uint32_t lb = 1024u + (uint32_t)(-f - 1) * 256u;
+      const uint32_t lb = 1024u + (uint32_t)(-f[g] - 1) * 256u;
+      // 4 batches of 4 chunk reads: the rotated offsets are kept opaque (hoisted, they held 16 VGPRs)
+      // and a batch's adds complete before the next batch's reads issue (all 16 in flight held 64)
+      uint32_t kr = rot;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        const uint32_t off = lb | ((rot + 16u * c) & 0xF0u);
-        acc[g][c] += *reinterpret_cast<const f32x4*>(buf + off);
+        acc[g][c] += *reinterpret_cast<const f32x4*>(buf + (lb | (kr & 0xF0u)));
+        kr += 16u;
+        asm volatile("" : "+v"(kr));
+        if ((c & 3) == 3) asm volatile("" : "+v"(acc[g][c - 3]), "+v"(acc[g][c - 2]), "+v"(acc[g][c - 1]), "+v"(acc[g][c]));
       }
     }
   }
@@ -1396,24 +1420,23 @@ EM_API int em_rf_predict(const uint64_t* X, int W, int64_t N, const int16_t* fea
         cus = 256;
       (void)hipFuncSetAttribute((const void*)rf_predict_lds<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * RFP_TREE);
       (void)hipFuncSetAttribute((const void*)rf_predict_lds<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * RFP_TREE);
-      (void)hipFuncSetAttribute((const void*)rf_predict_lds<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * RFP_TREE);
     }
-    // one workgroup per CU (the LDS double buffer), rows spread evenly; at most 3 x 64 rows per wave
-    int64_t grid = (N + 511) / 512;
+    // one workgroup per CU (the LDS double buffer), rows spread evenly; at most 2 x 64 rows per wave
+    constexpr int NW = RFP_WAVES;
+    int64_t grid = (N + 64 * NW - 1) / (64 * NW);
     if (grid > cus) grid = cus;
-    int64_t rpw = ((N + grid - 1) / grid + 7) / 8;
-    if (rpw > 192) {
-      rpw = 192;
-      grid = (N + 8 * rpw - 1) / (8 * rpw);
+    int64_t rpw = ((N + grid - 1) / grid + NW - 1) / NW;
+    if (rpw > 128) {
+      rpw = 128;
+      grid = (N + NW * rpw - 1) / (NW * rpw);
     }
     const int G = (int)((rpw + 63) / 64);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), 2 * RFP_TREE, stream, X, N, (const uint8_t*)prep, T,
-                         (int)rpw, 8 * rpw, out_logit, out, ldo);
+      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), 2 * RFP_TREE, stream, X, N, (const uint8_t*)prep,
+                         T, (int)rpw, NW * rpw, out_logit, out, ldo);
     };
     if (G == 1) go(rf_predict_lds<1>);
-    else if (G == 2) go(rf_predict_lds<2>);
-    else go(rf_predict_lds<3>);
+    else go(rf_predict_lds<2>);
     EM_CHECK_LAUNCH();
     return 0;
   }

@@ -169,9 +169,11 @@ constexpr int HIST_EXACT_LDS_BUDGET = HIST_LDS_BUDGET;
 constexpr int HIST_EXACT_THREADS = 256;
 constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
 // rows per histogram chunk at least HIST_MIN_CHUNK (compile-time A/B knob for side builds,
-// tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk)
+// tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk).  128 rows:
+// reference fit 0.045 -> 0.042 s on the same box (round 5, profiles/r5/gbdt_chunk_ab.txt: fewer
+// partials for the split to fold; 256 fell back to 0.045 s, too few blocks per level)
 #ifndef HIST_MIN_CHUNK
-#define HIST_MIN_CHUNK 64
+#define HIST_MIN_CHUNK 128
 #endif
 
 __global__ void __launch_bounds__(HIST_EXACT_THREADS)

@@ -114,13 +114,16 @@ xgmi_emulate_block_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, f
 // the exchange delay_ticks after this rank's train kernel ends).  It never waits on the consumer, so a
 // graph replay that happens to run it before the consumer cannot deadlock, and it adds no polling or
 // copy traffic of its own beside the consumer being timed (the 257-block waiting form above does).
+// saturate: every flag is set to INT_MAX instead (peers infinitely early: no consumer wait ever
+// blocks again on this communicator; the budget's lower bound, one launch before the timed steps)
 __global__ void __launch_bounds__(256)
-xgmi_emulate_block_flags_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, int nblocks, long long delay_ticks) {
+xgmi_emulate_block_flags_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, int nblocks, long long delay_ticks,
+                                int saturate) {
   __shared__ int s_sh;
   if (threadIdx.x == 0) {
     const long long t0 = wall_clock64();
     while (wall_clock64() - t0 < delay_ticks) __builtin_amdgcn_s_sleep(2);
-    s_sh = xg_next_seq(d.my_hdr);
+    s_sh = saturate ? 0x7FFFFFFF : xg_next_seq(d.my_hdr);
   }
   __syncthreads();
   const int s = s_sh;
@@ -321,7 +324,9 @@ EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t st
 }
 
 // block-flag form (the fused DP consumer, em_adam_slab_xgmi over nblocks = P / 64 slices of an n-float
-// slot): run on a side stream beside the consumer; see xgmi_emulate_block_peers_kernel
+// slot): run on a side stream beside the consumer.  copy 1: xgmi_emulate_block_peers_kernel (waits for
+// each own slice, copies it); 0: flags only, delay_us after launch; 2: flags saturated (see
+// xgmi_emulate_block_flags_kernel)
 EM_API int em_xgmi_emulate_block_peers(void* h, int nblocks, int n, int copy, double delay_us, hipStream_t stream) {
   XgmiComm* c = static_cast<XgmiComm*>(h);
   if (!c || !c->local_proxy || nblocks <= 0 || nblocks > XG_MAX_BFLAGS || n < 0 || n > c->desc.cap ||
@@ -333,12 +338,12 @@ EM_API int em_xgmi_emulate_block_peers(void* h, int nblocks, int n, int copy, do
   int* const* hdr = reinterpret_cast<int* const*>(c->peer_ptrs);
   float* const* data = reinterpret_cast<float* const*>(c->peer_ptrs) + XG_MAXW;
   const long long delay_ticks = (long long)(delay_us * 1e-3 * khz);
-  if (copy)
+  if (copy == 1)
     hipLaunchKernelGGL(xgmi_emulate_block_peers_kernel, dim3(nblocks), dim3(64), 0, stream, c->desc, hdr, data, n, 1,
                        delay_ticks);
   else
     hipLaunchKernelGGL(xgmi_emulate_block_flags_kernel, dim3(1), dim3(256), 0, stream, c->desc, hdr, nblocks,
-                       delay_ticks);
+                       delay_ticks, copy == 2 ? 1 : 0);
   EM_CHECK_LAUNCH();
   return 0;
 }

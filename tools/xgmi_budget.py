@@ -47,16 +47,17 @@ def main():
     draws = generate_masks(4 * B + 16, seed=1, planted=0.9, device=dev)
     P = FM.P_TOTAL
 
-    comms = []
-    for _ in range(world):
-        h = ctypes.c_void_p()
-        rc = N.lib().em_xgmi_create(P + 1, 5.0, ctypes.byref(h))
-        if rc != 0:
-            raise SystemExit(f"em_xgmi_create failed ({rc})")
-        comms.append(h)
-    arr = (ctypes.c_void_p * world)(*[c.value for c in comms])
-    N.call("em_xgmi_connect_local", comms[0], world, 0, arr)
-    h0 = comms[0].value
+    def make_comms():
+        comms = []
+        for _ in range(world):
+            h = ctypes.c_void_p()
+            rc = N.lib().em_xgmi_create(P + 1, 5.0, ctypes.byref(h))
+            if rc != 0:
+                raise SystemExit(f"em_xgmi_create failed ({rc})")
+            comms.append(h)
+        arr = (ctypes.c_void_p * world)(*[c.value for c in comms])
+        N.call("em_xgmi_connect_local", comms[0], world, 0, arr)
+        return comms
 
     def make_step(m, mode, skew_us, side):
         scale = 1.0 / (B * world)
@@ -70,19 +71,25 @@ def main():
             ev = torch.cuda.Event()
             ev.record()
             side.wait_event(ev)
-            with torch.cuda.stream(side):
-                N.call("em_xgmi_emulate_block_peers", h0, P // 64, P + 1, 1 if mode.endswith("copy") else 0,
-                       float(skew_us), N.stream_handle(dev))
+            if not mode.endswith("nowait"):
+                with torch.cuda.stream(side):
+                    N.call("em_xgmi_emulate_block_peers", h0, P // 64, P + 1, 1 if mode.endswith("copy") else 0,
+                           float(skew_us), N.stream_handle(dev))
             FM.adam_slab_xgmi(h0, m.slabs, nslab, scale, m.params, m.m, m.v, m.hp, m.state, m.loss_slabs, img=m.img,
                               loss_out=m.loss_out, loss_scale=scale, pre=True)
             torch.cuda.current_stream().wait_stream(side)
         return step
 
-    configs = ([("single", 0.0)] + [("dp%d" % world, s) for s in (0.0, 2.0, 5.0, 10.0)]
+    configs = ([("single", 0.0), ("dp%d-nowait" % world, 0.0)] + [("dp%d" % world, s) for s in (0.0, 2.0, 5.0, 10.0)]
                + [("dp%d-copy" % world, 0.0)])
-    for rnd in range(2):
+    for rnd in range(int(os.environ.get("XB_ROUNDS", "2"))):
         for mode, skew in configs:
             m = FusedSmallMLP(dev, lr=1e-3, seed=0)
+            comms = make_comms()
+            h0 = comms[0].value
+            if mode.endswith("nowait"):  # peers infinitely early: the consumer's own cost (lower bound)
+                N.call("em_xgmi_emulate_block_peers", h0, P // 64, P + 1, 2, 0.0, N.stream_handle(dev))
+                torch.cuda.synchronize()
             side = torch.cuda.Stream()
             step = make_step(m, mode, skew, side)
             step(0)  # eager first step (argument checks, LDS attributes)
@@ -107,12 +114,13 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / steps
             err = ctypes.c_int(0)
             N.call("em_xgmi_error", h0, ctypes.byref(err))
+            torch.cuda.synchronize()
             print(json.dumps({"round": rnd, "mode": mode, "world": world if mode != "single" else 1,
                               "peer_skew_us": skew, "us_per_step": round(us, 2), "per_gpu_batch": B,
                               "xgmi_error": int(err.value), "loss": float(m.loss_out.item())}), flush=True)
             del g
-    for c in comms:
-        N.lib().em_xgmi_destroy(c)
+            for c in comms:
+                N.lib().em_xgmi_destroy(c)
 
 
 if __name__ == "__main__":
