@@ -228,12 +228,14 @@ adam_slab4_kernel(const float* __restrict__ slabs, int nslab, int P, int stride,
   if (mode != 1 && !pre) adam_end(state, tstep);
 }
 
-// The data-parallel step's second (and last) launch over xGMI (xgmi.h, block-flag form): slice j
-// (parameters 64j .. 64j + 63) is reduced from this rank's slabs exactly as adam_slab4_kernel does,
-// written into slice j of the own slot (system-scope write-through stores; slice 0 adds the loss as
-// element P), published with block flag j; then the block waits for block flag j of every peer, sums
-// slice j of all N slots in rank order (bit-identical on every rank) and applies Adam.  No separate
-// slab-reduction launch and no grid-wide barrier: a slice travels as soon as it is reduced.
+// The data-parallel step's second (and last) launch over xGMI (xgmi.h, LL form): slice j (parameters
+// 64j .. 64j + 63) is reduced from this rank's slabs exactly as adam_slab4_kernel does and stored as
+// LL words {value, s} into slice j of the own LL slot (slice 0 adds the loss as element P); each of
+// the 64 lanes then polls the N - 1 peers' words of its parameter until they carry tag s, sums the N
+// values in rank order (bit-identical on every rank) and applies Adam.  No separate slab-reduction
+// launch, no drain, flag or barrier: a slice travels as soon as it is reduced, in one round trip.
+// (The round-5 block-flag form -- drained slot stores, a block flag, flag polls, then slot reads --
+// was three round trips: tools/xgmi_budget.py, profiles/r5/.)
 // One block per slice on a node (257 blocks); ranks that share a device launch fewer blocks that loop
 // over the slices, so the spinning consumer leaves CUs free for a peer's whole-CU train kernel.
 __global__ void __launch_bounds__(A4_T)
@@ -245,19 +247,30 @@ adam_slab_xgmi_kernel(XgmiDesc d, const float* __restrict__ slabs, int nslab, in
   const int s = xg_next_seq(d.my_hdr);
   int tstep = 0;
   if (threadIdx.x < 64) tstep = state[0] + (pre ? 0 : 1);
-  float* slot = d.my_data + (size_t)(s & 1) * d.cap;
+  __shared__ int bad;  // a peer wait of this block timed out: later slices skip their waits
+  if (threadIdx.x == 0) bad = 0;
   for (int j = blockIdx.x; j < P / 64; j += gridDim.x) {
-    if (j != (int)blockIdx.x) __syncthreads();  // the previous slice's LDS partials are consumed
+    __syncthreads();  // (bad initialised; the previous slice's LDS partials are consumed)
     const Slab4Out o = slab4_reduce(j, slabs, nslab, stride, grad_scale, true, tstep, params, m, v, hp);
     const int p = j * 64 + threadIdx.x;
-    if (threadIdx.x < 64) __hip_atomic_store(slot + p, o.g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // LL exchange (xgmi.h): store this rank's words, then poll every peer's words of the slice
+    if (threadIdx.x < 64) xg_ll_put(d, s, p, o.g);
+    float lsum = 0.f;
     if (j == 0 && threadIdx.x >= 64 && threadIdx.x < 128) {
       const float l = loss_sum(loss_slabs, nslab, threadIdx.x - 64);
-      if (threadIdx.x == 64) __hip_atomic_store(slot + P, l * loss_scale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (threadIdx.x == 64) {
+        lsum = l * loss_scale;
+        xg_ll_put(d, s, P, lsum);
+      }
     }
-    if (xg_publish_block_and_wait(d, s, j)) {
-      if (threadIdx.x < 64) adam_apply_bc(p, xg_sum(d, s, p), o.w0, o.m0, o.v0, o.bc1, o.bc2, params, m, v, hp, mlp_img);
-      if (j == 0 && threadIdx.x == 64 && loss_out) loss_out[0] = xg_sum(d, s, P);
+    bool ok = true;
+    if (threadIdx.x < 64) {
+      const float g = xg_ll_sum(d, s, p, o.g, ok, &bad);
+      if (ok) adam_apply_bc(p, g, o.w0, o.m0, o.v0, o.bc1, o.bc2, params, m, v, hp, mlp_img);
+    }
+    if (j == 0 && threadIdx.x == 64) {
+      const float l = xg_ll_sum(d, s, P, lsum, ok, &bad);
+      if (ok && loss_out) loss_out[0] = l;
     }
   }
   xg_finish(d, s);
@@ -387,8 +400,8 @@ EM_API int em_adam_slab(const float* slabs, int nslab, int P, int stride, float 
   return 0;
 }
 
-// The fused DP optimizer step (adam_slab_xgmi_kernel): slab reduction into the own xGMI slot, exchange,
-// rank-order sum and Adam in ONE launch.  Needs P % 64 == 0 and a 16-B aligned slab array; max_blocks > 0
+// The fused DP optimizer step (adam_slab_xgmi_kernel): slab reduction into the own xGMI LL slot,
+// exchange, rank-order sum and Adam in ONE launch.  Needs P % 64 == 0 and a 16-B aligned slab array; max_blocks > 0
 // caps the grid (ranks sharing a device);
 // loss_out (optional) receives the reduced loss; pre = the step counter was already advanced by this
 // step's train kernel (EM_ADAM_PRE).
@@ -401,7 +414,9 @@ EM_API int em_adam_slab_xgmi(void* xgmi, const float* slabs, int nslab, int stri
     return EM_ERR_ARG;
   if (mlp_img && P != P_TOTAL) return EM_ERR_ARG;
   int nb = P / 64;
-  if (nb > XG_MAX_BFLAGS) return EM_ERR_ARG;  // one block flag per slice (257 blocks: co-resident at 8 per CU)
+  // blocks loop over slices past the grid; <= 1024 blocks stay co-resident (4 per CU), so no block
+  // polls a peer while this rank's own block for the same slice is still waiting to be scheduled
+  if (nb > 1024) nb = 1024;
   if (max_blocks > 0 && nb > max_blocks) nb = max_blocks;
   hipLaunchKernelGGL(adam_slab_xgmi_kernel, dim3(nb), dim3(A4_T), 0, stream, xc->desc, slabs, nslab, stride, grad_scale,
                      params, m, v, hp, state, (uint8_t*)mlp_img, loss_slabs, loss_out, loss_scale, P, pre ? 1 : 0);

@@ -11,6 +11,7 @@
 //            error word (timeouts)                                @ 64
 //            seq_local, ticket (r only)                           @ 128, 132
 //   data   : two slots of `cap` floats                             @ 4096
+//   LL     : two slots of `cap` 8-byte words (the fused DP consumer) @ 4096 + 8 cap
 // step s = seq_local + 1:
 //   1. producer kernel (slab reduce / stage) writes slot[s & 1] of B_r.
 //   2. consumer kernel: block 0 publishes flag_r = s (system-scope release; the producer's
@@ -22,13 +23,14 @@
 // step-(s+1) consumer saw every flag_q >= s+1, and q publishes s+1 only after finishing its
 // step-s consumer (stream order).  Flags only grow, so nothing is ever reset.
 //
-// Block-flag form (the fused DP step, adam.hip adam_slab_xgmi_kernel): the consumer itself produces
-// the slot.  Block j reduces its own slice j of the slot, writes it with system-scope (write-through)
-// stores, drains them, and publishes BLOCK flag j (header int XG_BFLAG + j); peers' block j waits for
-// block flag j of every rank only, so no grid-wide barrier stands between the slab reduction and the
-// exchange.  The reuse argument above holds per slice: q publishes block flag j = s+1 only in its
-// step-(s+1) consumer, i.e. after its step-s consumer (which read slice j of every slot) finished.
-// Both flag kinds are raised only at the start of a consumer, so the two forms may be interleaved.
+// LL form (the fused DP step, adam.hip adam_slab_xgmi_kernel): the consumer itself produces the slot,
+// as "LL" words -- 8 bytes {float bits, sequence number s} stored with one 64-bit system-scope store --
+// in a second pair of slots after the float slots.  Block j reduces its own slice j, stores its 64 LL
+// words and, with no drain, no flag and no barrier, reads slice j of every peer: each reader polls the
+// peer's word itself until its tag reaches s.  One round trip per exchange instead of three (slot
+// stores drained, flag raised, flags polled, slots read).  The reuse argument above holds per word:
+// q writes tag s + 2 into the same-parity slot only in its step-(s+2) consumer, i.e. after its
+// step-(s+1) consumer read our tag-(s+1) words, which we store only after finishing step s.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,8 +41,6 @@ constexpr int XG_FLAG = 0;     // int index into the header
 constexpr int XG_ERROR = 16;   // byte 64
 constexpr int XG_SEQ = 32;     // byte 128
 constexpr int XG_TICKET = 33;  // byte 132
-constexpr int XG_BFLAG = 64;   // byte 256: block flags of the fused DP consumer
-constexpr int XG_MAX_BFLAGS = XG_HDR_BYTES / 4 - XG_BFLAG;
 
 struct XgmiDesc {
   const float* peer_data[XG_MAXW];  // slot 0 of every rank's buffer (own included), rank order
@@ -90,15 +90,53 @@ __device__ __forceinline__ bool xg_publish_and_wait(const XgmiDesc& d, int s) {
   return xg_wait_flags(d, s, XG_FLAG);
 }
 
-// Block-flag form: slice j of the own slot is written (system-scope stores by every writing thread of
-// this block); drain them, then one lane raises block flag j and the block waits for block flag j of
-// every rank.
-__device__ __forceinline__ bool xg_publish_block_and_wait(const XgmiDesc& d, int s, int j) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slice stores have landed
-  __syncthreads();                                   // ... and every other wave's
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&d.my_hdr[XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return xg_wait_flags(d, s, XG_BFLAG + j);
+// LL words: after the two float slots of a buffer, two slots of `cap` 8-byte words (parity s & 1)
+__device__ __forceinline__ const uint64_t* xg_ll(const float* data, int cap, int s) {
+  return reinterpret_cast<const uint64_t*>(data + 2 * (size_t)cap) + (size_t)(s & 1) * cap;
+}
+__device__ __forceinline__ uint64_t xg_ll_word(float v, int s) {
+  return ((uint64_t)(uint32_t)s << 32) | (uint64_t)__float_as_uint(v);
+}
+__device__ __forceinline__ bool xg_ll_ready(uint64_t w, int s) { return (int)(uint32_t)(w >> 32) >= s; }
+// this rank's element i of step s
+__device__ __forceinline__ void xg_ll_put(const XgmiDesc& d, int s, int i, float v) {
+  uint64_t* w = const_cast<uint64_t*>(xg_ll(d.my_data, d.cap, s)) + i;
+  __hip_atomic_store(w, xg_ll_word(v, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Element i of step s summed over all ranks in rank order (bitwise identical on every rank); `own` is
+// this rank's value (not read back).  Every peer word is polled until its tag reaches s; the loads of
+// all peers are in flight together.  A timeout raises the error word and *bad (an LDS flag the caller
+// shares across its block: later slices then skip their waits) and returns ok = false.
+__device__ __forceinline__ float xg_ll_sum(const XgmiDesc& d, int s, int i, float own, bool& ok, int* bad) {
+  uint64_t w[XG_MAXW];
+#pragma unroll
+  for (int q = 0; q < XG_MAXW; ++q)
+    w[q] = (q < d.world && q != d.rank)
+               ? __hip_atomic_load(xg_ll(d.peer_data[q], d.cap, s) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+               : xg_ll_word(own, s);
+  ok = *bad == 0;
+  const long long t0 = wall_clock64();
+  while (ok) {
+    bool all = true;
+#pragma unroll
+    for (int q = 0; q < XG_MAXW; ++q)
+      if (!xg_ll_ready(w[q], s)) {
+        all = false;
+        w[q] = __hip_atomic_load(xg_ll(d.peer_data[q], d.cap, s) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    if (all) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > d.timeout_ticks) {
+      ok = false;
+      *bad = 1;
+      __hip_atomic_store(&d.my_hdr[XG_ERROR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  float acc = __uint_as_float((uint32_t)w[0]);
+#pragma unroll
+  for (int q = 1; q < XG_MAXW; ++q)
+    if (q < d.world) acc += __uint_as_float((uint32_t)w[q]);
+  return acc;
 }
 
 // Sum element i of slot (s & 1) over all ranks, rank order (bitwise identical on every rank).
@@ -126,6 +164,9 @@ __device__ __forceinline__ void xg_finish(const XgmiDesc& d, int s) {
     }
   }
 }
+
+// Buffer bytes for a capacity of `cap` floats: header, two float slots, two LL slots.
+inline size_t xg_buffer_bytes(int cap) { return XG_HDR_BYTES + 2ull * cap * sizeof(float) + 2ull * cap * sizeof(uint64_t); }
 
 // Host side (xgmi.hip): the C++ communicator object behind the opaque handle.
 struct XgmiComm {

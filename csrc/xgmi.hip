@@ -60,78 +60,50 @@ xgmi_emulate_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, float* 
     __hip_atomic_store(&peer_hdr[threadIdx.x][XG_FLAG], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The same for the block-flag form (adam_slab_xgmi_kernel): emulated-peer block j waits until this
-// rank's block j has published its slice (own block flag j), waits `delay_ticks` more, copies the
-// slice (and, in block 0, the elements past the last full slice: the loss) into every emulated peer's
-// slot when `copy` is set, and raises the peers' block flag j.  Every wait is bounded by the
-// communicator's timeout (a missing own publication sets the error word).
+// The same for the LL form (adam_slab_xgmi_kernel, xgmi.h): block j stands in for the peers' words
+// of slice j (64 elements; block 0 also the elements past the last full slice: the loss).
+//   copy 1: each element waits until this rank's own LL word carries tag s (its slice is published),
+//           `delay_ticks` more, then copies the word into every emulated peer's slot (bit-exact sums).
+//           Every wait is bounded by the communicator's timeout (the error word is raised).
+//   copy 0: timing only: `delay_ticks` after the block starts, the peers' words get tag s (value 0)
+//           without waiting on the consumer, so a graph replay that runs it first cannot deadlock.
+//   copy 2: the peers' words get tag INT_MAX once (peers infinitely early: no consumer wait on this
+//           communicator ever blocks again; the budget's lower bound).
 __global__ void __launch_bounds__(64)
-xgmi_emulate_block_peers_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, float* const* __restrict__ peer_data,
-                                int n, int copy, long long delay_ticks) {
-  __shared__ int s_sh;
+xgmi_emulate_block_peers_kernel(XgmiDesc d, float* const* __restrict__ peer_data, int n, int copy,
+                                long long delay_ticks) {
   const int j = blockIdx.x;
-  if (threadIdx.x == 0) {
-    const int s = xg_next_seq(d.my_hdr);
+  const int s = copy == 2 ? 0x7FFFFFFF : xg_next_seq(d.my_hdr);
+  const int full = 64 * (int)gridDim.x;
+  auto one = [&](int i) {
+    uint64_t w = xg_ll_word(0.f, s);
     const long long t0 = wall_clock64();
-    while (__hip_atomic_load(&d.my_hdr[XG_BFLAG + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > d.timeout_ticks) {
-        __hip_atomic_store(&d.my_hdr[XG_ERROR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+    if (copy == 1) {
+      const uint64_t* own = xg_ll(d.my_data, d.cap, s) + i;
+      for (;;) {
+        w = __hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (xg_ll_ready(w, s)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > d.timeout_ticks) {
+          __hip_atomic_store(&d.my_hdr[XG_ERROR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return;
+        }
       }
     }
     const long long t1 = wall_clock64();
     while (wall_clock64() - t1 < delay_ticks) __builtin_amdgcn_s_sleep(2);
-    s_sh = s;
-  }
-  __syncthreads();
-  const int s = s_sh;
-  if (copy) {
-    const size_t base = (size_t)(s & 1) * d.cap;
-    const int i = 64 * j + threadIdx.x;
-    const bool tail = j == 0 && 64 * (int)gridDim.x + (int)threadIdx.x < n;  // the loss element(s)
     for (int q = 0; q < d.world; ++q) {
       if (q == d.rank) continue;
-      if (i < n)
-        __hip_atomic_store(peer_data[q] + base + i,
-                           __hip_atomic_load(d.my_data + base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (tail) {
-        const size_t k = base + 64 * gridDim.x + threadIdx.x;
-        __hip_atomic_store(peer_data[q] + k, __hip_atomic_load(d.my_data + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int par = 0; par < (copy == 2 ? 2 : 1); ++par) {  // (saturated: both parities' slots)
+        uint64_t* dst = const_cast<uint64_t*>(xg_ll(peer_data[q], d.cap, s + par)) + i;
+        __hip_atomic_store(dst, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (threadIdx.x < (unsigned)d.world && (int)threadIdx.x != d.rank)
-    __hip_atomic_store(&peer_hdr[threadIdx.x][XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Timing-only form (copy == 0, tools/xgmi_budget.py): ONE block raises every emulated peer's block
-// flags `delay_ticks` after it starts, without waiting for this rank's publications (peers that reach
-// the exchange delay_ticks after this rank's train kernel ends).  It never waits on the consumer, so a
-// graph replay that happens to run it before the consumer cannot deadlock, and it adds no polling or
-// copy traffic of its own beside the consumer being timed (the 257-block waiting form above does).
-// saturate: every flag is set to INT_MAX instead (peers infinitely early: no consumer wait ever
-// blocks again on this communicator; the budget's lower bound, one launch before the timed steps)
-__global__ void __launch_bounds__(256)
-xgmi_emulate_block_flags_kernel(XgmiDesc d, int* const* __restrict__ peer_hdr, int nblocks, long long delay_ticks,
-                                int saturate) {
-  __shared__ int s_sh;
-  if (threadIdx.x == 0) {
-    const long long t0 = wall_clock64();
-    while (wall_clock64() - t0 < delay_ticks) __builtin_amdgcn_s_sleep(2);
-    s_sh = saturate ? 0x7FFFFFFF : xg_next_seq(d.my_hdr);
-  }
-  __syncthreads();
-  const int s = s_sh;
-  for (int q = 0; q < d.world; ++q) {
-    if (q == d.rank) continue;
-    for (int j = threadIdx.x; j < nblocks; j += blockDim.x)
-      __hip_atomic_store(&peer_hdr[q][XG_BFLAG + j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  };
+  const int i = 64 * j + (int)threadIdx.x;
+  if (i < full && i < n) one(i);
+  if (j == 0)
+    for (int k = full + (int)threadIdx.x; k < n; k += 64) one(k);
 }
 
 // consumer blocks spin on peer flags, so keep the grid well inside one wave of residency
@@ -152,7 +124,7 @@ EM_API int em_xgmi_create(int cap_floats, double timeout_s, void** out) {
     return (int)e;
   }
   const int cap = (cap_floats + 255) & ~255;
-  c->bytes = XG_HDR_BYTES + 2ull * cap * sizeof(float);
+  c->bytes = xg_buffer_bytes(cap);
   // uncached: the flag/data words are exchanged between devices inside running kernels
   e = hipExtMallocWithFlags(&c->own, c->bytes, hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c->own, 0, c->bytes);
@@ -323,27 +295,20 @@ EM_API int em_xgmi_emulate_peers(void* h, int n, double delay_us, hipStream_t st
   return 0;
 }
 
-// block-flag form (the fused DP consumer, em_adam_slab_xgmi over nblocks = P / 64 slices of an n-float
-// slot): run on a side stream beside the consumer.  copy 1: xgmi_emulate_block_peers_kernel (waits for
-// each own slice, copies it); 0: flags only, delay_us after launch; 2: flags saturated (see
-// xgmi_emulate_block_flags_kernel)
+// LL form (the fused DP consumer, em_adam_slab_xgmi over nblocks = P / 64 slices of an n-element
+// exchange): run on a side stream beside the consumer (copy 0 / 1) or once before the timed steps
+// (copy 2); see xgmi_emulate_block_peers_kernel
 EM_API int em_xgmi_emulate_block_peers(void* h, int nblocks, int n, int copy, double delay_us, hipStream_t stream) {
   XgmiComm* c = static_cast<XgmiComm*>(h);
-  if (!c || !c->local_proxy || nblocks <= 0 || nblocks > XG_MAX_BFLAGS || n < 0 || n > c->desc.cap ||
-      n > 64 * nblocks + 64 || delay_us < 0)
+  if (!c || !c->local_proxy || nblocks <= 0 || n < 0 || n > c->desc.cap || n > 64 * nblocks + 64 || copy < 0 ||
+      copy > 2 || delay_us < 0)
     return EM_ERR_ARG;
   if (int e = peer_ptr_table(c)) return e;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
-  int* const* hdr = reinterpret_cast<int* const*>(c->peer_ptrs);
   float* const* data = reinterpret_cast<float* const*>(c->peer_ptrs) + XG_MAXW;
-  const long long delay_ticks = (long long)(delay_us * 1e-3 * khz);
-  if (copy == 1)
-    hipLaunchKernelGGL(xgmi_emulate_block_peers_kernel, dim3(nblocks), dim3(64), 0, stream, c->desc, hdr, data, n, 1,
-                       delay_ticks);
-  else
-    hipLaunchKernelGGL(xgmi_emulate_block_flags_kernel, dim3(1), dim3(256), 0, stream, c->desc, hdr, nblocks,
-                       delay_ticks, copy == 2 ? 1 : 0);
+  hipLaunchKernelGGL(xgmi_emulate_block_peers_kernel, dim3(nblocks), dim3(64), 0, stream, c->desc, data, n, copy,
+                     (long long)(delay_us * 1e-3 * khz));
   EM_CHECK_LAUNCH();
   return 0;
 }

@@ -51,7 +51,7 @@ def main():
         comms = []
         for _ in range(world):
             h = ctypes.c_void_p()
-            rc = N.lib().em_xgmi_create(P + 1, 5.0, ctypes.byref(h))
+            rc = N.lib().em_xgmi_create(P + 1, 0.2, ctypes.byref(h))  # a protocol fault: error word, not a hang
             if rc != 0:
                 raise SystemExit(f"em_xgmi_create failed ({rc})")
             comms.append(h)
