@@ -778,10 +778,12 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
         cfe[cb - 1] = -1;
       }
       __syncthreads();
+      GSTAMP(16 * level + 6);
       for (int c = threadIdx.x; c < C; c += blockDim.x) {
         const int f = cfe[c];
         if (f >= 0) cand(f, cbn[c], cGL[c], cHL[c]);
       }
+      GSTAMP(16 * level + 7);
     } else {
       for (int f = threadIdx.x; f < F; f += blockDim.x) {
         const int ca = f == (int)threadIdx.x ? myca : foff[f], cb = f == (int)threadIdx.x ? mycb : foff[f + 1];
