@@ -1121,9 +1121,6 @@ __global__ void __launch_bounds__(RFP_PREP_THREADS) rf_predict_prepare(const int
 // 2 waves per SIMD needed 192 accumulators and spilled 576 B per lane to scratch: 2.27 ms for 300 k
 // rows x 100 trees, round 5)
 constexpr int RFP_WAVES = 12;
-#ifndef RFP_V2
-#define RFP_V2 0
-#endif
 template <int G>
 __global__ void __launch_bounds__(RFP_WAVES * 64) rf_predict_lds(const uint64_t* __restrict__ X, int64_t N,
                                                       const uint8_t* __restrict__ prep, int T, int rows_per_wave,
@@ -1186,7 +1183,6 @@ __global__ void __launch_bounds__(RFP_WAVES * 64) rf_predict_lds(const uint64_t*
         }
       if (!__builtin_amdgcn_ballot_w64(more)) break;
     }
-#if RFP_V2
     // leaf chunks: lane l reads chunk (l + c) & 15 at step c from base A = leaf + ((l & 15) << 4), or
     // A - 256 once the rotation wraps: one select per step and the step's 16 c in the instruction's
     // immediate offset.  4 steps at a time for every group together (the groups' reads in flight at
@@ -1210,24 +1206,6 @@ __global__ void __launch_bounds__(RFP_WAVES * 64) rf_predict_lds(const uint64_t*
         asm volatile("" : "+v"(acc[g][c0]), "+v"(acc[g][c0 + 1]), "+v"(acc[g][c0 + 2]), "+v"(acc[g][c0 + 3]));
     }
   }
-#else
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (rw0 + 64 * g >= rend) break;  // (wave-uniform)
-      const uint32_t lb = 1024u + (uint32_t)(-f[g] - 1) * 256u;
-      // 4 batches of 4 chunk reads: the rotated offsets are kept opaque (hoisted, they held 16 VGPRs)
-      // and a batch's adds complete before the next batch's reads issue (all 16 in flight held 64)
-      uint32_t kr = rot;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        acc[g][c] += *reinterpret_cast<const f32x4*>(buf + (lb | (kr & 0xF0u)));
-        kr += 16u;
-        asm volatile("" : "+v"(kr));
-        if ((c & 3) == 3) asm volatile("" : "+v"(acc[g][c - 3]), "+v"(acc[g][c - 2]), "+v"(acc[g][c - 1]), "+v"(acc[g][c]));
-      }
-    }
-  }
-#endif
   const float invT = 1.f / (float)(T > 0 ? T : 1);
   (void)invT;
 #pragma unroll

@@ -162,18 +162,19 @@ __global__ void gbdt_round_start(int8_t* __restrict__ st, int16_t* __restrict__ 
 constexpr int HIST_MAX_CHUNK = 1024;             // rows staged in LDS per piece
 constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // 8-byte words of per-chunk partials (1 GiB) per level
 constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (+ staged rows)
-// exact form: up to 4 private copies in a 256-thread block.  (8 copies in 512-thread blocks halved a
-// block's serial read-modify-write chain but measured slower per level on the reference fit: the CUs
-// then run fewer, longer blocks and the level is bound by LDS throughput, not by one block's chain.)
-constexpr int HIST_EXACT_LDS_BUDGET = HIST_LDS_BUDGET;
-constexpr int HIST_EXACT_THREADS = 256;
+// exact form: up to 8 private copies in a 512-thread block (round 5, with 256-row chunks; round 4 had
+// measured 512-thread blocks slower with 64-row chunks, where they only added blocks' LDS)
+constexpr int HIST_EXACT_LDS_BUDGET = 72 * 1024;
+constexpr int HIST_EXACT_THREADS = 512;
 constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
 // rows per histogram chunk at least HIST_MIN_CHUNK (compile-time A/B knob for side builds,
-// tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk).  128 rows:
-// reference fit 0.045 -> 0.042 s on the same box (round 5, profiles/r5/gbdt_chunk_ab.txt: fewer
-// partials for the split to fold; 256 fell back to 0.045 s, too few blocks per level)
+// tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk).  Round 5 on the
+// reference fit (trees/s, same box, profiles/r5/gbdt_chunk_ab.txt, gbdt_threads_ab.txt): 256-thread
+// blocks with up to 4 row phases, 64-row chunks 689 k -> 128-row chunks 733 k; 512-thread blocks with
+// up to 8 phases (72 KB of private copies) and 256-row chunks 765 k (128-row: 737 k): half the blocks
+// per level, and each thread's serial update chain stays at ~37 rows.
 #ifndef HIST_MIN_CHUNK
-#define HIST_MIN_CHUNK 128
+#define HIST_MIN_CHUNK 256
 #endif
 
 __global__ void __launch_bounds__(HIST_EXACT_THREADS)
@@ -619,6 +620,7 @@ struct SplitFinal {
 };
 EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma);
 constexpr int SPLIT_FINAL_MAX_DEPTH = 8;
+constexpr int SPLIT_DIRECT_MAX_BINS = 32;  // direct candidate form up to this many bins per feature
 constexpr int EM_GBDT_SEPARATE = 1;  // em_gbdt_fit launch_flags: the separate launches instead of the fused round
 constexpr int SPLIT_ONESHOT_LDS = 48 * 1024;  // chunk partials staged at once up to this many bytes (+ the
                                               // finalize's <= 12 KB: within the default 64 KB)  // the fused finalize stages NN <= 511 nodes (23 B each) in LDS
@@ -628,7 +630,7 @@ __global__ void __launch_bounds__(256)
 gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
            int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
            int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
-           double qinv, SplitFinal fin, int oneshot, int pscan) {
+           double qinv, SplitFinal fin, int oneshot, int pscan, const int4* __restrict__ cellinfo) {
   constexpr bool Q = std::is_same<A, long long>::value;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nodesL = 1 << level, first = nodesL - 1;
@@ -638,19 +640,34 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
   // the thread's feature cells and feature 0's, loaded before the partials (one round trip for all)
   const int fa0 = foff[0], fb0 = foff[1];
   const int myca = (int)threadIdx.x < F ? foff[threadIdx.x] : 0, mycb = (int)threadIdx.x < F ? foff[threadIdx.x + 1] : 0;
+  // direct candidate form (cellinfo != null, every feature <= SPLIT_DIRECT_MAX_BINS bins): this thread's
+  // cell's {feature, first cell, end cell}, loaded with the rest
+  const int4 myci = cellinfo && (int)threadIdx.x < C ? cellinfo[threadIdx.x] : int4{0, 0, 0, 0};
+  // the first batch of the one-shot partial loads goes out with the node's status load (one round trip
+  // instead of status first, then partials; a closed node's partials are read and dropped)
+  const A* hs0 = hist + ((int64_t)t * nodesL + nd) * C * 2;
+  const bool one = nchunks > 1 && oneshot;
+  const int tot = nchunks * 2 * C;
+  A pre[32];
+  if (one) {
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = (int)threadIdx.x + u * (int)blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
+      pre[u] = idx < tot ? hs0[(int64_t)c * cstride + e] : A(0);
+    }
+  }
   if (st[i] == 2) {  // block-uniform: an open node
-    const A* hs = hist + ((int64_t)t * nodesL + nd) * C * 2;
-    if (nchunks > 1 && oneshot) {
+    const A* hs = hs0;
+    if (one) {
       // every chunk's cells staged at once (32 loads per thread in flight: one round trip, where the
       // per-element chunk loop took 2-3), then folded in chunk order (== gbdt_chunk_reduce)
       A* stg = reinterpret_cast<A*>(smem);
-      const int tot = nchunks * 2 * C;
       for (int b0 = threadIdx.x; b0 < tot; b0 += 32 * blockDim.x) {
         A v[32];
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
           const int idx = b0 + u * blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
-          v[u] = idx < tot ? hs[(int64_t)c * cstride + e] : A(0);
+          v[u] = b0 == (int)threadIdx.x ? pre[u] : (idx < tot ? hs[(int64_t)c * cstride + e] : A(0));
         }
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
@@ -737,7 +754,23 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
         }
       }
     };
-    if (pscan) {
+    if (cellinfo && nchunks > 1) {  // (the folded cells are in LDS)
+      // direct form: thread c sums its feature's cells up to c in bin order -- the very sums of the
+      // sequential scan below, so bitwise the same candidates -- and evaluates candidate c at once: no
+      // per-feature chain over a many-bin feature, no LDS pass, no barrier (round 5: the two-pass scan
+      // took ~2 us of the split's ~8.5, profiles/r5/gbdt_split_stamps.jsonl)
+      for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const int4 ci = c == (int)threadIdx.x ? myci : cellinfo[c];
+        if (c >= ci.z - 1) continue;  // the last bin is never a candidate (nothing to its right)
+        A GLa = 0, HLa = 0;
+#pragma unroll 8
+        for (int k = ci.y; k <= c; ++k) {
+          GLa += hs[2 * k];
+          HLa += hs[2 * k + 1];
+        }
+        cand(ci.x, c - ci.y, GLa, HLa);
+      }
+    } else if (pscan) {
       // two passes: thread f writes its feature's left sums in bin order (the same sequential sums),
       // then thread c evaluates candidate cell c -- the divisions of a 31-bin feature no longer
       // run one after another on one lane
@@ -796,20 +829,23 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
       }
     }
     // block arg-max: larger gain, then lower feature (a thread's features ascend with its loop)
+    // (the butterfly carries the owner lane of the best candidate, not its two sums: (gain, feature,
+    // bin) order every candidate uniquely, so the winner's sums are fetched once afterwards)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int bl = lane;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const double ov = __shfl_xor(best, o);
-      const A ogl = __shfl_xor(bGL, o), ohl = __shfl_xor(bHL, o);
-      const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o);
+      const int of = __shfl_xor(bf, o), ob = __shfl_xor(bb, o), ol = __shfl_xor(bl, o);
       if (ov > best || (ov == best && (of < bf || (of == bf && ob < bb)))) {
         best = ov;
         bf = of;
         bb = ob;
-        bGL = ogl;
-        bHL = ohl;
+        bl = ol;
       }
     }
+    bGL = __shfl(bGL, bl);
+    bHL = __shfl(bHL, bl);
     if (lane == 0) {
       rv[w] = best;
       rf[w] = bf;
@@ -1056,9 +1092,16 @@ gbdt_metric_final(const double* __restrict__ partial, int nb, int64_t count, int
 // and drains it before its single arrival add; the block whose add completes the count sums the
 // partials (sc1 loads) exactly as gbdt_metric_final does, writes the mean and re-arms the counter.
 // (b, nb: this block's index among the nb blocks of its metric set; a fused launch runs several sets)
+// ctr == nullptr: deferred form -- the block only stores its partial (the kernel boundary publishes it)
+// and gbdt_metric_rounds reduces every round's partials after the last round, in the same order: the
+// metric is history, not an input of the next round, so its reduction leaves each round's critical path.
 EM_DEVICE void metric_arrive_final(double bs, double* __restrict__ partial, int* __restrict__ ctr, int64_t count,
                                    int metric, float* __restrict__ out, int b, int nb) {
   __shared__ int last;
+  if (!ctr) {
+    if (threadIdx.x == 0) partial[b] = bs;
+    return;
+  }
   if (threadIdx.x == 0) {
     __hip_atomic_store(partial + b, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1102,6 +1145,7 @@ struct EvalSets {
   int n[4];
   int mb[4];
   int count = 0;
+  int64_t pstride = 4096;  // doubles between the sets' partial regions
 };
 struct NextRound {
   int round = -1;  // < 0: none
@@ -1133,7 +1177,8 @@ gbdt_update_metric(float* __restrict__ margin, const int16_t* __restrict__ node,
     while (s < evs.count - 1 && b >= evs.mb[s]) b -= evs.mb[s++];
     // (status / feat / sbin / leaf are this round's arrays: its trees are 0 .. T - 1 of them)
     predict_metric_body(evs.bins[s], evs.margin[s], T, evs.n[s], F, NN, 0, T, status, feat, sbin, leaf, evs.Y[s], obj,
-                        metric, partial + (int64_t)(1 + s) * 4096, ctr + 1 + s, out + 1 + s, b, evs.mb[s]);
+                        metric, partial + (int64_t)(1 + s) * evs.pstride, ctr ? ctr + 1 + s : nullptr, out + 1 + s, b,
+                        evs.mb[s]);
     return;
   }
   const int64_t total = (int64_t)T * n;
@@ -1197,6 +1242,24 @@ gbdt_predict_metric(const uint8_t* __restrict__ bins, float* __restrict__ margin
                       out, blockIdx.x, gridDim.x);
 }
 
+// the deferred metrics of `rounds` rounds x `sets` sets: block (r, s) reduces partials
+// [(r * sets + s) * stride, + nb[s]) as metric_arrive_final's last block would, into out[r * sets + s]
+struct MetricRounds {
+  int nb[5];
+  int64_t count[5];
+};
+__global__ void __launch_bounds__(256)
+gbdt_metric_rounds(const double* __restrict__ partial, int64_t stride, int sets, MetricRounds mr, int metric,
+                   float* __restrict__ out) {
+  const int r = blockIdx.x / sets, s = blockIdx.x % sets;
+  const double sum = block_sum_partials(partial + ((int64_t)r * sets + s) * stride, mr.nb[s]);
+  if (threadIdx.x == 0) {
+    double v = sum / (double)(mr.count[s] > 0 ? mr.count[s] : 1);
+    if (metric == MET_RMSE) v = sqrt(v);
+    out[(int64_t)r * sets + s] = (float)v;
+  }
+}
+
 __global__ void __launch_bounds__(256)
 gbdt_metric_sum(const double* __restrict__ partial, int nb, double* __restrict__ out) {
   const double s = block_sum_partials(partial, nb);
@@ -1240,7 +1303,7 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
       // read-modify-write chain is a P-th of the chunk), the fixed-point form one shared copy, so a
       // few-feature tile fills its 256-thread block with phases
       int P = (quant ? 256 : HIST_EXACT_THREADS) / lanes;
-      const int Pmax = quant ? 64 : 4;
+      const int Pmax = quant ? 64 : 8;
       P = P > Pmax ? Pmax : (P < 1 ? 1 : P);
       for (; P >= 1; --P)
         if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= (quant ? HIST_LDS_BUDGET : HIST_EXACT_LDS_BUDGET)) break;
@@ -1523,6 +1586,29 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       }
     }
   } qfree{qmem, stream};
+  // direct split candidates (gbdt_split): cell -> {feature, its first cell, its end cell} when no feature
+  // has more than SPLIT_DIRECT_MAX_BINS bins (the reference's calendar features: 31); stream-ordered
+  // allocation, freed after the last round's launches
+  int4* cellinfo_d = nullptr;
+  {
+    int maxb = 0;
+    for (int f = 0; f < F; ++f) maxb = foff_h[f + 1] - foff_h[f] > maxb ? foff_h[f + 1] - foff_h[f] : maxb;
+    if (maxb <= SPLIT_DIRECT_MAX_BINS && C > 0) {
+      std::vector<int4> ci((size_t)C);
+      for (int f = 0; f < F; ++f)
+        for (int c = foff_h[f]; c < foff_h[f + 1]; ++c) ci[c] = int4{f, foff_h[f], foff_h[f + 1], 0};
+      if (hipMallocAsync(reinterpret_cast<void**>(&cellinfo_d), ci.size() * sizeof(int4), stream) != hipSuccess ||
+          hipMemcpyAsync(cellinfo_d, ci.data(), ci.size() * sizeof(int4), hipMemcpyHostToDevice, stream) != hipSuccess)
+        return EM_ERR_ARG;
+    }
+  }
+  struct FreeAsync {
+    void* p;
+    hipStream_t s;
+    ~FreeAsync() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } cfree{cellinfo_d, stream};
   // Exact-form fits with an elementwise metric run the fused round: the previous level's partition
   // inside each histogram pass (double-buffered nodes), the prune / leaves in the last level's split
   // (last-arriving block per task), the last partition in the update, and -- per-task objectives --
@@ -1533,6 +1619,18 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   int* tctr = nullptr;
   const bool fuse = !(launch_flags & EM_GBDT_SEPARATE) && !quant_bits && metric < MET_MLOGLOSS &&
                     max_depth <= SPLIT_FINAL_MAX_DEPTH && node2 && (tctr = task_counters(T)) != nullptr;
+  // deferred metrics (metric_arrive_final with ctr == nullptr): every round's per-block partials of the
+  // train and eval sets, reduced by gbdt_metric_rounds after the last round
+  const int sets = 1 + n_evals;
+  const bool deferred = metric < MET_MLOGLOSS && n_evals <= 4;
+  int64_t mstride = grid_for(TN);
+  for (int e = 0; e < n_evals; ++e)
+    mstride = grid_for((int64_t)T * evals[e].n) > mstride ? grid_for((int64_t)T * evals[e].n) : mstride;
+  double* mround = nullptr;
+  if (deferred && hipMallocAsync(reinterpret_cast<void**>(&mround), (size_t)(r1 - r0) * sets * mstride * sizeof(double),
+                                 stream) != hipSuccess)
+    return EM_ERR_ARG;
+  FreeAsync mfree{mround, stream};
   // one round's kernel sequence (the arrays of `round` addressed from the host)
   auto enqueue_round = [&](int round, hipStream_t s) -> int {
     const int64_t ro = (int64_t)round * T * NN;
@@ -1583,11 +1681,11 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
       if (quant_bits)
         hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, s,
                            reinterpret_cast<const long long*>(partial), nch, cstride, foff_d, T, F, C, level, NN, Gs,
-                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, fin, oneshot, pscan);
+                           Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, fin, oneshot, pscan, cellinfo_d);
       else
         hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, s, partial, nch, cstride,
                            foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, fin,
-                           oneshot, pscan);
+                           oneshot, pscan, cellinfo_d);
       if (!fuse)
         hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, s, bins, node, T, n, F, NN, st, fe, sb,
                            level);
@@ -1629,9 +1727,12 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
           grid += evs.mb[e];
         }
         evs.count = n_evals;
+        if (deferred) evs.pstride = mstride;
       }
+      double* mp = deferred ? mround + (int64_t)(round - r0) * sets * mstride : mpart;
       hipLaunchKernelGGL(gbdt_update_metric, dim3(grid), dim3(256), 0, s, margin,
-                         fuse ? nb[(max_depth - 1) & 1] : node, T, n, NN, st, lf, Y, obj, metric, mpart, mctr, ho,
+                         fuse ? nb[(max_depth - 1) & 1] : node, T, n, NN, st, lf, Y, obj, metric, mp,
+                         deferred ? nullptr : mctr, ho,
                          bins, F, fuse ? max_depth - 1 : -1, fe, sb, nx, mb_train, evs);
       if (evs.count == n_evals) {
         EM_CHECK_LAUNCH();
@@ -1665,6 +1766,18 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   };
   for (int round = r0; round < r1; ++round)
     if (int rc = enqueue_round(round, stream)) return rc;
+  if (deferred) {
+    MetricRounds mr{};
+    mr.nb[0] = grid_for(TN);
+    mr.count[0] = TN;
+    for (int e = 0; e < n_evals; ++e) {
+      mr.nb[1 + e] = grid_for((int64_t)T * evals[e].n);
+      mr.count[1 + e] = (int64_t)T * evals[e].n;
+    }
+    hipLaunchKernelGGL(gbdt_metric_rounds, dim3((r1 - r0) * sets), dim3(256), 0, stream, mround, mstride, sets, mr,
+                       metric, hist_out + (int64_t)r0 * sets);
+    EM_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -1744,7 +1857,8 @@ EM_API int em_gbdt_dp_level_split(int level, const uint8_t* bins, const double* 
   const int64_t TN = (int64_t)T * n;
   const int sth = F >= 256 ? 256 : ((F + 63) / 64) * 64;
   hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), 0, stream, hist, 1, (int64_t)0, foff_d, T, F, C,
-                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, SplitFinal(), 0, 0);
+                     level, NN, Gs, Hs, status, feat, sbin, gainv, (double)lam, (double)mcw, 0.0, SplitFinal(), 0, 0,
+                     (const int4*)nullptr);
   hipLaunchKernelGGL(gbdt_partition, dim3(grid_for(TN)), dim3(256), 0, stream, bins, node, T, n, F, NN, status, feat,
                      sbin, level);
   EM_CHECK_LAUNCH();

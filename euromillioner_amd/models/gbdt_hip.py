@@ -63,7 +63,7 @@ class _Cells:
         return self.host.ctypes.data
 
 
-def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 100, dp=None):
+def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 500, dp=None):
     dev = _dev()
     n, F = bins.shape
     T = Y.shape[1]
