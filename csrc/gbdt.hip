@@ -91,21 +91,14 @@ __global__ void gbdt_init_margin(float* __restrict__ margin, int64_t total, floa
     margin[i] = base;
 }
 
-// margin/g/h/node: [T][n]; Y: [n][T]
-EM_DEVICE void grad_elem(int64_t i, const float* __restrict__ margin, const float* __restrict__ Y,
-                         float* __restrict__ g, float* __restrict__ h, int16_t* __restrict__ node, int T, int n,
-                         int obj, float subsample, uint32_t seed, int round) {
-  const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
-  const float m = margin[i], y = Y[(int64_t)r * T + t];
-  float gg, hh;
+// g / h of one (task t, row r) element of round `round` from its margin m and label y (per-task
+// objectives; the row subsample's hash drops the element)
+EM_DEVICE void grad_of(float m, float y, int obj, float subsample, uint32_t seed, int round, int t, int r, float& gg,
+                       float& hh) {
   if (obj == OBJ_LOGISTIC) {
     const float p = 1.f / (1.f + expf(-m));
     gg = p - y;
     hh = fmaxf(p * (1.f - p), 1e-16f);
-  } else if (obj == OBJ_SOFTMAX) {  // XGBoost SoftmaxMultiClassObj: g = p - y, h = max(2p(1-p), eps)
-    const float p = softmax_p(margin, T, n, r, t);
-    gg = p - y;
-    hh = fmaxf(2.f * p * (1.f - p), 1e-16f);
   } else {
     gg = m - y;
     hh = 1.f;
@@ -113,6 +106,26 @@ EM_DEVICE void grad_elem(int64_t i, const float* __restrict__ margin, const floa
   if (subsample < 1.f) {
     const float u = (hash3(seed, (uint32_t)round * 131071u + t, r) >> 8) * (1.f / 16777216.f);
     if (u >= subsample) gg = hh = 0.f;
+  }
+}
+
+// margin/g/h/node: [T][n]; Y: [n][T]
+EM_DEVICE void grad_elem(int64_t i, const float* __restrict__ margin, const float* __restrict__ Y,
+                         float* __restrict__ g, float* __restrict__ h, int16_t* __restrict__ node, int T, int n,
+                         int obj, float subsample, uint32_t seed, int round) {
+  const int t = (int)(i / n), r = (int)(i - (int64_t)t * n);
+  const float m = margin[i], y = Y[(int64_t)r * T + t];
+  float gg, hh;
+  if (obj == OBJ_SOFTMAX) {  // XGBoost SoftmaxMultiClassObj: g = p - y, h = max(2p(1-p), eps)
+    const float p = softmax_p(margin, T, n, r, t);
+    gg = p - y;
+    hh = fmaxf(2.f * p * (1.f - p), 1e-16f);
+    if (subsample < 1.f) {
+      const float u = (hash3(seed, (uint32_t)round * 131071u + t, r) >> 8) * (1.f / 16777216.f);
+      if (u >= subsample) gg = hh = 0.f;
+    }
+  } else {
+    grad_of(m, y, obj, subsample, seed, round, t, r, gg, hh);
   }
   g[i] = gg;
   h[i] = hh;
@@ -141,6 +154,67 @@ __global__ void gbdt_round_start(int8_t* __restrict__ st, int16_t* __restrict__ 
   }
 }
 
+EM_DEVICE int leaf_ancestor(const int8_t* st, int nd);
+EM_DEVICE double metric_term(float m, float y, int obj, int metric);
+
+// eval sets handled by trailing blocks of the update launch (or, see HistUpdate, by extra blocks of the
+// next round's level-0 histogram pass)
+struct EvalSets {
+  const uint8_t* bins[4];
+  float* margin[4];
+  const float* Y[4];
+  int n[4];
+  int mb[4];
+  int count = 0;
+  int64_t pstride = 4096;  // doubles between the sets' partial regions
+};
+
+// The level-0 histogram pass of round r doing the rows' part of round r - 1's update (exact fused form,
+// per-task objectives, one block per (chunk, task)): a block stages its rows' (g, h) by computing them --
+// the margin plus the leaf of round r - 1's tree (its last partition applied here), the metric term of
+// round r - 1, round r's g / h -- and writes margin, g, h and the reset node ids for the later levels;
+// extra blocks (z >= nz) predict round r - 1's trees on the eval sets.  The update launch of every
+// round but the last is gone; the arithmetic per element is the update's, so trees and margins are
+// bit-identical to the separate launches (the metric's per-block partial sums are grouped by chunk).
+struct HistUpdate {
+  int on = 0;     // compute the rows' g / h (round `round`) and initialise round `round`'s tree arrays
+  int apply = 0;  // first apply round - 1's tree (margins, metric partials, eval sets)
+  int round = 0, obj = 0, metric = 0, NN = 0, plevel = 0, nz = 1;
+  float subsample = 1.f;
+  uint32_t seed = 0;
+  float* margin = nullptr;
+  const float* Y = nullptr;
+  float* g = nullptr;
+  float* h = nullptr;
+  int16_t* node = nullptr;
+  int8_t* st = nullptr;  // round `round`'s tree arrays (task-major [T][NN])
+  int16_t* fe = nullptr;
+  uint8_t* sb = nullptr;
+  float* gn = nullptr;
+  const int8_t* pst = nullptr;  // round - 1's
+  const int16_t* pfe = nullptr;
+  const uint8_t* psb = nullptr;
+  const float* plf = nullptr;
+  const int16_t* pnode = nullptr;  // the rows' nodes before round - 1's last partition
+  double* mpart = nullptr;         // round - 1's deferred partials: train [T * chunks], eval set s at (1 + s) * mstride
+  int64_t mstride = 0;
+  EvalSets evs;
+};
+
+// fixed-order block sum (<= 1024 threads; thread 0 gets the result): a butterfly per wave, then the
+// waves in order.  (128 B of static LDS: the histogram kernels' dynamic LDS may take all the rest)
+EM_DEVICE double block_sum_waves(double acc) {
+  __shared__ double wsum[16];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  double tot = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < ((int)blockDim.x + 63) >> 6; ++w) tot += wsum[w];
+  return tot;
+}
+
 // ---------------------------------------------------------------- K8 histogram (compact cells)
 // Cells: feature f owns bins [foff[f], foff[f+1]) of a compact axis of C = foff[F] cells (a one-hot
 // lag feature has 2 cells, "day" 31 ...), so a (task, node) histogram of the reference features is
@@ -166,6 +240,10 @@ constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (
 // measured 512-thread blocks slower with 64-row chunks, where they only added blocks' LDS)
 constexpr int HIST_EXACT_LDS_BUDGET = 72 * 1024;
 constexpr int HIST_EXACT_THREADS = 512;
+// gbdt_hist's dynamic LDS ceiling: 160 KB less 1 KB for its static LDS (block_sum_waves); setting the
+// attribute to the full 160 KB fails once the kernel has any static LDS (and leaves hipErrorInvalidValue
+// as the last error, which the next launch check reports)
+constexpr int GBDT_HIST_MAX_DYN = 159 * 1024;
 constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
 // rows per histogram chunk at least HIST_MIN_CHUNK (compile-time A/B knob for side builds,
 // tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk).  Round 5 on the
@@ -182,7 +260,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
           int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, int stage_rows,
           int16_t* __restrict__ node_out, const int8_t* __restrict__ pst, const int16_t* __restrict__ pfe,
-          const uint8_t* __restrict__ psb, int NN) {
+          const uint8_t* __restrict__ psb, int NN, HistUpdate hu) {
   // stage_rows > 0: each piece's bin rows are staged in LDS with 16-B loads (one round trip instead of
   // one per 8 rows of byte loads); the host sets it when a piece's rows fit (stage_rows * F <= 16 KB).
   // node_out != nullptr (level >= 1): the rows' nodes are the previous level's partition, applied here
@@ -192,6 +270,25 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   const int nodesL = 1 << level, first = nodesL - 1;
   GSTAMP(64 + 16 * level);
   const int c = blockIdx.x, t = blockIdx.y;
+  if (hu.apply && (int)blockIdx.z >= hu.nz) {  // eval set es: round - 1's tree of task t on a chunk of its rows
+    const int es = (int)blockIdx.z - hu.nz, ne = hu.evs.n[es], per = (ne + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int eb = c * per, ee = min(ne, eb + per);
+    const int64_t o = (int64_t)t * hu.NN;
+    double acc = 0.0;
+    for (int r = eb + (int)threadIdx.x; r < ee; r += blockDim.x) {
+      const uint8_t* row = hu.evs.bins[es] + (int64_t)r * F;
+      int nd = 0;
+      while (hu.pst[o + nd] == 1) nd = 2 * nd + 1 + (row[hu.pfe[o + nd]] > hu.psb[o + nd] ? 1 : 0);
+      const int64_t i = (int64_t)t * ne + r;
+      const float m = hu.evs.margin[es][i] + hu.plf[o + nd];
+      hu.evs.margin[es][i] = m;
+      acc += metric_term(m, hu.evs.Y[es][(int64_t)r * T + t], hu.obj, hu.metric);
+    }
+    const double bs = block_sum_waves(acc);
+    if (threadIdx.x == 0) hu.mpart[(1 + es) * hu.mstride + (int64_t)t * gridDim.x + c] = bs;
+    return;
+  }
+  double macc = 0.0;  // (hu.apply) round - 1's metric terms of this thread's rows
   const int nft = (F + FT - 1) / FT;
   const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
   const int f0 = ft * FT, f1 = min(F, f0 + FT), n0 = nt * NTn;
@@ -247,6 +344,30 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
       rowb = reinterpret_cast<const uint8_t*>(sbw) + boff;
     }
     for (int r = r0 + (int)threadIdx.x; r < r1; r += blockDim.x) {
+      if (hu.on) {  // (level 0, one tile per (chunk, task): this thread is the row's only writer)
+        const int64_t i = base + r;
+        const float y = hu.Y[(int64_t)r * T + t];
+        float m = hu.margin[i];
+        if (hu.apply) {  // round - 1's last partition and leaf (gbdt_update_metric's arithmetic)
+          const int64_t o = (int64_t)t * hu.NN;
+          const int ppf = (1 << hu.plevel) - 1, ppl = 2 * ppf + 1;
+          int nd = hu.pnode[i];
+          if (nd >= ppf && nd < ppl && hu.pst[o + nd] == 1)
+            nd = 2 * nd + 1 + (bins[(int64_t)r * F + hu.pfe[o + nd]] > hu.psb[o + nd] ? 1 : 0);
+          m = m + hu.plf[o + leaf_ancestor(hu.pst + o, nd)];
+          hu.margin[i] = m;
+          macc += metric_term(m, y, hu.obj, hu.metric);
+        }
+        float gg, hh;
+        grad_of(m, y, hu.obj, hu.subsample, hu.seed, hu.round, t, r, gg, hh);
+        hu.g[i] = gg;
+        hu.h[i] = hh;
+        hu.node[i] = 0;
+        sg[r - r0] = gg;
+        sh[r - r0] = hh;
+        sn[r - r0] = 0;  // every row at the root
+        continue;
+      }
       sg[r - r0] = g[base + r];
       sh[r - r0] = h[base + r];
       const int nd = node[base + r];
@@ -317,6 +438,13 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
     o[0] = sgv;
     o[1] = shv;
   }
+  if (hu.apply) {
+    const double bs = block_sum_waves(macc);
+    if (threadIdx.x == 0) hu.mpart[(int64_t)t * gridDim.x + c] = bs;
+  }
+  if (hu.on && c == 0)  // round `round`'s tree arrays of task t
+    for (int k = threadIdx.x; k < hu.NN; k += blockDim.x)
+      round_init_elem(t * hu.NN + k, hu.st, hu.fe, hu.sb, hu.gn, hu.NN);
   GSTAMP(64 + 16 * level + 4);
 }
 
@@ -648,6 +776,12 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
   const A* hs0 = hist + ((int64_t)t * nodesL + nd) * C * 2;
   const bool one = nchunks > 1 && oneshot;
   const int tot = nchunks * 2 * C;
+  // below the root (exact form) the node's totals come from the parent's split: loaded with the rest
+  double pGn = 0.0, pHn = 0.0;
+  if (!Q && level > 0 && threadIdx.x == 0) {
+    pGn = G[(int64_t)t * NN + i];
+    pHn = H[(int64_t)t * NN + i];
+  }
   A pre[32];
   if (one) {
 #pragma unroll
@@ -726,8 +860,8 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
           __hip_atomic_store(H + (int64_t)t * NN, val(Hn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       } else {
-        Gn = G[(int64_t)t * NN + i];
-        Hn = H[(int64_t)t * NN + i];
+        Gn = pGn;
+        Hn = pHn;
       }
       sGn[0] = Gn;
       sGn[1] = Hn;
@@ -1138,15 +1272,6 @@ EM_DEVICE void predict_metric_body(const uint8_t* __restrict__ bins, float* __re
                                    int b, int nb);
 // eval sets handled by the update launch's trailing blocks (eager rounds): set s gets mb blocks, its own
 // partial region (partial + (1 + s) * 4096) and arrival counter (ctr + 1 + s)
-struct EvalSets {
-  const uint8_t* bins[4];
-  float* margin[4];
-  const float* Y[4];
-  int n[4];
-  int mb[4];
-  int count = 0;
-  int64_t pstride = 4096;  // doubles between the sets' partial regions
-};
 struct NextRound {
   int round = -1;  // < 0: none
   float* g = nullptr;
@@ -1381,7 +1506,7 @@ struct HistPartition {  // the previous level's partition fused into the exact-f
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
                       bool fold, double qscale, int* nchunks_out, hipStream_t stream, const QuantAux* qa = nullptr,
-                      const HistPartition& hp = HistPartition()) {
+                      const HistPartition& hp = HistPartition(), const HistUpdate* hu = nullptr) {
   const bool quant = qscale != 0.0;
   const int C = foff_h[F];
   const int nodesL = 1 << level;
@@ -1408,7 +1533,9 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
     if (!plan_hist(level, n, T, F, foff_h, quant, pl)) return EM_ERR_ARG;
     if ((int64_t)pl.nchunks * S > partial_doubles) return EM_ERR_ARG;
     nchunks = pl.nchunks;
-    const dim3 grid(pl.nchunks, T, pl.nft * pl.ntn);
+    // (hu: level 0 with one tile per (chunk, task); eval sets on extra z planes)
+    if (hu && (quant || level != 0 || pl.nft * pl.ntn != 1)) return EM_ERR_ARG;
+    const dim3 grid(pl.nchunks, T, pl.nft * pl.ntn + (hu && hu->apply ? hu->evs.count : 0));
     if (quant)
       hipLaunchKernelGGL(gbdt_hist_q, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d,
                          (const int*)nullptr, foff_d, qpart, T, n, F, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
@@ -1421,16 +1548,16 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
       const int npn = hp.node_out ? (1 << level) - (1 << (level - 1)) : 0;
       size_t lds = ((pl.lds + 15) & ~(size_t)15) + (((size_t)npn * 4 + 15) & ~(size_t)15);
       const size_t sbytes = (((size_t)srows * F + 32 + 15) & ~(size_t)15);
-      const int stage = ((int64_t)srows * F <= 16 * 1024 && lds + sbytes <= 160 * 1024) ? srows : 0;
+      const int stage = ((int64_t)srows * F <= 16 * 1024 && lds + sbytes <= GBDT_HIST_MAX_DYN) ? srows : 0;
       if (stage) lds += sbytes;
       static bool attr = false;
       if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gbdt_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)gbdt_hist, hipFuncAttributeMaxDynamicSharedMemorySize, GBDT_HIST_MAX_DYN);
         attr = true;
       }
       hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
                          C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece, stage, hp.node_out, hp.st, hp.fe,
-                         hp.sb, hp.NN);
+                         hp.sb, hp.NN, hu ? *hu : HistUpdate());
     }
   }
   const bool split_folds = !fold && nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
@@ -1626,6 +1753,13 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   int64_t mstride = grid_for(TN);
   for (int e = 0; e < n_evals; ++e)
     mstride = grid_for((int64_t)T * evals[e].n) > mstride ? grid_for((int64_t)T * evals[e].n) : mstride;
+  // update-in-histogram rounds (HistUpdate): the level-0 histogram pass of round r does round r - 1's
+  // update; one update launch for the call's last round
+  HistPlan p0;
+  const bool hist_update = fuse && obj != OBJ_SOFTMAX && deferred && plan_hist(0, n, T, F, foff_h, false, p0) &&
+                           p0.nft * p0.ntn == 1 && p0.nchunks * (int64_t)T <= (int64_t)1 << 20;
+  const int nch0 = hist_update ? p0.nchunks : 0;
+  if (hist_update && (int64_t)T * nch0 > mstride) mstride = (int64_t)T * nch0;
   double* mround = nullptr;
   if (deferred && hipMallocAsync(reinterpret_cast<void**>(&mround), (size_t)(r1 - r0) * sets * mstride * sizeof(double),
                                  stream) != hipSuccess)
@@ -1640,9 +1774,9 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     float* lf = leaf + ro;
     float* gn = gainv + ro;
     float* cv = cover + ro;
-    const bool next_in_update = fuse && obj != OBJ_SOFTMAX;  // round + 1 started by this update
+    const bool next_in_update = fuse && obj != OBJ_SOFTMAX && !hist_update;  // round + 1 started by this update
     int16_t* nb[2] = {node, fuse ? node2 : node};
-    if (!next_in_update || round == r0)
+    if (!hist_update && (!next_in_update || round == r0))
       hipLaunchKernelGGL(gbdt_round_start, dim3(grid_for(TN > (int64_t)T * NN ? TN : (int64_t)T * NN)), dim3(256), 0,
                          s, st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round);
     for (int level = 0; level < max_depth; ++level) {
@@ -1658,8 +1792,48 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         hp.sb = sb;
         hp.NN = NN;
       }
+      HistUpdate hu;
+      if (hist_update && level == 0) {
+        hu.on = 1;
+        hu.apply = round > r0;
+        hu.round = round;
+        hu.obj = obj;
+        hu.metric = metric;
+        hu.NN = NN;
+        hu.plevel = max_depth - 1;
+        hu.nz = 1;
+        hu.subsample = subsample;
+        hu.seed = seed;
+        hu.margin = margin;
+        hu.Y = Y;
+        hu.g = g;
+        hu.h = h;
+        hu.node = node;
+        hu.st = st;
+        hu.fe = fe;
+        hu.sb = sb;
+        hu.gn = gn;
+        if (hu.apply) {  // round - 1's tree, node ids and metric partials
+          const int64_t rp = ro - (int64_t)T * NN;
+          hu.pst = status + rp;
+          hu.pfe = feat + rp;
+          hu.psb = sbin + rp;
+          hu.plf = leaf + rp;
+          hu.pnode = nb[(max_depth - 1) & 1];
+          hu.mpart = mround + (int64_t)(round - 1 - r0) * sets * mstride;
+          hu.mstride = mstride;
+          for (int e = 0; e < n_evals; ++e) {
+            hu.evs.bins[e] = evals[e].bins;
+            hu.evs.margin[e] = evals[e].margin;
+            hu.evs.Y[e] = evals[e].Y;
+            hu.evs.n[e] = evals[e].n;
+          }
+          hu.evs.count = n_evals;
+        }
+      }
       const int rc = launch_level_hist(level, bins, g, h, nin, T, n, F, foff_h, foff_d, partial, partial_doubles,
-                                       false, qscale, &nch, s, qa.nb ? &qa : nullptr, hp);
+                                       false, qscale, &nch, s, qa.nb ? &qa : nullptr, hp,
+                                       hist_update && level == 0 ? &hu : nullptr);
       if (rc) return rc;
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
       const int64_t cstride = (int64_t)T * nodesL * C * 2;
@@ -1693,6 +1867,10 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     if (!fuse)
       hipLaunchKernelGGL(gbdt_finalize, dim3((T + 63) / 64), dim3(64), 0, s, T, NN, max_depth, st, fe, gn, Gs, Hs, lf,
                          cv, (double)lam, gamma, (double)eta);
+    if (hist_update && round < r1 - 1) {  // this round's update runs in the next round's level-0 pass
+      EM_CHECK_LAUNCH();
+      return 0;
+    }
     // metrics (train + evals) into hist_out[round].  Elementwise metrics: the leaf update / eval
     // prediction, the metric partials and the final sum are one launch each (last-arriving block)
     const int hs = 1 + n_evals;
@@ -1768,14 +1946,19 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     if (int rc = enqueue_round(round, stream)) return rc;
   if (deferred) {
     MetricRounds mr{};
-    mr.nb[0] = grid_for(TN);
     mr.count[0] = TN;
-    for (int e = 0; e < n_evals; ++e) {
-      mr.nb[1 + e] = grid_for((int64_t)T * evals[e].n);
-      mr.count[1 + e] = (int64_t)T * evals[e].n;
+    for (int e = 0; e < n_evals; ++e) mr.count[1 + e] = (int64_t)T * evals[e].n;
+    const int first = hist_update ? r1 - 1 : r0;  // rounds [r0, first): partials of the level-0 passes
+    if (first > r0) {
+      for (int k = 0; k < sets; ++k) mr.nb[k] = T * nch0;
+      hipLaunchKernelGGL(gbdt_metric_rounds, dim3((first - r0) * sets), dim3(256), 0, stream, mround, mstride, sets,
+                         mr, metric, hist_out + (int64_t)r0 * sets);
     }
-    hipLaunchKernelGGL(gbdt_metric_rounds, dim3((r1 - r0) * sets), dim3(256), 0, stream, mround, mstride, sets, mr,
-                       metric, hist_out + (int64_t)r0 * sets);
+    mr.nb[0] = grid_for(TN);
+    for (int e = 0; e < n_evals; ++e) mr.nb[1 + e] = grid_for((int64_t)T * evals[e].n);
+    hipLaunchKernelGGL(gbdt_metric_rounds, dim3((r1 - first) * sets), dim3(256), 0, stream,
+                       mround + (int64_t)(first - r0) * sets * mstride, mstride, sets, mr, metric,
+                       hist_out + (int64_t)first * sets);
     EM_CHECK_LAUNCH();
   }
   return 0;

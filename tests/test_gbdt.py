@@ -228,9 +228,10 @@ def test_hip_dp_primitives_match_single_call():
 @pytest.mark.gpu
 @pytest.mark.parametrize("obj", ["reg:logistic", "reg:squarederror"])
 def test_hip_fused_round_bit_identical(obj):
-    """The fused round (partition inside the histogram pass, prune/leaves in the last split, last
-    partition and next round start in the update) and the separate launches give bit-identical trees,
-    margins and histories.  (Round 4's hipGraph-replayed rounds were slower and are gone.)"""
+    """The fused round (partition inside the histogram pass, prune/leaves in the last split, the update
+    of round r - 1 -- last partition, margins, eval predictions, round r's g / h -- inside round r's
+    level-0 histogram pass) and the separate launches give bit-identical trees, margins and predictions,
+    and the same metric history to float rounding (the metric terms are summed in another grouping)."""
     from euromillioner_amd import config as C
     from euromillioner_amd.pipeline import gbdt_dataset
 
@@ -248,7 +249,11 @@ def test_hip_fused_round_bit_identical(obj):
     a, b = fits["fused"], fits["separate"]
     for k in ("status", "feat", "sbin", "leaf", "gain", "cover"):
         assert np.array_equal(getattr(a.trees, k), getattr(b.trees, k)), k
-    assert a.history == b.history
+    # (the fused rounds sum the per-round metric terms grouped by histogram chunk, the separate launches by
+    # update block: the same terms, summed in another order)
+    assert len(a.history) == len(b.history)
+    for ha, hb in zip(a.history, b.history):
+        assert ha.keys() == hb.keys() and all(abs(ha[k] - hb[k]) <= 1e-6 * max(1.0, abs(hb[k])) for k in ha), (ha, hb)
     assert np.array_equal(a.predict(X[m:], backend="hip"), b.predict(X[m:], backend="hip"))
 
 
