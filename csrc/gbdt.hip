@@ -215,6 +215,40 @@ EM_DEVICE double block_sum_waves(double acc) {
   return tot;
 }
 
+struct SplitFinal {
+  int* tctr = nullptr;  // [T] zeroed arrival counters (left zeroed)
+  float* leaf = nullptr;
+  float* cover = nullptr;
+  float gamma = 0.f;
+  double eta = 0.0;
+  int max_depth = 0;
+};
+EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma);
+template <typename A, bool COH>
+EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nchunks, int64_t cstride,
+                          const int* __restrict__ foff, int T, int F, int C, int level, int NN, double* __restrict__ G,
+                          double* __restrict__ H, int8_t* __restrict__ status, int16_t* __restrict__ feat,
+                          uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw, double qinv,
+                          SplitFinal fin, int oneshot, int pscan, const int4* __restrict__ cellinfo);
+
+// The level-0 histogram pass splitting its task's root itself (exact fused rounds, with HistUpdate): every
+// chunk block stores its partials write-through (agent-scope), drains them, and adds to the task's
+// counter; the last-arriving block reads them back with agent-scope loads and runs the split (gbdt_split's
+// body) -- the "write-through stores + vmcnt(0) + relaxed arrival" hand-off of the fused finalize.  The
+// round's tree arrays are initialised with write-through stores too (a plain store could sit in another
+// XCD's L2 and be written back over the split's results).  One launch less per round.
+struct HistSplit {
+  int on = 0;
+  int* ctr = nullptr;  // [T] arrival counters (left zeroed)
+  double* G = nullptr;
+  double* H = nullptr;
+  double lam = 0.0, mcw = 0.0;
+  SplitFinal fin;
+  int oneshot = 0, pscan = 0, NN = 0;
+  int64_t cstride = 0;
+  const int4* cellinfo = nullptr;
+};
+
 // ---------------------------------------------------------------- K8 histogram (compact cells)
 // Cells: feature f owns bins [foff[f], foff[f+1]) of a compact axis of C = foff[F] cells (a one-hot
 // lag feature has 2 cells, "day" 31 ...), so a (task, node) histogram of the reference features is
@@ -260,7 +294,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
           int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, int stage_rows,
           int16_t* __restrict__ node_out, const int8_t* __restrict__ pst, const int16_t* __restrict__ pfe,
-          const uint8_t* __restrict__ psb, int NN, HistUpdate hu) {
+          const uint8_t* __restrict__ psb, int NN, HistUpdate hu, HistSplit hsp) {
   // stage_rows > 0: each piece's bin rows are staged in LDS with 16-B loads (one round trip instead of
   // one per 8 rows of byte loads); the host sets it when a piece's rows fit (stage_rows * F <= 16 KB).
   // node_out != nullptr (level >= 1): the rows' nodes are the previous level's partition, applied here
@@ -435,16 +469,45 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
       shv += e[1];
     }
     double* o = out + ((int64_t)(n0 + nd) * C + c0 + cc) * 2;
-    o[0] = sgv;
-    o[1] = shv;
+    if (hsp.on) {  // (write-through: read back by this task's last-arriving block)
+      __hip_atomic_store(o, sgv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 1, shv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      o[0] = sgv;
+      o[1] = shv;
+    }
   }
   if (hu.apply) {
     const double bs = block_sum_waves(macc);
     if (threadIdx.x == 0) hu.mpart[(int64_t)t * gridDim.x + c] = bs;
   }
-  if (hu.on && c == 0)  // round `round`'s tree arrays of task t
-    for (int k = threadIdx.x; k < hu.NN; k += blockDim.x)
-      round_init_elem(t * hu.NN + k, hu.st, hu.fe, hu.sb, hu.gn, hu.NN);
+  if (hu.on && c == 0) {  // round `round`'s tree arrays of task t
+    for (int k = threadIdx.x; k < hu.NN; k += blockDim.x) {
+      const int e = t * hu.NN + k;
+      if (hsp.on) {
+        __hip_atomic_store(hu.st + e, (int8_t)(k == 0 ? 2 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hu.fe + e, (int16_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hu.sb + e, (uint8_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hu.gn + e, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        round_init_elem(e, hu.st, hu.fe, hu.sb, hu.gn, hu.NN);
+      }
+    }
+  }
+  if (hsp.on) {
+    __shared__ int lastblk;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores have completed
+    __syncthreads();                                   // ... and every thread's
+    if (threadIdx.x == 0)
+      lastblk = __hip_atomic_fetch_add(hsp.ctr + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (lastblk) {
+      if (threadIdx.x == 0) __hip_atomic_store(hsp.ctr + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      split_body<double, true>(t, smem, partial, gridDim.x, hsp.cstride, foff, T, F, C, 0, hsp.NN, hsp.G, hsp.H,
+                               hu.st, hu.fe, hu.sb, hu.gn, hsp.lam, hsp.mcw, 0.0, hsp.fin, hsp.oneshot, hsp.pscan,
+                               hsp.cellinfo);
+    }
+  }
   GSTAMP(64 + 16 * level + 4);
 }
 
@@ -738,31 +801,28 @@ __global__ void gbdt_chunk_reduce(A* __restrict__ partial, int nchunks, int64_t 
 // Finalize (tf != nullptr, the last level): each (task, node) block arrives on the task's counter after
 // its decision (release); the task's last block (acquire) runs gbdt_finalize's prune and leaves for the
 // task and re-arms the counter -- one launch less per round.
-struct SplitFinal {
-  int* tctr = nullptr;  // [T] zeroed arrival counters (left zeroed)
-  float* leaf = nullptr;
-  float* cover = nullptr;
-  float gamma = 0.f;
-  double eta = 0.0;
-  int max_depth = 0;
-};
-EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma);
 constexpr int SPLIT_FINAL_MAX_DEPTH = 8;
 constexpr int SPLIT_DIRECT_MAX_BINS = 32;  // direct candidate form up to this many bins per feature
 constexpr int EM_GBDT_SEPARATE = 1;  // em_gbdt_fit launch_flags: the separate launches instead of the fused round
 constexpr int SPLIT_ONESHOT_LDS = 48 * 1024;  // chunk partials staged at once up to this many bytes (+ the
                                               // finalize's <= 12 KB: within the default 64 KB)  // the fused finalize stages NN <= 511 nodes (23 B each) in LDS
 
-template <typename A>
-__global__ void __launch_bounds__(256)
-gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
-           int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
-           int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
-           double qinv, SplitFinal fin, int oneshot, int pscan, const int4* __restrict__ cellinfo) {
+// One node's split (block vb = task * nodesL + node of the level), shared by the split launch and the
+// level-0 histogram pass that splits its task's root itself (COH: the chunk partials and the node's
+// status come from other workgroups of the same launch -- agent-scope loads, see HistSplit).
+template <typename A, bool COH>
+EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nchunks, int64_t cstride,
+                          const int* __restrict__ foff, int T, int F, int C, int level, int NN, double* __restrict__ G,
+                          double* __restrict__ H, int8_t* __restrict__ status, int16_t* __restrict__ feat,
+                          uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw, double qinv,
+                          SplitFinal fin, int oneshot, int pscan, const int4* __restrict__ cellinfo) {
   constexpr bool Q = std::is_same<A, long long>::value;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto ldp = [](const A* p) -> A {
+    if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+  };
   const int nodesL = 1 << level, first = nodesL - 1;
-  const int t = blockIdx.x / nodesL, nd = blockIdx.x % nodesL, i = first + nd;
+  const int t = vb / nodesL, nd = vb % nodesL, i = first + nd;
   GSTAMP(16 * level);
   int8_t* st = status + (int64_t)t * NN;
   // the thread's feature cells and feature 0's, loaded before the partials (one round trip for all)
@@ -787,10 +847,15 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
       const int idx = (int)threadIdx.x + u * (int)blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
-      pre[u] = idx < tot ? hs0[(int64_t)c * cstride + e] : A(0);
+      pre[u] = idx < tot ? ldp(hs0 + (int64_t)c * cstride + e) : A(0);
     }
   }
-  if (st[i] == 2) {  // block-uniform: an open node
+  int8_t sti;
+  if constexpr (COH)
+    sti = __hip_atomic_load(st + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    sti = st[i];
+  if (sti == 2) {  // block-uniform: an open node
     const A* hs = hs0;
     if (one) {
       // every chunk's cells staged at once (32 loads per thread in flight: one round trip, where the
@@ -801,7 +866,7 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
           const int idx = b0 + u * blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
-          v[u] = b0 == (int)threadIdx.x ? pre[u] : (idx < tot ? hs[(int64_t)c * cstride + e] : A(0));
+          v[u] = b0 == (int)threadIdx.x ? pre[u] : (idx < tot ? ldp(hs + (int64_t)c * cstride + e) : A(0));
         }
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
@@ -843,9 +908,9 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
         return x;
     };
     __shared__ A sGn[2];
-    __shared__ double rv[4];
-    __shared__ int rf[4], rb[4];
-    __shared__ A rgl[4], rhl[4];
+    __shared__ double rv[16];  // (per wave: <= 1024 threads)
+    __shared__ int rf[16], rb[16];
+    __shared__ A rgl[16], rhl[16];
     if (threadIdx.x == 0) {
       A Gn, Hn;
       if (Q || level == 0) {  // node totals: feature 0's cells in bin order
@@ -1064,6 +1129,17 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
     fin.cover[o + k] = sst[k] ? (float)sH[k] : 0.f;
   }
   GSTAMP(16 * level + 5);
+}
+
+template <typename A>
+__global__ void __launch_bounds__(256)
+gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
+           int C, int level, int NN, double* __restrict__ G, double* __restrict__ H, int8_t* __restrict__ status,
+           int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
+           double qinv, SplitFinal fin, int oneshot, int pscan, const int4* __restrict__ cellinfo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  split_body<A, false>(blockIdx.x, smem, hist, nchunks, cstride, foff, T, F, C, level, NN, G, H, status, feat, sbin,
+                       gain, lam, mcw, qinv, fin, oneshot, pscan, cellinfo);
 }
 
 __global__ void gbdt_partition(const uint8_t* __restrict__ bins, int16_t* __restrict__ node, int T, int n, int F,
@@ -1506,7 +1582,8 @@ struct HistPartition {  // the previous level's partition fused into the exact-f
 int launch_level_hist(int level, const uint8_t* bins, const float* g, const float* h, const int16_t* node, int T,
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
                       bool fold, double qscale, int* nchunks_out, hipStream_t stream, const QuantAux* qa = nullptr,
-                      const HistPartition& hp = HistPartition(), const HistUpdate* hu = nullptr) {
+                      const HistPartition& hp = HistPartition(), const HistUpdate* hu = nullptr,
+                      const HistSplit* hsp = nullptr, size_t min_lds = 0) {
   const bool quant = qscale != 0.0;
   const int C = foff_h[F];
   const int nodesL = 1 << level;
@@ -1550,6 +1627,7 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
       const size_t sbytes = (((size_t)srows * F + 32 + 15) & ~(size_t)15);
       const int stage = ((int64_t)srows * F <= 16 * 1024 && lds + sbytes <= GBDT_HIST_MAX_DYN) ? srows : 0;
       if (stage) lds += sbytes;
+      if (lds < min_lds) lds = min_lds;  // (the fused root split reuses the histogram's LDS)
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute((const void*)gbdt_hist, hipFuncAttributeMaxDynamicSharedMemorySize, GBDT_HIST_MAX_DYN);
@@ -1557,7 +1635,7 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
       }
       hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
                          C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece, stage, hp.node_out, hp.st, hp.fe,
-                         hp.sb, hp.NN, hu ? *hu : HistUpdate());
+                         hp.sb, hp.NN, hu ? *hu : HistUpdate(), hsp ? *hsp : HistSplit());
     }
   }
   const bool split_folds = !fold && nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
@@ -1745,7 +1823,7 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
   // multi-class metrics always take them)
   int* tctr = nullptr;
   const bool fuse = !(launch_flags & EM_GBDT_SEPARATE) && !quant_bits && metric < MET_MLOGLOSS &&
-                    max_depth <= SPLIT_FINAL_MAX_DEPTH && node2 && (tctr = task_counters(T)) != nullptr;
+                    max_depth <= SPLIT_FINAL_MAX_DEPTH && node2 && (tctr = task_counters(2 * T)) != nullptr;
   // deferred metrics (metric_arrive_final with ctr == nullptr): every round's per-block partials of the
   // train and eval sets, reduced by gbdt_metric_rounds after the last round
   const int sets = 1 + n_evals;
@@ -1831,10 +1909,42 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
           hu.evs.count = n_evals;
         }
       }
+      // the root split inside the level-0 pass (HistSplit: its task's last-arriving chunk block)
+      HistSplit hsp;
+      size_t hsp_lds = 0;
+      const bool fsplit = hist_update && level == 0 && nch0 > 1 && nch0 <= SPLIT_FOLD_MAX_CHUNKS &&
+                          (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS && (int64_t)nch0 * C * 16 <= SPLIT_ONESHOT_LDS;
+      if (fsplit) {
+        hsp.on = 1;
+        hsp.ctr = tctr + T;
+        hsp.G = Gs;
+        hsp.H = Hs;
+        hsp.lam = (double)lam;
+        hsp.mcw = (double)mcw;
+        hsp.NN = NN;
+        hsp.cstride = (int64_t)T * C * 2;
+        hsp.oneshot = 1;
+        hsp.cellinfo = cellinfo_d;
+        size_t sl = ((size_t)nch0 * C * 16 + 15) & ~(size_t)15;
+        const size_t sb_ = ((size_t)C * 20 + 15) & ~(size_t)15;
+        hsp.pscan = sl + sb_ + (size_t)NN * 24 <= 60 * 1024;
+        if (hsp.pscan) sl += sb_;
+        if (max_depth == 1) {
+          hsp.fin.tctr = tctr;
+          hsp.fin.leaf = lf;
+          hsp.fin.cover = cv;
+          hsp.fin.gamma = gamma;
+          hsp.fin.eta = (double)eta;
+          hsp.fin.max_depth = max_depth;
+          sl += (size_t)NN * 24;
+        }
+        hsp_lds = sl;
+      }
       const int rc = launch_level_hist(level, bins, g, h, nin, T, n, F, foff_h, foff_d, partial, partial_doubles,
                                        false, qscale, &nch, s, qa.nb ? &qa : nullptr, hp,
-                                       hist_update && level == 0 ? &hu : nullptr);
+                                       hist_update && level == 0 ? &hu : nullptr, fsplit ? &hsp : nullptr, hsp_lds);
       if (rc) return rc;
+      if (fsplit) continue;  // (split done by the pass itself)
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
       const int64_t cstride = (int64_t)T * nodesL * C * 2;
       const int oneshot = nch > 1 && (int64_t)nch * C * 16 <= SPLIT_ONESHOT_LDS;
