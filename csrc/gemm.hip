@@ -238,37 +238,74 @@ EM_DEVICE void g_tile(int bid, int tiles_m, int tiles_n, int& m0, int& n0) {
   n0 = (in / gm) * G_BN;
 }
 
-// One operand's K-tile piece for this wave: 4 x buffer_load_dwordx4 ... lds (1 KiB = 8 rows each).
+// One operand's K-tile piece for this wave: 4 x buffer_load_dwordx4 ... lds (1 KiB each).
 // The descriptor covers the block's 256-row panel; the per-lane part is one 32-bit voffset per
 // row-group parity (the swizzle depends on (row >> 1) & 7), everything else is scalar.
+//
+// MN-contiguous operands (MN = 1: element (row r, k) at P + k * ld + r -- the natural layout of a
+// wgrad's dZ and X and of a dgrad's W, so no transposed copies): the 64 x 256 K-tile is stored as 8
+// sub-units of 32 rows, sub-unit s = [64 k][64 B] at s * 4 KiB; 1-KiB piece `grp` = sub-unit grp >> 2,
+// k-rows 16 (grp & 3) .. + 15 (4 lanes x 16 B per k-row, one 64-B global segment each), so a piece
+// sits at grp * 1 KiB exactly like the K-contiguous image and the staging schedule is unchanged.
+// The 32-B half h of k-row k is stored at half h ^ ((k >> 3) & 1): the ds_read_b64_tr_b16 fragment
+// reads (16 lanes = 4 k-rows x 32 B, 4 groups 8 k-rows apart) then cover 8 distinct 32-B bank slots
+// per half-wave.
 struct GPanel {
   __amdgpu_buffer_rsrc_t rsrc;
-  uint32_t voff[2];  // per-lane byte offsets for even / odd 8-row groups
+  uint32_t voff[2];  // per-lane byte offsets for even / odd 8-row groups (MN: both the same)
   uint32_t row_bytes;
 };
 
+template <int MN>
 EM_DEVICE GPanel g_panel(const __bf16* P, int64_t ld, int r0, int lane) {
   GPanel g;
-  const __bf16* base = P + (int64_t)r0 * ld;
+  const __bf16* base = MN ? P + r0 : P + (int64_t)r0 * ld;
   g.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
-  const int lr = lane >> 3;  // row within the 8-row group
+  if (MN) {
+    const int lr = lane >> 2;                                 // k-row within the 16-row piece
+    const int c = (lane & 3) ^ (((lr >> 3) & 1) << 1);       // stored 16-B chunk -> source chunk
+    g.voff[0] = g.voff[1] = (uint32_t)((lr * ld + 8 * c) * 2);
+  } else {
+    const int lr = lane >> 3;  // row within the 8-row group
 #pragma unroll
-  for (int par = 0; par < 2; ++par) {
-    const int c = (lane & 7) ^ ((4 * par + (lane >> 4)) & 7);  // (row >> 1) & 7 with row = 8g + lr
-    g.voff[par] = (uint32_t)((lr * ld + 8 * c) * 2);
+    for (int par = 0; par < 2; ++par) {
+      const int c = (lane & 7) ^ ((4 * par + (lane >> 4)) & 7);  // (row >> 1) & 7 with row = 8g + lr
+      g.voff[par] = (uint32_t)((lr * ld + 8 * c) * 2);
+    }
   }
   g.row_bytes = (uint32_t)(ld * 2);
   return g;
 }
 
-EM_DEVICE void g_stage(const GPanel& g, int k0, char* lds_tile, int wave) {
+// scalar source offset of 1-KiB piece `grp` of the K-tile at k0
+template <int MN>
+EM_DEVICE uint32_t g_soff(const GPanel& g, int grp, int k0) {
+  if (MN) return (uint32_t)(k0 + 16 * (grp & 3)) * g.row_bytes + (uint32_t)(grp >> 2) * 64;
+  return (uint32_t)(grp * 8) * g.row_bytes + (uint32_t)k0 * 2;
+}
+
+// (mn is a compile-time constant at every call site; the staging helpers are plain functions because
+// the host pass of a template rejects the LDS-pointer builtin)
+EM_DEVICE void g_stage(const GPanel& g, int k0, char* lds_tile, int wave, bool mn) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int grp = wave * 4 + i;
-    const uint32_t soff = (uint32_t)(grp * 8) * g.row_bytes + (uint32_t)k0 * 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rsrc, (EM_LDS void*)(lds_tile + grp * 1024), 16, g.voff[i & 1], soff,
-                                             0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rsrc, (EM_LDS void*)(lds_tile + grp * 1024), 16, g.voff[i & 1],
+                                             mn ? g_soff<1>(g, grp, k0) : g_soff<0>(g, grp, k0), 0, 0);
   }
+}
+
+// 16x16x32 operand fragment of rows row0 .. row0 + 15 (row0 % 16 == 0), k-step ks of the K-tile image:
+// lane l gets row row0 + (l & 15), k = 32 ks + 8 (l >> 4) + 0..7
+template <int MN>
+EM_DEVICE bf16x8 g_frag(const char* l, int row0, int ks, int lane) {
+  const int r16 = lane & 15, c4 = lane >> 4;
+  if (!MN) return *reinterpret_cast<const bf16x8*>(l + g_off(row0 + r16, 4 * ks + c4));
+  // transposed reads: lane (q4, p4) of a 16-lane group addresses k-row kr + q4, rows row0 + 4 p4 .. + 3
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const uint32_t o = (uint32_t)((row0 >> 5) * 4096 + (32 * ks + 8 * c4 + q4) * 64 +
+                                ((((row0 >> 4) & 1) ^ (c4 & 1)) << 5) + 8 * p4);
+  return cat_tr(lds_tr16(l, o), lds_tr16(l, o + 256));  // k-rows + 0..3, + 4..7
 }
 
 template <int FN>
@@ -323,19 +360,21 @@ EM_DEVICE float bit_mul(uint32_t w, int b, float v) { return ((w >> b) & 1u) ? v
 //     WAR: the same unit of K-tile kt-2 was last read at (B lo 2, A0 3, A2 4, A1 5, A3 6, B hi 4)-16;
 //          each reader retires its reads (lgkmcnt(0)) before the barrier that ends its next slot,
 //          so a restage 2 slots after the last read is safe: every o above is >= last + 2 - 16.
+// (MN operands: piece grp = sub-unit grp >> 2, so a 64-row unit is sub-units 2u, 2u + 1 and the B
+// halves B(lo / hi, p) are the sub-units 2 (2p + b) + hsel -- the same 1-KiB slots as the KC image)
 __device__ __forceinline__ void pp_stage_unit(const GPanel& g, int k0, char* lds_op, int first_grp, bool split_b,
-                                               int hsel, int pair, int wi) {
+                                               int hsel, int pair, int wi, bool mn) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int j = 2 * wi + i;  // this wave's row-group of the unit's 8
     const int grp = split_b ? (2 * pair + (j >> 2)) * 8 + hsel * 4 + (j & 3) : first_grp + j;
-    const uint32_t soff = (uint32_t)(grp * 8) * g.row_bytes + (uint32_t)k0 * 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rsrc, (EM_LDS void*)(lds_op + grp * 1024), 16, g.voff[grp & 1], soff,
-                                             0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rsrc, (EM_LDS void*)(lds_op + grp * 1024), 16, g.voff[grp & 1],
+                                             mn ? g_soff<1>(g, grp, k0) : g_soff<0>(g, grp, k0), 0, 0);
   }
 }
 
 // issue the unit scheduled for slot s (wave-uniform); false when it belongs past the last K-tile
+template <int AMN, int BMN>
 __device__ __forceinline__ bool pp_stage_slot(const GPanel& pa, const GPanel& pb, char* smem, int s, int ktiles,
                                                int wi) {
   const int r = s & 7, w = s >> 3;  // arithmetic shift: s = -1 -> w = -1, r = 7
@@ -344,14 +383,14 @@ __device__ __forceinline__ bool pp_stage_slot(const GPanel& pa, const GPanel& pb
   char* buf = smem + (kt & 1) * 2 * G_TILE;
   const int k0 = kt * G_BK;
   switch (r) {
-    case 0: pp_stage_unit(pa, k0, buf, 8, false, 0, 0, wi); break;            // A1
-    case 1: pp_stage_unit(pa, k0, buf, 24, false, 0, 0, wi); break;           // A3
-    case 2: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 1, 0, wi); break;    // B(hi,0)
-    case 3: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 1, 1, wi); break;    // B(hi,1)
-    case 4: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 0, 0, wi); break;    // B(lo,0)
-    case 5: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 0, 1, wi); break;    // B(lo,1)
-    case 6: pp_stage_unit(pa, k0, buf, 0, false, 0, 0, wi); break;            // A0
-    default: pp_stage_unit(pa, k0, buf, 16, false, 0, 0, wi); break;          // A2
+    case 0: pp_stage_unit(pa, k0, buf, 8, false, 0, 0, wi, AMN); break;            // A1
+    case 1: pp_stage_unit(pa, k0, buf, 24, false, 0, 0, wi, AMN); break;           // A3
+    case 2: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 1, 0, wi, BMN); break;    // B(hi,0)
+    case 3: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 1, 1, wi, BMN); break;    // B(hi,1)
+    case 4: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 0, 0, wi, BMN); break;    // B(lo,0)
+    case 5: pp_stage_unit(pb, k0, buf + G_TILE, 0, true, 0, 1, wi, BMN); break;    // B(lo,1)
+    case 6: pp_stage_unit(pa, k0, buf, 0, false, 0, 0, wi, AMN); break;            // A0
+    default: pp_stage_unit(pa, k0, buf, 16, false, 0, 0, wi, AMN); break;          // A2
   }
   return true;
 }
@@ -528,7 +567,8 @@ __device__ uint64_t g_gstamps[G_STAMP_BLOCKS * 8 * 8];
 // A0 / A2 of K-tile kt+1 are issued in slots 8kt-2 / 8kt-1 (-10 / -9 relative to 8(kt+1)), so they are
 // readable from 8kt+5 / 8kt+6 -- exactly the slots in which G0 / G1 read phase 3 of kt; their last read
 // now sits 3 slots earlier than before, so the WAR distance to the restage only grows.
-template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+// AMN / BMN: operand MN-contiguous (see GPanel); 0 = K-contiguous
+template <int OUT_BF16, int FN, int DACT, int HAS_CT, int AMN, int BMN>
 __global__ void __launch_bounds__(G_NT, 1)
 gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                     void* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
@@ -560,23 +600,22 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   const int wi = wave_s & 3;
   const bool g1 = wave_s >= 4;
-  const GPanel pa = g_panel(A, lda, m0, lane), pb = g_panel(B, ldb, n0, lane);
-  g_stage(pa, 0, smem, wave_s);
-  g_stage(pb, 0, smem + G_TILE, wave_s);
+  const GPanel pa = g_panel<AMN>(A, lda, m0, lane), pb = g_panel<BMN>(B, ldb, n0, lane);
+  g_stage(pa, 0, smem, wave_s, AMN);
+  g_stage(pb, 0, smem + G_TILE, wave_s, BMN);
   // (issuing every unit 2 slots ahead of its schedule with vmcnt(8) -- a staging "lead" -- measured
   // mixed, +-1.5 %, and was removed in round 5; docs/DESIGN.md §6)
   if (g1) {
-    const bool a = pp_stage_slot(pa, pb, smem, -4, ktiles, wi);
-    const bool b = pp_stage_slot(pa, pb, smem, -2, ktiles, wi);
+    const bool a = pp_stage_slot<AMN, BMN>(pa, pb, smem, -4, ktiles, wi);
+    const bool b = pp_stage_slot<AMN, BMN>(pa, pb, smem, -2, ktiles, wi);
     if (a && b) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    if (pp_stage_slot(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (pp_stage_slot<AMN, BMN>(pa, pb, smem, -3, ktiles, wi)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
 
-  const int r16 = lane & 15, c4 = lane >> 4;
   // fragment registers: both A halves (qm) stay resident across their two quadrants, so a K-tile
   // reads A once and B once (24 ds_read_b128 per wave instead of 40): phase 0 reads A(qm 0) + B(qn 0),
   // phase 1 A(qm 1), phase 2 B(qn 1), phase 3 nothing.  Reads only move earlier than in the 32x32
@@ -592,7 +631,7 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            fb[jj][ks] = *reinterpret_cast<const bf16x8*>(lb + g_off(wn * 64 + (q >> 1) * 32 + 16 * jj + r16, 4 * ks + c4));
+            fb[jj][ks] = g_frag<BMN>(lb, wn * 64 + (q >> 1) * 32 + 16 * jj, ks, lane);
       }
       const bool rd_a = q == 1 || (q == 0 && kt == 0) || (q == 3 && kt + 1 < ktiles);
       if (rd_a) {
@@ -602,11 +641,10 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            fa[qa ^ (q == 3)][ii][ks] =
-                *reinterpret_cast<const bf16x8*>(lsrc + g_off(wm * 128 + (qa ^ (q == 3)) * 64 + 16 * ii + r16, 4 * ks + c4));
+            fa[qa ^ (q == 3)][ii][ks] = g_frag<AMN>(lsrc, wm * 128 + (qa ^ (q == 3)) * 64 + 16 * ii, ks, lane);
       }
     }
-    const bool staged = pp_stage_slot(pa, pb, smem, slot, ktiles, wi);
+    const bool staged = pp_stage_slot<AMN, BMN>(pa, pb, smem, slot, ktiles, wi);
     if (G_STAMPS) {
       uint64_t t;
       G_MARK(t);
@@ -705,14 +743,14 @@ gemm256_pp16_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
 #endif
 }
 
-template <int OUT_BF16, int FN, int DACT, int HAS_CT>
+template <int OUT_BF16, int FN, int DACT, int HAS_CT, int AMN = 0, int BMN = 0>
 int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
              int64_t ldc, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask,
              int64_t ldm, float alpha, float beta, float* colpart, uint32_t* bits) {
   // (the 32x32x16 ping-pong kernel, the non-ping-pong 256 kernel and the unbalanced fragment-read
   // schedule were measured slower and removed in round 5; docs/DESIGN.md §2 and §6 keep their numbers)
   static bool attr = false;
-  auto kern = gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT>;
+  auto kern = gemm256_pp16_kernel<OUT_BF16, FN, DACT, HAS_CT, AMN, BMN>;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     attr = true;
@@ -722,13 +760,33 @@ int g_launch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf
   return 0;
 }
 
-// runtime (out, act/dact, ct) -> one of 15 instantiations
-int g_dispatch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, void* C,
-               int64_t ldc, int c_bf16, __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act,
-               const __bf16* mask, int64_t ldm, int dact, float alpha, float beta, float* colpart, uint32_t* bits) {
-#define EM_G(OB, FN, DA, CTV) \
-  return g_launch<OB, FN, DA, CTV>(grid, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, beta, \
-                                   colpart, bits)
+// runtime (layout, out, act/dact, ct) -> one of 20 instantiations.  Layouts besides NT (a_kc = b_kc = 1):
+// wgrad dW = dZ^T X from the natural [batch][features] tensors (both operands MN: fp32 out, no
+// activation) and dgrad (dZ W) * act' from the natural weight (B MN: bf16 out, act' or none, no C^T).
+// Whether a layout is taken is decided by g_layout_ok.
+int g_dispatch(dim3 grid, hipStream_t st, int a_kc, int b_kc, const __bf16* A, int64_t lda, const __bf16* B,
+               int64_t ldb, void* C, int64_t ldc, int c_bf16, __bf16* CT, int64_t ldct, int M, int N, int K,
+               const float* bias, int act, const __bf16* mask, int64_t ldm, int dact, float alpha, float beta,
+               float* colpart, uint32_t* bits) {
+#define EM_GL(OB, FN, DA, CTV, AM, BM)                                                                              \
+  return g_launch<OB, FN, DA, CTV, AM, BM>(grid, st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, \
+                                           beta, colpart, bits)
+#define EM_G(OB, FN, DA, CTV) EM_GL(OB, FN, DA, CTV, 0, 0)
+  if (!a_kc && !b_kc) {
+    if (c_bf16 || act != ACT_NONE || mask || dact || CT || bits) return EM_ERR_ARG;
+    EM_GL(0, ACT_NONE, 0, 0, 1, 1);
+  }
+  if (!b_kc) {
+    if (!a_kc || !c_bf16 || act != ACT_NONE || CT) return EM_ERR_ARG;
+    switch (dact) {
+      case 0: EM_GL(1, ACT_NONE, 0, 0, 0, 1);
+      case ACT_RELU: EM_GL(1, ACT_RELU, 1, 0, 0, 1);
+      case ACT_SIGMOID: EM_GL(1, ACT_SIGMOID, 1, 0, 0, 1);
+      case ACT_TANH: EM_GL(1, ACT_TANH, 1, 0, 0, 1);
+      default: return EM_ERR_ARG;
+    }
+  }
+  if (!a_kc) return EM_ERR_ARG;
   if (!c_bf16) {
     if (act != ACT_NONE || mask || dact || CT || bits) return EM_ERR_ARG;
     EM_G(0, ACT_NONE, 0, 0);
@@ -751,6 +809,17 @@ int g_dispatch(dim3 grid, hipStream_t st, const __bf16* A, int64_t lda, const __
     default: return EM_ERR_ARG;
   }
 #undef EM_G
+#undef EM_GL
+}
+
+// The 256-tile kernel's layouts (see g_dispatch); MN operands need 32-bit buffer offsets over all of K
+bool g_layout_ok(int a_kc, int b_kc, int c_bf16, int act, const void* mask, int dact, const void* ct,
+                 const void* bits, int64_t lda, int64_t ldb, int K) {
+  if (a_kc && b_kc) return true;
+  if ((!a_kc && (int64_t)K * lda * 2 >= (1ll << 31)) || (!b_kc && (int64_t)K * ldb * 2 >= (1ll << 31))) return false;
+  if (!a_kc && !b_kc) return !c_bf16 && act == ACT_NONE && !mask && !dact && !ct && !bits;
+  if (!b_kc) return c_bf16 && act == ACT_NONE && !ct;
+  return false;
 }
 
 // bf16 transpose: dst[c][r] = src[r][c]; 64x64 tiles through LDS, 16-B global accesses
@@ -1299,11 +1368,12 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
     (void)hipFuncSetAttribute((const void*)gemm_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = true;
   }
-  const bool big = splits == 1 && a_kc && b_kc && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
+  const bool big = splits == 1 && (M % G_BM) == 0 && (N % G_BN) == 0 && (K % G_BK) == 0 && K > 0 &&
                    (((uintptr_t)A | (uintptr_t)B) & 15) == 0 &&
-                   (c_bf16 || (act == ACT_NONE && !mask));  // fp32 + act / act' epilogues: any-layout kernel
+                   (c_bf16 || (act == ACT_NONE && !mask)) &&  // fp32 + act / act' epilogues: any-layout kernel
+                   g_layout_ok(a_kc, b_kc, c_bf16, act, mask, dact, ct, bits, lda, ldb, K);
   // skinny K (64 / 128) with a bf16 output: the store-stream kernel (see gemm_k64_kernel)
-  if (big && c_bf16 && (K == 64 || K == 128) && beta == 0.f) {
+  if (big && a_kc && b_kc && c_bf16 && (K == 64 || K == 128) && beta == 0.f) {
     const int rc = k64_dispatch(stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, (__bf16*)C, ldc, (__bf16*)ct,
                                 ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha, colpart, bits);
     if (rc) return rc;
@@ -1311,8 +1381,8 @@ static int gemm_impl(const void* A, int64_t lda, int a_kc, const void* B, int64_
     return 0;
   }
   if (big) {
-    const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, (const __bf16*)A, lda, (const __bf16*)B, ldb, C,
-                              ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
+    const int rc = g_dispatch(dim3((M / G_BM) * (N / G_BN)), stream, a_kc, b_kc, (const __bf16*)A, lda,
+                              (const __bf16*)B, ldb, C, ldc, c_bf16, (__bf16*)ct, ldct, M, N, K, bias, act, (const __bf16*)mask, ldm, dact, alpha,
                               beta, colpart, bits);
     if (rc) return rc;
     EM_CHECK_LAUNCH();

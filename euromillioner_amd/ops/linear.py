@@ -83,8 +83,14 @@ def relu_bits(M: int, N_: int, device) -> torch.Tensor:
 
 
 def big_ok(M: int, N_: int, K: int) -> bool:
-    """Shapes the 256x256 NT kernel takes (otherwise the 128x128 any-layout kernel runs)."""
+    """Shapes the 256x256 kernel takes (otherwise the 128x128 any-layout kernel runs)."""
     return M % BIG_M == 0 and N_ % BIG_N == 0 and K % BIG_K == 0 and K > 0
+
+
+def big_mn_ok(t: torch.Tensor, K: int) -> bool:
+    """An MN-contiguous operand ([K, rows] storage) on the 256-tile path: 32-bit buffer offsets over K rows
+    (``g_layout_ok`` in csrc/gemm.hip)."""
+    return K * t.stride(0) * 2 < (1 << 31)
 
 
 def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Tensor, M: int, N_: int, K: int,
@@ -123,9 +129,10 @@ def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Te
         N.check_cuda(bits, "bits", torch.int32)
         if not (read_bits or (act == "relu" and dact_src is None)):
             raise ValueError("bits: written by act='relu' or read by dact='relu' without dact_src")
-        if (out.dtype != torch.bfloat16 or not (a_kc and b_kc and big_ok(M, N_, K))
+        if (out.dtype != torch.bfloat16 or not (a_kc and big_ok(M, N_, K) and (b_kc or big_mn_ok(b, K)))
                 or tuple(bits.shape) != (M // 32, N_)):
-            raise ValueError("bits need the 256-tile NT path, a bf16 output and an int32 [M / 32, N] buffer")
+            raise ValueError("bits need the 256-tile path (A K-contiguous), a bf16 output and an int32 [M / 32, N] "
+                             "buffer")
     if ct is not None:
         N.check_cuda(ct, "ct", torch.bfloat16, contiguous=False)
         if not (a_kc and b_kc and big_ok(M, N_, K)) or tuple(ct.shape) != (N_, M) or not is_aligned(ct):
@@ -138,8 +145,8 @@ def gemm(a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, out: torch.Te
             float(alpha), float(beta), ct.data_ptr() if ct is not None else None, ct.stride(0) if ct is not None else 0)
     if colpart is not None:
         N.check_cuda(colpart, "colpart", torch.float32)
-        if not (a_kc and b_kc and big_ok(M, N_, K)) or colpart.numel() < (M // 128) * N_:
-            raise ValueError("colpart needs the 256-tile NT path and M / 128 * N floats")
+        if not (a_kc and big_ok(M, N_, K) and (b_kc or big_mn_ok(b, K))) or colpart.numel() < (M // 128) * N_:
+            raise ValueError("colpart needs the 256-tile path (A K-contiguous) and M / 128 * N floats")
     if bits is not None:
         N.call("em_gemm_bf16_ex", *args, colpart.data_ptr() if colpart is not None else None, bits.data_ptr(),
                N.stream_handle(out.device))
@@ -218,19 +225,26 @@ def linear_wgrad_nt(dzt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | Non
 
 
 def linear_dgrad(dz: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None = None, dact: str = "relu",
-                 out: torch.Tensor | None = None) -> torch.Tensor:
-    """``(dz @ w) * act'(y_prev)``; dz bf16 [M, N], w bf16 [N, K] -> bf16 [M, K]."""
+                 out: torch.Tensor | None = None, colpart: torch.Tensor | None = None,
+                 bits: torch.Tensor | None = None) -> torch.Tensor:
+    """``(dz @ w) * act'(y_prev)``; dz bf16 [M, N], w bf16 [N, K] -> bf16 [M, K]; ``colpart`` / ``bits`` as
+    in :func:`linear_dgrad_nt` (256-tile shapes)."""
     M, N_ = dz.shape
     K = w.shape[1]
     if out is None:
         out = empty_aligned(M, K, torch.bfloat16, dz.device)
     if dact in ("none", "identity"):
+        y_prev = bits = None
+    if bits is not None:
         y_prev = None
     if big_ok(M, K, N_) and is_aligned(dz):
-        # 256-tile shapes: transpose the (weight-sized) w once and take the NT path
-        # (65536 x 8192 x 8192: 1250 TF/s vs 648 for the any-layout kernel, tools/gemm_bench.py)
-        return gemm(dz, True, transpose(w), True, out, M, K, N_, dact_src=y_prev, dact=dact)
-    return gemm(dz, True, w, False, out, M, K, N_, dact_src=y_prev, dact=dact)
+        # 256-tile shapes: transpose the (weight-sized) w once and take the NT path.  Reading w in place
+        # (the kernel's MN-operand form, gemm(..., b_kc=False)) measured slower: 7.49 vs 6.72 ms at
+        # 65536 x 8192 x 8192 -- its ds_read_b64_tr_b16 fragment reads double the LDS read instructions in
+        # the ping-pong load segment (profiles/r5/gemm_mn_operands.txt); the transpose costs ~0.03 ms
+        return gemm(dz, True, transpose(w), True, out, M, K, N_, dact_src=y_prev, dact=dact, colpart=colpart,
+                    bits=bits)
+    return gemm(dz, True, w, False, out, M, K, N_, dact_src=y_prev, dact=dact, colpart=colpart, bits=bits)
 
 
 def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None, alpha: float = 1.0,
@@ -246,8 +260,9 @@ def linear_wgrad(dz: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
     if split_k is None and _skinny_ok(dz, x, out):
         return _wgrad_skinny(dz, x, out, alpha, beta)
     if split_k is None and alpha == 1.0 and big_ok(N_, K, M) and out.dtype == torch.float32:
-        # 256-tile shapes: both operands transposed to K-major (two LDS-tiled copies, ~7 % of the
-        # GEMM at 65536 x 8192 x 8192) and the NT path (~1.2 PF/s vs 330 TF/s any-layout)
+        # 256-tile shapes: both operands transposed to K-major (two LDS-tiled copies, ~0.45 ms each at
+        # 65536 x 8192) and the NT path: 6.27 + 0.9 ms against 8.18 ms for the MN-operand form reading dz
+        # and x in place (profiles/r5/gemm_mn_operands.txt)
         return gemm(transpose(dz), True, transpose(x), True, out, N_, K, M, beta=beta)
     tiles = ((N_ + 127) // 128) * ((K + 127) // 128)
     if split_k is None:

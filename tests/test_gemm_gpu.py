@@ -322,6 +322,65 @@ def test_relu_bits_forward_and_dgrad(M, N, K):
         LIN.linear_fwd(x, w, b, "tanh", torch.bfloat16, bits=bits)
 
 
+@pytest.mark.parametrize("M,N", [(256, 256), (768, 512)])
+def test_big_mn_operands_exact_and_repeatable(M, N):
+    """The 256-tile kernel reading MN-contiguous operands in place (csrc/gemm.hip GPanel, g_frag): the wgrad
+    layout (both operands [K][rows]) and the dgrad layout (B [K][cols]) at 1..40 K-tiles, on exact
+    asymmetric small-integer operands (every fp32 sum exact, so a mis-swizzled or transposed LDS read of
+    either operand cannot cancel out), and bitwise repeatable over 4 launches."""
+    from euromillioner_amd.ops import linear as LIN
+
+    for K in (64, 128, 320, 2560):
+        kk = torch.arange(K, device="cuda").view(K, 1)
+        a = ((3 * kk + 5 * torch.arange(M, device="cuda").view(1, M)) % 7 - 3).bfloat16()   # [K, M]
+        b = ((2 * kk + 7 * torch.arange(N, device="cuda").view(1, N)) % 11 - 5).bfloat16()  # [K, N]
+        ref = a.double().t() @ b.double()
+        out = torch.full((M, N), float("nan"), device="cuda")
+        LIN.gemm(a, False, b, False, out, M, N, K)
+        assert torch.equal(out.double(), ref), (M, N, K)
+        for _ in range(3):
+            again = LIN.gemm(a, False, b, False, torch.empty_like(out), M, N, K)
+            assert torch.equal(again, out)
+        # dgrad layout: A [M][K] K-contiguous, B [K][N] MN-contiguous, bf16 out (one rounding of an exact sum)
+        at = a.t().contiguous()
+        outb = LIN.gemm(at, True, b, False, torch.empty(M, N, dtype=torch.bfloat16, device="cuda"), M, N, K)
+        assert torch.equal(outb, ref.float().bfloat16()), (M, N, K)
+
+
+@pytest.mark.parametrize("dact", ["relu", "tanh"])
+def test_big_mn_forms_bitwise_equal_nt(dact):
+    """The MN-operand forms of the 256-tile kernel (``gemm(..., a_kc / b_kc = False)``: dgrad reading w in
+    place, wgrad reading dz and x in place) are bitwise the NT kernel on explicitly transposed copies -- same
+    MFMA order, same epilogue: output, bias partials, relu-bits act'; a column-panel view of dz (the DP wgrad
+    panels) gives the matching rows of the whole wgrad, and beta = 1 accumulates exactly."""
+    from euromillioner_amd.ops import linear as LIN
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 1024, 512, 768
+    dz = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / N ** 0.5).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = torch.randn(K, device="cuda", generator=g) * 0.1
+    bits = LIN.relu_bits(M, K, "cuda") if dact == "relu" else None
+    xw = (torch.randn(K, 256, device="cuda", generator=g) / 16).bfloat16()
+    y = LIN.linear_fwd(LIN.aligned(torch.randn(M, 256, device="cuda", generator=g).bfloat16()), xw, b, dact,
+                       torch.bfloat16, bits=bits)
+    res = []
+    for wm, kc in ((w, False), (LIN.transpose(w), True)):
+        part = torch.full(((M // 128) * K,), float("nan"), device="cuda")
+        o = torch.empty(M, K, dtype=torch.bfloat16, device="cuda")
+        LIN.gemm(dz, True, wm, kc, o, M, K, N, dact_src=None if bits is not None else y, dact=dact, colpart=part,
+                 bits=bits)
+        res.append((o, part))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    gw = LIN.gemm(dz, False, x, False, torch.empty(N, K, device="cuda"), N, K, M)
+    assert torch.equal(gw, LIN.linear_wgrad_nt(LIN.transpose(dz), LIN.transpose(x)))
+    panel = LIN.gemm(dz[:, 256:512], False, x, False, torch.empty(256, K, device="cuda"), 256, K, M)
+    assert torch.equal(panel, gw[256:512])
+    acc = LIN.gemm(dz, False, x, False, gw.clone(), N, K, M, beta=1.0)
+    assert torch.equal(acc, gw + gw)
+
+
 def test_wgrad_split_k_and_colsum_big_batch():
     from euromillioner_amd.ops import linear as LIN
 
