@@ -218,10 +218,11 @@ def main():
 
         import torch.distributed as dist
 
-        if a.dist_backend == "nccl" and a.model == "mlp-wide":  # bucketed all-reduces beside the GEMMs
-            from euromillioner_amd.parallel.dist import high_priority_comm
+        if a.dist_backend == "nccl":
+            if a.model == "mlp-wide":  # bucketed all-reduces beside the GEMMs: high-priority RCCL streams
+                from euromillioner_amd.parallel.dist import high_priority_comm
 
-            high_priority_comm()
+                high_priority_comm()
             dist.init_process_group("nccl", timeout=datetime.timedelta(minutes=10), device_id=dev)
         else:
             dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
@@ -302,6 +303,29 @@ def main():
     for i in range(a.warmup if not use_graph else min(a.warmup, 1)):
         loss_t = step(i)
     torch.cuda.synchronize()
+    comm_fallback = None
+    if world > 1 and getattr(model, "comm", None) == "xgmi" and a.comm == "auto":
+        # the fused xGMI exchange has passed its self-test; if its first real step still reports a peer
+        # wait that timed out on any rank, every rank rebuilds on the captured RCCL step instead of
+        # failing the run (collective decision, same seed -> same initial parameters)
+        try:
+            model.check_comm()
+            bad = 0
+        except Exception as e:  # noqa: BLE001 -- reported, then handled by the fallback
+            print(f"bench.py: rank {rank}: xGMI step failed ({e}); falling back to RCCL", file=sys.stderr)
+            bad = 1
+        t = torch.tensor([bad], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if int(t.item()):
+            model.close()
+            model = FusedSmallMLP(dev, loss=a.loss, lr=a.lr, seed=a.seed, process_group=group, comm="rccl",
+                                  dtype=a.dtype)
+            model.broadcast_parameters()
+            comm_fallback = "xgmi step error -> rccl"
+            use_graph = bool(a.graph) and not getattr(model, "no_graph", False) and getattr(model, "graph_safe", False)
+            for i in range(a.warmup if not use_graph else min(a.warmup, 1)):
+                loss_t = step(i)
+            torch.cuda.synchronize()
     extra_warm = 0
 
     def clock_warmup(fn, n_per_call):
@@ -447,6 +471,7 @@ def main():
                                   else a.impl + ("_f32" if a.dtype == "fp32" else "")),
                        "graph_steps": C if use_graph else 0,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
+                       "comm_fallback": comm_fallback,
                        **({"comm_dtype": a.comm_dtype, "bucket_mb": a.bucket_mb} if a.model == "mlp-wide" else {}),
                        "dist_backend": a.dist_backend if world > 1 else None},
             "ms_per_step_median": med,

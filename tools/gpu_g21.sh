@@ -17,6 +17,6 @@ for r in 1 2 3; do
     echo "$v $r $(grep -o '"hip_s": [0-9.]*, "hip_test_logloss": [0-9.]*, "hip_trees_per_s": [0-9.]*' $O/gbdt_${v}_$r.jsonl)"
   done
 done
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_dp2.json 2> $O/bench_dp2.err || { tail -20 $O/bench_dp2.err; exit 4; }
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo > $O/bench_dp2.json 2> $O/bench_dp2.err || { tail -20 $O/bench_dp2.err; exit 4; }
 grep '^{' $O/bench_dp2.json | cut -c1-400
 echo rc=0
