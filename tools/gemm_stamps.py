@@ -50,6 +50,12 @@ def main():
     per_slot = sum(out["G0"][n] for n in NAMES[:6]) / 2  # a wave spends 2 slots per phase (load + MFMA)
     out["slot_cycles"] = round(per_slot, 1)
     out["mfma_issue_share"] = round(out["G0"]["mf_issue"] / per_slot, 3)
+    # per block: the K loop's segments + prologue + epilogue; the fixed share is what a persistent kernel
+    # overlapping a tile's epilogue with the next tile's first K-tiles could hide at most
+    loop = segs * sum(out["G0"][n] for n in NAMES[:6]) / 2
+    blk = loop + out["G0"]["prologue"] + out["G0"]["epilogue"]
+    out["block_cycles"] = round(blk, 1)
+    out["fixed_share"] = round((out["G0"]["prologue"] + out["G0"]["epilogue"]) / blk, 4)
     print(json.dumps(out))
 
 
