@@ -880,11 +880,15 @@ constexpr int K64_BM = 128, K64_BN = 128, K64_NT = 256;
 constexpr int K64_TS = 144;                          // bytes per T row: 64 bf16 + 16 pad
 constexpr int K64_WEPI = 64 * K64_TS;                // 9216 B per wave
 constexpr int K64_LDS = 4 * K64_WEPI + 4 * 8 * 1024;  // T images + staged 64 x 64 mask blocks (8 KB / wave)
-static_assert(K64_LDS >= 2 * K64_BM * 64 * 2, "operand tiles must fit");
+static_assert(K64_LDS >= 2 * K64_BM * 64 * 2 && 4 * K64_WEPI >= 2 * K64_BM * 64 * 2, "operand tiles must fit");
 
 // CROW = 1: the C rows go out row-contiguous -- the transposed reads of T land in a row image in the (then
 // free) mask block, and 8 lanes store one 128-B row segment, so a store instruction covers 8 whole lines
 // instead of 16 B of 64 lines (EM_K64_CROW=0: the direct form).
+// CROW = 2 (round 5 default): the same row image built in place of T once T's transposed reads (held in 32
+// VGPRs) and the C^T stores have read it, so without a staged mask a block needs 36 KB of LDS instead of
+// 68 KB: 4 workgroups per CU instead of 2 to overlap each other's load and epilogue phases.
+constexpr int K64_LDS_SLIM = 4 * K64_WEPI;
 template <int FN, int DACT, int HAS_CT, int CROW>
 __global__ void __launch_bounds__(K64_NT, 4)
 gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
@@ -996,9 +1000,37 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
       }
   }
   wave_lds_sync();
+  if (CROW == 2) {
+    bf16x8 rv[8];  // C rows: per iteration a 16-lane group reads 16 rows x 8 columns (one 16-B piece per lane)
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int cb = 8 * it, r0 = 16 * gq;
+      rv[it] = cat_tr(lds_tr16(tb, (uint32_t)((cb + q4) * K64_TS + (r0 + 4 * p4) * 2)),
+                      lds_tr16(tb, (uint32_t)((cb + 4 + q4) * K64_TS + (r0 + 4 * p4) * 2)));
+    }
+    if (HAS_CT) {  // C^T row = one column of the block: 64 rows = 128 B straight from T (before T is reused)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = lane + 64 * k, col = q >> 3, part = q & 7;
+        *reinterpret_cast<u32x4*>(CT + (int64_t)(colw + col) * ldct + rowb + part * 8) =
+            *reinterpret_cast<const u32x4*>(tb + col * K64_TS + part * 16);
+      }
+    }
+    wave_lds_sync();  // T consumed: the row image [64 rows][128 B] (8 KB of T's 9 KB) takes its place
+    const int row = 16 * gq + i16;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) *reinterpret_cast<bf16x8*>(tb + row * 128 + ((it ^ (row & 7)) << 4)) = rv[it];
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = lane + 64 * k, rr = q >> 3, ch = q & 7;
+      *reinterpret_cast<u32x4*>(C + (int64_t)(rowb + rr) * ldc + colw + ch * 8) =
+          *reinterpret_cast<const u32x4*>(tb + rr * 128 + ((ch ^ (rr & 7)) << 4));
+    }
+  }
   // C rows: per iteration a 16-lane group reads 16 rows x 8 columns (one 16-B piece per lane)
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < (CROW == 2 ? 0 : 8); ++it) {
     const int cb = 8 * it, r0 = 16 * gq, row = r0 + i16;
     const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * K64_TS + (r0 + 4 * p4) * 2));
     const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * K64_TS + (r0 + 4 * p4) * 2));
@@ -1007,7 +1039,7 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
     else
       *reinterpret_cast<bf16x8*>(C + (int64_t)(rowb + row) * ldc + colw + cb) = cat_tr(lo, hi);
   }
-  if (CROW) {
+  if (CROW == 1) {
     wave_lds_sync();
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1016,7 +1048,7 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
           *reinterpret_cast<const u32x4*>(yb + row * 128 + ((ch ^ (row & 7)) << 4));
     }
   }
-  if (HAS_CT) {  // C^T row = one column of the block: 64 rows = 128 B straight from T
+  if (HAS_CT && CROW != 2) {  // C^T row = one column of the block: 64 rows = 128 B straight from T
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int q = lane + 64 * k, col = q >> 3, part = q & 7;
@@ -1052,7 +1084,9 @@ int k64_launch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, in
                               hipFuncAttributeMaxDynamicSharedMemorySize, K64_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT, CROW>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), K64_LDS, st,
+  // (CROW = 2 without a staged act' mask: the slim LDS footprint)
+  const int lds = (CROW == 2 && !(DACT && !bits)) ? K64_LDS_SLIM : K64_LDS;
+  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT, CROW>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), lds, st,
                      A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits);
   return 0;
 }
@@ -1062,8 +1096,11 @@ int k64_dispatch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, 
                  __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act, const __bf16* mask,
                  int64_t ldm, int dact, float alpha, float* colpart, uint32_t* bits) {
   // (CROW = 0, the direct 16-B-per-line store form, measured slower: docs/DESIGN.md §6)
+#ifndef K64_CROW
+#define K64_CROW 2
+#endif
 #define EM_K(FN, DA, CTV) \
-  return k64_launch<FN, DA, CTV, 1>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits)
+  return k64_launch<FN, DA, CTV, K64_CROW>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits)
   const bool ct = CT != nullptr;
   if (mask || dact) {
     if (act != ACT_NONE) return EM_ERR_ARG;

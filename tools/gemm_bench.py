@@ -55,6 +55,8 @@ def main():
     wt = LIN.transpose(w)
     xt = LIN.transpose(x)
     ct = torch.empty(H, B, dtype=torch.bfloat16, device=dev)
+    bits = LIN.relu_bits(B, H, dev)
+    colpart = torch.empty((B // 128) * H, dtype=torch.float32, device=dev)
     cases = [
         ("fwd_hidden_ct", 2.0 * B * H * H, lambda: LIN.linear_fwd(x, w, bias, "relu", out=y, ct=ct),
          lambda: torch.relu(torch.nn.functional.linear(x, w))),
@@ -71,6 +73,11 @@ def main():
          lambda: torch.matmul(x.t(), x, out=None).float()),
         ("fwd_in", 2.0 * B * 64 * H, lambda: LIN.linear_fwd(x64, w1, bias, "relu", out=y),
          lambda: torch.relu(torch.nn.functional.linear(x64, w1))),
+        ("fwd_in_ct", 2.0 * B * 64 * H, lambda: LIN.linear_fwd(x64, w1, bias, "relu", out=y, ct=ct, bits=bits),
+         lambda: torch.relu(torch.nn.functional.linear(x64, w1))),
+        ("dgrad_out_ct", 2.0 * B * 64 * H,
+         lambda: LIN.linear_dgrad_nt(x64, w1, None, "relu", out=y, ct=ct, colpart=colpart, bits=bits),
+         lambda: (x64 @ w3) * (y > 0)),
         ("fwd_out", 2.0 * B * 64 * H, lambda: LIN.linear_fwd(x, w3, None, "none", torch.float32, out=y64),
          lambda: torch.nn.functional.linear(x, w3).float()),
         ("square_8192", 2.0 * 8192 ** 3, lambda: LIN.linear_fwd(x[:8192], w, None, "none", out=y[:8192]),
