@@ -505,7 +505,7 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
         else
           *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(C) + (int64_t)(rowb + row) * ldc + colw + cb) = v8;
       }
-      if (G_CROW) {  // 8 lanes per 128-B row segment: each store covers 8 whole lines (gemm_k64_kernel CROW)
+      if (G_CROW) {  // 8 lanes per 128-B row segment: each store covers 8 whole lines (as gemm_k64_kernel)
         wave_lds_sync();
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -870,7 +870,8 @@ __global__ void __launch_bounds__(256) transpose_kernel(const __bf16* __restrict
 // arithmetic (2 GB written per 8 MFLOP-ish tile work).  On the 256-tile ping-pong kernel (1 block /
 // CU, 226 VGPRs, epilogue serialized per wave) they ran at 2.9-3.4 TB/s.  This kernel is built for
 // the store stream instead: 128 x 128 tiles, 4 waves (2 x 2, 64 x 64 each, 16 MFMAs), <= 128 VGPRs
-// and 40 KB of LDS so 4 workgroups share a CU and hide each other's epilogue latencies.
+// and 36 KB of LDS (68 KB with a staged act' mask) so 4 workgroups share a CU and hide each other's
+// epilogue latencies.
 //   * the whole K of the tile is staged once (register staging, XOR-swizzled [128][64] images);
 //   * epilogue per wave: act'(mask) via ds_read_b64_tr_b16 of a staged 64 x 64 mask block (4 rows of
 //     one column per read = the accumulator layout), bf16 values into a [col][row] image T, then C
@@ -882,14 +883,14 @@ constexpr int K64_WEPI = 64 * K64_TS;                // 9216 B per wave
 constexpr int K64_LDS = 4 * K64_WEPI + 4 * 8 * 1024;  // T images + staged 64 x 64 mask blocks (8 KB / wave)
 static_assert(K64_LDS >= 2 * K64_BM * 64 * 2 && 4 * K64_WEPI >= 2 * K64_BM * 64 * 2, "operand tiles must fit");
 
-// CROW = 1: the C rows go out row-contiguous -- the transposed reads of T land in a row image in the (then
-// free) mask block, and 8 lanes store one 128-B row segment, so a store instruction covers 8 whole lines
-// instead of 16 B of 64 lines (EM_K64_CROW=0: the direct form).
-// CROW = 2 (round 5 default): the same row image built in place of T once T's transposed reads (held in 32
-// VGPRs) and the C^T stores have read it, so without a staged mask a block needs 36 KB of LDS instead of
-// 68 KB: 4 workgroups per CU instead of 2 to overlap each other's load and epilogue phases.
+// The C rows go out row-contiguous: the transposed reads of T (held in 32 VGPRs) become a row image built in
+// place of T once T's reads and the C^T stores are issued, and 8 lanes store one 128-B row segment (a store
+// instruction covers 8 whole lines instead of 16 B of 64 lines).  Without a staged act' mask a block then needs
+// 36 KB of LDS: 4 workgroups per CU to overlap each other's load and epilogue phases (round 5; the row image
+// in a separate 8 KB-per-wave block, 68 KB and 2 workgroups per CU, measured 16-21 % slower:
+// profiles/r5/k64_inplace_rowimage_ab.txt; the direct 16-B-per-line form slower still, docs/DESIGN.md §6).
 constexpr int K64_LDS_SLIM = 4 * K64_WEPI;
-template <int FN, int DACT, int HAS_CT, int CROW>
+template <int FN, int DACT, int HAS_CT>
 __global__ void __launch_bounds__(K64_NT, 4)
 gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                 __bf16* __restrict__ C, int64_t ldc, __bf16* __restrict__ CT, int64_t ldct, int M, int N, int K,
@@ -910,7 +911,7 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   // the dgrad's ReLU activity words are loaded before the operands: with K = 64 the MFMA phase is one
   // K tile, and loaded at the epilogue their round trip sat between the MFMAs and the stores (dgrad
-  // 615 -> 559 us on the wide MLP; the CROW = 0 form has no registers left for them and loads late)
+  // 615 -> 559 us on the wide MLP)
   uint32_t bw[2][2] = {{0u, 0u}, {0u, 0u}};  // ReLU activity words [32-row block i][column half j] (g_epilogue)
   auto load_bits = [&]() {
     const int rb = m0 + wm * 64, cw = n0 + wn * 64;
@@ -919,7 +920,7 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 #pragma unroll
       for (int j = 0; j < 2; ++j) bw[i][j] = bits[(int64_t)((rb >> 5) + i) * N + cw + 32 * j + r];
   };
-  if (DACT && CROW && bits) load_bits();
+  if (DACT && bits) load_bits();
   for (int k0 = 0; k0 < K; k0 += 64) {
     u32x4 rs[4];  // one staging set for both operands (keeps the kernel at <= 128 VGPRs, 4 blocks / CU)
     if (k0) __syncthreads();  // the previous K tile's fragments are read
@@ -947,7 +948,6 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   const int rowb = m0 + wm * 64, colw = n0 + wn * 64;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, gq = lane >> 4;
   constexpr bool WBITS = !DACT && FN == ACT_RELU;
-  if (DACT && !CROW && bits) load_bits();
   if (DACT && !bits) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // 512 chunks of 16 B: rows q >> 3, chunk q & 7
@@ -1000,7 +1000,7 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
       }
   }
   wave_lds_sync();
-  if (CROW == 2) {
+  {
     bf16x8 rv[8];  // C rows: per iteration a 16-lane group reads 16 rows x 8 columns (one 16-B piece per lane)
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -1028,34 +1028,6 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
           *reinterpret_cast<const u32x4*>(tb + rr * 128 + ((ch ^ (rr & 7)) << 4));
     }
   }
-  // C rows: per iteration a 16-lane group reads 16 rows x 8 columns (one 16-B piece per lane)
-#pragma unroll
-  for (int it = 0; it < (CROW == 2 ? 0 : 8); ++it) {
-    const int cb = 8 * it, r0 = 16 * gq, row = r0 + i16;
-    const s16x4 lo = lds_tr16(tb, (uint32_t)((cb + q4) * K64_TS + (r0 + 4 * p4) * 2));
-    const s16x4 hi = lds_tr16(tb, (uint32_t)((cb + 4 + q4) * K64_TS + (r0 + 4 * p4) * 2));
-    if (CROW)  // row image [64 rows][128 B], 16-B chunk c of row at c ^ (row & 7)
-      *reinterpret_cast<bf16x8*>(yb + row * 128 + ((it ^ (row & 7)) << 4)) = cat_tr(lo, hi);
-    else
-      *reinterpret_cast<bf16x8*>(C + (int64_t)(rowb + row) * ldc + colw + cb) = cat_tr(lo, hi);
-  }
-  if (CROW == 1) {
-    wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int q = lane + 64 * k, row = q >> 3, ch = q & 7;
-      *reinterpret_cast<u32x4*>(C + (int64_t)(rowb + row) * ldc + colw + ch * 8) =
-          *reinterpret_cast<const u32x4*>(yb + row * 128 + ((ch ^ (row & 7)) << 4));
-    }
-  }
-  if (HAS_CT && CROW != 2) {  // C^T row = one column of the block: 64 rows = 128 B straight from T
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int q = lane + 64 * k, col = q >> 3, part = q & 7;
-      *reinterpret_cast<u32x4*>(CT + (int64_t)(colw + col) * ldct + rowb + part * 8) =
-          *reinterpret_cast<const u32x4*>(tb + col * K64_TS + part * 16);
-    }
-  }
   if (colpart) {  // bias-gradient partials, row (m0 >> 7) of [M / 128][N]: the two wm waves add via LDS
 #pragma unroll
     for (int j = 0; j < 2; ++j) cs[j] = xhalf_sum(cs[j]);
@@ -1074,19 +1046,18 @@ gemm_k64_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   }
 }
 
-template <int FN, int DACT, int HAS_CT, int CROW>
+template <int FN, int DACT, int HAS_CT>
 int k64_launch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
                __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, const __bf16* mask, int64_t ldm,
                float alpha, float* colpart, uint32_t* bits) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_k64_kernel<FN, DACT, HAS_CT, CROW>,
+    (void)hipFuncSetAttribute((const void*)gemm_k64_kernel<FN, DACT, HAS_CT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, K64_LDS);
     attr = true;
   }
-  // (CROW = 2 without a staged act' mask: the slim LDS footprint)
-  const int lds = (CROW == 2 && !(DACT && !bits)) ? K64_LDS_SLIM : K64_LDS;
-  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT, CROW>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), lds, st,
+  const int lds = (DACT && !bits) ? K64_LDS : K64_LDS_SLIM;  // (the staged act' mask needs its 32 KB)
+  hipLaunchKernelGGL((gemm_k64_kernel<FN, DACT, HAS_CT>), dim3((M / K64_BM) * (N / K64_BN)), dim3(K64_NT), lds, st,
                      A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits);
   return 0;
 }
@@ -1095,12 +1066,8 @@ int k64_launch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, in
 int k64_dispatch(hipStream_t st, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, __bf16* C, int64_t ldc,
                  __bf16* CT, int64_t ldct, int M, int N, int K, const float* bias, int act, const __bf16* mask,
                  int64_t ldm, int dact, float alpha, float* colpart, uint32_t* bits) {
-  // (CROW = 0, the direct 16-B-per-line store form, measured slower: docs/DESIGN.md §6)
-#ifndef K64_CROW
-#define K64_CROW 2
-#endif
 #define EM_K(FN, DA, CTV) \
-  return k64_launch<FN, DA, CTV, K64_CROW>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits)
+  return k64_launch<FN, DA, CTV>(st, A, lda, B, ldb, C, ldc, CT, ldct, M, N, K, bias, mask, ldm, alpha, colpart, bits)
   const bool ct = CT != nullptr;
   if (mask || dact) {
     if (act != ACT_NONE) return EM_ERR_ARG;
