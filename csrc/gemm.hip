@@ -434,13 +434,22 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
   const int c16 = lane & 15, r4 = 4 * (lane >> 4);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of the epilogue values over the wave's 128 rows (colpart)
   constexpr bool WBITS = !DACT && FN == ACT_RELU && OUT_BF16;
+  // a relu dgrad's activity words for all four 32-row blocks, loaded at once (one round trip instead of
+  // one per block between the stores)
+  uint32_t bpre[4][4];
+  if (DACT && bits) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) bpre[i][nb] = bits[(int64_t)((rowbase >> 5) + i) * N + colw + 16 * nb + c16];
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rowb = rowbase + 32 * i;
     uint32_t bw[4] = {0u, 0u, 0u, 0u};  // per 16-column group nb (see g_epilogue)
     if (DACT && bits) {
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) bw[nb] = bits[(int64_t)(rowb >> 5) * N + colw + 16 * nb + c16];
+      for (int nb = 0; nb < 4; ++nb) bw[nb] = bpre[i][nb];
     } else if (DACT) {
       const __bf16* ysrc = mask + (int64_t)rowb * ldm + colw;
 #pragma unroll

@@ -62,6 +62,9 @@ def main():
          lambda: torch.relu(torch.nn.functional.linear(x, w))),
         ("dgrad_hidden_nt", 2.0 * B * H * H, lambda: LIN.linear_dgrad_nt(x, wt, x, "relu", out=y, ct=ct),
          lambda: (x @ w) * (x > 0)),
+        ("dgrad_hidden_bits", 2.0 * B * H * H,
+         lambda: LIN.linear_dgrad_nt(x, wt, None, "relu", out=y, colpart=colpart, bits=bits),
+         lambda: (x @ w) * (x > 0)),
         ("wgrad_hidden_nt", 2.0 * B * H * H, lambda: LIN.linear_wgrad_nt(xt, xt, out=gw),
          lambda: torch.matmul(x.t(), x, out=None).float()),
         ("transpose", 2.0 * B * H, lambda: LIN.transpose(x, out=xt), lambda: x.t().contiguous()),
