@@ -224,7 +224,7 @@ struct SplitFinal {
   int max_depth = 0;
 };
 EM_DEVICE void prune_task(int8_t* st, int16_t* fe, const float* gn, int max_depth, float gamma);
-template <typename A, bool COH>
+template <typename A, bool COH, int NPRE = 32>
 EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nchunks, int64_t cstride,
                           const int* __restrict__ foff, int T, int F, int C, int level, int NN, double* __restrict__ G,
                           double* __restrict__ H, int8_t* __restrict__ status, int16_t* __restrict__ feat,
@@ -272,8 +272,18 @@ constexpr int64_t HIST_PARTIAL_CAP = 1ll << 27;  // 8-byte words of per-chunk pa
 constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (+ staged rows)
 // exact form: up to 8 private copies in a 512-thread block (round 5, with 256-row chunks; round 4 had
 // measured 512-thread blocks slower with 64-row chunks, where they only added blocks' LDS)
-constexpr int HIST_EXACT_LDS_BUDGET = 72 * 1024;
-constexpr int HIST_EXACT_THREADS = 512;
+// (side-build knobs: GBDT_HIST_THREADS / GBDT_HIST_PMAX / GBDT_HIST_LDS_KB)
+#ifndef GBDT_HIST_THREADS
+#define GBDT_HIST_THREADS 512
+#endif
+#ifndef GBDT_HIST_PMAX
+#define GBDT_HIST_PMAX 8
+#endif
+#ifndef GBDT_HIST_LDS_KB
+#define GBDT_HIST_LDS_KB 72
+#endif
+constexpr int HIST_EXACT_LDS_BUDGET = GBDT_HIST_LDS_KB * 1024;
+constexpr int HIST_EXACT_THREADS = GBDT_HIST_THREADS;
 // gbdt_hist's dynamic LDS ceiling: 160 KB less 1 KB for its static LDS (block_sum_waves); setting the
 // attribute to the full 160 KB fails once the kernel has any static LDS (and leaves hipErrorInvalidValue
 // as the last error, which the next launch check reports)
@@ -305,18 +315,25 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   GSTAMP(64 + 16 * level);
   const int c = blockIdx.x, t = blockIdx.y;
   if (hu.apply && (int)blockIdx.z >= hu.nz) {  // eval set es: round - 1's tree of task t on a chunk of its rows
-    const int es = (int)blockIdx.z - hu.nz, ne = hu.evs.n[es], per = (ne + (int)gridDim.x - 1) / (int)gridDim.x;
+    // (the set's fields picked with selects: a dynamic index into the by-value argument arrays would
+    // copy them to scratch memory for every block of the launch)
+    const int es = (int)blockIdx.z - hu.nz;
+    auto pick = [es](auto a0, auto a1, auto a2, auto a3) { return es == 0 ? a0 : es == 1 ? a1 : es == 2 ? a2 : a3; };
+    const uint8_t* ebins = pick(hu.evs.bins[0], hu.evs.bins[1], hu.evs.bins[2], hu.evs.bins[3]);
+    float* emargin = pick(hu.evs.margin[0], hu.evs.margin[1], hu.evs.margin[2], hu.evs.margin[3]);
+    const float* eY = pick(hu.evs.Y[0], hu.evs.Y[1], hu.evs.Y[2], hu.evs.Y[3]);
+    const int ne = pick(hu.evs.n[0], hu.evs.n[1], hu.evs.n[2], hu.evs.n[3]), per = (ne + (int)gridDim.x - 1) / (int)gridDim.x;
     const int eb = c * per, ee = min(ne, eb + per);
     const int64_t o = (int64_t)t * hu.NN;
     double acc = 0.0;
     for (int r = eb + (int)threadIdx.x; r < ee; r += blockDim.x) {
-      const uint8_t* row = hu.evs.bins[es] + (int64_t)r * F;
+      const uint8_t* row = ebins + (int64_t)r * F;
       int nd = 0;
       while (hu.pst[o + nd] == 1) nd = 2 * nd + 1 + (row[hu.pfe[o + nd]] > hu.psb[o + nd] ? 1 : 0);
       const int64_t i = (int64_t)t * ne + r;
-      const float m = hu.evs.margin[es][i] + hu.plf[o + nd];
-      hu.evs.margin[es][i] = m;
-      acc += metric_term(m, hu.evs.Y[es][(int64_t)r * T + t], hu.obj, hu.metric);
+      const float m = emargin[i] + hu.plf[o + nd];
+      emargin[i] = m;
+      acc += metric_term(m, eY[(int64_t)r * T + t], hu.obj, hu.metric);
     }
     const double bs = block_sum_waves(acc);
     if (threadIdx.x == 0) hu.mpart[(1 + es) * hu.mstride + (int64_t)t * gridDim.x + c] = bs;
@@ -503,7 +520,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
     __syncthreads();
     if (lastblk) {
       if (threadIdx.x == 0) __hip_atomic_store(hsp.ctr + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      split_body<double, true>(t, smem, partial, gridDim.x, hsp.cstride, foff, T, F, C, 0, hsp.NN, hsp.G, hsp.H,
+      split_body<double, true, 8192 / HIST_EXACT_THREADS>(t, smem, partial, gridDim.x, hsp.cstride, foff, T, F, C, 0, hsp.NN, hsp.G, hsp.H,
                                hu.st, hu.fe, hu.sb, hu.gn, hsp.lam, hsp.mcw, 0.0, hsp.fin, hsp.oneshot, hsp.pscan,
                                hsp.cellinfo);
     }
@@ -810,7 +827,7 @@ constexpr int SPLIT_ONESHOT_LDS = 48 * 1024;  // chunk partials staged at once u
 // One node's split (block vb = task * nodesL + node of the level), shared by the split launch and the
 // level-0 histogram pass that splits its task's root itself (COH: the chunk partials and the node's
 // status come from other workgroups of the same launch -- agent-scope loads, see HistSplit).
-template <typename A, bool COH>
+template <typename A, bool COH, int NPRE>
 EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nchunks, int64_t cstride,
                           const int* __restrict__ foff, int T, int F, int C, int level, int NN, double* __restrict__ G,
                           double* __restrict__ H, int8_t* __restrict__ status, int16_t* __restrict__ feat,
@@ -842,10 +859,10 @@ EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nc
     pGn = G[(int64_t)t * NN + i];
     pHn = H[(int64_t)t * NN + i];
   }
-  A pre[32];
+  A pre[NPRE];
   if (one) {
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
+    for (int u = 0; u < NPRE; ++u) {
       const int idx = (int)threadIdx.x + u * (int)blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
       pre[u] = idx < tot ? ldp(hs0 + (int64_t)c * cstride + e) : A(0);
     }
@@ -861,15 +878,15 @@ EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nc
       // every chunk's cells staged at once (32 loads per thread in flight: one round trip, where the
       // per-element chunk loop took 2-3), then folded in chunk order (== gbdt_chunk_reduce)
       A* stg = reinterpret_cast<A*>(smem);
-      for (int b0 = threadIdx.x; b0 < tot; b0 += 32 * blockDim.x) {
-        A v[32];
+      for (int b0 = threadIdx.x; b0 < tot; b0 += NPRE * blockDim.x) {
+        A v[NPRE];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) {
+        for (int u = 0; u < NPRE; ++u) {
           const int idx = b0 + u * blockDim.x, c = idx / (2 * C), e = idx - c * 2 * C;
           v[u] = b0 == (int)threadIdx.x ? pre[u] : (idx < tot ? ldp(hs + (int64_t)c * cstride + e) : A(0));
         }
 #pragma unroll
-        for (int u = 0; u < 32; ++u) {
+        for (int u = 0; u < NPRE; ++u) {
           const int idx = b0 + u * blockDim.x;
           if (idx < tot) stg[idx] = v[u];
         }
@@ -1504,7 +1521,7 @@ bool plan_hist(int level, int n, int T, int F, const int* foff, bool quant, Hist
       // read-modify-write chain is a P-th of the chunk), the fixed-point form one shared copy, so a
       // few-feature tile fills its 256-thread block with phases
       int P = (quant ? 256 : HIST_EXACT_THREADS) / lanes;
-      const int Pmax = quant ? 64 : 8;
+      const int Pmax = quant ? 64 : GBDT_HIST_PMAX;
       P = P > Pmax ? Pmax : (P < 1 ? 1 : P);
       for (; P >= 1; --P)
         if ((int64_t)(quant ? 1 : P) * NTn * W * 16 <= (quant ? HIST_LDS_BUDGET : HIST_EXACT_LDS_BUDGET)) break;
