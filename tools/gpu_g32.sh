@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-5 batch 30: GBDT histogram chunk size re-tested on the scratch-free kernel: 256 (base) vs 128 vs 512 rows.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+R=$PWD
+O=$R/gpurun_out/g32
+mkdir -p $O
+L=$R/euromillioner_amd/lib/ab
+for r in 1 2 3; do
+  for v in base gbdt_c128 gbdt_c512; do
+    if [ $v = base ]; then E=""; else E="EUROM_NATIVE_LIB=$L/$v.so"; fi
+    env $E timeout -k 10 200 python tools/gbdt_bench.py reference > $O/gbdt_${v}_$r.jsonl 2>&1 || { tail $O/gbdt_${v}_$r.jsonl; exit 3; }
+    echo "$v $r $(grep -o '"hip_s": [0-9.]*, "hip_test_logloss": [0-9.]*, "hip_trees_per_s": [0-9.]*' $O/gbdt_${v}_$r.jsonl)"
+  done
+done
+echo rc=0
