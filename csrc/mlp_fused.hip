@@ -1,8 +1,10 @@
 // K7 -- fused persistent small-MLP training step for MI355X (gfx950).
-// EM_BUILD_FLAGS: -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-use-amdgpu-trackers -mllvm -amdgpu-schedule-metric-bias=0
+// EM_BUILD_FLAGS: -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-use-amdgpu-trackers -mllvm -amdgpu-schedule-metric-bias=0 -mllvm -amdgpu-sched-strategy=max-memory-clause
 // (VGPR-form MFMAs give every wave 256 arch VGPRs; the register-pressure trackers and a latency-first
 // schedule remove the default build's 2 spilled dwords: +0.35 % and +0.6 % in same-box A/Bs,
-// profiles/r3/ab_sched_fused*.jsonl)
+// profiles/r3/ab_sched_fused*.jsonl.  The max-memory-clause scheduling strategy (round 5): 87.1 -> 86.7 us
+// per 1M-sample step over 6 interleaved rounds, bit-identical parameters; max-ilp 90.6 us, rejected --
+// profiles/r5/ab_sched_strategy_headline.jsonl)
 //
 // Model (BASELINE.json config 2): multi-hot 62-wide draw
 // vector -> Linear(62,128) -> ReLU -> Linear(128,62) -> grouped softmax-CE
