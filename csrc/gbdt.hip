@@ -284,6 +284,12 @@ constexpr int HIST_LDS_BUDGET = 36 * 1024;       // per-block histogram copies (
 #endif
 constexpr int HIST_EXACT_LDS_BUDGET = GBDT_HIST_LDS_KB * 1024;
 constexpr int HIST_EXACT_THREADS = GBDT_HIST_THREADS;
+// partial loads in flight per thread of the split inside the level-0 histogram pass (see GBDT_SPLIT_NPRE):
+// 4 x 512 threads cover a root's 1488 doubles; 4 instead of 16 takes the histogram kernel from 126 to 69
+// VGPRs, +3.1 % trees/s (profiles/r5/gbdt_hist_regs_ab.txt)
+#ifndef GBDT_HSPLIT_NPRE
+#define GBDT_HSPLIT_NPRE 4
+#endif
 // gbdt_hist's dynamic LDS ceiling: 160 KB less 1 KB for its static LDS (block_sum_waves); setting the
 // attribute to the full 160 KB fails once the kernel has any static LDS (and leaves hipErrorInvalidValue
 // as the last error, which the next launch check reports)
@@ -520,7 +526,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
     __syncthreads();
     if (lastblk) {
       if (threadIdx.x == 0) __hip_atomic_store(hsp.ctr + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      split_body<double, true, 8192 / HIST_EXACT_THREADS>(t, smem, partial, gridDim.x, hsp.cstride, foff, T, F, C, 0, hsp.NN, hsp.G, hsp.H,
+      split_body<double, true, GBDT_HSPLIT_NPRE>(t, smem, partial, gridDim.x, hsp.cstride, foff, T, F, C, 0, hsp.NN, hsp.G, hsp.H,
                                hu.st, hu.fe, hu.sb, hu.gn, hsp.lam, hsp.mcw, 0.0, hsp.fin, hsp.oneshot, hsp.pscan,
                                hsp.cellinfo);
     }
@@ -1148,6 +1154,13 @@ EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nc
   GSTAMP(16 * level + 5);
 }
 
+// Partial loads kept in flight per thread by the split launch's one-shot prefetch: 1488 doubles per node at
+// the reference depth-2 level; 8 x 256 threads cover them in one round trip, 4 in two (larger nodes loop).
+// 8 instead of 32 takes the kernel from 256 VGPRs (+ AGPRs) to 66: reference fit +4.7 % trees/s, same box
+// (16: +2.4 %); 4 another +1.2 % (profiles/r5/gbdt_hist_regs_ab.txt).  (side-build knob)
+#ifndef GBDT_SPLIT_NPRE
+#define GBDT_SPLIT_NPRE 4
+#endif
 template <typename A>
 __global__ void __launch_bounds__(256)
 gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* __restrict__ foff, int T, int F,
@@ -1155,7 +1168,7 @@ gbdt_split(const A* __restrict__ hist, int nchunks, int64_t cstride, const int* 
            int16_t* __restrict__ feat, uint8_t* __restrict__ sbin, float* __restrict__ gain, double lam, double mcw,
            double qinv, SplitFinal fin, int oneshot, int pscan, const int4* __restrict__ cellinfo) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  split_body<A, false>(blockIdx.x, smem, hist, nchunks, cstride, foff, T, F, C, level, NN, G, H, status, feat, sbin,
+  split_body<A, false, GBDT_SPLIT_NPRE>(blockIdx.x, smem, hist, nchunks, cstride, foff, T, F, C, level, NN, G, H, status, feat, sbin,
                        gain, lam, mcw, qinv, fin, oneshot, pscan, cellinfo);
 }
 
