@@ -96,6 +96,14 @@ class _TorchBaseline:
         return draw_metrics_torch(z, y.float(), self.loss_name)
 
 
+def _pg_choice(dist_backend: str, model: str) -> tuple[str, bool]:
+    """(process-group backend, high-priority RCCL streams) for N > 1: the requested backend for every model
+    (the fused MLP's fallback all-reduce and its control plane run on it); high priority only for the wide
+    model's bucketed all-reduces beside the GEMMs, where it was measured."""
+    backend = "nccl" if dist_backend == "nccl" else "gloo"
+    return backend, backend == "nccl" and model == "mlp-wide"
+
+
 def _parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
@@ -218,11 +226,12 @@ def main():
 
         import torch.distributed as dist
 
-        if a.dist_backend == "nccl":
-            if a.model == "mlp-wide":  # bucketed all-reduces beside the GEMMs: high-priority RCCL streams
-                from euromillioner_amd.parallel.dist import high_priority_comm
+        backend, high_prio = _pg_choice(a.dist_backend, a.model)
+        if high_prio:
+            from euromillioner_amd.parallel.dist import high_priority_comm
 
-                high_priority_comm()
+            high_priority_comm()
+        if backend == "nccl":
             dist.init_process_group("nccl", timeout=datetime.timedelta(minutes=10), device_id=dev)
         else:
             dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))

@@ -131,3 +131,18 @@ def test_bench_gpus_mismatch_with_torchrun_env_fails():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_process_group_backend_choice():
+    """bench.py initialises the requested backend for every model at N > 1 (a round-5 edit had put the fused MLP
+    on gloo under --dist-backend nccl, so its RCCL fallback would have run on gloo); high-priority RCCL streams
+    only for the wide model's bucketed all-reduces."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench._pg_choice("nccl", "mlp") == ("nccl", False)
+    assert bench._pg_choice("nccl", "mlp-wide") == ("nccl", True)
+    assert bench._pg_choice("gloo", "mlp") == ("gloo", False)
+    assert bench._pg_choice("gloo", "mlp-wide") == ("gloo", False)
