@@ -924,7 +924,7 @@ EM_DEVICE void split_body(int vb, char* smem, const A* __restrict__ hist, int nc
       __syncthreads();
       hs = fold;
     }
-    auto val = [qinv](A x) -> double {
+    auto val = [=](A x) -> double {
       if constexpr (Q)
         return (double)x * qinv;
       else

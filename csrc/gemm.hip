@@ -555,8 +555,8 @@ EM_DEVICE void g_epilogue16(f32x4 (&acc)[8][NBT], int nb0, char* smem, int wave,
 #ifndef G_STAMPS
 #define G_STAMPS 0
 #endif
-constexpr int G_STAMP_BLOCKS = 4096;
 #if G_STAMPS
+constexpr int G_STAMP_BLOCKS = 4096;
 __device__ uint64_t g_gstamps[G_STAMP_BLOCKS * 8 * 8];
 #define G_MARK(t)                                                                 \
   do {                                                                            \

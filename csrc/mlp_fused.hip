@@ -51,8 +51,6 @@ constexpr int SLAB_STRIDE = 16640;
 // weight images (mlp_adam.h): padded rows instead of an XOR swizzle, so a fragment address is one
 // per-lane base + an immediate, not one VGPR per (row, chunk) pair
 
-constexpr uint64_t MAIN_BITS = (1ull << 50) - 1;
-constexpr uint64_t STAR_BITS = ((1ull << 12) - 1) << 50;
 constexpr uint64_t BIAS_BIT = 1ull << 62;
 
 // Samples are read as precomputed 64-bit feature masks (bit n-1: main number n, bit 49+s: star s;
