@@ -572,6 +572,412 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   }
 }
 
+// ============================================================================================
+// v8: THREE waves per SIMD -- two forward waves and one backward wave on every SIMD.
+//
+// v6's phase stamps (profiles/r5/fused_timeline_xcc.txt) put the forward wave at the pole: per tile
+// 4.5 k cycles of work + 0.7 k waiting for a slot, of which ~2.2 k is the softmax's in-order VALU
+// chain, while the matrix pipe idles ~half the time.  One forward chain per SIMD cannot hide its own
+// latency, and at 256 VGPRs (weights in registers, half-hidden dW accumulators) no third wave fits.
+// v8 trades registers for LDS traffic so that 12 waves fit at <= 168 VGPRs:
+//   * 8 forward waves (tiles f, f + 8, ... of the workgroup's stream) read their W1ᵀ / W2ᵀ fragments
+//     from the LDS images for every tile (32 ds_read_b128 per tile) instead of holding them, and write
+//     the tile's X / H / dZ2 images into a ring slot only at the END of the tile (X fragments and Hᵀ
+//     stay in registers through F2 and the softmax), so a slot is held only from that write burst to
+//     the backward waves' reads: 6 slots serve 8 producers;
+//   * 4 backward waves, one per hidden QUARTER, each consume EVERY tile in order (13 MFMAs per tile:
+//     B1 4, dW2 4, dW1ᵀ 4, db2 on v_dot2 instead of a 16-register MFMA accumulator): 64 dW accumulator
+//     registers per wave instead of 144, and no parity copies to fold;
+//   * a slot is free again when all four backward waves have read it (one LDS counter, +1 per wave).
+// Waves 0-7 forward, 8-11 backward: wave w runs on SIMD w % 4, so every SIMD hosts two forward and one
+// backward wave.  Gradient summation order is fixed (every backward wave walks the tiles in order), so
+// slabs stay bit-reproducible run to run.  Selected at run time (EUROM_FUSED_V=8); v6 stays the default
+// until a same-box A/B says otherwise.
+#ifndef V8_FPRIO
+#define V8_FPRIO 0
+#endif
+#ifndef V8_BPRIO
+#define V8_BPRIO 1
+#endif
+// V8_DYN: 0 = static tiles f, f + 8, ... per forward wave; 1 = tiles claimed from an LDS counter one tile
+// ahead (masks prefetched); 2 = claimed when the wave starts the tile (its mask loads exposed)
+#ifndef V8_DYN
+#define V8_DYN 1
+#endif
+constexpr int V8_NF = 8, V8_NB = 4, V8_THREADS = 64 * (V8_NF + V8_NB);
+constexpr int V8_NSLOT = 6;
+constexpr int V8_SLOT = V6_SLOT + 256;   // + the tile's per-lane loss terms (64 floats)
+constexpr int V8_SLOSS = V6_SLOT;
+constexpr int V8_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
+constexpr int V8_YLUT = V8_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
+constexpr int V8_FLAGS = V8_YLUT + 256;  // FULL[8] | DONE[8] (ints)
+constexpr int V8_DONE = V8_FLAGS + 32;
+constexpr int V8_CLAIM = V8_FLAGS + 64;
+constexpr int V8_RING = V8_FLAGS + 128;
+constexpr int V8_LDS = V8_RING + V8_NSLOT * V8_SLOT;
+constexpr int V8_RED = 0, V8_DB2S = 65536, V8_LOSSS = V8_DB2S + 1024;  // epilogue (after the loop)
+static_assert(V8_LDS <= 163840 && V8_RING % 16 == 0 && V8_LOSSS + 64 <= V8_LDS, "v8 LDS budget");
+static_assert(V8_NSLOT <= 8, "flag words");
+EM_DEVICE uint32_t v8_slot(int slot) { return V8_RING + slot * V8_SLOT; }
+
+// forward wave f: tiles k = f, f + V8_NF, ... of the workgroup's stream
+template <int LOSS, bool SIDX>
+EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                          int offset, int f, int lane, float& loss_acc, bool& ok, Stamps& st) {
+  const int r = lane & 31, h = lane >> 5;
+  const int nunits = gridDim.x, U = blockIdx.x;
+  const int K = v6_ntiles_of_unit(B, U, nunits);
+  auto fetch = [&](int k, uint64_t& mi, uint64_t& mt) {  // branch-free prefetch (see v6_forward)
+    const int s = (U + k * nunits) * 32 + r;
+    const int sc = (k < K && s < B) ? s : 0;
+    const int idx = SIDX ? sidx[sc] : (offset + sc);
+    mi = masks[idx];
+    mt = masks[idx + 1];
+  };
+  uint64_t nin = 0, ntg = 0;
+  st.start();
+  auto ftile = [&](int k, int slot, int knext) {
+    const bool valid = (U + k * nunits) * 32 + r < B;
+    const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
+    const uint64_t tmask = valid ? ntg : 0ull;
+    fetch(knext, nin, ntg);
+
+    bf16x8 xf[4];
+    {
+      const uint32_t wlo = (uint32_t)imask >> (8 * h), whi = (uint32_t)(imask >> 32) >> (8 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xf[q] = nib_xfrag<V8_XLUT>(smem, q < 2 ? wlo : whi, q);
+    }
+    // F1: Z1ᵀ = W1ᵀ·Xᵀ (W1ᵀ fragments from the LDS image) -> relu -> Hᵀ fragments (kept in registers)
+    bf16x8 hT[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x16 a1 = f32x16{};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a1 = mfma32(lds_frag(smem, w1t_off(32 * t + r, 2 * q + h)), xf[q], a1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) hT[t][q] = relu_pack(a1, q);
+    }
+    st.mark(1);
+
+    // F2: Z2ᵀ = W2ᵀ·Hᵀ + b2
+    f32x16 z2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
+        z2[u][4 * g + 0] = b[0]; z2[u][4 * g + 1] = b[1]; z2[u][4 * g + 2] = b[2]; z2[u][4 * g + 3] = b[3];
+      }
+    auto w2f = [&](int u, int kk) { return lds_frag(smem, w2p_off(32 * u + r, kk * 2 + h)); };
+    // tile 1's chain runs inside the softmax hook (fenced by sched_barriers), so its W2ᵀ fragments are
+    // read two MFMAs ahead there instead of being hoisted by the scheduler
+    bf16x8 w2n[8];
+    auto hook = [&](auto&& step) {
+      w2n[0] = w2f(1, 0);
+      w2n[1] = w2f(1, 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j + 2 < 8) w2n[j + 2] = w2f(1, j + 2);
+        z2[1] = mfma32(w2n[j], hT[j >> 1][j & 1], z2[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        step(j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if (LOSS == 0) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) z2[0] = mfma32(w2f(0, kk), hT[kk >> 1][kk & 1], z2[0]);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) z2[u] = mfma32(w2f(u, kk), hT[kk >> 1][kk & 1], z2[u]);
+    }
+    st.mark(2);
+
+    float dz[2][16];
+    float lt = 0.f;
+    if (LOSS == 0)
+      v6_softmax_split<V8_YLUT>(smem, z2, tmask, h, dz, lt, hook);
+    else
+      bce_tile_loss<V8_YLUT>(smem, z2, tmask, valid, h, dz, lt);
+    st.mark(3);
+
+    // the slot's previous tile (k - V8_NSLOT) must have been read by all four backward waves
+    if (k >= V8_NSLOT) v6_wait(smem, V8_DONE + slot * 4, V8_NB * (k / V8_NSLOT), ok);
+    st.mark(0);
+    const uint32_t SB = v8_slot(slot);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(smem + tile_img<false>(SB + V6_SX, r, 16 * q + 8 * h)) = xf[q];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t HB = SB + V6_SH + (t >> 1) * 4096;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const u32x4 d = __builtin_bit_cast(u32x4, hT[t][q]);
+        *reinterpret_cast<u32x2*>(smem + tile_img<true>(HB, r, 32 * (t & 1) + 16 * q + 4 * h)) = u32x2{d[0], d[1]};
+        *reinterpret_cast<u32x2*>(smem + tile_img<true>(HB, r, 32 * (t & 1) + 16 * q + 8 + 4 * h)) = u32x2{d[2], d[3]};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const u32x4 fq = __builtin_bit_cast(
+            u32x4, pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2], dz[u][8 * q + 3], dz[u][8 * q + 4],
+                         dz[u][8 * q + 5], dz[u][8 * q + 6], dz[u][8 * q + 7]));
+        *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 4 * h)) = u32x2{fq[0], fq[1]};
+        *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
+            u32x2{fq[2], fq[3]};
+      }
+    // the tile's loss terms travel with it: backward wave 0 sums them in tile order (bit-reproducible
+    // however the tiles were distributed over the forward waves)
+    reinterpret_cast<float*>(smem + SB + V8_SLOSS)[lane] = lt;
+    lds_signal(smem, V8_FLAGS + slot * 4, k + 1);  // FULL
+    st.mark(4);
+  };
+  if (V8_DYN == 0) {
+    if (K > 0) fetch(f, nin, ntg);
+    for (int k = f; k < K; k += V8_NF) ftile(k, k % V8_NSLOT, k + V8_NF);
+  } else {
+    auto claim = [&]() {
+      int t = 0;
+      if (lane == 0)
+        t = __hip_atomic_fetch_add(reinterpret_cast<int*>(smem + V8_CLAIM), 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+      return __builtin_amdgcn_readfirstlane(t);
+    };
+    int cur = claim();
+    if (V8_DYN == 1) {
+      if (cur < K) fetch(cur, nin, ntg);
+      while (cur < K) {
+        const int nxt = claim();
+        ftile(cur, cur % V8_NSLOT, nxt);
+        cur = nxt;
+      }
+    } else {
+      while (cur < K) {
+        fetch(cur, nin, ntg);
+        ftile(cur, cur % V8_NSLOT, K);
+        cur = claim();
+      }
+    }
+  }
+}
+
+// backward wave of hidden quarter Q (hidden units 32Q .. 32Q + 31): every tile of the stream, in order
+template <int Q>
+EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16 (&dW1T)[2], float& db2,
+                           float& loss_acc, bool& ok, Stamps& st) {
+  const int r = lane & 31, h = lane >> 5;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
+  const int K = v6_ntiles_of_unit(B, blockIdx.x, gridDim.x);
+  const uint32_t HOFF = V6_SH + (Q >> 1) * 4096;  // H sub-image holding this quarter
+  const int hcol = 32 * (Q & 1), du = Q >> 1, ds = Q & 1;  // db2 share: output tile du, sample half ds
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  const bf16x2v one2 = {(__bf16)1.0f, (__bf16)1.0f};
+  st.start();
+  int slot = 0;
+  for (int k = 0; k < K; ++k) {
+    const uint32_t SB = v8_slot(slot), D2 = SB + V6_SD2;
+    v6_wait(smem, V8_FLAGS + slot * 4, k + 1, ok);
+    st.mark(5);
+    bf16x8 dzA[2][2], hR[2], bd[2][2], bx[2][2], w2q[4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // dZ2 as B1's A operand (samples x outputs): the forward wave's granules
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, r, 32 * u + 16 * q + 4 * h));
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, r, 32 * u + 16 * q + 8 + 4 * h));
+        dzA[u][q] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) w2q[kk] = lds_frag(smem, w2q_off(32 * Q + r, kk * 2 + h));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) hR[q] = tile_tr_frag<true>(smem, SB + HOFF, hcol, q, h, q4, p4, g1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) bd[u][q] = tile_tr_frag<true>(smem, D2, 32 * u, q, h, q4, p4, g1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) bx[u][q] = tile_tr_frag<false>(smem, SB + V6_SX, 32 * u, q, h, q4, p4, g1);
+    if (Q == 0) loss_acc += reinterpret_cast<const float*>(smem + SB + V8_SLOSS)[lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every read above has landed
+    if (lane == 0)
+      __hip_atomic_fetch_add(reinterpret_cast<int*>(smem + V8_DONE + slot * 4), 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    slot = slot + 1 == V8_NSLOT ? 0 : slot + 1;
+    st.mark(6);
+
+    // B1: dH = dZ2·W2ᵀ for the own hidden quarter
+    f32x16 aD = f32x16{};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) aD = mfma32(dzA[kk >> 1][kk & 1], w2q[kk], aD);
+    // dW2[own hid][out] += Hᵀ·dZ2 (independent of B1)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dW2[u] = mfma32(hR[q], bd[u][q], dW2[u]);
+    {  // db2[out tile du] += this lane's 8 samples of sample half ds (v_dot2 with ones)
+      uint32_t b[4];  // memcpy, not a bit_cast of a vector element: see as_s16x2
+      __builtin_memcpy(b, &bd[du][ds], 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x2v p;
+        __builtin_memcpy(&p, &b[j], 4);
+        db2 = __builtin_amdgcn_fdot2_f32_bf16(p, one2, db2, false);
+      }
+    }
+    st.mark(7);
+    bf16x8 dz1[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) dz1[q] = mask_by(hR[q], aD, q);
+    st.mark(8);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dW1T[u] = mfma32(dz1[q], bx[u][q], dW1T[u]);
+    st.mark(9);
+  }
+}
+
+template <int LOSS, bool SIDX>
+__device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
+                                         int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                                         float* __restrict__ loss_slabs, int* __restrict__ step) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t ts[4] = {};
+  if (FUSED_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
+  if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] = step[0] + 1;  // see train_v6
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  {
+    constexpr int N16 = IMG_BYTES / 16, KK = (N16 + V8_THREADS - 1) / V8_THREADS;
+    const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
+    u32x4* dst = reinterpret_cast<u32x4*>(smem);
+    u32x4 v[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) v[k] = src[min(tid + V8_THREADS * k, N16 - 1)];  // branch-free loads
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+      if (tid + V8_THREADS * k < N16) dst[tid + V8_THREADS * k] = v[k];
+  }
+  if (tid < 64) reinterpret_cast<float*>(smem + V8_YLUT)[tid] = (float)(((tid >> 2) >> (tid & 3)) & 1);
+  if (tid < 32) {
+    const uint32_t n = (uint32_t)tid >> 1, b = 2u * (tid & 1);
+    reinterpret_cast<uint32_t*>(smem + V8_XLUT)[tid] =
+        (((n >> b) & 1u) ? 0x3F80u : 0u) | (((n >> (b + 1)) & 1u) ? 0x3F800000u : 0u);
+  }
+  if (tid < 32) reinterpret_cast<int*>(smem + V8_FLAGS)[tid] = 0;  // FULL, DONE, CLAIM
+  __syncthreads();
+  float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
+  if (FUSED_STAMPS) ts[1] = __builtin_amdgcn_s_memrealtime();
+  float* RED = reinterpret_cast<float*>(smem + V8_RED);
+  float* DB2S = reinterpret_cast<float*>(smem + V8_DB2S);
+  float* LOSSS = reinterpret_cast<float*>(smem + V8_LOSSS);
+  bool ok = true;
+  Stamps st;
+  auto dump = [&]() {
+    if (FUSED_STAMPS && lane < 10) {
+      uint64_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) v = (lane == k) ? st.acc[k] : v;
+      slab_spare[wave * 16 + lane] = (float)v;
+    }
+  };
+  if (wave < V8_NF) {
+    float loss_acc = 0.f;  // (unused: the loss terms go to backward wave 0 with their tile)
+    __builtin_amdgcn_s_setprio(V8_FPRIO);
+    v8_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, wave, lane, loss_acc, ok, st);
+    dump();
+    __syncthreads();  // every wave is out of the loop: the loop's LDS is free
+    if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
+    __syncthreads();
+  } else {
+    const int Q = wave - V8_NF;
+    __builtin_amdgcn_s_setprio(V8_BPRIO);
+    f32x16 dW2[2] = {f32x16{}, f32x16{}}, dW1T[2] = {f32x16{}, f32x16{}};
+    float db2 = 0.f, loss_acc = 0.f;
+    // (Q as a template argument: the db2 share bd[Q >> 1][Q & 1] indexed at run time went to scratch)
+    if (Q == 0)
+      v8_backward<0>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+    else if (Q == 1)
+      v8_backward<1>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+    else if (Q == 2)
+      v8_backward<2>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+    else
+      v8_backward<3>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+    float lsum = wave_sum(loss_acc);
+    if (!ok) lsum = __builtin_nanf("");
+    dump();
+    __syncthreads();
+    DB2S[Q * 64 + lane] = db2;
+    if (lane == 0) LOSSS[wave] = lsum;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int which = 0; which < 2; ++which) {
+        const f32x16& acc = which ? dW1T[u] : dW2[u];
+        const int T = 8 * which + 2 * Q + u;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(RED + v6_red_slot(T, g, lane & 31, lane >> 5) * 4) =
+              f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+      }
+    __syncthreads();
+  }
+  if (FUSED_STAMPS) ts[2] = __builtin_amdgcn_s_memrealtime();
+
+  float* slab = slabs + (size_t)blockIdx.x * SLAB_STRIDE;
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(slab, 0, SLAB_STRIDE * 4, 0x00020000);
+  for (int e = tid; e < 2048; e += V8_THREADS) {  // W1[f][c..c+3] (see train_v6)
+    const int f = e >> 5, c = (e & 31) * 4;
+    const int T = 8 + 2 * (c >> 5) + (f >> 5), g = (c & 31) >> 3;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + v6_red_slot(T, g, f & 31, (c >> 2) & 1) * 4);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, e * 16, 0, 16 /* sc1 */);
+  }
+  for (int q = tid; q < 2048; q += V8_THREADS) {  // W2[c + k][o]
+    const int T = q >> 8, g = (q >> 6) & 3, L = q & 31, hh = (q >> 5) & 1;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(RED + q * 4);
+    const int c = 32 * (T >> 1) + 8 * g + 4 * hh, o = 32 * (T & 1) + L;
+    uint32_t vb[4];
+    __builtin_memcpy(vb, &v, 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      __builtin_amdgcn_raw_buffer_store_b32(vb[k], srd, (P_W2 + (c + k) * OUT + o) * 4, 0, 16 /* sc1 */);
+  }
+  if (tid < 64) {  // b2[32u + L]: quarters 2u, 2u + 1 (sample halves) x lane halves, fixed order
+    const int u = tid >> 5, L = tid & 31;
+    const float v = (DB2S[(2 * u) * 64 + L] + DB2S[(2 * u) * 64 + 32 + L]) +
+                    (DB2S[(2 * u + 1) * 64 + L] + DB2S[(2 * u + 1) * 64 + 32 + L]);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), srd, (P_B2 + tid) * 4, 0, 16 /* sc1 */);
+  }
+  if (tid == 0) {
+    float l = 0.f;
+    for (int w = 0; w < V8_NF + V8_NB; ++w) l += LOSSS[w];
+    __hip_atomic_store(loss_slabs + blockIdx.x, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (FUSED_STAMPS && tid == 0) {  // wave 0's spare stamp lanes 10..14
+    ts[3] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) slab_spare[10 + k] = __builtin_bit_cast(float, (uint32_t)ts[k]);
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    slab_spare[14] = __builtin_bit_cast(float, xcc & 15u);
+  }
+}
+
+template <int LOSS, bool SIDX>
+__global__ void __launch_bounds__(V8_THREADS, 1)
+mlp_fused_train_v8_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
+                          const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
+                          float* __restrict__ loss_slabs, int* __restrict__ step) {
+  train_v8<LOSS, SIDX>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step);
+}
+
 // Slabs only: em_adam_slab reduces them (or the DP paths all-reduce them first).  A one-launch form
 // with the slab reduction and Adam inside this kernel was measured 4.3 us per step slower (round 3,
 // docs/DESIGN.md §6b) and removed in round 4.
@@ -763,6 +1169,18 @@ void set_lds_attr() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
   (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, V8_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, V8_LDS);
+}
+// train kernel generation: EUROM_FUSED_V=8 selects v8 (read once per process)
+int fused_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("EUROM_FUSED_V");
+    return (e && std::atoi(e) == 8) ? 8 : 6;
+  }();
+  return v;
 }
 int check_train_args(const uint64_t*& draws, const int32_t* sidx, int64_t B, int64_t& offset, const void* wimg,
                      float* slabs, float* loss_slabs, int nslab) {
@@ -792,13 +1210,21 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
   if (int e = check_train_args(draws, sidx, B, offset, wimg, slabs, loss_slabs, nslab)) return e;
   const int Bi = (int)B, oi = (int)offset;
   const uint8_t* w = (const uint8_t*)wimg;
+  const bool v8 = fused_variant() == 8;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nslab), dim3(512), V6_LDS, stream, draws, sidx, Bi, oi, w, slabs, loss_slabs, step);
+    hipLaunchKernelGGL(kern, dim3(nslab), dim3(v8 ? V8_THREADS : 512), v8 ? V8_LDS : V6_LDS, stream, draws, sidx, Bi,
+                       oi, w, slabs, loss_slabs, step);
   };
-  if (loss_kind == 0)
+  if (v8) {
+    if (loss_kind == 0)
+      sidx ? go(mlp_fused_train_v8_kernel<0, true>) : go(mlp_fused_train_v8_kernel<0, false>);
+    else
+      sidx ? go(mlp_fused_train_v8_kernel<1, true>) : go(mlp_fused_train_v8_kernel<1, false>);
+  } else if (loss_kind == 0) {
     sidx ? go(mlp_fused_train_v6_kernel<0, true>) : go(mlp_fused_train_v6_kernel<0, false>);
-  else
+  } else {
     sidx ? go(mlp_fused_train_v6_kernel<1, true>) : go(mlp_fused_train_v6_kernel<1, false>);
+  }
   EM_CHECK_LAUNCH();
   return 0;
 }

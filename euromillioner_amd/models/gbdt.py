@@ -185,7 +185,11 @@ def predict_margin_values(trees: TreeArrays, X: np.ndarray, tree_task: np.ndarra
 
 # ----------------------------------------------------------------------------- objectives
 def _sigmoid(x):
-    return 1.0 / (1.0 + np.exp(-x))
+    """1 / (1 + exp(-x)) in x's dtype, exactly the HIP kernels' form (csrc/gbdt.hip:99, :1255) so trees stay
+    bit-identical.  For margins below the dtype's exp range exp(-x) is +inf and the result the correct
+    0.0: that overflow is expected here, so it is silenced for this expression only."""
+    with np.errstate(over="ignore"):
+        return 1.0 / (1.0 + np.exp(-x))
 
 
 def base_margin_for(objective: str, base_score: float) -> float:

@@ -47,7 +47,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         per = e0.elapsed_time(e1) * 1e3 / 10
-        raw = m.slabs[:nslab, FM.P_TOTAL + 128:FM.P_TOTAL + 132].contiguous().view(torch.int32).cpu().numpy()
+        v8 = os.environ.get("EUROM_FUSED_V") == "8"  # v8: 12 waves, wall-clock marks in wave 0's spare lanes 10-14
+        T0 = FM.P_TOTAL + (10 if v8 else 128)
+        raw = m.slabs[:nslab, T0:T0 + 4].contiguous().view(torch.int32).cpu().numpy()
         t = raw.astype(np.int64) & 0xFFFFFFFF
         t -= t[:, 0].min()
         us = t / 100.0
@@ -64,22 +66,30 @@ def main():
             with torch.cuda.stream(s):
                 FM.train_partials(draws, B, m.img, m.slabs, m.loss_slabs, loss="softmax")
             torch.cuda.synchronize()
-            raw = m.slabs[:nslab, FM.P_TOTAL + 128:FM.P_TOTAL + 133].contiguous().view(torch.int32).cpu().numpy()
+            raw = m.slabs[:nslab, T0:T0 + 5].contiguous().view(torch.int32).cpu().numpy()
             t = raw[:, :4].astype(np.int64) & 0xFFFFFFFF
             lp = (t[:, 2] - t[:, 1]) / 100.0
             xc = raw[:, 4]
             print(f"   launch {rep}: loop median per XCC_ID:",
                   " ".join("%d:%.1f" % (k, np.median(lp[xc == k])) for k in range(8) if (xc == k).any()),
                   "| blockIdx%8 -> XCC_ID:", " ".join(str(int(np.bincount(xc[xcd == k]).argmax())) for k in range(8)))
-        st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 128].reshape(nslab, 8, 16)[:, :, :10].double().cpu().numpy()
+        nw = 12 if v8 else 8
+        st = m.slabs[:nslab, FM.P_TOTAL:FM.P_TOTAL + 16 * nw].reshape(nslab, nw, 16)[:, :, :10].double().cpu().numpy()
         shared = os.environ.get("TL_SHARED", "1") == "1"  # FUSED_SHARED layout: waves 0-3 forward
-        roles = (("forward", [0, 1, 2, 3]), ("backward", [4, 5, 6, 7])) if shared else \
-            (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5]))
+        if v8:
+            roles = (("forward", list(range(8))), ("backward", [8, 9, 10, 11]))
+        else:
+            roles = (("forward", [0, 1, 2, 3]), ("backward", [4, 5, 6, 7])) if shared else \
+                (("forward", [0, 1, 6, 7]), ("backward", [2, 3, 4, 5]))
         for nm, ws in roles:  # wave -> role map of the kernel
             v = st[:, ws, :].reshape(-1, 10).mean(0)
             tot = v.sum()
             print(f"   {nm}: {tot / 1e3:.1f} k cycles/wave; " +
                   ", ".join(f"{n} {x / 1e3:.1f}k" for n, x in zip(NAMES, v) if x > 0))
+            # per wave slot: total / waiting (phase 0 forward, 5 backward), medians over blocks
+            wi = 0 if nm == "forward" else 5
+            print("      per wave (total/wait k):", " ".join(
+                "w%d %.0f/%.0f" % (w, np.median(st[:, w, :].sum(1)) / 1e3, np.median(st[:, w, wi]) / 1e3) for w in ws))
 
 
 if __name__ == "__main__":

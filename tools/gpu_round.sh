@@ -40,6 +40,29 @@ for stage in "$@"; do
       cat $O/timeline.txt
     fi
     ;;
+  v8)
+    # K7 v8 (three waves per SIMD): fused-kernel GPU tests on v8, same-box v6/v8 A/B, v8 phase timeline
+    EUROM_FUSED_V=8 timeout -k 10 400 python -u -m pytest tests/test_fused_mlp_gpu.py -x -v --timeout 120 --timeout-method thread > $O/pytest_v8.log 2>&1 || { tail -40 $O/pytest_v8.log; exit 30; }
+    tail -3 $O/pytest_v8.log
+    ARMS=${V8_ARMS:-"v6|EUROM_FUSED_V=6;v8|EUROM_FUSED_V=8"} ROUNDS=${V8_ROUNDS:-3} bash tools/gpu_ab.sh || exit 31
+    if [ -f euromillioner_amd/lib/ab/stamps.so ]; then
+      EUROM_FUSED_V=8 EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/stamps.so TL_B=1048576 timeout -k 10 200 python tools/fused_timeline.py > $O/timeline_v8.txt 2>&1 || { tail -20 $O/timeline_v8.txt; exit 32; }
+      cat $O/timeline_v8.txt
+    fi
+    ;;
+  pmc-ab)
+    # the same two PMC passes for each arm of PMC_ARMS="name|ENV=..;name2|ENV=.." (train-kernel counters, eager launches)
+    IFS=';' read -ra LIST <<< "${PMC_ARMS:-v6|EUROM_FUSED_V=6;v8|EUROM_FUSED_V=8}"
+    for arm in "${LIST[@]}"; do
+      name=${arm%%|*}; envs=${arm#*|}
+      for pass in 1 2; do
+        if [ $pass = 1 ]; then C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE";
+        else C="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_ACTIVE_INST_MISC SQ_INSTS_SALU"; fi
+        env $envs timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/$name/p$pass -o run -- python bench.py --steps 20 --warmup 5 --no-eval --graph 0 > $O/${name}_p$pass.log 2>&1 || { tail -20 $O/${name}_p$pass.log; exit 40; }
+      done
+    done
+    python tools/summarize_profiles.py pmc-ab $O > $O/pmc_ab.md 2>&1; cat $O/pmc_ab.md
+    ;;
   gbdt)
     timeout -k 10 400 python -u -m pytest tests/test_gbdt.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 13; }
     tail -1 $O/pytest.log

@@ -10,7 +10,7 @@ import os
 import shutil
 import sys
 
-SRC = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/profiles"
+SRC = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] != "pmc-ab" else "gpurun_out/profiles"
 DST = sys.argv[2] if len(sys.argv) > 2 else "profiles"
 
 
@@ -147,6 +147,59 @@ def main():
         f.write("\n".join(lines) + "\n")
     print(f"wrote {DST}/README.md")
 
+
+def pmc_ab(root: str, kernel_substr: str = "mlp_fused_train") -> None:
+    """Markdown table of the train kernel's PMC (median per dispatch) for every arm directory under
+    root (tools/gpu_round.sh pmc-ab: <arm>/p1, <arm>/p2), with the derived utilisations."""
+    import statistics
+
+    rows = []
+    for arm in sorted(d for d in os.listdir(root) if os.path.isdir(os.path.join(root, d))):
+        vals = collections.defaultdict(list)
+        for p in ("p1", "p2"):
+            path = os.path.join(root, arm, p, "run_counter_collection.csv")
+            if not os.path.exists(path):
+                continue
+            for r in csv.DictReader(open(path)):
+                if kernel_substr in r["Kernel_Name"]:
+                    vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if not vals:
+            continue
+        m = {k: statistics.median(v) for k, v in vals.items()}
+        rows.append((arm, m))
+    if not rows:
+        print("no counter data under", root)
+        return
+    keys = sorted({k for _, m in rows for k in m})
+    print("| counter | " + " | ".join(a for a, _ in rows) + " |")
+    print("|---|" + "---|" * len(rows))
+    for k in keys:
+        print(f"| {k} | " + " | ".join(f"{m.get(k, float('nan')):.4g}" for _, m in rows) + " |")
+
+    def der(m):
+        g = m.get("GRBM_GUI_ACTIVE", float("nan")) / 8  # cycles per XCD
+        wc = m.get("SQ_WAVE_CYCLES", float("nan"))
+        return {
+            "MFMA busy (of 1024 SIMDs)": m.get("SQ_VALU_MFMA_BUSY_CYCLES", float("nan")) / 1024 / g,
+            "LDS active (IDX_ACTIVE / 256 CUs / cycles)": m.get("SQ_LDS_IDX_ACTIVE", float("nan")) * 4 / 256 / g,
+            "LDS bank conflict / IDX_ACTIVE": m.get("SQ_LDS_BANK_CONFLICT", float("nan")) / m.get("SQ_LDS_IDX_ACTIVE", float("nan")),
+            "VALU active / wave-cycles": m.get("SQ_ACTIVE_INST_VALU", float("nan")) / wc,
+            "LDS issue-wait / wave-cycles": m.get("SQ_WAIT_INST_LDS", float("nan")) / wc,
+            "WAIT_INST_ANY / wave-cycles": m.get("SQ_WAIT_INST_ANY", float("nan")) / wc,
+            "WAIT_ANY / wave-cycles": m.get("SQ_WAIT_ANY", float("nan")) / wc,
+            "kernel cycles per XCD": g,
+        }
+    print()
+    print("| derived | " + " | ".join(a for a, _ in rows) + " |")
+    print("|---|" + "---|" * len(rows))
+    ds = [der(m) for _, m in rows]
+    for k in ds[0]:
+        print(f"| {k} | " + " | ".join(f"{d[k]:.3f}" if d[k] < 100 else f"{d[k]:.4g}" for d in ds) + " |")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "pmc-ab":
+    pmc_ab(sys.argv[2])
+    sys.exit(0)
 
 if __name__ == "__main__":
     main()
