@@ -191,6 +191,29 @@ class _Shards:
         return generate_masks(n, seed=seed, planted=planted, seg_len=SEG, device=dev, first=first), skip
 
 
+def _params_identical(model, world: int):
+    """world > 1: True iff every rank ends the timed window with bit-identical parameters (the DP
+    invariant; after a comm fallback it also shows the rebuilt model stayed in lockstep).  Small models
+    compare the whole vector, large ones a 64-bit digest of the bits."""
+    if world == 1:
+        return None
+    import torch.distributed as dist
+
+    ps = [p for p in (getattr(model, "params", None),) if isinstance(p, torch.Tensor)]
+    if not ps and hasattr(model, "parameters"):
+        ps = [p for p in model.parameters() if isinstance(p, torch.Tensor)]
+    if not ps:
+        return None
+    flat = torch.cat([p.detach().reshape(-1).float() for p in ps])
+    if flat.numel() > (1 << 20):  # digest: int64 sum of the fp32 bit patterns, position-weighted
+        bits = flat.view(torch.int32).to(torch.int64)
+        w = torch.arange(1, bits.numel() + 1, device=bits.device, dtype=torch.int64) % 1000003
+        flat = torch.stack([bits.sum(), (bits * w).sum()]).to(torch.float64)
+    got = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(got, flat)
+    return all(torch.equal(got[0], g) for g in got[1:])
+
+
 def main():
     a = _parse()
     from euromillioner_amd.parallel import launch
@@ -418,6 +441,7 @@ def main():
     med = step_ms[len(step_ms) // 2] if step_ms else float("nan")
     if hasattr(model, "check_comm"):
         model.check_comm()  # an xGMI peer wait that timed out is an error, not a fast step
+    params_identical = _params_identical(model, world)
     med_max = med
     if world > 1:
         t = torch.tensor([ms, med], device=dev)
@@ -481,6 +505,7 @@ def main():
                        "graph_steps": C if use_graph else 0,
                        "grad_allreduce": getattr(model, "comm", "rccl" if world > 1 else "none"),
                        "comm_fallback": comm_fallback,
+                       "params_identical_across_ranks": params_identical,
                        **({"comm_dtype": a.comm_dtype, "bucket_mb": a.bucket_mb} if a.model == "mlp-wide" else {}),
                        "dist_backend": a.dist_backend if world > 1 else None},
             "ms_per_step_median": med,

@@ -1405,7 +1405,10 @@ EM_API int em_rf_fit(const uint64_t* X, int W, const uint64_t* Y, int64_t N, int
 
 // scratch bytes em_rf_predict's tree-streamed path needs (0: that path does not apply)
 EM_API int64_t em_rf_predict_scratch(int W, int T, int max_depth) {
-  return (W == 1 && max_depth <= 8 && T > 0) ? (int64_t)T * RFP_TREE : 0;
+  // rf_predict_lds addresses tree t at the 32-bit buffer offset t * RFP_TREE: forests whose images would
+  // pass 2^31 bytes (~32 k trees) take the one-wave-per-row kernel instead of reading out of range
+  if (W != 1 || max_depth > 8 || T <= 0 || (int64_t)T * RFP_TREE >= (int64_t(1) << 31)) return 0;
+  return (int64_t)T * RFP_TREE;
 }
 
 // prep: em_rf_predict_scratch(W, T, max_depth) bytes (16-B aligned), or null for the one-wave-per-row path

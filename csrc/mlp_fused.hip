@@ -600,9 +600,16 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
 #define V8_BPRIO 1
 #endif
 // V8_DYN: 0 = static tiles f, f + 8, ... per forward wave; 1 = tiles claimed from an LDS counter one tile
-// ahead (masks prefetched); 2 = claimed when the wave starts the tile (its mask loads exposed)
+// ahead (masks prefetched).  Measured equal (93.2 / 94.2 us per step); claiming at the tile start, with the
+// mask loads exposed, 94.6 (removed).
 #ifndef V8_DYN
-#define V8_DYN 1
+#define V8_DYN 0
+#endif
+// FUSED_TRACE (diagnostic builds only, tools/fused_trace.py): block 0 records s_memtime per tile into
+// loss_slabs[gridDim.x ...] (12 words per tile: forward start / computed / written / wave, then FULL seen
+// and DONE per backward wave)
+#ifndef FUSED_TRACE
+#define FUSED_TRACE 0
 #endif
 constexpr int V8_NF = 8, V8_NB = 4, V8_THREADS = 64 * (V8_NF + V8_NB);
 constexpr int V8_NSLOT = 6;
@@ -619,11 +626,14 @@ constexpr int V8_RED = 0, V8_DB2S = 65536, V8_LOSSS = V8_DB2S + 1024;  // epilog
 static_assert(V8_LDS <= 163840 && V8_RING % 16 == 0 && V8_LOSSS + 64 <= V8_LDS, "v8 LDS budget");
 static_assert(V8_NSLOT <= 8, "flag words");
 EM_DEVICE uint32_t v8_slot(int slot) { return V8_RING + slot * V8_SLOT; }
+EM_DEVICE void v8_trace(uint32_t* tr, int k, int word, int lane) {
+  if (FUSED_TRACE && tr && blockIdx.x == 0 && lane == 0) tr[k * 12 + word] = (uint32_t)__builtin_amdgcn_s_memtime();
+}
 
 // forward wave f: tiles k = f, f + V8_NF, ... of the workgroup's stream
 template <int LOSS, bool SIDX>
 EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
-                          int offset, int f, int lane, float& loss_acc, bool& ok, Stamps& st) {
+                          int offset, int f, int lane, float& loss_acc, bool& ok, Stamps& st, uint32_t* tr) {
   const int r = lane & 31, h = lane >> 5;
   const int nunits = gridDim.x, U = blockIdx.x;
   const int K = v6_ntiles_of_unit(B, U, nunits);
@@ -641,6 +651,8 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
     const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
     const uint64_t tmask = valid ? ntg : 0ull;
     fetch(knext, nin, ntg);
+    v8_trace(tr, k, 0, lane);
+    if (FUSED_TRACE && tr && blockIdx.x == 0 && lane == 0) tr[k * 12 + 3] = f;
 
     bf16x8 xf[4];
     {
@@ -703,6 +715,7 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
     else
       bce_tile_loss<V8_YLUT>(smem, z2, tmask, valid, h, dz, lt);
     st.mark(3);
+    v8_trace(tr, k, 1, lane);
 
     // the slot's previous tile (k - V8_NSLOT) must have been read by all four backward waves
     if (k >= V8_NSLOT) v6_wait(smem, V8_DONE + slot * 4, V8_NB * (k / V8_NSLOT), ok);
@@ -736,6 +749,7 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
     reinterpret_cast<float*>(smem + SB + V8_SLOSS)[lane] = lt;
     lds_signal(smem, V8_FLAGS + slot * 4, k + 1);  // FULL
     st.mark(4);
+    v8_trace(tr, k, 2, lane);
   };
   if (V8_DYN == 0) {
     if (K > 0) fetch(f, nin, ntg);
@@ -749,98 +763,119 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
       return __builtin_amdgcn_readfirstlane(t);
     };
     int cur = claim();
-    if (V8_DYN == 1) {
-      if (cur < K) fetch(cur, nin, ntg);
-      while (cur < K) {
-        const int nxt = claim();
-        ftile(cur, cur % V8_NSLOT, nxt);
-        cur = nxt;
-      }
-    } else {
-      while (cur < K) {
-        fetch(cur, nin, ntg);
-        ftile(cur, cur % V8_NSLOT, K);
-        cur = claim();
-      }
+    if (cur < K) fetch(cur, nin, ntg);
+    while (cur < K) {
+      const int nxt = claim();
+      ftile(cur, cur % V8_NSLOT, nxt);
+      cur = nxt;
     }
   }
 }
 
-// backward wave of hidden quarter Q (hidden units 32Q .. 32Q + 31): every tile of the stream, in order
+// backward wave of hidden quarter Q (hidden units 32Q .. 32Q + 31): every tile of the stream, in order.
+// The tile's reads go out in three groups with the MFMAs that need only the earlier groups in between.
+// tools/fused_trace.py puts this wave at ~1.5 k cycles per tile either way (one read burst: 0.64 k burst +
+// 0.85 k MFMA issue), which bounds v8 (profiles/r6/k7_v8_runs.md).  Reading tile k + 1 under tile k's MFMAs
+// (a cross-tile pipeline) needs ~25 VGPRs more than the 168 of three waves per SIMD: built, spilled 80-96 B
+// per lane in the loop, removed.
 template <int Q>
 EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16 (&dW1T)[2], float& db2,
-                           float& loss_acc, bool& ok, Stamps& st) {
+                           float& loss_acc, bool& ok, Stamps& st, uint32_t* tr) {
   const int r = lane & 31, h = lane >> 5;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
   const int K = v6_ntiles_of_unit(B, blockIdx.x, gridDim.x);
   const uint32_t HOFF = V6_SH + (Q >> 1) * 4096;  // H sub-image holding this quarter
-  const int hcol = 32 * (Q & 1), du = Q >> 1, ds = Q & 1;  // db2 share: output tile du, sample half ds
+  constexpr int hcol = 32 * (Q & 1), du = Q >> 1, ds = Q & 1;  // db2 share: output tile du, sample half ds
   typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
   const bf16x2v one2 = {(__bf16)1.0f, (__bf16)1.0f};
-  st.start();
-  int slot = 0;
-  for (int k = 0; k < K; ++k) {
-    const uint32_t SB = v8_slot(slot), D2 = SB + V6_SD2;
-    v6_wait(smem, V8_FLAGS + slot * 4, k + 1, ok);
-    st.mark(5);
-    bf16x8 dzA[2][2], hR[2], bd[2][2], bx[2][2], w2q[4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {  // dZ2 as B1's A operand (samples x outputs): the forward wave's granules
-        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, r, 32 * u + 16 * q + 4 * h));
-        const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, r, 32 * u + 16 * q + 8 + 4 * h));
-        dzA[u][q] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
-      }
+  bf16x8 w2q[4], dzA[2][2], hR[2], bd[2][2], bx[2][2];
+  auto rd_dzA = [&](uint32_t SB) {  // dZ2 as B1's A operand (samples x outputs): the forward wave's granules
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) w2q[kk] = lds_frag(smem, w2q_off(32 * Q + r, kk * 2 + h));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) hR[q] = tile_tr_frag<true>(smem, SB + HOFF, hcol, q, h, q4, p4, g1);
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 4 * h));
+        const u32x2 hi =
+            *reinterpret_cast<const u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h));
+        dzA[u][q] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      }
+  };
+  auto rd_bd = [&](uint32_t SB) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) bd[u][q] = tile_tr_frag<true>(smem, D2, 32 * u, q, h, q4, p4, g1);
+      for (int q = 0; q < 2; ++q) bd[u][q] = tile_tr_frag<true>(smem, SB + V6_SD2, 32 * u, q, h, q4, p4, g1);
+  };
+  auto rd_hR = [&](uint32_t SB) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) hR[q] = tile_tr_frag<true>(smem, SB + HOFF, hcol, q, h, q4, p4, g1);
+  };
+  auto rd_bx = [&](uint32_t SB) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 2; ++q) bx[u][q] = tile_tr_frag<false>(smem, SB + V6_SX, 32 * u, q, h, q4, p4, g1);
     if (Q == 0) loss_acc += reinterpret_cast<const float*>(smem + SB + V8_SLOSS)[lane];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every read above has landed
+  };
+  auto release = [&](int slot, int k) {  // every read of the slot has landed
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0)
       __hip_atomic_fetch_add(reinterpret_cast<int*>(smem + V8_DONE + slot * 4), 1, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    slot = slot + 1 == V8_NSLOT ? 0 : slot + 1;
-    st.mark(6);
-
-    // B1: dH = dZ2·W2ᵀ for the own hidden quarter
-    f32x16 aD = f32x16{};
+    v8_trace(tr, k, 5 + 2 * Q, lane);
+  };
+  auto wait_full = [&](int slot, int k) {
+    v6_wait(smem, V8_FLAGS + slot * 4, k + 1, ok);
+    v8_trace(tr, k, 4 + 2 * Q, lane);
+  };
+  auto db2_share = [&]() {  // db2[out tile du] += this lane's 8 samples of sample half ds (v_dot2 with ones)
+    uint32_t b[4];  // memcpy, not a bit_cast of a vector element: see as_s16x2
+    __builtin_memcpy(b, &bd[du][ds], 16);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) aD = mfma32(dzA[kk >> 1][kk & 1], w2q[kk], aD);
-    // dW2[own hid][out] += Hᵀ·dZ2 (independent of B1)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) dW2[u] = mfma32(hR[q], bd[u][q], dW2[u]);
-    {  // db2[out tile du] += this lane's 8 samples of sample half ds (v_dot2 with ones)
-      uint32_t b[4];  // memcpy, not a bit_cast of a vector element: see as_s16x2
-      __builtin_memcpy(b, &bd[du][ds], 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bf16x2v p;
-        __builtin_memcpy(&p, &b[j], 4);
-        db2 = __builtin_amdgcn_fdot2_f32_bf16(p, one2, db2, false);
-      }
+    for (int j = 0; j < 4; ++j) {
+      bf16x2v pr;
+      __builtin_memcpy(&pr, &b[j], 4);
+      db2 = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, db2, false);
     }
-    st.mark(7);
-    bf16x8 dz1[2];
+  };
+  st.start();
+  {  // staged reads inside the tile: each group's read latency runs under the MFMAs before it
+    int slot = 0;
+    for (int k = 0; k < K; ++k) {
+      const uint32_t SB = v8_slot(slot);
+      wait_full(slot, k);
+      st.mark(5);
+      rd_dzA(SB);  // (+ the W2ᵀ fragments)
+      __builtin_amdgcn_sched_barrier(0);
+      rd_hR(SB);
+      rd_bd(SB);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 aD = f32x16{};  // B1: dH = dZ2·W2ᵀ for the own hidden quarter
 #pragma unroll
-    for (int q = 0; q < 2; ++q) dz1[q] = mask_by(hR[q], aD, q);
-    st.mark(8);
+      for (int kk = 0; kk < 4; ++kk) aD = mfma32(dzA[kk >> 1][kk & 1], w2q[kk], aD);
+      __builtin_amdgcn_sched_barrier(0);
+      rd_bx(SB);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)  // dW2[own hid][out] += Hᵀ·dZ2 (independent of B1)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) dW1T[u] = mfma32(dz1[q], bx[u][q], dW1T[u]);
-    st.mark(9);
+        for (int q = 0; q < 2; ++q) dW2[u] = mfma32(hR[q], bd[u][q], dW2[u]);
+      db2_share();
+      __builtin_amdgcn_sched_barrier(0);
+      release(slot, k);
+      slot = slot + 1 == V8_NSLOT ? 0 : slot + 1;
+      st.mark(6);
+      bf16x8 dz1[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dz1[q] = mask_by(hR[q], aD, q);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) dW1T[u] = mfma32(dz1[q], bx[u][q], dW1T[u]);
+      st.mark(9);
+    }
   }
 }
 
@@ -875,6 +910,7 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
   __syncthreads();
   float* slab_spare = slabs + (size_t)blockIdx.x * SLAB_STRIDE + P_TOTAL;  // 192 spare floats per slab
   if (FUSED_STAMPS) ts[1] = __builtin_amdgcn_s_memrealtime();
+  uint32_t* tr = FUSED_TRACE ? reinterpret_cast<uint32_t*>(loss_slabs + gridDim.x) : nullptr;
   float* RED = reinterpret_cast<float*>(smem + V8_RED);
   float* DB2S = reinterpret_cast<float*>(smem + V8_DB2S);
   float* LOSSS = reinterpret_cast<float*>(smem + V8_LOSSS);
@@ -891,7 +927,7 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
   if (wave < V8_NF) {
     float loss_acc = 0.f;  // (unused: the loss terms go to backward wave 0 with their tile)
     __builtin_amdgcn_s_setprio(V8_FPRIO);
-    v8_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, wave, lane, loss_acc, ok, st);
+    v8_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, wave, lane, loss_acc, ok, st, tr);
     dump();
     __syncthreads();  // every wave is out of the loop: the loop's LDS is free
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
@@ -903,13 +939,13 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
     float db2 = 0.f, loss_acc = 0.f;
     // (Q as a template argument: the db2 share bd[Q >> 1][Q & 1] indexed at run time went to scratch)
     if (Q == 0)
-      v8_backward<0>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+      v8_backward<0>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     else if (Q == 1)
-      v8_backward<1>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+      v8_backward<1>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     else if (Q == 2)
-      v8_backward<2>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+      v8_backward<2>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     else
-      v8_backward<3>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st);
+      v8_backward<3>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     float lsum = wave_sum(loss_acc);
     if (!ok) lsum = __builtin_nanf("");
     dump();

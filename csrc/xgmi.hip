@@ -95,7 +95,8 @@ xgmi_emulate_block_peers_kernel(XgmiDesc d, float* const* __restrict__ peer_data
     for (int q = 0; q < d.world; ++q) {
       if (q == d.rank) continue;
       for (int par = 0; par < (copy == 2 ? 2 : 1); ++par) {  // (saturated: both parities' slots)
-        uint64_t* dst = const_cast<uint64_t*>(xg_ll(peer_data[q], d.cap, s + par)) + i;
+        // (unsigned: copy == 2 sets s = INT_MAX, and s + par must wrap to parity 0 without signed overflow)
+        uint64_t* dst = const_cast<uint64_t*>(xg_ll(peer_data[q], d.cap, (int)((unsigned)s + (unsigned)par))) + i;
         __hip_atomic_store(dst, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }

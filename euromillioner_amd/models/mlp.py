@@ -202,19 +202,20 @@ class FusedSmallMLP:
 
     @property
     def graph_safe(self) -> bool:
-        """True when a step can be replayed from a hipGraph: single GPU, xGMI, or the RCCL path
-        (an RCCL all-reduce is a stream-ordered kernel, captured like any other: the step has no
-        host sync, so the fallback does not pay ~4 Python launches per 90 us step).  gloo
-        collectives run on the host and are never captured.  The captured RCCL step is the default
-        (tests/test_train_gpu.py checks graph replay == eager on an RCCL group); ``EUROM_RCCL_GRAPH=0``
-        opts out."""
+        """True when a step can be replayed from a hipGraph: single GPU, xGMI, or -- opt-in with
+        ``EUROM_RCCL_GRAPH=1`` -- the RCCL path (an RCCL all-reduce is a stream-ordered kernel and
+        captures like any other, so the fallback would not pay ~4 Python launches per 90 us step).
+        The captured RCCL step is checked only on a 1-rank NCCL group (tests/test_train_gpu.py: replay
+        == eager): RCCL refuses two ranks on one GPU, so no world >= 2 capture has run on this pool's
+        1-GPU boxes, and the fallback steps eagerly until a multi-GPU node has confirmed it.  gloo
+        collectives run on the host and are never captured."""
         if self.group is None or self.xgmi is not None:
             return True
         import os
 
         import torch.distributed as dist
 
-        return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "1") != "0"
+        return dist.get_backend(self.group) == "nccl" and os.environ.get("EUROM_RCCL_GRAPH", "0") == "1"
 
     def check_comm(self) -> None:
         """Raise if an xGMI peer wait timed out (synchronises)."""

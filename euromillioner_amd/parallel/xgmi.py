@@ -181,7 +181,12 @@ class XgmiComm:
         return int(e.value)
 
     def check(self) -> None:
-        """Raise if any in-kernel wait on a peer timed out (synchronises with the device)."""
+        """Raise if any in-kernel wait on a peer timed out (synchronises with the device).
+        ``EUROM_XGMI_FAULT_RANK=r`` (tests only) makes rank r report such a timeout, to drive the
+        callers' fallbacks (bench.py rebuilds every rank on the RCCL step)."""
+        fault = os.environ.get("EUROM_XGMI_FAULT_RANK")
+        if fault is not None and fault.strip() != "" and int(fault) == self.rank:
+            raise XgmiError(f"rank {self.rank}: injected xGMI peer-wait timeout (EUROM_XGMI_FAULT_RANK)")
         if self.error():
             raise XgmiError(f"rank {self.rank}: xGMI all-reduce timed out waiting for a peer "
                             f"(EUROM_XGMI_TIMEOUT={DEFAULT_TIMEOUT_S:g}s)")

@@ -373,10 +373,16 @@ def _mlp_sizes(cfg: RunConfig) -> tuple:
     return (62 * cfg.data.lags,) + hidden + (62,)
 
 
+def _fused_shape(cfg: RunConfig, sizes) -> bool:
+    """The configurations the fused train kernel covers (62 -> 128 -> 62 relu, no parameter averaging);
+    every other stack, lag window or averaging run takes the GEMM engine."""
+    return tuple(sizes) == (62, 128, 62) and cfg.mlp.activation == "relu" and not cfg.dist.avg_frequency
+
+
 def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
     if info.device.type != "cuda":
         return "torch"  # CPU plumbing path
-    if sizes == (62, 128, 62) and cfg.mlp.activation == "relu" and not cfg.dist.avg_frequency:
+    if _fused_shape(cfg, sizes):
         return "fused"  # the fused train kernel: bf16 (mlp_fused.hip) or exact fp32 (mlp_fused_f32.hip)
     return "gemm"  # any other stack, lag windows, parameter averaging
 
@@ -384,7 +390,7 @@ def _pick_engine(cfg: RunConfig, info: D.DistInfo, sizes) -> str:
 def train_mlp(cfg: RunConfig) -> dict:
     log = L.get("Trainer")
     # RCCL at high stream priority only for the GEMM engine's bucketed all-reduces (parallel/dist.py)
-    gemm_like = _mlp_sizes(cfg) != (62 * cfg.data.lags, 128, 62) or bool(cfg.dist.avg_frequency)
+    gemm_like = not _fused_shape(cfg, _mlp_sizes(cfg))  # the same predicate as _pick_engine
     info = D.init(cfg.dist.backend, cfg.dist.timeout_s, device=cfg.device, high_priority=gemm_like)
     try:
         return _train_mlp(cfg, info, log)

@@ -87,3 +87,25 @@ def test_wide_dp_panels_bf16_wire(world, backend):
     r0 = res[0]
     assert r0["max_diff"] <= 2 * r0["lr"] * r0["steps"] + 1e-6, r0
     assert r0["mean_diff"] <= 0.05 * r0["lr"], r0
+
+
+def test_bench_xgmi_fault_falls_back_to_rccl():
+    """bench.py's fallback: when the fused xGMI exchange passes its self-test but a rank then
+    reports a timed-out peer wait, every rank rebuilds on the RCCL step.  Rank 1's wait is faulted by the
+    test hook (EUROM_XGMI_FAULT_RANK=1); 2 ranks share the GPU over gloo.  The JSON must name the
+    fallback, the step must run on the RCCL path, and the ranks must end bit-identical."""
+    env = dict(os.environ, EUROM_XGMI_FAULT_RANK="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="2",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+                        "--no-eval", "--dist-backend", "gloo", "--batch", "65536", "--draws-per-gpu", str(1 << 20),
+                        "--warmup-ms", "0", "--launch-timeout", "150"],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=170)
+    assert p.returncode == 0, p.stdout[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, p.stdout[-3000:]
+    d = json.loads(lines[-1])
+    cfg = d["config"]
+    assert cfg["comm_fallback"] == "xgmi step error -> rccl", cfg
+    assert cfg["grad_allreduce"] == "rccl", cfg
+    assert cfg["params_identical_across_ranks"] is True, cfg
+    assert d["value"] > 0 and d["n_gpus"] == 2

@@ -94,11 +94,12 @@ def test_dp_code_path_on_one_rank_matches_local(engine):
 
 def test_rccl_step_replays_from_a_hipgraph(monkeypatch):
     """The fused model's RCCL fallback (slab reduce -> RCCL all-reduce -> Adam) replays from a hipGraph
-    by default (EUROM_RCCL_GRAPH=0 opts out): steps captured in one hipGraph and
-    replayed equal the same steps run eagerly, on the RCCL model and on a local model."""
+    when opted in (EUROM_RCCL_GRAPH=1; eager by default until a multi-GPU node confirms capture at
+    world >= 2): steps captured in one hipGraph and replayed equal the same steps run eagerly, on the
+    RCCL model and on a local model."""
     import torch
 
-    monkeypatch.delenv("EUROM_RCCL_GRAPH", raising=False)
+    monkeypatch.setenv("EUROM_RCCL_GRAPH", "1")
 
     from euromillioner_amd.data.draws import DrawSet
     from euromillioner_amd.models.mlp import FusedSmallMLP
@@ -109,9 +110,9 @@ def test_rccl_step_replays_from_a_hipgraph(monkeypatch):
     try:
         dp = FusedSmallMLP("cuda", seed=1, lr=3e-3, process_group=dist.group.WORLD, comm="rccl")
         assert dp.comm == "rccl" and dp.graph_safe
-        monkeypatch.setenv("EUROM_RCCL_GRAPH", "0")
-        assert not dp.graph_safe
         monkeypatch.delenv("EUROM_RCCL_GRAPH")
+        assert not dp.graph_safe  # the default: eager RCCL steps
+        monkeypatch.setenv("EUROM_RCCL_GRAPH", "1")
         eager = FusedSmallMLP("cuda", seed=1, lr=3e-3, process_group=dist.group.WORLD, comm="rccl")
         for k in (0, 1, 2, 1, 2):  # the same RCCL step, eager, for the graph's equality check below
             eager.step(masks, 2048, offset=1000 * k)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU measurements as named stages (run through gpurun; every GPU step has its own time
+# GPU measurements as named stages (run through gpurun; every GPU step has its own time
 # limit and a failing step ends the script).  Outputs under gpurun_out/round/<stage>/.
 #   bash tools/gpu_round.sh full            GPU suite + smoke() + driver-shape and default bench
 #   bash tools/gpu_round.sh headline-prof   kernel trace + 2 PMC passes of the headline step, phase
@@ -13,6 +13,15 @@
 #                                           forest.hip: SRC=... build_variant.sh rf_head), kernel stats
 #   bash tools/gpu_round.sh dp-proxy        one-GPU DP=8 small-MLP exchange proxy (tools/xgmi_budget.py)
 #   bash tools/gpu_round.sh hbm-fill        HBM-filling 256M-sample runs on p = 0.9 and p = 0.7
+#   bash tools/gpu_round.sh v8              K7 v8 (EUROM_FUSED_V=8): fused GPU tests, v6/v8 A/B, phase timeline
+#   bash tools/gpu_round.sh pmc-ab          two PMC passes of the train kernel per arm of PMC_ARMS
+#   bash tools/gpu_round.sh tests           pytest -m gpu over TESTS (default: the whole suite)
+#   bash tools/gpu_round.sh ab              tools/gpu_ab.sh with ARMS / ROUNDS / BENCH_ARGS
+#   bash tools/gpu_round.sh dp2             2-rank shared-GPU bench rehearsal + the 1-rank driver shape
+#   bash tools/gpu_round.sh gbdt-host       host-side profile of the GBDT reference fit
+#   bash tools/gpu_round.sh k7-trace        per-tile event trace of the v8 train kernel
+# (round 6 folded the one-off tools/gpu_gNN.sh batch scripts of rounds 3-5 into these stages; git history
+# keeps them)
 # Several stages run in order: bash tools/gpu_round.sh gbdt fp32
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -114,6 +123,35 @@ for stage in "$@"; do
       timeout -k 10 300 python bench.py --device-data-gb -1 --batch 268435456 --steps 10 --warmup 2 --planted $pl > $O/fill_$pl.json 2> $O/fill_$pl.err || { tail $O/fill_$pl.err; exit 29; }
       summ $O/fill_$pl.json fill_$pl || exit 30
     done
+    ;;
+  tests)
+    # named GPU test files / node ids: TESTS="tests/test_gbdt.py tests/test_forest.py::test_x" (default: the suite)
+    timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 41; }
+    tail -1 $O/pytest.log
+    ;;
+  ab)
+    # same-box interleaved bench A/B: ARMS="name|ENV=..;name2|EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/x.so"
+    # (side libraries from tools/build_variant.sh), ROUNDS, BENCH_ARGS as in tools/gpu_ab.sh
+    bash tools/gpu_ab.sh || exit 42
+    cp gpurun_out/ab/results.jsonl $O/results.jsonl
+    ;;
+  dp2)
+    # 2-rank bench.py rehearsal of the DP path with both ranks on the one GPU (gloo control plane; the fused
+    # xGMI exchange carries the gradients), then the 1-rank driver shape
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo > $O/bench_dp2.json 2> $O/bench_dp2.err || { grep -v amdgpu.ids $O/bench_dp2.err | tail -20; exit 43; }
+    grep '^{' $O/bench_dp2.json | cut -c1-600
+    timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_dp1.json 2> $O/bench_dp1.err || { tail $O/bench_dp1.err; exit 44; }
+    summ $O/bench_dp1.json dp1 || exit 45
+    ;;
+  gbdt-host)
+    # host-side profile of the GBDT reference fit (tools/gbdt_fit_profile.py)
+    timeout -k 10 300 python tools/gbdt_fit_profile.py > $O/gbdt_fit_profile.txt 2>&1 || { tail -20 $O/gbdt_fit_profile.txt; exit 46; }
+    head -60 $O/gbdt_fit_profile.txt
+    ;;
+  k7-trace)
+    # per-tile event trace of the v8 train kernel (needs lib/ab/trace.so: build_variant.sh trace -DFUSED_TRACE=1)
+    EUROM_FUSED_V=8 EUROM_NATIVE_LIB=$PWD/euromillioner_amd/lib/ab/trace.so timeout -k 10 120 python tools/fused_trace.py > $O/trace.txt 2>&1 || { tail $O/trace.txt; exit 47; }
+    tail -9 $O/trace.txt
     ;;
   *) echo "unknown stage $stage"; exit 2;;
   esac
