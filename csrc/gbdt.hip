@@ -249,6 +249,34 @@ struct HistSplit {
   const int4* cellinfo = nullptr;
 };
 
+// The previous level's split run by the leading blocks of a histogram pass (levels >= 2 of the exact fused
+// round): z-planes 0 .. nz - 1 are split blocks (node zb * gridDim.x + x of task y), the
+// remaining planes the histogram.  Split blocks come first in dispatch order; each runs gbdt_split's body
+// (its stores are write-through), drains them and adds 1 to its task's counter.  A histogram block of task
+// t polls that counter (one lane, agent-scope loads, bounded) until the task's nodes are all decided, then
+// reads the split arrays with agent-scope loads -- the "write-through stores + vmcnt(0) + relaxed arrival"
+// hand-off of HistSplit.  A task's next level starts when its own splits finish instead of at a launch
+// boundary; no block waits on another task.  The levels' chunk partials alternate between two buffer halves,
+// so this level's histogram never overwrites what the split blocks still read.  Counters are cumulative
+// over the fit (want = the running total); a timed-out poll raises err[0] (em_gbdt_fused_error).
+struct HistPre {
+  int on = 0, nz = 0, nodes = 0, level = 0, nchunks = 0, oneshot = 0, pscan = 0, NN = 0;
+  int want = 0;
+  int* ctr = nullptr;  // [T] cumulative arrivals
+  int* err = nullptr;  // set when a poll timed out (em_gbdt_fused_error)
+  const double* hist = nullptr;
+  int64_t cstride = 0;
+  double* G = nullptr;
+  double* H = nullptr;
+  int8_t* st = nullptr;
+  int16_t* fe = nullptr;
+  uint8_t* sb = nullptr;
+  float* gn = nullptr;
+  double lam = 0.0, mcw = 0.0;
+  const int4* cellinfo = nullptr;
+};
+constexpr int64_t PRE_SPIN_LIMIT = 1ll << 24;  // ~1 s of polling at s_sleep 1: a legitimate wait is microseconds
+
 // ---------------------------------------------------------------- K8 histogram (compact cells)
 // Cells: feature f owns bins [foff[f], foff[f+1]) of a compact axis of C = foff[F] cells (a one-hot
 // lag feature has 2 cells, "day" 31 ...), so a (task, node) histogram of the reference features is
@@ -290,10 +318,10 @@ constexpr int HIST_EXACT_THREADS = GBDT_HIST_THREADS;
 #ifndef GBDT_HSPLIT_NPRE
 #define GBDT_HSPLIT_NPRE 4
 #endif
-// gbdt_hist's dynamic LDS ceiling: 160 KB less 1 KB for its static LDS (block_sum_waves); setting the
-// attribute to the full 160 KB fails once the kernel has any static LDS (and leaves hipErrorInvalidValue
-// as the last error, which the next launch check reports)
-constexpr int GBDT_HIST_MAX_DYN = 159 * 1024;
+// gbdt_hist's dynamic LDS ceiling: 160 KB less 2 KB for its static LDS (block_sum_waves, two split_body
+// instantiations: 1200 B); setting the attribute to the full 160 KB fails once the kernel has any static
+// LDS (and leaves hipErrorInvalidValue as the last error, which the next launch check reports)
+constexpr int GBDT_HIST_MAX_DYN = 158 * 1024;
 constexpr int HIST_QBIN_LDS = 16 * 1024;         // fixed point: staged bin bytes per piece
 // rows per histogram chunk at least HIST_MIN_CHUNK (compile-time A/B knob for side builds,
 // tools/build_variant.sh -DHIST_MIN_CHUNK=...; the split folds one partial per chunk).  Round 5 on the
@@ -310,7 +338,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
           const int16_t* __restrict__ node, const int* __restrict__ foff, double* __restrict__ partial, int T, int n,
           int F, int C, int level, int chunk, int FT, int NTn, int P, int ldsC, int piece, int stage_rows,
           int16_t* __restrict__ node_out, const int8_t* __restrict__ pst, const int16_t* __restrict__ pfe,
-          const uint8_t* __restrict__ psb, int NN, HistUpdate hu, HistSplit hsp) {
+          const uint8_t* __restrict__ psb, int NN, HistUpdate hu, HistSplit hsp, HistPre pre) {
   // stage_rows > 0: each piece's bin rows are staged in LDS with 16-B loads (one round trip instead of
   // one per 8 rows of byte loads); the host sets it when a piece's rows fit (stage_rows * F <= 16 KB).
   // node_out != nullptr (level >= 1): the rows' nodes are the previous level's partition, applied here
@@ -320,10 +348,41 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   const int nodesL = 1 << level, first = nodesL - 1;
   GSTAMP(64 + 16 * level);
   const int c = blockIdx.x, t = blockIdx.y;
-  if (hu.apply && (int)blockIdx.z >= hu.nz) {  // eval set es: round - 1's tree of task t on a chunk of its rows
+  if (pre.on && (int)blockIdx.z < pre.nz) {  // a split block of the previous level (see HistPre)
+    const int nd = (int)blockIdx.z * (int)gridDim.x + c;
+    if (nd < pre.nodes) {
+      split_body<double, false, GBDT_HSPLIT_NPRE>(t * pre.nodes + nd, smem, pre.hist, pre.nchunks, pre.cstride, foff, T,
+                                                  F, C, pre.level, pre.NN, pre.G, pre.H, pre.st, pre.fe, pre.sb,
+                                                  pre.gn, pre.lam, pre.mcw, 0.0, SplitFinal(), pre.oneshot, pre.pscan,
+                                                  pre.cellinfo);
+      if (threadIdx.x == 0) {  // (thread 0 made every store of the split, all write-through)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(pre.ctr + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
+  const int zb = (int)blockIdx.z - (pre.on ? pre.nz : 0);  // this block's plane of the histogram pass
+  if (pre.on) {  // the task's previous-level nodes must all be decided before their partition is applied
+    __shared__ int pre_ok;
+    if (threadIdx.x == 0) {
+      int64_t spins = 0;
+      while (__hip_atomic_load(pre.ctr + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pre.want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > PRE_SPIN_LIMIT) {
+          __hip_atomic_fetch_or(pre.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      pre_ok = 1;
+    }
+    __syncthreads();
+    (void)pre_ok;
+  }
+  if (hu.apply && zb >= hu.nz) {  // eval set es: round - 1's tree of task t on a chunk of its rows
     // (the set's fields picked with selects: a dynamic index into the by-value argument arrays would
     // copy them to scratch memory for every block of the launch)
-    const int es = (int)blockIdx.z - hu.nz;
+    const int es = zb - hu.nz;
     auto pick = [es](auto a0, auto a1, auto a2, auto a3) { return es == 0 ? a0 : es == 1 ? a1 : es == 2 ? a2 : a3; };
     const uint8_t* ebins = pick(hu.evs.bins[0], hu.evs.bins[1], hu.evs.bins[2], hu.evs.bins[3]);
     float* emargin = pick(hu.evs.margin[0], hu.evs.margin[1], hu.evs.margin[2], hu.evs.margin[3]);
@@ -347,7 +406,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   }
   double macc = 0.0;  // (hu.apply) round - 1's metric terms of this thread's rows
   const int nft = (F + FT - 1) / FT;
-  const int ft = blockIdx.z % nft, nt = blockIdx.z / nft;
+  const int ft = zb % nft, nt = zb / nft;
   const int f0 = ft * FT, f1 = min(F, f0 + FT), n0 = nt * NTn;
   const int c0 = foff[f0], c1 = foff[f1], Ct = c1 - c0;
   double* hist = reinterpret_cast<double*>(smem);  // [P][NTn][ldsC][2]
@@ -362,8 +421,16 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   u32x4* sbw = reinterpret_cast<u32x4*>(reinterpret_cast<char*>(ptree) + (((size_t)npn * 4 + 15) & ~(size_t)15));
   if (npn) {
     const int64_t k0 = (int64_t)t * NN + pf;
-    for (int i = threadIdx.x; i < npn; i += blockDim.x)
-      ptree[i] = (int32_t)(uint8_t)pst[k0 + i] | ((int32_t)psb[k0 + i] << 8) | ((int32_t)pfe[k0 + i] << 16);
+    for (int i = threadIdx.x; i < npn; i += blockDim.x) {
+      if (pre.on) {  // written in this launch by the split blocks (write-through): agent-scope loads
+        const int8_t a = __hip_atomic_load(pst + k0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint8_t b = __hip_atomic_load(psb + k0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int16_t e = __hip_atomic_load(pfe + k0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ptree[i] = (int32_t)(uint8_t)a | ((int32_t)b << 8) | ((int32_t)e << 16);
+      } else {
+        ptree[i] = (int32_t)(uint8_t)pst[k0 + i] | ((int32_t)psb[k0 + i] << 8) | ((int32_t)pfe[k0 + i] << 16);
+      }
+    }
   }
   const int64_t base = (int64_t)t * n;
   const int nth = f1 - f0;
@@ -439,7 +506,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
           const int32_t e = ptree[nd - pf];
           if ((e & 0xFF) == 1) nd = 2 * nd + 1 + ((int)rowb[(int64_t)(r - r0) * F + (e >> 16)] > ((e >> 8) & 0xFF) ? 1 : 0);
         }
-        if (blockIdx.z == 0) node_out[base + r] = (int16_t)nd;
+        if (zb == 0) node_out[base + r] = (int16_t)nd;
         sn[r - r0] = (int16_t)(nd - first - n0);
       }
       __syncthreads();
@@ -827,6 +894,7 @@ __global__ void gbdt_chunk_reduce(A* __restrict__ partial, int nchunks, int64_t 
 constexpr int SPLIT_FINAL_MAX_DEPTH = 8;
 constexpr int SPLIT_DIRECT_MAX_BINS = 32;  // direct candidate form up to this many bins per feature
 constexpr int EM_GBDT_SEPARATE = 1;  // em_gbdt_fit launch_flags: the separate launches instead of the fused round
+constexpr int EM_GBDT_PRESPLIT = 2;  // em_gbdt_fit launch_flags: splits inside the next level's histogram pass
 constexpr int SPLIT_ONESHOT_LDS = 48 * 1024;  // chunk partials staged at once up to this many bytes (+ the
                                               // finalize's <= 12 KB: within the default 64 KB)  // the fused finalize stages NN <= 511 nodes (23 B each) in LDS
 
@@ -1613,7 +1681,7 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
                       int n, int F, const int* foff_h, const int* foff_d, double* partial, int64_t partial_doubles,
                       bool fold, double qscale, int* nchunks_out, hipStream_t stream, const QuantAux* qa = nullptr,
                       const HistPartition& hp = HistPartition(), const HistUpdate* hu = nullptr,
-                      const HistSplit* hsp = nullptr, size_t min_lds = 0) {
+                      const HistSplit* hsp = nullptr, size_t min_lds = 0, const HistPre* pre = nullptr) {
   const bool quant = qscale != 0.0;
   const int C = foff_h[F];
   const int nodesL = 1 << level;
@@ -1642,7 +1710,10 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
     nchunks = pl.nchunks;
     // (hu: level 0 with one tile per (chunk, task); eval sets on extra z planes)
     if (hu && (quant || level != 0 || pl.nft * pl.ntn != 1)) return EM_ERR_ARG;
-    const dim3 grid(pl.nchunks, T, pl.nft * pl.ntn + (hu && hu->apply ? hu->evs.count : 0));
+    if (pre && (quant || hu || hsp)) return EM_ERR_ARG;
+    HistPre pr = pre ? *pre : HistPre();
+    if (pre) pr.nz = (pr.nodes + pl.nchunks - 1) / pl.nchunks;  // split planes in front of the histogram's
+    const dim3 grid(pl.nchunks, T, pr.nz + pl.nft * pl.ntn + (hu && hu->apply ? hu->evs.count : 0));
     if (quant)
       hipLaunchKernelGGL(gbdt_hist_q, grid, dim3(pl.threads), pl.lds, stream, bins, g, h, node, foff_d,
                          (const int*)nullptr, foff_d, qpart, T, n, F, F, C, level, pl.chunk, pl.FT, pl.NTn, pl.P,
@@ -1665,7 +1736,7 @@ int launch_level_hist(int level, const uint8_t* bins, const float* g, const floa
       }
       hipLaunchKernelGGL(gbdt_hist, grid, dim3(pl.threads), lds, stream, bins, g, h, node, foff_d, partial, T, n, F,
                          C, level, pl.chunk, pl.FT, pl.NTn, pl.P, pl.ldsC, pl.piece, stage, hp.node_out, hp.st, hp.fe,
-                         hp.sb, hp.NN, hu ? *hu : HistUpdate(), hsp ? *hsp : HistSplit());
+                         hp.sb, hp.NN, hu ? *hu : HistUpdate(), hsp ? *hsp : HistSplit(), pr);
     }
   }
   const bool split_folds = !fold && nchunks <= SPLIT_FOLD_MAX_CHUNKS && (int64_t)C * 16 <= SPLIT_FOLD_MAX_LDS;
@@ -1725,6 +1796,22 @@ int* metric_counter() {
   }
   return ctr;
 }
+// one zeroed device int per process (per device in use): raised by a histogram block whose HistPre poll timed
+// out (the fit's trees are then invalid); read and cleared by em_gbdt_fused_error
+int* fused_error_word() {
+  static int* w = nullptr;
+  static int dev = -1;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  if (!w || dev != d) {
+    int* p = nullptr;
+    if (hipMalloc(&p, 64) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    w = p;
+    dev = d;
+  }
+  return w;
+}
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
@@ -1744,7 +1831,8 @@ EM_API int64_t em_gbdt_partial_doubles(int n, int T, int F, const int* foff, int
     if (v < 0) return -1;
     need = v > need ? v : need;
   }
-  return need;
+  // two halves (consecutive levels' partials, em_gbdt_fit's HistPre levels) while that stays small
+  return need <= (int64_t(1) << 24) ? 2 * need : need;
 }
 
 // Trains rounds [r0, r1).  Tree arrays hold ALL rounds: [R*T][NN] (tree k = round*T + task).
@@ -1873,6 +1961,33 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
                                  stream) != hipSuccess)
     return EM_ERR_ARG;
   FreeAsync mfree{mround, stream};
+  // EM_GBDT_PRESPLIT=1: levels >= 1 of the exact fused round run level L's split in the leading blocks of
+  // level L + 1's histogram pass (HistPre) when the partial buffer holds two levels' partials (double-
+  // buffered halves).  Bit-identical trees; measured equal on the reference fit (849-855 k vs 844-853 k
+  // trees/s, 3 interleaved rounds, profiles/r6/gbdt_presplit_ab.txt): the launch boundary it removes is
+  // paid back as the in-launch hand-off, so the split launches stay the default
+  int64_t pneed = 0;
+  for (int l = 0; l < max_depth; ++l) {
+    const int64_t v = partial_need(l, n, T, F, foff_h);
+    pneed = v > pneed ? v : pneed;
+  }
+  static const bool presplit_env = [] {
+    const char* e = std::getenv("EM_GBDT_PRESPLIT");
+    return e && e[0] == '1';
+  }();
+  const bool presplit = (presplit_env || (launch_flags & EM_GBDT_PRESPLIT)) && fuse && max_depth >= 3 && pneed > 0 &&
+                        partial_doubles >= 2 * pneed;
+  const int64_t half = presplit ? (partial_doubles / 2) & ~(int64_t)1 : partial_doubles;
+  int* sctr = nullptr;  // [T] cumulative split arrivals of this fit
+  if (presplit) {
+    if (hipMallocAsync(reinterpret_cast<void**>(&sctr), (size_t)T * sizeof(int), stream) != hipSuccess ||
+        hipMemsetAsync(sctr, 0, (size_t)T * sizeof(int), stream) != hipSuccess)
+      return EM_ERR_ARG;
+  }
+  FreeAsync sfree{sctr, stream};
+  int* perr = presplit ? fused_error_word() : nullptr;
+  if (presplit && !perr) return EM_ERR_ARG;
+  int pre_cum = 0;  // arrivals per task so far
   // one round's kernel sequence (the arrays of `round` addressed from the host)
   auto enqueue_round = [&](int round, hipStream_t s) -> int {
     const int64_t ro = (int64_t)round * T * NN;
@@ -1884,6 +1999,8 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     float* cv = cover + ro;
     const bool next_in_update = fuse && obj != OBJ_SOFTMAX && !hist_update;  // round + 1 started by this update
     int16_t* nb[2] = {node, fuse ? node2 : node};
+    HistPre pending;  // the previous level's split, deferred into this level's histogram pass
+    size_t pending_lds = 0;
     if (!hist_update && (!next_in_update || round == r0))
       hipLaunchKernelGGL(gbdt_round_start, dim3(grid_for(TN > (int64_t)T * NN ? TN : (int64_t)T * NN)), dim3(256), 0,
                          s, st, fe, sb, gn, T * NN, NN, margin, Y, g, h, node, T, n, obj, subsample, seed, round);
@@ -1970,9 +2087,18 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         }
         hsp_lds = sl;
       }
-      const int rc = launch_level_hist(level, bins, g, h, nin, T, n, F, foff_h, foff_d, partial, partial_doubles,
+      double* lpart = presplit ? partial + (level & 1) * half : partial;  // this level's partials
+      HistPre* prep = nullptr;
+      if (pending.on) {
+        pre_cum += pending.nodes;
+        pending.want = pre_cum;
+        prep = &pending;
+      }
+      const int rc = launch_level_hist(level, bins, g, h, nin, T, n, F, foff_h, foff_d, lpart, half,
                                        false, qscale, &nch, s, qa.nb ? &qa : nullptr, hp,
-                                       hist_update && level == 0 ? &hu : nullptr, fsplit ? &hsp : nullptr, hsp_lds);
+                                       hist_update && level == 0 ? &hu : nullptr, fsplit ? &hsp : nullptr,
+                                       prep ? pending_lds : hsp_lds, prep);
+      pending = HistPre();
       if (rc) return rc;
       if (fsplit) continue;  // (split done by the pass itself)
       const int sth = (F >= 256 || nch > 1) ? 256 : ((F + 63) / 64) * 64;
@@ -1992,12 +2118,36 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
         fin.max_depth = max_depth;
         slds += (size_t)NN * 24;
       }
+      if (presplit && level >= 1 && level + 1 < max_depth) {  // runs in the next level's histogram pass
+        pending.on = 1;
+        pending.nodes = nodesL;
+        pending.level = level;
+        pending.nchunks = nch;
+        pending.oneshot = oneshot;
+        pending.pscan = pscan;
+        pending.NN = NN;
+        pending.ctr = sctr;
+        pending.err = perr;
+        pending.hist = lpart;
+        pending.cstride = cstride;
+        pending.G = Gs;
+        pending.H = Hs;
+        pending.st = st;
+        pending.fe = fe;
+        pending.sb = sb;
+        pending.gn = gn;
+        pending.lam = (double)lam;
+        pending.mcw = (double)mcw;
+        pending.cellinfo = cellinfo_d;
+        pending_lds = slds;
+        continue;
+      }
       if (quant_bits)
         hipLaunchKernelGGL(gbdt_split<long long>, dim3(T * nodesL), dim3(sth), slds, s,
-                           reinterpret_cast<const long long*>(partial), nch, cstride, foff_d, T, F, C, level, NN, Gs,
+                           reinterpret_cast<const long long*>(lpart), nch, cstride, foff_d, T, F, C, level, NN, Gs,
                            Hs, st, fe, sb, gn, (double)lam, (double)mcw, qinv, fin, oneshot, pscan, cellinfo_d);
       else
-        hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, s, partial, nch, cstride,
+        hipLaunchKernelGGL(gbdt_split<double>, dim3(T * nodesL), dim3(sth), slds, s, lpart, nch, cstride,
                            foff_d, T, F, C, level, NN, Gs, Hs, st, fe, sb, gn, (double)lam, (double)mcw, 0.0, fin,
                            oneshot, pscan, cellinfo_d);
       if (!fuse)
@@ -2102,6 +2252,18 @@ EM_API int em_gbdt_fit(const uint8_t* bins, const float* Y, int n, int F, const 
     EM_CHECK_LAUNCH();
   }
   return 0;
+}
+
+// 1 if a fused-level poll timed out since the last call (the trees of that fit are invalid), else 0;
+// synchronises the device and clears the word
+EM_API int em_gbdt_fused_error() {
+  int* w = fused_error_word();
+  if (!w) return -1;
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (v) (void)hipMemset(w, 0, sizeof(int));
+  return v;
 }
 
 // GBDT_STAMPS builds: the 256 phase stamps (100 MHz ticks) and the matching 256 shader-clock counts

@@ -230,7 +230,10 @@ constexpr int V6_SLOT = 16384;
 constexpr int V6_NSTREAM = FUSED_SHARED ? 1 : 2;  // tile streams (rings) per workgroup
 constexpr int V6_NF = FUSED_SHARED ? 4 : 2;       // forward waves per stream
 constexpr int V6_NBP = FUSED_SHARED ? 2 : 1;      // backward waves per hidden half (tile parities)
-constexpr int V6_RSLOTS = FUSED_SHARED ? 6 : 3;   // slots per stream in the ring area
+#ifndef V6_RSLOTS_SHARED
+#define V6_RSLOTS_SHARED 6
+#endif
+constexpr int V6_RSLOTS = FUSED_SHARED ? V6_RSLOTS_SHARED : 3;  // slots per stream in the ring area
 // + the recycled weight-image slots (the W1ᵀ / W2ᵀ images are dead once the forward waves hold their
 // weights in registers)
 constexpr int V6_NREC = FUSED_RECYCLE ? 2 / V6_NSTREAM : 0;

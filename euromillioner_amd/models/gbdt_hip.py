@@ -25,6 +25,7 @@ N.register_signatures({
     "em_gbdt_fit": (_i, [_v, _v, _i, _i, _v, _v, _i, _v, ctypes.POINTER(_Eval), _i, _i, _i, _i, _i, _i, _f, _f, _f,
                          _f, _f, _u32, _v, _v, _v, _v, _v, _i64, _v, _v, _v, _v, _v, _v, _v, _v, _v, _v, _i, _i, _v]),
     "em_gbdt_partial_doubles": (_i64, [_i, _i, _i, _v, _i]),
+    "em_gbdt_fused_error": (_i, []),
     "em_gbdt_init_margin": (_i, [_v, _i64, _f, _v]),
     "em_gbdt_predict": (_i, [_v, _v, _i, _i, _i, _i, _i, _i, _v, _v, _v, _v, _v]),
     "em_gbdt_dp_round_begin": (_i, [_i, _i, _i, _i, _v, _v, _v, _v, _v, _i, _f, _u32, _v, _v, _v, _v, _v]),
@@ -121,8 +122,10 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 500, dp=None):
                node.data_ptr(), node2.data_ptr(), partial.data_ptr(), partial.numel(), Gs.data_ptr(), Hs.data_ptr(), mpart.data_ptr(),
                status.data_ptr(), feat.data_ptr(), sbin.data_ptr(), leaf.data_ptr(), gain.data_ptr(),
                cover.data_ptr(), hist.data_ptr(), qbits,
-               # separate launches instead of the fused round (bit-identity tests; csrc/gbdt.hip)
-               1 if getattr(model, "separate_launches", False) else 0, stream)
+               # separate launches instead of the fused round (bit-identity tests; csrc/gbdt.hip), and the
+               # opt-in fused levels (splits inside the next level's histogram pass, EM_GBDT_PRESPLIT)
+               (1 if getattr(model, "separate_launches", False) else 0)
+               | (2 if getattr(model, "presplit_levels", False) else 0), stream)
         hh = hist.view(R, 1 + len(ev_names))[r0:r1].cpu().numpy()
         for i, rnd in enumerate(range(r0, r1)):
             rec = {"round": rnd}
@@ -144,6 +147,10 @@ def fit(model, X, bins, nbins, Y, evals, rounds_per_call: int = 500, dp=None):
         arrs.append(host[o:o + nb].view(dt).reshape(R * T, NN))
         o += nb
     lf, gn, cv, fe, sb, st = arrs
+    # a histogram block that waited past its bound for its task's splits (the fused levels of em_gbdt_fit,
+    # csrc/gbdt.hip HistPre) leaves invalid trees: fail loudly instead of returning them
+    if N.query("em_gbdt_fused_error") != 0:
+        raise RuntimeError("GPU GBDT: a fused level's wait for its task's splits timed out (trees invalid)")
     trees = TreeArrays.from_arrays(D, st, fe, sb, lf, gn, cv)
     model._device_trees = (status, feat, sbin, leaf)
     return trees, history

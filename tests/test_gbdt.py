@@ -242,13 +242,15 @@ def test_hip_fused_round_bit_identical(obj):
               eval_metric="logloss" if obj == "reg:logistic" else "rmse", subsample=0.8, backend="hip")
     ev = {"test": (X[m:], Y[m:])}
     fits = {}
-    for name in ("fused", "separate"):
+    for name in ("fused", "separate", "presplit"):
         g = G.GBDT(**kw)
         g.separate_launches = name == "separate"
+        g.presplit_levels = name == "presplit"  # level L's split inside level L + 1's histogram pass
         fits[name] = g.fit(X[:m], Y[:m], evals=ev)
     a, b = fits["fused"], fits["separate"]
     for k in ("status", "feat", "sbin", "leaf", "gain", "cover"):
         assert np.array_equal(getattr(a.trees, k), getattr(b.trees, k)), k
+        assert np.array_equal(getattr(fits["presplit"].trees, k), getattr(b.trees, k)), k
     # (the fused rounds sum the per-round metric terms grouped by histogram chunk, the separate launches by
     # update block: the same terms, summed in another order)
     assert len(a.history) == len(b.history)
