@@ -364,8 +364,7 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
   }
   const int zb = (int)blockIdx.z - (pre.on ? pre.nz : 0);  // this block's plane of the histogram pass
   if (pre.on) {  // the task's previous-level nodes must all be decided before their partition is applied
-    __shared__ int pre_ok;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // (the other threads load the split arrays after the barrier below)
       int64_t spins = 0;
       while (__hip_atomic_load(pre.ctr + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pre.want) {
         __builtin_amdgcn_s_sleep(1);
@@ -374,10 +373,8 @@ gbdt_hist(const uint8_t* __restrict__ bins, const float* __restrict__ g, const f
           break;
         }
       }
-      pre_ok = 1;
     }
     __syncthreads();
-    (void)pre_ok;
   }
   if (hu.apply && zb >= hu.nz) {  // eval set es: round - 1's tree of task t on a chunk of its rows
     // (the set's fields picked with selects: a dynamic index into the by-value argument arrays would
