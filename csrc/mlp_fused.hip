@@ -615,26 +615,35 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
 #define FUSED_TRACE 0
 #endif
 constexpr int V8_NF = 8, V8_NB = 4, V8_THREADS = 64 * (V8_NF + V8_NB);
-constexpr int V8_NSLOT = 6;
-constexpr int V8_SLOT = V6_SLOT + 256;   // + the tile's per-lane loss terms (64 floats)
-constexpr int V8_SLOSS = V6_SLOT;
+// Slot layouts.  v8: H 8K | D2 4K | X 4K | loss terms 256 B, 6 slots.  v9 (VER = 9): the forward waves also
+// run B1 and the relu mask, and hand the backward waves dZ1 as an 8 KB image (after X), 4 slots.
+template <int VER>
+struct V8L {
+  static constexpr int NSLOT = VER == 9 ? 4 : 6;
+  static constexpr int SD1 = V6_SLOT;                          // v9: dZ1 image [32 samples][128 hidden]
+  static constexpr int SLOSS = VER == 9 ? V6_SLOT + 8192 : V6_SLOT;  // the tile's per-lane loss terms
+  static constexpr int SLOT = SLOSS + 256;
+};
 constexpr int V8_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V8_YLUT = V8_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
 constexpr int V8_FLAGS = V8_YLUT + 256;  // FULL[8] | DONE[8] (ints)
 constexpr int V8_DONE = V8_FLAGS + 32;
 constexpr int V8_CLAIM = V8_FLAGS + 64;
 constexpr int V8_RING = V8_FLAGS + 128;
-constexpr int V8_LDS = V8_RING + V8_NSLOT * V8_SLOT;
+template <int VER>
+constexpr int v8_lds() { return V8_RING + V8L<VER>::NSLOT * V8L<VER>::SLOT; }
 constexpr int V8_RED = 0, V8_DB2S = 65536, V8_LOSSS = V8_DB2S + 1024;  // epilogue (after the loop)
-static_assert(V8_LDS <= 163840 && V8_RING % 16 == 0 && V8_LOSSS + 64 <= V8_LDS, "v8 LDS budget");
-static_assert(V8_NSLOT <= 8, "flag words");
-EM_DEVICE uint32_t v8_slot(int slot) { return V8_RING + slot * V8_SLOT; }
+static_assert(v8_lds<8>() <= 163840 && v8_lds<9>() <= 163840 && V8_RING % 16 == 0, "v8 / v9 LDS budget");
+static_assert(V8_LOSSS + 64 <= v8_lds<9>() && V8_LOSSS + 64 <= v8_lds<8>(), "epilogue area");
+static_assert(V8L<8>::NSLOT <= 8, "flag words");
+template <int VER>
+EM_DEVICE uint32_t v8_slot(int slot) { return V8_RING + slot * V8L<VER>::SLOT; }
 EM_DEVICE void v8_trace(uint32_t* tr, int k, int word, int lane) {
   if (FUSED_TRACE && tr && blockIdx.x == 0 && lane == 0) tr[k * 12 + word] = (uint32_t)__builtin_amdgcn_s_memtime();
 }
 
 // forward wave f: tiles k = f, f + V8_NF, ... of the workgroup's stream
-template <int LOSS, bool SIDX>
+template <int LOSS, bool SIDX, int VER>
 EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                           int offset, int f, int lane, float& loss_acc, bool& ok, Stamps& st, uint32_t* tr) {
   const int r = lane & 31, h = lane >> 5;
@@ -717,13 +726,40 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
       v6_softmax_split<V8_YLUT>(smem, z2, tmask, h, dz, lt, hook);
     else
       bce_tile_loss<V8_YLUT>(smem, z2, tmask, valid, h, dz, lt);
+    // dZ2ᵀ as bf16 fragments: [u][q] holds outputs 32u + acc_perm(q, h, 0..7) of sample r -- the D2 image's
+    // granules, and (v9) the B operand of B1
+    u32x4 dzq[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        dzq[u][q] = __builtin_bit_cast(
+            u32x4, pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2], dz[u][8 * q + 3], dz[u][8 * q + 4],
+                         dz[u][8 * q + 5], dz[u][8 * q + 6], dz[u][8 * q + 7]));
     st.mark(3);
+    // v9: B1 on the forward wave, chained from its own dZ2ᵀ fragments: dHᵀ = W2·dZ2ᵀ (W2 rows = hidden, k =
+    // outputs in accumulator-perm order: the W2Q image), the relu mask from Hᵀ in the same layout, dZ1ᵀ to the
+    // slot for the backward waves' dW1ᵀ
+    bf16x8 dz1[4][2];
+    if (VER == 9) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x16 aT = f32x16{};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          aT = mfma32(lds_frag(smem, w2q_off(32 * t + r, kk * 2 + h)), __builtin_bit_cast(bf16x8, dzq[kk >> 1][kk & 1]),
+                      aT);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) dz1[t][q] = mask_by(hT[t][q], aT, q);
+      }
+    }
     v8_trace(tr, k, 1, lane);
 
-    // the slot's previous tile (k - V8_NSLOT) must have been read by all four backward waves
-    if (k >= V8_NSLOT) v6_wait(smem, V8_DONE + slot * 4, V8_NB * (k / V8_NSLOT), ok);
+    // the slot's previous tile (k - NSLOT) must have been read by all four backward waves
+    constexpr int NSLOT = V8L<VER>::NSLOT;
+    if (k >= NSLOT) v6_wait(smem, V8_DONE + slot * 4, V8_NB * (k / NSLOT), ok);
     st.mark(0);
-    const uint32_t SB = v8_slot(slot);
+    const uint32_t SB = v8_slot<VER>(slot);
 #pragma unroll
     for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(smem + tile_img<false>(SB + V6_SX, r, 16 * q + 8 * h)) = xf[q];
 #pragma unroll
@@ -740,23 +776,33 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const u32x4 fq = __builtin_bit_cast(
-            u32x4, pack8(dz[u][8 * q + 0], dz[u][8 * q + 1], dz[u][8 * q + 2], dz[u][8 * q + 3], dz[u][8 * q + 4],
-                         dz[u][8 * q + 5], dz[u][8 * q + 6], dz[u][8 * q + 7]));
+        const u32x4 fq = dzq[u][q];
         *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 4 * h)) = u32x2{fq[0], fq[1]};
         *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
             u32x2{fq[2], fq[3]};
       }
+    if (VER == 9) {  // dZ1 image: the H image's layout (the backward waves read it with the same transposes)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t DB = SB + V8L<VER>::SD1 + (t >> 1) * 4096;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const u32x4 d = __builtin_bit_cast(u32x4, dz1[t][q]);
+          *reinterpret_cast<u32x2*>(smem + tile_img<true>(DB, r, 32 * (t & 1) + 16 * q + 4 * h)) = u32x2{d[0], d[1]};
+          *reinterpret_cast<u32x2*>(smem + tile_img<true>(DB, r, 32 * (t & 1) + 16 * q + 8 + 4 * h)) = u32x2{d[2], d[3]};
+        }
+      }
+    }
     // the tile's loss terms travel with it: backward wave 0 sums them in tile order (bit-reproducible
     // however the tiles were distributed over the forward waves)
-    reinterpret_cast<float*>(smem + SB + V8_SLOSS)[lane] = lt;
+    reinterpret_cast<float*>(smem + SB + V8L<VER>::SLOSS)[lane] = lt;
     lds_signal(smem, V8_FLAGS + slot * 4, k + 1);  // FULL
     st.mark(4);
     v8_trace(tr, k, 2, lane);
   };
   if (V8_DYN == 0) {
     if (K > 0) fetch(f, nin, ntg);
-    for (int k = f; k < K; k += V8_NF) ftile(k, k % V8_NSLOT, k + V8_NF);
+    for (int k = f; k < K; k += V8_NF) ftile(k, k % V8L<VER>::NSLOT, k + V8_NF);
   } else {
     auto claim = [&]() {
       int t = 0;
@@ -769,7 +815,7 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
     if (cur < K) fetch(cur, nin, ntg);
     while (cur < K) {
       const int nxt = claim();
-      ftile(cur, cur % V8_NSLOT, nxt);
+      ftile(cur, cur % V8L<VER>::NSLOT, nxt);
       cur = nxt;
     }
   }
@@ -781,7 +827,9 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
 // 0.85 k MFMA issue), which bounds v8 (profiles/r6/k7_v8_runs.md).  Reading tile k + 1 under tile k's MFMAs
 // (a cross-tile pipeline) needs ~25 VGPRs more than the 168 of three waves per SIMD: built, spilled 80-96 B
 // per lane in the loop, removed.
-template <int Q>
+// v9 (VER = 9): the forward wave already ran B1 and the mask; this wave reads dZ1ᵀ from the slot's dZ1 image
+// (the same transposing reads as Hᵀ) and runs only dW2, db2 and dW1ᵀ -- 8 MFMAs, no dependency chain.
+template <int Q, int VER>
 EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16 (&dW1T)[2], float& db2,
                            float& loss_acc, bool& ok, Stamps& st, uint32_t* tr) {
   const int r = lane & 31, h = lane >> 5;
@@ -820,7 +868,7 @@ EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 2; ++q) bx[u][q] = tile_tr_frag<false>(smem, SB + V6_SX, 32 * u, q, h, q4, p4, g1);
-    if (Q == 0) loss_acc += reinterpret_cast<const float*>(smem + SB + V8_SLOSS)[lane];
+    if (Q == 0) loss_acc += reinterpret_cast<const float*>(smem + SB + V8L<VER>::SLOSS)[lane];
   };
   auto release = [&](int slot, int k) {  // every read of the slot has landed
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -844,10 +892,39 @@ EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16
     }
   };
   st.start();
+  if (VER == 9) {
+    int slot = 0;
+    for (int k = 0; k < K; ++k) {
+      const uint32_t SB = v8_slot<VER>(slot);
+      wait_full(slot, k);
+      st.mark(5);
+      bf16x8 dz1[2];
+      rd_hR(SB);
+      rd_bd(SB);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        dz1[q] = tile_tr_frag<true>(smem, SB + V8L<VER>::SD1 + (Q >> 1) * 4096, hcol, q, h, q4, p4, g1);
+      rd_bx(SB);
+      release(slot, k);
+      slot = slot + 1 == V8L<VER>::NSLOT ? 0 : slot + 1;
+      st.mark(6);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)  // dW2[own hid][out] += Hᵀ·dZ2
+#pragma unroll
+        for (int q = 0; q < 2; ++q) dW2[u] = mfma32(hR[q], bd[u][q], dW2[u]);
+      db2_share();
+#pragma unroll
+      for (int u = 0; u < 2; ++u)  // dW1ᵀ[own hid][feat] += dZ1ᵀ·X
+#pragma unroll
+        for (int q = 0; q < 2; ++q) dW1T[u] = mfma32(dz1[q], bx[u][q], dW1T[u]);
+      st.mark(9);
+    }
+    return;
+  }
   {  // staged reads inside the tile: each group's read latency runs under the MFMAs before it
     int slot = 0;
     for (int k = 0; k < K; ++k) {
-      const uint32_t SB = v8_slot(slot);
+      const uint32_t SB = v8_slot<VER>(slot);
       wait_full(slot, k);
       st.mark(5);
       rd_dzA(SB);  // (+ the W2ᵀ fragments)
@@ -868,7 +945,7 @@ EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16
       db2_share();
       __builtin_amdgcn_sched_barrier(0);
       release(slot, k);
-      slot = slot + 1 == V8_NSLOT ? 0 : slot + 1;
+      slot = slot + 1 == V8L<VER>::NSLOT ? 0 : slot + 1;
       st.mark(6);
       bf16x8 dz1[2];
 #pragma unroll
@@ -882,7 +959,7 @@ EM_DEVICE void v8_backward(char* smem, int B, int lane, f32x16 (&dW2)[2], f32x16
   }
 }
 
-template <int LOSS, bool SIDX>
+template <int LOSS, bool SIDX, int VER>
 __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                                          int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                                          float* __restrict__ loss_slabs, int* __restrict__ step) {
@@ -930,7 +1007,7 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
   if (wave < V8_NF) {
     float loss_acc = 0.f;  // (unused: the loss terms go to backward wave 0 with their tile)
     __builtin_amdgcn_s_setprio(V8_FPRIO);
-    v8_forward<LOSS, SIDX>(smem, masks, sidx, B, offset, wave, lane, loss_acc, ok, st, tr);
+    v8_forward<LOSS, SIDX, VER>(smem, masks, sidx, B, offset, wave, lane, loss_acc, ok, st, tr);
     dump();
     __syncthreads();  // every wave is out of the loop: the loop's LDS is free
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
@@ -942,13 +1019,13 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
     float db2 = 0.f, loss_acc = 0.f;
     // (Q as a template argument: the db2 share bd[Q >> 1][Q & 1] indexed at run time went to scratch)
     if (Q == 0)
-      v8_backward<0>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
+      v8_backward<0, VER>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     else if (Q == 1)
-      v8_backward<1>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
+      v8_backward<1, VER>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     else if (Q == 2)
-      v8_backward<2>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
+      v8_backward<2, VER>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     else
-      v8_backward<3>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
+      v8_backward<3, VER>(smem, B, lane, dW2, dW1T, db2, loss_acc, ok, st, tr);
     float lsum = wave_sum(loss_acc);
     if (!ok) lsum = __builtin_nanf("");
     dump();
@@ -1009,12 +1086,12 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
   }
 }
 
-template <int LOSS, bool SIDX>
+template <int LOSS, bool SIDX, int VER>
 __global__ void __launch_bounds__(V8_THREADS, 1)
 mlp_fused_train_v8_kernel(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B, int offset,
                           const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                           float* __restrict__ loss_slabs, int* __restrict__ step) {
-  train_v8<LOSS, SIDX>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step);
+  train_v8<LOSS, SIDX, VER>(masks, sidx, B, offset, wimg, slabs, loss_slabs, step);
 }
 
 // Slabs only: em_adam_slab reduces them (or the DP paths all-reduce them first).  A one-launch form
@@ -1208,16 +1285,21 @@ void set_lds_attr() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
   (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
-  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, V8_LDS);
-  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, V8_LDS);
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, false, 8>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v8_lds<8>());
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, true, 8>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v8_lds<8>());
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, false, 9>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v8_lds<9>());
+  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, true, 9>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v8_lds<9>());
 }
-// train kernel generation: EUROM_FUSED_V=8 selects v8 (read once per process)
+// train kernel generation: EUROM_FUSED_V=8 / 9 selects v8 / v9 (read once per process)
 int fused_variant() {
   static const int v = [] {
     const char* e = std::getenv("EUROM_FUSED_V");
-    return (e && std::atoi(e) == 8) ? 8 : 6;
+    const int x = e ? std::atoi(e) : 6;
+    return (x == 8 || x == 9) ? x : 6;
   }();
   return v;
 }
@@ -1249,16 +1331,23 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
   if (int e = check_train_args(draws, sidx, B, offset, wimg, slabs, loss_slabs, nslab)) return e;
   const int Bi = (int)B, oi = (int)offset;
   const uint8_t* w = (const uint8_t*)wimg;
-  const bool v8 = fused_variant() == 8;
+  const int ver = fused_variant();
+  const bool v8 = ver != 6;
+  const int lds = ver == 9 ? v8_lds<9>() : ver == 8 ? v8_lds<8>() : V6_LDS;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nslab), dim3(v8 ? V8_THREADS : 512), v8 ? V8_LDS : V6_LDS, stream, draws, sidx, Bi,
-                       oi, w, slabs, loss_slabs, step);
+    hipLaunchKernelGGL(kern, dim3(nslab), dim3(v8 ? V8_THREADS : 512), lds, stream, draws, sidx, Bi, oi, w, slabs,
+                       loss_slabs, step);
   };
-  if (v8) {
+  if (ver == 9) {
     if (loss_kind == 0)
-      sidx ? go(mlp_fused_train_v8_kernel<0, true>) : go(mlp_fused_train_v8_kernel<0, false>);
+      sidx ? go(mlp_fused_train_v8_kernel<0, true, 9>) : go(mlp_fused_train_v8_kernel<0, false, 9>);
     else
-      sidx ? go(mlp_fused_train_v8_kernel<1, true>) : go(mlp_fused_train_v8_kernel<1, false>);
+      sidx ? go(mlp_fused_train_v8_kernel<1, true, 9>) : go(mlp_fused_train_v8_kernel<1, false, 9>);
+  } else if (v8) {
+    if (loss_kind == 0)
+      sidx ? go(mlp_fused_train_v8_kernel<0, true, 8>) : go(mlp_fused_train_v8_kernel<0, false, 8>);
+    else
+      sidx ? go(mlp_fused_train_v8_kernel<1, true, 8>) : go(mlp_fused_train_v8_kernel<1, false, 8>);
   } else if (loss_kind == 0) {
     sidx ? go(mlp_fused_train_v6_kernel<0, true>) : go(mlp_fused_train_v6_kernel<0, false>);
   } else {

@@ -1,10 +1,6 @@
 set -o pipefail
-O=gpurun_out/xg; mkdir -p $O
+O=gpurun_out/v9; mkdir -p $O
 L=$PWD/euromillioner_amd/lib/ab
-timeout -k 10 400 python -u -m pytest tests/test_xgmi_proxy_gpu.py tests/test_xgmi_gpu.py -x -q --timeout 150 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 2; }
-tail -1 $O/pytest.log
-for r in 1 2 3; do
-  XB_ROUNDS=1 timeout -k 10 240 python tools/xgmi_budget.py > $O/new_$r.jsonl 2>&1 || { tail -20 $O/new_$r.jsonl; exit 3; }
-  XB_ROUNDS=1 EUROM_NATIVE_LIB=$L/adam_head.so timeout -k 10 240 python tools/xgmi_budget.py > $O/head_$r.jsonl 2>&1 || { tail -20 $O/head_$r.jsonl; exit 4; }
-done
-for f in $O/head_?.jsonl $O/new_?.jsonl; do echo "== $f"; grep '^{' $f | cut -c1-220; done
+EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/tracedyn.so timeout -k 10 120 python tools/fused_trace.py > $O/trace_v9dyn.txt 2>&1 || { tail $O/trace_v9dyn.txt; exit 3; }
+tail -9 $O/trace_v9dyn.txt
+ARMS="v6|EUROM_FUSED_V=6;v9|EUROM_FUSED_V=9;v9dyn|EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/dyn1.so;v9dynb0|EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/dyn1b0.so;v9dynf1|EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/dyn1f1.so" ROUNDS=2 bash tools/gpu_ab.sh

@@ -47,7 +47,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         per = e0.elapsed_time(e1) * 1e3 / 10
-        v8 = os.environ.get("EUROM_FUSED_V") == "8"  # v8: 12 waves, wall-clock marks in wave 0's spare lanes 10-14
+        v8 = os.environ.get("EUROM_FUSED_V") in ("8", "9")  # v8 / v9: 12 waves, wall-clock marks in wave 0's spare lanes 10-14
         T0 = FM.P_TOTAL + (10 if v8 else 128)
         raw = m.slabs[:nslab, T0:T0 + 4].contiguous().view(torch.int32).cpu().numpy()
         t = raw.astype(np.int64) & 0xFFFFFFFF
