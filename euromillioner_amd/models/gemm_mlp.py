@@ -36,6 +36,8 @@ block padded to 64), the target is draw i+k.  Layer 0 is then ``W [N_pad, 64k]``
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -119,6 +121,7 @@ class GemmMLPTrainer:
         # stands in for the all-reduce on one GPU, e.g. a side-stream reduce-copy per bucket)
         self.comm_emulator = None
         self.last_buckets: list[tuple[int, int]] = []
+
 
     # ------------------------------------------------------------------ layout
     def _views(self, flat: torch.Tensor, i: int):
@@ -288,6 +291,9 @@ class GemmMLPTrainer:
             beta = 1.0 if accumulate else 0.0
             a, b_off, c = self.offsets[i]
             K = self.padded[i]
+            # (a big layer's dgrad on a side stream beside its wgrad -- the two GEMMs' workgroups interleaved
+            # on the CUs -- measured 20.8-21.0 vs 18.8-18.9 ms per wide step, round 6: their L2 tile groups
+            # and XCD placement fight; one stream)
             if plan["wgrad"][i]:
                 panels = self.wgrad_panels(i) if on_ready is not None else [(0, gw.shape[0])]
                 for r0, r1 in panels:  # each panel's all-reduce starts while the next panels run
@@ -305,21 +311,29 @@ class GemmMLPTrainer:
             if on_ready is not None:
                 on_ready(b_off, c)
             if i > 0:
-                w, _ = self._views(self.shadow, i)
                 if plan["dgrad"][i]:
-                    wt = LIN.transpose(w, out=ws["wt"][i])
-                    # K3 bias gradient of layer i - 1 fused into this dgrad's epilogue: per-128-row column
-                    # sums of dZ_{i-1} (fp32, before the bf16 store), then one fixed-order reduce
-                    part = ws["colpart"] if B % 128 == 0 else None
-                    dz = LIN.linear_dgrad_nt(dz, wt, inputs[i], self.activation, out=ws["dz"][i - 1],
-                                             ct=ws["dzt"].get(i - 1), colpart=part, bits=ws["bits"].get(i))
-                    if part is not None:
-                        _, gb_prev = self._views(self.grads, i - 1)
-                        LIN.colpart_reduce(part, B // 128, self.padded[i], gb_prev, accumulate=accumulate)
-                        fused_bias.add(i - 1)
+                    dz = self._dgrad_big(i, dz, inputs, ws, accumulate, fused_bias)
                 else:
+                    w, _ = self._views(self.shadow, i)
                     dz = LIN.linear_dgrad(dz, w, inputs[i], self.activation, out=ws["dz"][i - 1])
         return dz
+
+    def _dgrad_big(self, i, dz, inputs, ws, accumulate, fused_bias):
+        """dZ_{i-1} of a big layer: the NT dgrad on W_i^T with act' from the relu bits, the K3 bias gradient
+        of layer i - 1 fused into its epilogue (per-128-row column sums of dZ_{i-1}, fp32, before the bf16
+        store) and one fixed-order reduce of them."""
+        B = dz.shape[0]
+        w, _ = self._views(self.shadow, i)
+        wt = LIN.transpose(w, out=ws["wt"][i])
+        part = ws["colpart"] if B % 128 == 0 else None
+        dz = LIN.linear_dgrad_nt(dz, wt, inputs[i], self.activation, out=ws["dz"][i - 1],
+                                 ct=ws["dzt"].get(i - 1), colpart=part, bits=ws["bits"].get(i))
+        if part is not None:
+            _, gb_prev = self._views(self.grads, i - 1)
+            LIN.colpart_reduce(part, B // 128, self.padded[i], gb_prev, accumulate=accumulate)
+            fused_bias.add(i - 1)
+        return dz
+
 
     def _check(self, masks, B, offset, sidx):
         if not self._checked:

@@ -1,6 +1,5 @@
 set -o pipefail
-O=gpurun_out/v9; mkdir -p $O
-L=$PWD/euromillioner_amd/lib/ab
-EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/tracedyn.so timeout -k 10 120 python tools/fused_trace.py > $O/trace_v9dyn.txt 2>&1 || { tail $O/trace_v9dyn.txt; exit 3; }
-tail -9 $O/trace_v9dyn.txt
-ARMS="v6|EUROM_FUSED_V=6;v9|EUROM_FUSED_V=9;v9dyn|EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/dyn1.so;v9dynb0|EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/dyn1b0.so;v9dynf1|EUROM_FUSED_V=9 EUROM_NATIVE_LIB=$L/dyn1f1.so" ROUNDS=2 bash tools/gpu_ab.sh
+O=gpurun_out/wc; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gemm_accum_gpu.py tests/test_train_gpu.py tests/test_gemm_gpu.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 2; }
+tail -1 $O/pytest.log
+ARMS="seq|EUROM_WIDE_CONCURRENT=0;conc|EUROM_WIDE_CONCURRENT=1" ROUNDS=3 BENCH_ARGS="--model mlp-wide --steps 10 --warmup 3 --no-eval" bash tools/gpu_ab.sh
