@@ -72,6 +72,14 @@ EM_DEVICE bf16x8 lds_frag(const char* lds_base, uint32_t byte_off) {
   return *reinterpret_cast<const bf16x8*>(lds_base + byte_off);
 }
 
+// Byte offset of entry `nib` (0..15, bits 4+ of `word >> sh` ignored) of a 16-entry LDS table at LUT with
+// 2^SH-byte entries: shift + mask, the base in the DS instruction's 16-bit immediate when the table sits
+// below 64K and the LDS base is a compile-time constant (static __shared__); otherwise a third VALU adds it
+template <int LUT, int SH>
+EM_DEVICE uint32_t lut_off(uint32_t word, int sh) {
+  return (uint32_t)LUT + (__builtin_amdgcn_ubfe(word, sh, 4) << SH);
+}
+
 // ds_read_b64_tr_b16: 4 rows x 16 cols block per 16-lane group, column-major to lanes
 EM_DEVICE s16x4 lds_tr16(const char* lds_base, uint32_t byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((EM_LDS s16x4*)(lds_base + byte_off));

@@ -141,6 +141,17 @@ EM_DEVICE void lds_signal(char* smem, uint32_t flag_off, int value) {
 #ifndef FUSED_FPRIO
 #define FUSED_FPRIO 1
 #endif
+// FUSED_PROBE (diagnostic side builds only: the gradients are WRONG under it; profiles/r6/k7_probes.md)
+// prices moving the softmax from the forward to the backward waves before building it.  Bit 1: the
+// forward wave's softmax replaced by dZ2 = Z2 / 64 (its VALU gone, F2's latency kept).  Bit 2: every
+// backward tile issues FUSED_PROBE_VALU independent VALU (FMA chains + exp2, 1 in 8) on registers of
+// its own between its MFMAs, about the share of a split softmax a backward wave would take.
+#ifndef FUSED_PROBE
+#define FUSED_PROBE 0
+#endif
+#ifndef FUSED_PROBE_VALU
+#define FUSED_PROBE_VALU 128
+#endif
 struct Stamps {
   uint64_t last = 0;
   uint64_t acc[10] = {};
@@ -183,8 +194,8 @@ EM_DEVICE bf16x8 tile_tr_frag(const char* smem, uint32_t base, int colbase, int 
 template <int LUT>
 EM_DEVICE bf16x8 nib_xfrag(const char* smem, uint32_t w, int q) {
   const int sh = 16 * (q & 1);
-  const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + LUT + (__builtin_amdgcn_ubfe(w, sh, 4) << 3));
-  const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + LUT + (__builtin_amdgcn_ubfe(w, sh + 4, 4) << 3));
+  const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + lut_off<LUT, 3>(w, sh));
+  const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + lut_off<LUT, 3>(w, sh + 4));
   return __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
 }
 
@@ -241,17 +252,45 @@ constexpr int V6_NSLOT = V6_RSLOTS + V6_NREC;
 static_assert(V6_NREC == 0 || 2 * V6_SLOT <= IMG_W2Q, "recycled slots must fit below the W2Q image");
 static_assert(V6_NSLOT % V6_NBP == 0, "a slot's tiles share one parity");
 constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
-constexpr int V6_XLUT = IMG_BYTES;       // 16 x 8 B: input nibble -> 4 bf16 {0,1}
-constexpr int V6_YLUT = V6_XLUT + 128;   // 16 x f32x4: target nibble -> 4 {0,1} floats
-constexpr int V6_FLAGS = V6_YLUT + 256;  // [streams][32 / streams ints]: full[N] | done0[N] | done1[N]
+// V6_WIN: the SIMD's vector issue port bounds the loop (profiles/r6/k7_probes.md: 128 extra VALU per
+// backward tile cost +14 %, the forward softmax's VALU is 16 % of the step), and ~50 of the VALU per SIMD
+// per tile period are slot-address adds (slot base + lane offset, the slot known only at run time).  The
+// windowed layout puts each tile parity's four slots in one 64 KB window -- slot s at RING + (s & 1) * 64K
+// + (s >> 1) * 16K, the ring over the dead W1ᵀ / W2ᵀ images -- and unrolls the forward loop by 2 and the
+// backward loop by 4, so that within an unrolled copy the slot is a constant offset from a per-wave base:
+// DS immediates instead of adds.  b2, the LUTs and the flags stay below 64K (at 0, ahead of the ring: their
+// lookups keep the base in the immediate too), the W2Q image moves above the ring.
+// Bit 0 unrolls the forward loop, bit 1 the backward loop (either bit selects the layout).  Same-box A/B
+// (4 rounds, profiles/r6/ab_v6_win.jsonl, median µs per step): round-5 kernel 87.8; with static LDS:
+// old layout 89.1, windowed + forward unrolled 87.0, + backward unrolled 86.8, both 87.1 -- the unrolled
+// forward copy trades its adds for register moves at 256 VGPRs.  Default 2.
+#ifndef V6_WIN
+#define V6_WIN 2
+#endif
+static_assert(!V6_WIN || (FUSED_SHARED && V6_NSLOT == 8), "windowed layout: shared ring of 8 slots");
+// windowed: b2 256 | YLUT 256 | XLUT 128 | flags 128 | ring 8 x 16K (W1ᵀ / W2ᵀ images at its start) | W2Q
+constexpr int V6_IMGB = V6_WIN ? 768 : 0;                        // LDS base of the W1ᵀ / W2ᵀ images
+constexpr int V6_B2B = V6_WIN ? 0 : IMG_B2;                      // b2 (forward waves)
+constexpr int V6_XLUT = V6_WIN ? 512 : IMG_BYTES;                // 16 x 8 B: input nibble -> 4 bf16 {0,1}
+constexpr int V6_YLUT = V6_WIN ? 256 : V6_XLUT + 128;            // 16 x f32x4: target nibble -> 4 {0,1} floats
+constexpr int V6_FLAGS = V6_WIN ? 640 : V6_YLUT + 256;  // [streams][32 / streams ints]: full[N] | done0[N] | done1[N]
 constexpr int V6_FLAG_STRIDE = 128 / V6_NSTREAM;
 static_assert(3 * V6_NSLOT * 4 <= V6_FLAG_STRIDE, "flag words");
 constexpr int V6_RING = V6_FLAGS + 128;  // [streams][ring slots][16 KB]
-constexpr int V6_LOOP_LDS = V6_RING + V6_NSTREAM * V6_RSLOTS * V6_SLOT;
+constexpr int V6_W2QB = V6_WIN ? V6_RING + 8 * V6_SLOT : IMG_W2Q;  // W2Q image base (backward waves)
+constexpr int V6_LOOP_LDS = V6_WIN ? V6_W2QB + (IMG_B2 - IMG_W2Q) : V6_RING + V6_NSTREAM * V6_RSLOTS * V6_SLOT;
+static_assert(!V6_WIN || (V6_RING == V6_IMGB && IMG_W2Q <= 8 * V6_SLOT), "windowed layout");
 // byte offset of slot `slot` of stream `st`
 EM_DEVICE uint32_t v6_slot(int st, int slot) {
+  if (V6_WIN) return V6_RING + (slot & 1) * 65536 + (slot >> 1) * V6_SLOT;
   return slot < V6_RSLOTS ? V6_RING + (st * V6_RSLOTS + slot) * V6_SLOT
                           : (FUSED_SHARED ? slot - V6_RSLOTS : st) * V6_SLOT;
+}
+EM_DEVICE uint32_t v6_w2q_off(int row, int k8) { return V6_W2QB + row * W2Q_RS + k8 * 16; }
+// LDS destination of byte `b` of the weight image
+EM_DEVICE uint32_t v6_img_dst(uint32_t b) {
+  if (!V6_WIN) return b;
+  return b < (uint32_t)IMG_W2Q ? V6_IMGB + b : b < (uint32_t)IMG_B2 ? b - IMG_W2Q + V6_W2QB : b - IMG_B2 + V6_B2B;
 }
 constexpr int V6_RED = 131072;  // epilogue: two fp32 dW images [2][16384] below, DB2S [2][64] + LOSSS [8] above
 constexpr int V6_LDS = (V6_LOOP_LDS > V6_RED + 2048 ? V6_LOOP_LDS : V6_RED + 2048);
@@ -309,21 +348,20 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) w1r[t][q] = lds_frag(smem, w1t_off(32 * t + r, 2 * q + h));
+    for (int q = 0; q < 4; ++q) w1r[t][q] = lds_frag(smem, V6_IMGB + w1t_off(32 * t + r, 2 * q + h));
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) w2r[u][kk] = lds_frag(smem, w2p_off(32 * u + r, kk * 2 + h));
+    for (int kk = 0; kk < 8; ++kk) w2r[u][kk] = lds_frag(smem, V6_IMGB + w2p_off(32 * u + r, kk * 2 + h));
   __syncthreads();  // every forward wave holds its weights: the W1ᵀ / W2ᵀ images are free (recycled slots)
   st.start();
   // (one tile as a lambda called from the loop below: written inline in the loop, the same body
   // compiles to 9 more VALU per tile -- slot addresses recomputed -- and measured 3 % slower)
-  auto ftile = [&](int k, int slot, int knext) {
+  auto ftile = [&](int k, int slot, int knext, uint32_t SB) {
     const bool valid = (U + k * nunits) * 32 + r < B;
     const uint64_t imask = valid ? (nin | BIAS_BIT) : 0ull;
     const uint64_t tmask = valid ? ntg : 0ull;
     fetch(knext, nin, ntg);
-    const uint32_t SB = v6_slot(unit, slot);
     if (k >= V6_NSLOT) {  // the slot's previous tile (k - 4) must be consumed by both backward waves
       v6_wait(smem, FL + (V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
       v6_wait(smem, FL + (2 * V6_NSLOT + slot) * 4, k - V6_NSLOT + 1, ok);
@@ -364,7 +402,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + IMG_B2 + (32 * u + 8 * g + 4 * h) * 4);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + V6_B2B + (32 * u + 8 * g + 4 * h) * 4);
         z2[u][4 * g + 0] = b[0]; z2[u][4 * g + 1] = b[1]; z2[u][4 * g + 2] = b[2]; z2[u][4 * g + 3] = b[3];
       }
     auto f2mfma = [&](int u, int kk) { z2[u] = mfma32(w2r[u][kk], hT[kk >> 1][kk & 1], z2[u]); };
@@ -392,7 +430,15 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 
     float dz[2][16];
     float lt = 0.f;  // this lane's loss terms of the tile
-    if (LOSS == 0)
+    if ((FUSED_PROBE & 1) && LOSS == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f2mfma(1, j);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dz[u][i] = z2[u][i] * 0.015625f;
+      lt = (float)(tmask & 1);
+    } else if (LOSS == 0)
       v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, lt, hook);
     else
       bce_tile_loss<V6_YLUT>(smem, z2, tmask, valid, h, dz, lt);
@@ -415,7 +461,15 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
     lds_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
   };
-  for (int k = f; k < K; k += V6_NF) ftile(k, k % V6_NSLOT, k + V6_NF);
+  if (V6_WIN & 1) {  // tiles f, f + 4, ... alternate slots f and f + 4: the second is the first + 32K
+    const uint32_t SB0 = v6_slot(unit, f);
+    for (int k = f; k < K; k += 2 * V6_NF) {
+      ftile(k, f, k + V6_NF, SB0);
+      if (k + V6_NF < K) ftile(k + V6_NF, f + V6_NF, k + 2 * V6_NF, SB0 + 2 * V6_SLOT);
+    }
+  } else {
+    for (int k = f; k < K; k += V6_NF) ftile(k, k % V6_NSLOT, k + V6_NF, v6_slot(unit, k % V6_NSLOT));
+  }
 }
 
 // backward wave of hidden half RHO: every tile of the unit's stream.  Every LDS read of the tile
@@ -433,9 +487,8 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   __syncthreads();  // matches the forward waves' barrier (recycled images)
   st.start();
-  for (int k = parity; k < K; k += V6_NBP) {
-    const int slot = k % V6_NSLOT;
-    const uint32_t SB = v6_slot(unit, slot), D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
+  auto btile = [&](int k, int slot, uint32_t SB) {
+    const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
     v6_wait(smem, FL + slot * 4, k + 1, ok);
     st.mark(5);
 
@@ -455,7 +508,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
+      for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, v6_w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -482,6 +535,17 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
         for (int tt = 0; tt < 2; ++tt) dW2[tt][u] = mfma32(hR[tt][q], bd[u][q], dW2[tt][u]);
         if (u == RHO) db2 = mfma32(ones, bd[u][q], db2);
       }
+    if (FUSED_PROBE & 2) {
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = (float)(lane + j) * 1e-3f + (float)k * 1e-6f;
+#pragma unroll
+      for (int it = 0; it < FUSED_PROBE_VALU / 8; ++it)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          a[j] = (it & 7) == 7 ? __builtin_amdgcn_exp2f(a[j]) : __builtin_fmaf(a[j], 0.999f, 0.25f);
+      asm volatile("" ::"v"(a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7]));
+    }
     st.mark(7);
     // dZ1 = dH * (H > 0), then dW1ᵀ[own hid][feat] += dZ1ᵀ·X
     bf16x8 dz1[2][2];
@@ -497,6 +561,17 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) dW1T[tt][u] = mfma32(dz1[tt][q], bx[u][q], dW1T[tt][u]);
     st.mark(9);
+  };
+  if (V6_WIN & 2) {  // tiles parity, parity + 2, ... cycle through slots parity + 0/2/4/6: base + 0/16/32/48K
+    const uint32_t SB0 = v6_slot(unit, parity);
+    for (int k = parity; k < K; k += 4 * V6_NBP) {
+      btile(k, parity, SB0);
+      if (k + V6_NBP < K) btile(k + V6_NBP, parity + 2, SB0 + V6_SLOT);
+      if (k + 2 * V6_NBP < K) btile(k + 2 * V6_NBP, parity + 4, SB0 + 2 * V6_SLOT);
+      if (k + 3 * V6_NBP < K) btile(k + 3 * V6_NBP, parity + 6, SB0 + 3 * V6_SLOT);
+    }
+  } else {
+    for (int k = parity; k < K; k += V6_NBP) btile(k, k % V6_NSLOT, v6_slot(unit, k % V6_NSLOT));
   }
 }
 
@@ -1101,7 +1176,9 @@ template <int LOSS, bool SIDX>
 __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, const int32_t* __restrict__ sidx, int B,
                                          int offset, const uint8_t* __restrict__ wimg, float* __restrict__ slabs,
                                          float* __restrict__ loss_slabs, int* __restrict__ step) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // static, not dynamic, LDS: the base is then a link-time-free constant 0, so a data-dependent LUT
+  // address folds its table offset into the DS immediate instead of paying a v_add of the LDS base
+  __shared__ __attribute__((aligned(16))) char smem[V6_LDS];
   uint64_t ts[4] = {};  // FUSED_STAMPS: 100 MHz wall-clock marks (entry, prologue done, loop done, slab written)
   if (FUSED_STAMPS) ts[0] = __builtin_amdgcn_s_memrealtime();
   if (step && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1114,14 +1191,13 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
   {  // all loads of the weight image in flight before the first LDS store
     constexpr int N16 = IMG_BYTES / 16, KK = (N16 + 511) / 512;
     const u32x4* src = reinterpret_cast<const u32x4*>(wimg);
-    u32x4* dst = reinterpret_cast<u32x4*>(smem);
     u32x4 v[KK];
 #pragma unroll
     for (int k = 0; k < KK; ++k)
       if (tid + 512 * k < N16) v[k] = src[tid + 512 * k];
 #pragma unroll
     for (int k = 0; k < KK; ++k)
-      if (tid + 512 * k < N16) dst[tid + 512 * k] = v[k];
+      if (tid + 512 * k < N16) *reinterpret_cast<u32x4*>(smem + v6_img_dst(16u * (tid + 512 * k))) = v[k];
   }
   if (tid < 64) {
     const float bit = (float)(((tid >> 2) >> (tid & 3)) & 1);
@@ -1281,10 +1357,7 @@ EM_API int em_mlp_fused_lds_bytes() { return V6_LDS; }
 namespace {
 template <int LOSS>
 void set_lds_attr() {
-  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
-  (void)hipFuncSetAttribute((const void*)mlp_fused_train_v6_kernel<LOSS, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, V6_LDS);
+  // (v6 uses static LDS: nothing to raise)
   (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, false, 8>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, v8_lds<8>());
   (void)hipFuncSetAttribute((const void*)mlp_fused_train_v8_kernel<LOSS, true, 8>,
@@ -1333,7 +1406,7 @@ EM_API int em_mlp_fused_train(const uint64_t* draws, const int32_t* sidx, int64_
   const uint8_t* w = (const uint8_t*)wimg;
   const int ver = fused_variant();
   const bool v8 = ver != 6;
-  const int lds = ver == 9 ? v8_lds<9>() : ver == 8 ? v8_lds<8>() : V6_LDS;
+  const int lds = ver == 9 ? v8_lds<9>() : ver == 8 ? v8_lds<8>() : 0;  // v6: static LDS
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(nslab), dim3(v8 ? V8_THREADS : 512), lds, stream, draws, sidx, Bi, oi, w, slabs,
                        loss_slabs, step);

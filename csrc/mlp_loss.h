@@ -28,7 +28,7 @@ EM_DEVICE void bce_tile_loss(const char* smem, const f32x16 (&z2)[2], uint64_t t
     const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + lut_off<YL, 4>(tmh, 8 * g));
       yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
     }
 #pragma unroll
@@ -75,7 +75,7 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + YL + (__builtin_amdgcn_ubfe(tmh, 8 * g, 4) << 4));
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + lut_off<YL, 4>(tmh, 8 * g));
       yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
     }
   };
