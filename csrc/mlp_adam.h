@@ -16,6 +16,25 @@ constexpr int W1T_RS = 144, W2P_RS = 272, W2Q_RS = 144;
 constexpr int IMG_W1T = 0, IMG_W2P = IMG_W1T + 128 * W1T_RS, IMG_W2Q = IMG_W2P + 64 * W2P_RS,
               IMG_B2 = IMG_W2Q + 128 * W2Q_RS, IMG_BYTES = IMG_B2 + 256;  // 54528
 
+// Physical output order of the weight images (W2P rows, W2Q k index, b2): the train kernels hold a
+// 32-sample tile's logits with output 32u + 8g + 4h + (i & 3) in register i = 4g + (i & 3) of lane half
+// h, so lane halves h = 0 / 1 share a register for physical nibbles 2m / 2m + 1.  Logical nibbles 13, 14
+// (stars 52-59) move to physical 14, 15 and logical nibble 15 (stars 60, 61, pads 62, 63) to physical
+// 13, rotated by two: every register then has ONE class (main / star) in both lane halves -- main 0-51
+// incl. the pads, which carry b2 = PAD_B2 in the image (exp underflows to 0, never the max, target 0)
+// -- and the softmax drops its lane-half selects (csrc/mlp_loss.h SOFTMAX_PERM).  Targets are permuted
+// the same way per sample (phys_targets_hi).  Nibble-granular, so f32x4 logit stores stay aligned.
+EM_DEVICE constexpr int out_phys(int o) {
+  return o < 52 ? o : o < 60 ? o + 4 : o < 62 ? o - 6 : o - 10;
+}
+EM_DEVICE constexpr int out_logical(int p) {
+  return p < 52 ? p : p < 54 ? p + 10 : p < 56 ? p + 6 : p - 4;
+}
+static_assert(out_logical(out_phys(52)) == 52 && out_logical(out_phys(61)) == 61 && out_logical(out_phys(62)) == 62 &&
+                  out_phys(60) == 54 && out_phys(62) == 52 && out_phys(59) == 63,
+              "output permutation");
+constexpr float PAD_B2 = -1.0e30f;  // image value of the pad logits' bias
+
 // true for padding slots that must stay exactly zero (W1 row 63, W2 cols 62/63, b2[62/63])
 EM_DEVICE bool pad_slot(int p) {
   if (p < P_W2) return (p >> 7) == 63;
@@ -30,8 +49,8 @@ EM_DEVICE void pack_one(int p, float val, uint8_t* img) {
     const int f = p >> 7, c = p & 127;
     const uint32_t off = IMG_W1T + c * W1T_RS + (f >> 3) * 16 + (f & 7) * 2;
     *reinterpret_cast<uint16_t*>(img + off) = b;
-  } else if (p < P_B2) {  // W2[c][o]
-    const int q = p - P_W2, c = q >> 6, o = q & 63;
+  } else if (p < P_B2) {  // W2[c][o], o at its physical position
+    const int q = p - P_W2, c = q >> 6, o = out_phys(q & 63);
     {  // W2P: row o, hid c = 32t + perm(s,h,j)
       const int t = c >> 5, cc = c & 31, s = cc >> 4, a = (cc >> 3) & 1, hh = (cc >> 2) & 1, bb = cc & 3;
       const int j = 4 * a + bb, k16 = (2 * t + s) * 2 + hh;
@@ -43,7 +62,8 @@ EM_DEVICE void pack_one(int p, float val, uint8_t* img) {
       *reinterpret_cast<uint16_t*>(img + IMG_W2Q + c * W2Q_RS + k8 * 16 + j * 2) = b;
     }
   } else {
-    *reinterpret_cast<float*>(img + IMG_B2 + (p - P_B2) * 4) = val;
+    const int o = p - P_B2;
+    *reinterpret_cast<float*>(img + IMG_B2 + out_phys(o) * 4) = o >= 62 ? PAD_B2 : val;
   }
 }
 

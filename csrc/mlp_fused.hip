@@ -439,9 +439,9 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
         for (int i = 0; i < 16; ++i) dz[u][i] = z2[u][i] * 0.015625f;
       lt = (float)(tmask & 1);
     } else if (LOSS == 0)
-      v6_softmax_split<V6_YLUT>(smem, z2, tmask, h, dz, lt, hook);
+      v6_softmax_split<V6_YLUT, true>(smem, z2, tmask, h, dz, lt, hook);
     else
-      bce_tile_loss<V6_YLUT>(smem, z2, tmask, valid, h, dz, lt);
+      bce_tile_loss<V6_YLUT, true>(smem, z2, tmask, valid, h, dz, lt);
     loss_acc += lt;
     st.mark(3);
 
@@ -798,9 +798,9 @@ EM_DEVICE void v8_forward(char* smem, const uint64_t* __restrict__ masks, const 
     float dz[2][16];
     float lt = 0.f;
     if (LOSS == 0)
-      v6_softmax_split<V8_YLUT>(smem, z2, tmask, h, dz, lt, hook);
+      v6_softmax_split<V8_YLUT, true>(smem, z2, tmask, h, dz, lt, hook);
     else
-      bce_tile_loss<V8_YLUT>(smem, z2, tmask, valid, h, dz, lt);
+      bce_tile_loss<V8_YLUT, true>(smem, z2, tmask, valid, h, dz, lt);
     // dZ2ᵀ as bf16 fragments: [u][q] holds outputs 32u + acc_perm(q, h, 0..7) of sample r -- the D2 image's
     // granules, and (v9) the B operand of B1
     u32x4 dzq[2][2];
@@ -1133,7 +1133,7 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
   for (int q = tid; q < 2048; q += V8_THREADS) {  // W2[c + k][o]
     const int T = q >> 8, g = (q >> 6) & 3, L = q & 31, hh = (q >> 5) & 1;
     const f32x4 v = *reinterpret_cast<const f32x4*>(RED + q * 4);
-    const int c = 32 * (T >> 1) + 8 * g + 4 * hh, o = 32 * (T & 1) + L;
+    const int c = 32 * (T >> 1) + 8 * g + 4 * hh, o = mlp::out_logical(32 * (T & 1) + L);  // physical -> logical
     uint32_t vb[4];
     __builtin_memcpy(vb, &v, 16);
 #pragma unroll
@@ -1144,7 +1144,8 @@ __device__ __forceinline__ void train_v8(const uint64_t* __restrict__ masks, con
     const int u = tid >> 5, L = tid & 31;
     const float v = (DB2S[(2 * u) * 64 + L] + DB2S[(2 * u) * 64 + 32 + L]) +
                     (DB2S[(2 * u + 1) * 64 + L] + DB2S[(2 * u + 1) * 64 + 32 + L]);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), srd, (P_B2 + tid) * 4, 0, 16 /* sc1 */);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), srd, (P_B2 + mlp::out_logical(tid)) * 4, 0,
+                                          16 /* sc1 */);
   }
   if (tid == 0) {
     float l = 0.f;
@@ -1250,7 +1251,7 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
   for (int q = tid; q < 2048; q += 512) {  // dW2 tiles read in slot order; W2[c + k][o] as 4 coalesced scalars
     const int T = q >> 8, g = (q >> 6) & 3, L = q & 31, hh = (q >> 5) & 1;
     const f32x4 v = *reinterpret_cast<const f32x4*>(RED + q * 4) + *reinterpret_cast<const f32x4*>(RED + 16384 + q * 4);
-    const int c = 32 * (T >> 1) + 8 * g + 4 * hh, o = 32 * (T & 1) + L;
+    const int c = 32 * (T >> 1) + 8 * g + 4 * hh, o = mlp::out_logical(32 * (T & 1) + L);  // physical -> logical
     uint32_t vb[4];  // memcpy, not a bit_cast of v[k]: see as_s16x2
     __builtin_memcpy(vb, &v, 16);
 #pragma unroll
@@ -1259,7 +1260,7 @@ __device__ __forceinline__ void train_v6(const uint64_t* __restrict__ masks, con
   }
   if (tid < 64)
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, DB2S[tid] + DB2S[64 + tid]), srd,
-                                          (P_B2 + tid) * 4, 0, 16 /* sc1 */);
+                                          (P_B2 + mlp::out_logical(tid)) * 4, 0, 16 /* sc1 */);
   if (tid == 0) {
     float l = 0.f;
     for (int w = 0; w < 8; ++w) l += LOSSS[w];
@@ -1338,9 +1339,11 @@ mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __re
           z = mfma32(lds_frag(smem, w2p_off(32 * u + r, (2 * t + q) * 2 + h)), hT[t][q], z);
       if (valid) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 v = {z[4 * g + 0], z[4 * g + 1], z[4 * g + 2], z[4 * g + 3]};
-          *reinterpret_cast<f32x4*>(logits + (int64_t)s * OUT + 32 * u + 8 * g + 4 * h) = v;
+        for (int g = 0; g < 4; ++g) {  // physical nibble n -> logical (mlp_adam.h out_phys): 13 -> 15 rotated
+          const int n = 8 * u + 2 * g + h, ln = n <= 12 ? n : n == 13 ? 15 : n - 1;
+          const f32x4 v = n == 13 ? f32x4{z[4 * g + 2], z[4 * g + 3], z[4 * g + 0], z[4 * g + 1]}
+                                  : f32x4{z[4 * g + 0], z[4 * g + 1], z[4 * g + 2], z[4 * g + 3]};
+          *reinterpret_cast<f32x4*>(logits + (int64_t)s * OUT + 4 * ln) = v;
         }
       }
     }

@@ -192,7 +192,7 @@ mlp_fused_train_f32_kernel(const uint64_t* __restrict__ masks, const int32_t* __
 #pragma unroll
         for (int j = 0; j < 8; ++j) stepf(j);
       };
-      v6_softmax_split<F32_WAVE - 256>(smem, z2, valid ? tm : 0ull, h, dz, lt, hook);
+      v6_softmax_split<F32_WAVE - 256, false>(smem, z2, valid ? tm : 0ull, h, dz, lt, hook);
     } else {
       bce_tile_loss<F32_WAVE - 256>(smem, z2, valid ? tm : 0ull, valid, h, dz, lt);
     }

@@ -3,23 +3,40 @@
 // accumulator layout: lane (r, h) = sample r, register i of output tile u = output 32u + oo0(i) + 4h.
 #pragma once
 #include "common.h"
+#include "mlp_adam.h"
 
 // o(u,i,h) = 32u + (i&3) + 8(i>>2) + 4h : output index held in register i of Z2ᵀ tile u
 EM_DEVICE constexpr int oo0(int i) { return (i & 3) + 8 * (i >> 2); }
 
 
-// class of output o = 32 u + oo0(i) + 4h: 0 main, 1 star, 2 pad
+// class of the output at position o = 32 u + oo0(i) + 4h: 0 main, 1 star, 2 pad.  PERM: positions are
+// physical (mlp_adam.h out_phys) -- the pads count as main (their logits are PAD_B2) and no class depends
+// on the lane half h.
+template <bool PERM = false>
 EM_DEVICE constexpr int out_cls(int u, int i, int h) {
-  return 32 * u + oo0(i) + 4 * h < 50 ? 0 : (32 * u + oo0(i) + 4 * h < 62 ? 1 : 2);
+  const int o = PERM ? mlp::out_logical(32 * u + oo0(i) + 4 * h) : 32 * u + oo0(i) + 4 * h;
+  return o < 50 ? 0 : (o < 62 ? 1 : (PERM ? 0 : 2));
+}
+static_assert(out_cls<true>(1, 8, 0) == out_cls<true>(1, 8, 1) && out_cls<true>(1, 9, 1) == 0 &&
+                  out_cls<true>(1, 10, 0) == 1 && out_cls<true>(1, 10, 1) == 1 && out_cls<true>(1, 12, 1) == 1,
+              "PERM: one class per register");
+
+// the target mask in physical output order (PERM): logical bits 52-59 -> 56-63, 60/61 -> 54/55; the pad
+// bits 62/63 (-> 52/53) are zero in every target
+EM_DEVICE uint64_t phys_targets(uint64_t t) {
+  const uint32_t hi = (uint32_t)(t >> 32);
+  const uint32_t ph = (hi & 0x000FFFFFu) | ((hi & 0x0FF00000u) << 4) | ((hi >> 6) & 0x00C00000u);
+  return ((uint64_t)ph << 32) | (uint32_t)t;
 }
 
 // Sigmoid-BCE loss + dZ2 of a whole 32-sample tile in ONE wave: the lane's 32 logits z2[u][i] (output
 // 32u + oo0(i) + 4h of sample r; lanes r and r + 32 share the sample).  Targets as {0,1} floats from
 // a 16-entry nibble table (YL): register group g of tile u holds outputs 32u + 8g + 4h .. +3 = one
 // nibble of the target mask.
-template <int YL>
+template <int YL, bool PERM = false>
 EM_DEVICE void bce_tile_loss(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, bool valid, int h,
                              float (&dz)[2][16], float& loss_acc) {
+  if (PERM) tmask = phys_targets(tmask);
   constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
   float l = 0.f;
 #pragma unroll
@@ -33,7 +50,7 @@ EM_DEVICE void bce_tile_loss(const char* smem, const f32x16 (&z2)[2], uint64_t t
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = out_cls(u, i, h);
+      const int c = out_cls<PERM>(u, i, h);
       const float v = z2[u][i], y = yb[i];
       const float en = __builtin_amdgcn_exp2f(-fabsf(v) * L2E);  // stable sigmoid / softplus
       const float rp = __builtin_amdgcn_rcpf(1.f + en);
@@ -66,9 +83,10 @@ EM_DEVICE void bce_tile_loss(const char* smem, const f32x16 (&z2)[2], uint64_t t
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 EM_DEVICE f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-template <int YL, typename Hook>
+template <int YL, bool PERM = false, typename Hook>
 EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_t tmask, int h, float (&dz)[2][16],
                                 float& loss_acc, Hook&& hook) {
+  if (PERM) tmask = phys_targets(tmask);
   constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
   const f32x2 L2E2 = {L2E, L2E};
   auto targets = [&](int u, float (&yb)[16]) {
@@ -84,7 +102,7 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   const bool h0 = h == 0;
   const uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
   const int nm = __builtin_popcount(tlo) + __builtin_popcount(thi & 0x3FFFFu);  // bits 0..49
-  const int ns = __builtin_popcount(thi & 0x3FFC0000u);                          // bits 50..61
+  const int ns = __builtin_popcount(thi & (PERM ? 0xFFFC0000u : 0x3FFC0000u));   // bits 50..61 (PERM: 50..63)
   const float inv_m = nm ? __builtin_amdgcn_rcpf((float)nm) : 0.f;
   const float inv_s = ns ? __builtin_amdgcn_rcpf((float)ns) : 0.f;
   // target dots: tm[q] holds elements with (i & 3) >> 1 == q (x: even i, y: odd i), ts by i & 1
@@ -124,7 +142,7 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   float mm[2] = {-3.0e38f, -3.0e38f}, ms[2] = {-3.0e38f, -3.0e38f};
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
+    const int c0 = out_cls<PERM>(1, i, 0), c1 = out_cls<PERM>(1, i, 1);
     const float v = z2[1][i];
     if (c0 == c1) {
       if (c0 == 0) mm[i & 1] = fmaxf(mm[i & 1], v);
@@ -147,8 +165,10 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     float (&yb)[16] = yb1;
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
-      const int c0 = out_cls(1, i, 0), c1 = out_cls(1, i, 1);
-      static_assert(out_cls(1, 9, 0) == out_cls(1, 8, 0) && out_cls(1, 15, 1) == out_cls(1, 14, 1), "pair classes");
+      const int c0 = out_cls<PERM>(1, i, 0), c1 = out_cls<PERM>(1, i, 1);
+      static_assert(out_cls<PERM>(1, 9, 0) == out_cls<PERM>(1, 8, 0) && out_cls<PERM>(1, 15, 1) == out_cls<PERM>(1, 14, 1) &&
+                        out_cls<PERM>(1, 11, 0) == out_cls<PERM>(1, 10, 0),
+                    "pair classes");
       const f32x2 zz = zpair(1, i), yy = {yb[i], yb[i + 1]};
       f32x2 e;
       if (c0 == c1 && c0 == 0) {
@@ -191,7 +211,7 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
     const float (&yb)[16] = u == 0 ? yb0 : yb1;  // the targets, read once per tile
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c0 = out_cls(u, i, 0), c1 = out_cls(u, i, 1);
+      const int c0 = out_cls<PERM>(u, i, 0), c1 = out_cls<PERM>(u, i, 1);
       const float fm = u == 0 ? f0 : f1;
       if (c0 == c1) {
         if (c0 == 0) dz[u][i] = __builtin_fmaf(dz[u][i], fm, yb[i] * ni_m);
