@@ -115,6 +115,19 @@ EM_DEVICE float xhalf_max(float v) {
   return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
 }
 
+// max without the NaN canonicalisation the compiler puts in front of fmaxf (IEEE maxNum) on operands it
+// cannot prove canonical (a v_max_f32 x, x each, e.g. after a permlane or a phi): IEEE-754-2019 maximum
+// (NaN-propagating), which gfx950 runs as v_maximum3_f32 with no canonicalisation.  (An inline-asm
+// v_max3_f32 was tried first: the hazard recognizer does not see asm operands, so it read MFMA results
+// before they were written -- caught by tests/test_xgmi_proxy_gpu.py's bit-identity check.)
+EM_DEVICE float raw_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+EM_DEVICE float raw_max3(float a, float b, float c) { return raw_max(raw_max(a, b), c); }
+EM_DEVICE float xhalf_max_raw(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return raw_max(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
 EM_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

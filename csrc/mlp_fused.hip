@@ -262,10 +262,13 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 // lookups keep the base in the immediate too), the W2Q image moves above the ring.
 // Bit 0 unrolls the forward loop, bit 1 the backward loop (either bit selects the layout).  Same-box A/B
 // (4 rounds, profiles/r6/ab_v6_win.jsonl, median µs per step): round-5 kernel 87.8; with static LDS:
-// old layout 89.1, windowed + forward unrolled 87.0, + backward unrolled 86.8, both 87.1 -- the unrolled
-// forward copy trades its adds for register moves at 256 VGPRs.  Default 2.
+// old layout 89.1, windowed + forward unrolled 87.0, + backward unrolled 86.8, both 87.1 -- at 256
+// VGPRs the unrolled forward copy traded its adds for register moves.  Once the softmax's max trees
+// dropped their NaN canonicalisation (common.h raw_max: v_maximum3_f32) both unrolled measured 80.8 vs
+// 82.5 for the backward alone and 83.0 for the previous commit (profiles/r6/ab_v6_maxtree.jsonl).
+// Default 3.
 #ifndef V6_WIN
-#define V6_WIN 2
+#define V6_WIN 3
 #endif
 static_assert(!V6_WIN || (FUSED_SHARED && V6_NSLOT == 8), "windowed layout: shared ring of 8 slots");
 // windowed: b2 256 | YLUT 256 | XLUT 128 | flags 128 | ring 8 x 16K (W1ᵀ / W2ᵀ images at its start) | W2Q

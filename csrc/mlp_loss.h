@@ -113,14 +113,23 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   f32x2 nL2 = {0.f, 0.f};
   float mm0[4], yb0[16];
   f32x2 sm[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+  // PERM (the bf16 train kernels): max trees of v_max3_f32 without canonicalisation (raw_max3): 8
+  // instructions per 16 logits instead of ~15
+  const auto& z0 = z2[0];
   auto step = [&](int j) {
     if (j == 0) {
-      mm0[0] = z2[0][0]; mm0[1] = z2[0][1]; mm0[2] = z2[0][2]; mm0[3] = z2[0][3];
+      if (PERM) {
+        mm0[0] = raw_max3(raw_max3(z0[0], z0[1], z0[2]), raw_max3(z0[3], z0[4], z0[5]), raw_max3(z0[6], z0[7], z0[8]));
+        mm0[1] = raw_max3(raw_max3(z0[9], z0[10], z0[11]), raw_max3(z0[12], z0[13], z0[14]), z0[15]);
+      } else {
+        mm0[0] = z2[0][0]; mm0[1] = z2[0][1]; mm0[2] = z2[0][2]; mm0[3] = z2[0][3];
 #pragma unroll
-      for (int i = 4; i < 16; ++i) mm0[i & 3] = fmaxf(mm0[i & 3], z2[0][i]);
+        for (int i = 4; i < 16; ++i) mm0[i & 3] = fmaxf(mm0[i & 3], z2[0][i]);
+      }
       targets(0, yb0);
     } else if (j == 1) {
-      m0 = xhalf_max(fmaxf(fmaxf(mm0[0], mm0[1]), fmaxf(mm0[2], mm0[3])));
+      m0 = PERM ? xhalf_max_raw(raw_max(mm0[0], mm0[1]))
+                : xhalf_max(fmaxf(fmaxf(mm0[0], mm0[1]), fmaxf(mm0[2], mm0[3])));
       nL2 = f32x2{-m0 * L2E, -m0 * L2E};
     } else if (j < 6) {
 #pragma unroll
@@ -154,8 +163,17 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
       ms[i & 1] = h0 ? fmaxf(ms[i & 1], v) : ms[i & 1];
     }
   }
-  const float m1 = xhalf_max(fmaxf(mm[0], mm[1]));
-  const float mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
+  float m1, mx_s;
+  if (PERM) {  // main: registers 0-9, star: 10-15 (out_cls<true>)
+    const auto& z = z2[1];
+    static_assert(out_cls<PERM>(1, 9, 0) == 0 && out_cls<PERM>(1, 10, 0) == 1, "PERM tile-1 classes");
+    const float a = raw_max3(raw_max3(z[0], z[1], z[2]), raw_max3(z[3], z[4], z[5]), raw_max3(z[6], z[7], z[8]));
+    m1 = xhalf_max_raw(raw_max(a, z[9]));
+    mx_s = xhalf_max_raw(raw_max(raw_max3(z[10], z[11], z[12]), raw_max3(z[13], z[14], z[15])));
+  } else {
+    m1 = xhalf_max(fmaxf(mm[0], mm[1]));
+    mx_s = xhalf_max(fmaxf(ms[0], ms[1]));
+  }
   const float nmL = -m1 * L2E, nsL = -mx_s * L2E;
   const f32x2 nmL2 = {nmL, nmL}, nsL2 = {nsL, nsL};
   f32x2 s1p = {0.f, 0.f}, ss = {0.f, 0.f};
@@ -198,7 +216,7 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   }
   const float s1 = xhalf_sum(s1p.x + s1p.y), s_s = xhalf_sum(ss.x + ss.y);
   // ---- online merge of the main group: M = max(m0, m1), S = a0 s0 + a1 s1 ----
-  const float M = fmaxf(m0, m1);
+  const float M = PERM ? raw_max(m0, m1) : fmaxf(m0, m1);
   const float a0 = __builtin_amdgcn_exp2f((m0 - M) * L2E), a1 = __builtin_amdgcn_exp2f((m1 - M) * L2E);
   const float S = __builtin_fmaf(a0, s0, a1 * s1);
   const float rS = nm ? __builtin_amdgcn_rcpf(S) : 0.f;
