@@ -80,6 +80,18 @@ EM_DEVICE uint32_t lut_off(uint32_t word, int sh) {
   return (uint32_t)LUT + (__builtin_amdgcn_ubfe(word, sh, 4) << SH);
 }
 
+// Byte BYTE of v, shifted left by SH, in ONE VALU (SDWA source select): the byte-per-entry form of a
+// table lookup when the byte already holds (entry + table_base >> SH).  The operand is a plain VALU
+// result (no MFMA hazard for the recognizer to miss), so inline asm is safe here.
+template <int BYTE, int SH>
+EM_DEVICE uint32_t sdwa_byte_shl(uint32_t v) {
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_%3"
+      : "=v"(r)
+      : "v"(v), "i"(SH), "i"(BYTE));
+  return r;
+}
+
 // ds_read_b64_tr_b16: 4 rows x 16 cols block per 16-lane group, column-major to lanes
 EM_DEVICE s16x4 lds_tr16(const char* lds_base, uint32_t byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((EM_LDS s16x4*)(lds_base + byte_off));

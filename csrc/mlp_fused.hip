@@ -270,10 +270,17 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 #ifndef V6_WIN
 #define V6_WIN 3
 #endif
+// V6_W2Q_REGS: the backward wave holds its W2 fragments in 32 VGPRs for the launch instead of reading them
+// (8 KB of LDS) every tile -- 100 B of scratch per lane at 256 VGPRs: 94.4 vs 82.0 µs (profiles/r6/
+// ab_v6_sdwa_w2q.jsonl).  Kept off.
+#ifndef V6_W2Q_REGS
+#define V6_W2Q_REGS 0
+#endif
 static_assert(!V6_WIN || (FUSED_SHARED && V6_NSLOT == 8), "windowed layout: shared ring of 8 slots");
 // windowed: b2 256 | YLUT 256 | XLUT 128 | flags 128 | ring 8 x 16K (W1ᵀ / W2ᵀ images at its start) | W2Q
 constexpr int V6_IMGB = V6_WIN ? 768 : 0;                        // LDS base of the W1ᵀ / W2ᵀ images
 constexpr int V6_B2B = V6_WIN ? 0 : IMG_B2;                      // b2 (forward waves)
+// (the tables at 256 / 512 let mlp_loss.h / nib_xfrag take the SDWA byte-select lookup form)
 constexpr int V6_XLUT = V6_WIN ? 512 : IMG_BYTES;                // 16 x 8 B: input nibble -> 4 bf16 {0,1}
 constexpr int V6_YLUT = V6_WIN ? 256 : V6_XLUT + 128;            // 16 x f32x4: target nibble -> 4 {0,1} floats
 constexpr int V6_FLAGS = V6_WIN ? 640 : V6_YLUT + 256;  // [streams][32 / streams ints]: full[N] | done0[N] | done1[N]
@@ -489,13 +496,23 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
   const uint32_t MYDONE = FL + ((1 + RHO) * V6_NSLOT) * 4;
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   __syncthreads();  // matches the forward waves' barrier (recycled images)
+#if V6_W2Q_REGS  // the backward wave's W2 fragments held for the whole launch (8 KB of LDS reads per tile saved)
+  bf16x8 w2q[2][4];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, v6_w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
+#endif
   st.start();
   auto btile = [&](int k, int slot, uint32_t SB) {
     const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
     v6_wait(smem, FL + slot * 4, k + 1, ok);
     st.mark(5);
 
-    bf16x8 dzA[2][2], hR[2][2], bd[2][2], bx[2][2], w2q[2][4];
+    bf16x8 dzA[2][2], hR[2][2], bd[2][2], bx[2][2];
+#if !V6_W2Q_REGS
+    bf16x8 w2q[2][4];
+#endif
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -508,10 +525,12 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int q = 0; q < 2; ++q) hR[tt][q] = tile_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
+#if !V6_W2Q_REGS
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, v6_w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
+#endif
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll

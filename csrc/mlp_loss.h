@@ -91,9 +91,20 @@ EM_DEVICE void v6_softmax_split(const char* smem, const f32x16 (&z2)[2], uint64_
   const f32x2 L2E2 = {L2E, L2E};
   auto targets = [&](int u, float (&yb)[16]) {
     const uint32_t tmh = (uint32_t)(tmask >> (32 * u)) >> (4 * h);
+    // SDWA form (table at 256, the K7 windowed layout): byte g of sp = nibble 8g + 16, so one byte-select
+    // shift per lookup gives 256 + 16 nib -- 5 VALU per word instead of 8
+    constexpr bool SD = YL == 256 && PERM;
+    const uint32_t sp = (tmh & 0x0F0F0F0Fu) | 0x10101010u;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + lut_off<YL, 4>(tmh, 8 * g));
+      uint32_t off;
+      if constexpr (SD) {
+        off = g == 0 ? sdwa_byte_shl<0, 4>(sp) : g == 1 ? sdwa_byte_shl<1, 4>(sp) : g == 2 ? sdwa_byte_shl<2, 4>(sp)
+                                                                                          : sdwa_byte_shl<3, 4>(sp);
+      } else {
+        off = lut_off<YL, 4>(tmh, 8 * g);
+      }
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(smem + off);
       yb[4 * g + 0] = y4[0]; yb[4 * g + 1] = y4[1]; yb[4 * g + 2] = y4[2]; yb[4 * g + 3] = y4[3];
     }
   };
