@@ -228,8 +228,11 @@ def main():
         sys.exit(launch.spawn(argv, world, timeout_s=a.launch_timeout, quiet_ranks=True))
 
     if a.model == "mlp-wide":
+        # 256k rows per optimizer step: the GEMMs' M, large enough that the per-step fixed costs (Adam over
+        # 68M parameters, the skinny first/last layers' reductions) stay ~2 % of the step; measured
+        # 3.57 / 3.59 / 3.61 M samples/s at 64k / 128k / 256k on one box (profiles/r6/bench_wide_batch.txt)
         if a.batch == 1 << 20:
-            a.batch = 1 << 16
+            a.batch = 1 << 18
         if a.draws_per_gpu == 1 << 24:
             a.draws_per_gpu = (1 << 20) * 3
 

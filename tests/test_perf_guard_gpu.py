@@ -4,8 +4,8 @@ catch a structural regression (e.g. the run-time staging-lead flag in the GEMM's
 
 * 256-tile GEMM: our kernel against hipBLASLt (torch.matmul) on the same GPU, same call.  Measured
   ratio 0.88-0.90 on 8192^3; the regressed build ran at 0.78.
-* fused 62->128->62 train step at 1M samples (train kernel + Adam, 10-step hipGraph): 88-92 us on
-  every box measured; the guard is 115 us.
+* fused 62->128->62 train step at 1M samples (train kernel + Adam, 10-step hipGraph): 80-84 us on the
+  round-6 boxes (88-92 before the round-6 K7 work); the guard is 100 us.
 """
 import pytest
 import torch
@@ -39,11 +39,12 @@ def test_gemm_256_tile_within_reach_of_hipblaslt():
         t_ours = _time(lambda: LIN.linear_fwd(x, w, None, "none", out=y), 10)
         t_lib = _time(lambda: torch.nn.functional.linear(x, w), 10)
         best = max(best, t_lib / t_ours)
-    # 0.75: below the box-to-box spread (~15 %, profiles/gemm_box_variance.md) of the 0.88-0.90 measured;
-    # EUROM_PERF_GEMM_FLOOR=0.82 restores the tighter structural guard on a known box
+    # 0.82: catches the regressed build (0.78) with ~7 % of the measured 0.88-0.90 to spare for the ratio's
+    # box-to-box spread (both sides run on the same box, in the same process: the ratio moves far less than the
+    # absolute times, profiles/gemm_box_variance.md); EUROM_PERF_GEMM_FLOOR overrides it
     import os
 
-    floor = float(os.environ.get("EUROM_PERF_GEMM_FLOOR", "0.75"))
+    floor = float(os.environ.get("EUROM_PERF_GEMM_FLOOR", "0.82"))
     assert best > floor, f"256-tile GEMM at {best:.2f} x hipBLASLt throughput (measured 0.88-0.90)"
 
 
@@ -68,4 +69,4 @@ def test_fused_step_time():
         gr.replay()
     torch.cuda.synchronize()
     us = min(_time(gr.replay, 20) for _ in range(2)) * 1e3 / 10
-    assert us < 115.0, f"fused 1M-sample step {us:.1f} us (measured 88-92 us)"
+    assert us < 100.0, f"fused 1M-sample step {us:.1f} us (measured 80-84 us)"
