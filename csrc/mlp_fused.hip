@@ -1379,7 +1379,8 @@ mlp_fused_forward_kernel(const uint64_t* __restrict__ masks, const int32_t* __re
 #pragma unroll
         for (int g = 0; g < 4; ++g) {  // physical nibble n -> logical (mlp_adam.h out_phys): 13 -> 15 rotated
           const int n = 8 * u + 2 * g + h, ln = n <= 12 ? n : n == 13 ? 15 : n - 1;
-          const f32x4 v = n == 13 ? f32x4{z[4 * g + 2], z[4 * g + 3], z[4 * g + 0], z[4 * g + 1]}
+          // (the pads 62 / 63 read 0, as the parameters say: PAD_B2 exists for the train kernels' softmax only)
+          const f32x4 v = n == 13 ? f32x4{z[4 * g + 2], z[4 * g + 3], 0.f, 0.f}
                                   : f32x4{z[4 * g + 0], z[4 * g + 1], z[4 * g + 2], z[4 * g + 3]};
           *reinterpret_cast<f32x4*>(logits + (int64_t)s * OUT + 4 * ln) = v;
         }

@@ -106,6 +106,9 @@ def test_fused_forward_and_metrics(data):
     lg = m.logits(draws, B, offset=off)
     _, _, zref = _ref_grads(m.state_dict(), ds.numbers, off, B, "softmax")
     assert torch.allclose(lg[:, :62], zref, atol=2e-2, rtol=2e-2)
+    # the pad outputs read 0 (zero weights and bias) although the kernels' image gives them a -1e30 bias
+    # (csrc/mlp_adam.h PAD_B2: the train kernels' softmax class trick)
+    assert float(lg[:, 62:].abs().max()) == 0.0
     part = FM.draw_metrics(lg, draws, B, offset=off)
     tot = part.double().sum(0).cpu().numpy()
     Y = torch.from_numpy(multi_hot(ds.numbers[off + 1:off + 1 + B])).cuda()
