@@ -3,7 +3,11 @@
 instruction mix (MFMA / VALU / LDS / waits) of every basic block -- the quick check that a kernel
 edit removed VALU work or spills before spending GPU time on it.
 
-usage: tools/isa_stats.py file.s [kernel-substring] [--blocks]"""
+--loops: every loop (a backward branch to an earlier label) with its instruction mix and top opcodes --
+the census behind round 6's K7 VALU work (docs/DESIGN.md §6d): the forward / backward loop bodies' VALU
+count per tile, slot-address adds, NaN canonicalisations (v_max_f32 x, x).
+
+usage: tools/isa_stats.py file.s [kernel-substring] [--blocks] [--loops]"""
 from __future__ import annotations
 
 import collections
@@ -70,6 +74,39 @@ def main():
             for bname, cnt in blocks:
                 if sum(cnt.values()):
                     print(f"    {bname:12s} {dict(cnt)}")
+        if "--loops" in sys.argv:
+            loops(body)
+
+
+def loops(body: str, min_len: int = 100) -> None:
+    """Loops of one kernel body: label .. backward branch, longest form per header, with their mix."""
+    lines = body.split("\n")
+    labels = {}
+    for i, l in enumerate(lines):
+        m = re.match(r"^(\.LBB\S+):", l)
+        if m:
+            labels[m.group(1)] = i
+    seen = {}
+    for i, l in enumerate(lines):
+        m = re.search(r"s_c?branch\w*\s+(\.LBB\S+)", l)
+        if m and m.group(1) in labels and labels[m.group(1)] < i:
+            seen[m.group(1)] = i  # the last back edge to a header spans the whole loop
+    for head, end in seen.items():
+        a = labels[head]
+        if end - a < min_len:
+            continue
+        mix, ops = collections.Counter(), collections.Counter()
+        for raw in lines[a:end + 1]:
+            line = raw.split(";")[0].strip()
+            if not line or line.startswith(".") or line.endswith(":"):
+                continue
+            op = line.split()[0]
+            mix[classify(op)] += 1
+            ops[op] += 1
+            if op == "v_max_f32_e32" and len(set(line.replace(",", " ").split()[2:4])) == 1:
+                ops["(canonicalise)"] += 1
+        print(f"    loop {head} ({end - a} lines): {dict(mix)}")
+        print("      " + "  ".join(f"{o}:{n}" for o, n in ops.most_common(24)))
 
 
 if __name__ == "__main__":
