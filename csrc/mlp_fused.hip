@@ -289,6 +289,20 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 // V6_W2Q_REGS: the backward wave holds its W2 fragments in 32 VGPRs for the launch instead of reading them
 // (8 KB of LDS) every tile -- 100 B of scratch per lane at 256 VGPRs: 94.4 vs 82.0 µs (profiles/r6/
 // ab_v6_sdwa_w2q.jsonl).  Kept off.
+// V6_DB2_16: the backward wave's db2 (ones x dZ2, summed over the tile's samples) on two
+// v_mfma_f32_16x16x32_bf16 (16 cycles each, 4 accumulator VGPRs) fed by their own transposed dZ2 reads,
+// instead of two 32x32x16 (32 cycles each, a 16-VGPR accumulator whose 32 rows are all equal).  With ones
+// as A the k order of the samples is free, so each 16-lane group just takes 8 rows of the image.  Also takes
+// the backward waves off scratch (12 B -> 0).  81.95 vs 82.85 µs per step, 4 rounds (profiles/r6/ab_v6_db2_16.jsonl).
+#ifndef V6_DB2_16
+#define V6_DB2_16 1
+#endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+#if V6_DB2_16
+typedef f32x4v v6_db2_t[2];
+#else
+typedef f32x16 v6_db2_t;
+#endif
 #ifndef V6_W2Q_REGS
 #define V6_W2Q_REGS 0
 #endif
@@ -503,7 +517,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 // FULL, the slot is released as soon as they have landed, and the 26 MFMAs then run from registers.
 template <int RHO>
 EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f32x16 (&dW2)[2][2], f32x16 (&dW1T)[2][2],
-                           f32x16& db2, bool& ok, Stamps& st) {
+                           v6_db2_t& db2, bool& ok, Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
   const int nunits = gridDim.x * V6_NSTREAM, U = v6_unit_id(unit);
@@ -555,6 +569,15 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 2; ++q) bx[u][q] = tile_tr_frag<false>(smem, SB + V6_SX, 32 * u, q, h, q4, p4, g1);
+#if V6_DB2_16
+    // db2's B operands: dZ2 columns 32 RHO + 16 m + (lane & 15), samples 8 (lane >> 4) .. + 7
+    bf16x8 bdb[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int col = 32 * RHO + 16 * m + 4 * p4, rr = 8 * (lane >> 4) + q4;
+      bdb[m] = cat_tr(lds_tr16(smem, tile_img<true>(D2, rr, col)), lds_tr16(smem, tile_img<true>(D2, rr + 4, col)));
+    }
+#endif
     lds_signal_ordered(smem, MYDONE + slot * 4, k + 1);  // DONE (fenced form: waits for every read above)
     st.mark(6);
 
@@ -571,8 +594,14 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
       for (int q = 0; q < 2; ++q) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) dW2[tt][u] = mfma32(hR[tt][q], bd[u][q], dW2[tt][u]);
+#if !V6_DB2_16
         if (u == RHO) db2 = mfma32(ones, bd[u][q], db2);
+#endif
       }
+#if V6_DB2_16
+#pragma unroll
+    for (int m = 0; m < 2; ++m) db2[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bdb[m], db2[m], 0, 0, 0);
+#endif
     if (FUSED_PROBE & 2) {
       float a[8];
 #pragma unroll
@@ -664,12 +693,25 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
         dW2[t][u] = f32x16{};
         dW1T[t][u] = f32x16{};
       }
-    f32x16 db2 = f32x16{};
+    v6_db2_t db2;
+#if V6_DB2_16
+    db2[0] = f32x4v{};
+    db2[1] = f32x4v{};
+#else
+    db2 = f32x16{};
+#endif
     v6_backward<RHO>(smem, B, unit, sub, lane, dW2, dW1T, db2, ok, st);
     const int part = FUSED_SHARED ? sub : unit;
     dump();
     __syncthreads();
+#if V6_DB2_16
+    if (lane < 16) {  // 16x16 accumulator column lane = output 32 RHO + 16 m + lane (every row holds the sum)
+      DB2S[part * 64 + 32 * RHO + lane] = db2[0][0];
+      DB2S[part * 64 + 32 * RHO + 16 + lane] = db2[1][0];
+    }
+#else
     if (h == 0) DB2S[part * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
+#endif
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
