@@ -118,6 +118,20 @@ EM_DEVICE bf16x8 mask_by(const bf16x8 hfrag, const f32x16& a, int q) {
   }
   return __builtin_bit_cast(bf16x8, d);
 }
+// the same on two 16x16 accumulator quads (V6_B16: k 0-3 from sample tile 0, 4-7 from sample tile 1)
+template <class V4>
+EM_DEVICE bf16x8 mask_by4(const bf16x8 hfrag, const V4& a0, const V4& a1) {
+  const bf16x8 p = pack8(a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]);
+  u32x4 d = __builtin_bit_cast(u32x4, p);
+  const u32x4 hh = __builtin_bit_cast(u32x4, hfrag);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t m;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(hh[k]), "s"(0x00010001u));
+    asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(d[k]) : "v"(d[k]), "v"(m));
+  }
+  return __builtin_bit_cast(bf16x8, d);
+}
 
 // ============================================================================================
 // LDS protocol helpers (workgroup scope), diagnostic stamps, swizzled tile images
@@ -203,6 +217,14 @@ template <bool G>
 EM_DEVICE bf16x8 tile_tr_frag(const char* smem, uint32_t base, int colbase, int q, int h, int q4, int p4, int g1) {
   const int col = colbase + 16 * g1 + 4 * p4;
   const int r0 = 16 * q + 4 * h + q4;
+  return cat_tr(lds_tr16(smem, tile_img<G>(base, r0, col)), lds_tr16(smem, tile_img<G>(base, r0 + 8, col)));
+}
+// The 16x16x32 form (V6_B16): lane column colbase + (lane & 15), k = samples σ of lane group g = lane >> 4:
+// rows 16 (g >> 1) + 4 (g & 1) + 0..3, then + 8 (the same two 4-row blocks as tile_tr_frag)
+template <bool G>
+EM_DEVICE bf16x8 tile_tr16_frag(const char* smem, uint32_t base, int colbase, int lane) {
+  const int col = colbase + 4 * (lane & 3);
+  const int r0 = 16 * ((lane >> 5) & 1) + 4 * ((lane >> 4) & 1) + ((lane >> 2) & 3);
   return cat_tr(lds_tr16(smem, tile_img<G>(base, r0, col)), lds_tr16(smem, tile_img<G>(base, r0 + 8, col)));
 }
 // X fragments from a 16-entry nibble table (4 bf16 {0,1} per entry, 128 B): two ds_read_b64 per
@@ -297,15 +319,35 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 #ifndef V6_DB2_16
 #define V6_DB2_16 1
 #endif
+// V6_B16: the whole backward wave on v_mfma_f32_16x16x32_bf16 (B1, dW2, dW1ᵀ, db2: 50 MFMAs of 16 cycles
+// per tile instead of 24 of 32 + 2 of 16).  K = 32 samples fits one instruction, so every operand is read
+// once, as now: the same fragment count and VGPRs.  The samples take the order σ(st, i) = 8 st + 16 (i >> 3)
+// + (i & 7) as B1's rows (sample tile st) and the same order as the k index of dW2 / dW1ᵀ, i.e. the existing
+// two-4-row transposing reads (tile_tr_frag) and conflict-free 8-B dZ2 row reads (rows {0-7, 16-23} of a tile
+// have distinct img_fr per row parity).  The accumulators are 16x16 tiles; the epilogue stores each f32x4 at
+// the 32x32 layout's slot, so the fold is unchanged.  (MI355X_MICROARCH.md DVFS item 7: bf16 loops on the
+// 16x16x32 shape hold a higher clock on random data.)  79.5 vs 80.6 µs per step, 4 same-box rounds
+// (profiles/r6/ab_v6_b16.jsonl); 37 fused / train GPU tests pass on it.  At the 4-tile backward unroll the
+// per-slot address registers spill 14 VGPRs (2 scratch reloads per tile); a 2-tile unroll without spills
+// (81.9 µs) and no unroll (82.7) measured slower than the spilling 4-tile loop (80.8, ab_v6_b16_unroll.jsonl).
+#ifndef V6_B16
+#define V6_B16 1
+#endif
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-#if V6_DB2_16
+#if V6_DB2_16 || V6_B16
 typedef f32x4v v6_db2_t[2];
 #else
 typedef f32x16 v6_db2_t;
 #endif
+#if V6_B16
+typedef f32x4v v6_acc_t[4][4];  // [hidden 16-tile of the own half][output / feature 16-tile]
+#else
+typedef f32x16 v6_acc_t[2][2];  // [hidden 32-tile of the own half][output / feature 32-tile]
+#endif
 #ifndef V6_W2Q_REGS
 #define V6_W2Q_REGS 0
 #endif
+static_assert(!(V6_B16 && V6_W2Q_REGS), "V6_B16 reads its W2 fragments per tile");
 static_assert(!V6_WIN || (FUSED_SHARED && V6_NSLOT == 8), "windowed layout: shared ring of 8 slots");
 // windowed: b2 256 | YLUT 256 | XLUT 128 | flags 128 | ring 8 x 16K (W1ᵀ / W2ᵀ images at its start) | W2Q
 constexpr int V6_IMGB = V6_WIN ? 768 : 0;                        // LDS base of the W1ᵀ / W2ᵀ images
@@ -516,7 +558,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
 // (dZ2 A fragments, H / dZ2 / X transposes, W2ᵀ fragments: ~96 VGPRs) is issued at once right after
 // FULL, the slot is released as soon as they have landed, and the 26 MFMAs then run from registers.
 template <int RHO>
-EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f32x16 (&dW2)[2][2], f32x16 (&dW1T)[2][2],
+EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6_acc_t& dW2, v6_acc_t& dW1T,
                            v6_db2_t& db2, bool& ok, Stamps& st) {
   const int r = lane & 31, h = lane >> 5;
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g1 = (lane >> 4) & 1;
@@ -534,6 +576,73 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
     for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, v6_w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
 #endif
   st.start();
+#if V6_B16
+  auto btile = [&](int k, int slot, uint32_t SB) {
+    const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
+    const int g = lane >> 4;
+    v6_wait(smem, FL + slot * 4, k + 1, ok);
+    st.mark(5);
+
+    // dZ2 as B1's A operand: row i = sample σ(st, i) = 8 st + 16 (i >> 3) + (i & 7), k = W2Q granule 4 kk + g
+    // (outputs 16 c + 4 (g & 1) + 0..3 and + 8.., c = 2 kk + (g >> 1): the granule's own order)
+    bf16x8 dzA[2][2], w2q[4][2], hR[4], bd[4], bx[4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 8 * s + 16 * ((lane >> 3) & 1) + (lane & 7), col = 16 * (2 * kk + (g >> 1)) + 4 * (g & 1);
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, row, col));
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, row, col + 8));
+        dzA[s][kk] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) hR[t] = tile_tr16_frag<true>(smem, HB, 16 * t, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) w2q[t][kk] = lds_frag(smem, v6_w2q_off(64 * RHO + 16 * t + (lane & 15), 4 * kk + g));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bd[u] = tile_tr16_frag<true>(smem, D2, 16 * u, lane);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bx[u] = tile_tr16_frag<false>(smem, SB + V6_SX, 16 * u, lane);
+    lds_signal_ordered(smem, MYDONE + slot * 4, k + 1);  // DONE (fenced form: waits for every read above)
+    st.mark(6);
+
+    // B1: dH[sample σ][own hidden] = dZ2·W2ᵀ, two sample tiles x four hidden tiles
+    f32x4v aD[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) aD[s][t] = f32x4v{};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          aD[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dzA[s][kk], w2q[t][kk], aD[s][t], 0, 0, 0);
+    // dW2[own hid][out] += Hᵀ·dZ2 ; db2 += ones·dZ2 (independent of B1: fills the pipe)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dW2[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hR[t], bd[u], dW2[t][u], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      db2[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bd[2 * RHO + m], db2[m], 0, 0, 0);
+    st.mark(7);
+    // dZ1 = dH * (H > 0): lane group g's k = samples σ(0, 4g..) then σ(1, 4g..) = aD[0][t], aD[1][t]
+    bf16x8 dz1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dz1[t] = mask_by4(hR[t], aD[0][t], aD[1][t]);
+    st.mark(8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        dW1T[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dz1[t], bx[u], dW1T[t][u], 0, 0, 0);
+    st.mark(9);
+  };
+#else
   auto btile = [&](int k, int slot, uint32_t SB) {
     const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
     v6_wait(smem, FL + slot * 4, k + 1, ok);
@@ -629,6 +738,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, f3
         for (int tt = 0; tt < 2; ++tt) dW1T[tt][u] = mfma32(dz1[tt][q], bx[u][q], dW1T[tt][u]);
     st.mark(9);
   };
+#endif
   if (V6_WIN & 2) {  // tiles parity, parity + 2, ... cycle through slots parity + 0/2/4/6: base + 0/16/32/48K
     const uint32_t SB0 = v6_slot(unit, parity);
     for (int k = parity; k < K; k += 4 * V6_NBP) {
@@ -685,7 +795,16 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
     __syncthreads();
   } else {
     constexpr int RHO = ROLE - 2;
-    f32x16 dW2[2][2], dW1T[2][2];
+    v6_acc_t dW2, dW1T;
+#if V6_B16
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        dW2[t][u] = f32x4v{};
+        dW1T[t][u] = f32x4v{};
+      }
+#else
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -693,8 +812,9 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
         dW2[t][u] = f32x16{};
         dW1T[t][u] = f32x16{};
       }
+#endif
     v6_db2_t db2;
-#if V6_DB2_16
+#if V6_DB2_16 || V6_B16
     db2[0] = f32x4v{};
     db2[1] = f32x4v{};
 #else
@@ -704,7 +824,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
     const int part = FUSED_SHARED ? sub : unit;
     dump();
     __syncthreads();
-#if V6_DB2_16
+#if V6_DB2_16 || V6_B16
     if (lane < 16) {  // 16x16 accumulator column lane = output 32 RHO + 16 m + lane (every row holds the sum)
       DB2S[part * 64 + 32 * RHO + lane] = db2[0][0];
       DB2S[part * 64 + 32 * RHO + 16 + lane] = db2[1][0];
@@ -713,6 +833,22 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
     if (h == 0) DB2S[part * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
 #endif
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
+#if V6_B16
+    // 16x16 tile (t, u), lane (j, g'): rows 16 (t & 1) + 4 g' .. + 3 of 32x32 tile (t >> 1, u >> 1), column
+    // 16 (u & 1) + j -- the 32x32 layout's group 2 (t & 1) + (g' >> 1) of lane (16 (u & 1) + j, g' & 1)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int which = 0; which < 2; ++which) {
+          const f32x4v& acc = which ? dW1T[t][u] : dW2[t][u];
+          const int T = 8 * which + 2 * (2 * RHO + (t >> 1)) + (u >> 1), gq = lane >> 4;
+          *reinterpret_cast<f32x4*>(RED + part * 16384 +
+                                    v6_red_slot(T, 2 * (t & 1) + (gq >> 1), 16 * (u & 1) + (lane & 15), gq & 1) * 4) =
+              f32x4{acc[0], acc[1], acc[2], acc[3]};
+        }
+#else
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -726,6 +862,7 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
             *reinterpret_cast<f32x4*>(RED + part * 16384 + v6_red_slot(T, g, r, h) * 4) =
                 f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
         }
+#endif
     __syncthreads();
   }
 }
