@@ -35,6 +35,13 @@ static_assert(out_logical(out_phys(52)) == 52 && out_logical(out_phys(61)) == 61
               "output permutation");
 constexpr float PAD_B2 = -1.0e30f;  // image value of the pad logits' bias
 
+// W2Q granule swizzle: rows with (row & 15) in 4..11 swap granules k8 ^ 1.  K7's 16x16x32 backward wave
+// (mlp_fused.hip V6_B16) reads granule 4 kk + g in lane group g = lane >> 4 from row (lane & 15); the
+// ds_read_b128 lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31} then mix rows 4-11 of one granule
+// with rows 0-3 / 12-15 of its neighbour, and at 144-B rows (9 16-B units) those collide on a bank unless
+// the neighbour granules of rows 4-11 trade places (tools/lds_conflicts.py, tests/test_lds_model.py).
+EM_DEVICE constexpr int w2q_swz(int row) { return ((row + 4) >> 3) & 1; }
+
 // true for padding slots that must stay exactly zero (W1 row 63, W2 cols 62/63, b2[62/63])
 EM_DEVICE bool pad_slot(int p) {
   if (p < P_W2) return (p >> 7) == 63;
@@ -59,7 +66,7 @@ EM_DEVICE void pack_one(int p, float val, uint8_t* img) {
     {  // W2Q: row c, out o = 32u + perm(s,h,j)
       const int u = o >> 5, oo = o & 31, s = oo >> 4, a = (oo >> 3) & 1, hh = (oo >> 2) & 1, bb = oo & 3;
       const int j = 4 * a + bb, k8 = (2 * u + s) * 2 + hh;
-      *reinterpret_cast<uint16_t*>(img + IMG_W2Q + c * W2Q_RS + k8 * 16 + j * 2) = b;
+      *reinterpret_cast<uint16_t*>(img + IMG_W2Q + c * W2Q_RS + (k8 ^ w2q_swz(c)) * 16 + j * 2) = b;
     }
   } else {
     const int o = p - P_B2;

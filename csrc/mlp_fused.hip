@@ -70,7 +70,7 @@ EM_DEVICE bf16x8 lut_frag(const char* lut, uint64_t m, int q, int h) {
 // byte offsets into the LDS weight images (see em_adam_pack for the writer)
 EM_DEVICE uint32_t w1t_off(int row, int k8) { return IMG_W1T + row * W1T_RS + k8 * 16; }
 EM_DEVICE uint32_t w2p_off(int row, int k16) { return IMG_W2P + row * W2P_RS + k16 * 16; }
-EM_DEVICE uint32_t w2q_off(int row, int k8) { return IMG_W2Q + row * W2Q_RS + k8 * 16; }
+EM_DEVICE uint32_t w2q_off(int row, int k8) { return IMG_W2Q + row * W2Q_RS + (k8 ^ mlp::w2q_swz(row)) * 16; }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -368,7 +368,7 @@ EM_DEVICE uint32_t v6_slot(int st, int slot) {
   return slot < V6_RSLOTS ? V6_RING + (st * V6_RSLOTS + slot) * V6_SLOT
                           : (FUSED_SHARED ? slot - V6_RSLOTS : st) * V6_SLOT;
 }
-EM_DEVICE uint32_t v6_w2q_off(int row, int k8) { return V6_W2QB + row * W2Q_RS + k8 * 16; }
+EM_DEVICE uint32_t v6_w2q_off(int row, int k8) { return V6_W2QB + row * W2Q_RS + (k8 ^ mlp::w2q_swz(row)) * 16; }
 // LDS destination of byte `b` of the weight image
 EM_DEVICE uint32_t v6_img_dst(uint32_t b) {
   if (!V6_WIN) return b;
@@ -579,7 +579,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6
 #if V6_B16
   auto btile = [&](int k, int slot, uint32_t SB) {
     const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
-    const int g = lane >> 4;
+    const int g = lane >> 4, gw = g ^ mlp::w2q_swz(lane & 15);
     v6_wait(smem, FL + slot * 4, k + 1, ok);
     st.mark(5);
 
@@ -600,7 +600,8 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) w2q[t][kk] = lds_frag(smem, v6_w2q_off(64 * RHO + 16 * t + (lane & 15), 4 * kk + g));
+      for (int kk = 0; kk < 2; ++kk)  // v6_w2q_off with the swizzle taken from lane & 15 (= row & 15) once
+        w2q[t][kk] = lds_frag(smem, V6_W2QB + (64 * RHO + 16 * t + (lane & 15)) * W2Q_RS + 64 * kk + 16 * gw);
 #pragma unroll
     for (int u = 0; u < 4; ++u) bd[u] = tile_tr16_frag<true>(smem, D2, 16 * u, lane);
 #pragma unroll

@@ -52,8 +52,12 @@ def w2p_off(row, k16):
     return 18432 + row * 272 + k16 * 16
 
 
-def w2q_off(row, k8):
-    return 35840 + row * 144 + k8 * 16
+def w2q_swz(row):  # csrc/mlp_adam.h w2q_swz: rows (row & 15) in 4..11 swap granules k8 ^ 1
+    return ((row + 4) >> 3) & 1
+
+
+def w2q_off(row, k8, swz=True):
+    return 35840 + row * 144 + (k8 ^ (w2q_swz(row) if swz else 0)) * 16
 
 
 def img_off(base, row, col, swz):
@@ -75,6 +79,39 @@ def v4_gr(r):
 def swz_v4g(row, col):  # the kernel's v4_img<true> (H, D2 images)
     c = ((col >> 3) ^ v4_fr(row)) << 4
     return row * 128 + c + ((((col >> 2) & 1) ^ v4_gr(row)) << 3) + (col & 3) * 2
+
+
+def v6_b16_patterns(swz=True):
+    """The 16x16x32 backward wave's per-tile reads (mlp_fused.hip V6_B16): lane group g = lane >> 4 holds
+    k = samples 16 (g >> 1) + 4 (g & 1) + 0..3 (+ 8) in the transposing reads, B1's dZ2 rows 8 s + 16 (i >> 3)
+    + (i & 7) for i = lane & 15, and W2Q granule 4 kk + g of hidden row 64 rho + 16 t + i."""
+    D2, HB, XB = 8192, 4096, 12288  # slot-relative (tile_img bases; any 128-B-aligned base models the same)
+    out = []
+    for rho in (0, 1):
+        for t in range(4):
+            for kk in range(2):
+                out.append((f"W2Q rho{rho} t{t} kk{kk}", "read_b128",
+                            [w2q_off(64 * rho + 16 * t + (l & 15), 4 * kk + (l >> 4), swz) for l in range(64)]))
+    for s_ in range(2):
+        for kk in range(2):
+            for hi in (0, 8):
+                addr = []
+                for l in range(64):
+                    g = l >> 4
+                    row = 8 * s_ + 16 * ((l >> 3) & 1) + (l & 7)
+                    addr.append(D2 + swz_v4g(row, 16 * (2 * kk + (g >> 1)) + 4 * (g & 1) + hi))
+                out.append((f"dZ2 A s{s_} kk{kk} +{hi}", "read_b64", addr))
+    for nm, base, sw in (("H tr", HB, swz_v4g), ("D2 tr", D2, swz_v4g), ("X tr", XB, swz_x)):
+        for t in range(4):
+            for dr in (0, 8):
+                addr = [base + sw(16 * ((l >> 5) & 1) + 4 * ((l >> 4) & 1) + ((l >> 2) & 3) + dr, 16 * t + 4 * (l & 3))
+                        for l in range(64)]
+                out.append((f"{nm} t{t} +{dr}", "read_tr", addr))
+    return out
+
+
+def swz_x(row, col):  # the kernel's tile_img<false> (X image: whole 16-B chunks, no 8-B half swap)
+    return row * 128 + (((col >> 3) ^ v4_fr(row)) << 4) + (col & 7) * 2
 
 
 def report(name, kind, addr, count):
