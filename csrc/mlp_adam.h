@@ -36,7 +36,7 @@ static_assert(out_logical(out_phys(52)) == 52 && out_logical(out_phys(61)) == 61
 constexpr float PAD_B2 = -1.0e30f;  // image value of the pad logits' bias
 
 // W2Q granule swizzle: rows with (row & 15) in 4..11 swap granules k8 ^ 1.  K7's 16x16x32 backward wave
-// (mlp_fused.hip V6_B16) reads granule 4 kk + g in lane group g = lane >> 4 from row (lane & 15); the
+// (mlp_fused.hip v6_backward) reads granule 4 kk + g in lane group g = lane >> 4 from row (lane & 15); the
 // ds_read_b128 lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31} then mix rows 4-11 of one granule
 // with rows 0-3 / 12-15 of its neighbour, and at 144-B rows (9 16-B units) those collide on a bank unless
 // the neighbour granules of rows 4-11 trade places (tools/lds_conflicts.py, tests/test_lds_model.py).

@@ -118,7 +118,7 @@ EM_DEVICE bf16x8 mask_by(const bf16x8 hfrag, const f32x16& a, int q) {
   }
   return __builtin_bit_cast(bf16x8, d);
 }
-// the same on two 16x16 accumulator quads (V6_B16: k 0-3 from sample tile 0, 4-7 from sample tile 1)
+// the same on two 16x16 accumulator quads (the backward wave: k 0-3 from sample tile 0, 4-7 from sample tile 1)
 template <class V4>
 EM_DEVICE bf16x8 mask_by4(const bf16x8 hfrag, const V4& a0, const V4& a1) {
   const bf16x8 p = pack8(a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]);
@@ -219,7 +219,7 @@ EM_DEVICE bf16x8 tile_tr_frag(const char* smem, uint32_t base, int colbase, int 
   const int r0 = 16 * q + 4 * h + q4;
   return cat_tr(lds_tr16(smem, tile_img<G>(base, r0, col)), lds_tr16(smem, tile_img<G>(base, r0 + 8, col)));
 }
-// The 16x16x32 form (V6_B16): lane column colbase + (lane & 15), k = samples σ of lane group g = lane >> 4:
+// The 16x16x32 form (backward wave): lane column colbase + (lane & 15), k = samples σ of lane group g = lane >> 4:
 // rows 16 (g >> 1) + 4 (g & 1) + 0..3, then + 8 (the same two 4-row blocks as tile_tr_frag)
 template <bool G>
 EM_DEVICE bf16x8 tile_tr16_frag(const char* smem, uint32_t base, int colbase, int lane) {
@@ -308,46 +308,23 @@ constexpr int V6_SH = 0, V6_SD2 = 8192, V6_SX = 12288;
 #ifndef V6_WIN
 #define V6_WIN 3
 #endif
-// V6_W2Q_REGS: the backward wave holds its W2 fragments in 32 VGPRs for the launch instead of reading them
-// (8 KB of LDS) every tile -- 100 B of scratch per lane at 256 VGPRs: 94.4 vs 82.0 µs (profiles/r6/
-// ab_v6_sdwa_w2q.jsonl).  Kept off.
-// V6_DB2_16: the backward wave's db2 (ones x dZ2, summed over the tile's samples) on two
-// v_mfma_f32_16x16x32_bf16 (16 cycles each, 4 accumulator VGPRs) fed by their own transposed dZ2 reads,
-// instead of two 32x32x16 (32 cycles each, a 16-VGPR accumulator whose 32 rows are all equal).  With ones
-// as A the k order of the samples is free, so each 16-lane group just takes 8 rows of the image.  Also takes
-// the backward waves off scratch (12 B -> 0).  81.95 vs 82.85 µs per step, 4 rounds (profiles/r6/ab_v6_db2_16.jsonl).
-#ifndef V6_DB2_16
-#define V6_DB2_16 1
-#endif
-// V6_B16: the whole backward wave on v_mfma_f32_16x16x32_bf16 (B1, dW2, dW1ᵀ, db2: 50 MFMAs of 16 cycles
-// per tile instead of 24 of 32 + 2 of 16).  K = 32 samples fits one instruction, so every operand is read
-// once, as now: the same fragment count and VGPRs.  The samples take the order σ(st, i) = 8 st + 16 (i >> 3)
-// + (i & 7) as B1's rows (sample tile st) and the same order as the k index of dW2 / dW1ᵀ, i.e. the existing
-// two-4-row transposing reads (tile_tr_frag) and conflict-free 8-B dZ2 row reads (rows {0-7, 16-23} of a tile
-// have distinct img_fr per row parity).  The accumulators are 16x16 tiles; the epilogue stores each f32x4 at
-// the 32x32 layout's slot, so the fold is unchanged.  (MI355X_MICROARCH.md DVFS item 7: bf16 loops on the
-// 16x16x32 shape hold a higher clock on random data.)  79.5 vs 80.6 µs per step, 4 same-box rounds
-// (profiles/r6/ab_v6_b16.jsonl); 37 fused / train GPU tests pass on it.  At the 4-tile backward unroll the
-// per-slot address registers spill 14 VGPRs (2 scratch reloads per tile); a 2-tile unroll without spills
-// (81.9 µs) and no unroll (82.7) measured slower than the spilling 4-tile loop (80.8, ab_v6_b16_unroll.jsonl).
-#ifndef V6_B16
-#define V6_B16 1
-#endif
+// The backward wave runs on v_mfma_f32_16x16x32_bf16 (B1, dW2, dW1ᵀ, db2: 50 MFMAs of 16 cycles per tile;
+// round 6 replaced 24 of 32x32x16 + 2 for db2).  K = 32 samples fits one instruction, so every operand is read
+// once: the same fragment count and VGPRs as the 32x32 form.  The samples take the order σ(st, i) = 8 st +
+// 16 (i >> 3) + (i & 7) as B1's rows (sample tile st) and the same order as the k index of dW2 / dW1ᵀ, i.e. the
+// two-4-row transposing reads of tile_tr16_frag and conflict-free 8-B dZ2 row reads (rows {0-7, 16-23} of a tile
+// have distinct img_fr per row parity).  The accumulators are 16x16 tiles; the epilogue stores each f32x4 at the
+// 32x32 layout's slot, so the fold is unchanged.  db2 uses ones as A, so its k order is free.  (MI355X_MICROARCH.md
+// DVFS item 7: bf16 loops on the 16x16x32 shape hold a higher clock on random data.)  Measured, same box:
+// db2 alone on 16x16x32 81.95 vs 82.85 µs per step (profiles/r6/ab_v6_db2_16.jsonl), then the whole wave 79.5 vs
+// 80.6 (ab_v6_b16.jsonl).  At the 4-tile backward unroll the per-slot address registers spill 14 VGPRs (2 scratch
+// reloads per tile); a 2-tile unroll without spills (81.9 µs) and no unroll (82.7) measured slower than the
+// spilling 4-tile loop (80.8, ab_v6_b16_unroll.jsonl).  W2 fragments held in registers for the launch instead of
+// read per tile (32x32 form) spilled 100 B per lane: 94.4 vs 82.0 µs (ab_v6_sdwa_w2q.jsonl).  The 32x32 backward
+// wave and those knobs are in git history (round 6).
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-#if V6_DB2_16 || V6_B16
-typedef f32x4v v6_db2_t[2];
-#else
-typedef f32x16 v6_db2_t;
-#endif
-#if V6_B16
+typedef f32x4v v6_db2_t[2];     // db2 of output 16-tiles 2 rho, 2 rho + 1 (every accumulator row holds the sum)
 typedef f32x4v v6_acc_t[4][4];  // [hidden 16-tile of the own half][output / feature 16-tile]
-#else
-typedef f32x16 v6_acc_t[2][2];  // [hidden 32-tile of the own half][output / feature 32-tile]
-#endif
-#ifndef V6_W2Q_REGS
-#define V6_W2Q_REGS 0
-#endif
-static_assert(!(V6_B16 && V6_W2Q_REGS), "V6_B16 reads its W2 fragments per tile");
 static_assert(!V6_WIN || (FUSED_SHARED && V6_NSLOT == 8), "windowed layout: shared ring of 8 slots");
 // windowed: b2 256 | YLUT 256 | XLUT 128 | flags 128 | ring 8 x 16K (W1ᵀ / W2ᵀ images at its start) | W2Q
 constexpr int V6_IMGB = V6_WIN ? 768 : 0;                        // LDS base of the W1ᵀ / W2ᵀ images
@@ -568,15 +545,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6
   const uint32_t MYDONE = FL + ((1 + RHO) * V6_NSLOT) * 4;
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   __syncthreads();  // matches the forward waves' barrier (recycled images)
-#if V6_W2Q_REGS  // the backward wave's W2 fragments held for the whole launch (8 KB of LDS reads per tile saved)
-  bf16x8 w2q[2][4];
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, v6_w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
-#endif
   st.start();
-#if V6_B16
   auto btile = [&](int k, int slot, uint32_t SB) {
     const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
     const int g = lane >> 4, gw = g ^ mlp::w2q_swz(lane & 15);
@@ -630,6 +599,17 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6
 #pragma unroll
     for (int m = 0; m < 2; ++m)
       db2[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bd[2 * RHO + m], db2[m], 0, 0, 0);
+    if (FUSED_PROBE & 2) {
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = (float)(lane + j) * 1e-3f + (float)k * 1e-6f;
+#pragma unroll
+      for (int it = 0; it < FUSED_PROBE_VALU / 8; ++it)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          a[j] = (it & 7) == 7 ? __builtin_amdgcn_exp2f(a[j]) : __builtin_fmaf(a[j], 0.999f, 0.25f);
+      asm volatile("" ::"v"(a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7]));
+    }
     st.mark(7);
     // dZ1 = dH * (H > 0): lane group g's k = samples σ(0, 4g..) then σ(1, 4g..) = aD[0][t], aD[1][t]
     bf16x8 dz1[4];
@@ -643,103 +623,6 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6
         dW1T[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dz1[t], bx[u], dW1T[t][u], 0, 0, 0);
     st.mark(9);
   };
-#else
-  auto btile = [&](int k, int slot, uint32_t SB) {
-    const uint32_t D2 = SB + V6_SD2, HB = SB + V6_SH + RHO * 4096;
-    v6_wait(smem, FL + slot * 4, k + 1, ok);
-    st.mark(5);
-
-    bf16x8 dzA[2][2], hR[2][2], bd[2][2], bx[2][2];
-#if !V6_W2Q_REGS
-    bf16x8 w2q[2][4];
-#endif
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {  // dZ2 as B1's A operand (samples x outputs): F's own granules
-        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, r, 32 * u + 16 * q + 4 * h));
-        const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + tile_img<true>(D2, r, 32 * u + 16 * q + 8 + 4 * h));
-        dzA[u][q] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
-      }
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) hR[tt][q] = tile_tr_frag<true>(smem, HB, 32 * tt, q, h, q4, p4, g1);
-#if !V6_W2Q_REGS
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) w2q[tt][kk] = lds_frag(smem, v6_w2q_off(32 * (2 * RHO + tt) + r, kk * 2 + h));
-#endif
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) bd[u][q] = tile_tr_frag<true>(smem, D2, 32 * u, q, h, q4, p4, g1);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) bx[u][q] = tile_tr_frag<false>(smem, SB + V6_SX, 32 * u, q, h, q4, p4, g1);
-#if V6_DB2_16
-    // db2's B operands: dZ2 columns 32 RHO + 16 m + (lane & 15), samples 8 (lane >> 4) .. + 7
-    bf16x8 bdb[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int col = 32 * RHO + 16 * m + 4 * p4, rr = 8 * (lane >> 4) + q4;
-      bdb[m] = cat_tr(lds_tr16(smem, tile_img<true>(D2, rr, col)), lds_tr16(smem, tile_img<true>(D2, rr + 4, col)));
-    }
-#endif
-    lds_signal_ordered(smem, MYDONE + slot * 4, k + 1);  // DONE (fenced form: waits for every read above)
-    st.mark(6);
-
-    // B1: dH = dZ2·W2ᵀ for the own hidden half
-    f32x16 aD[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) aD[tt] = mfma32(dzA[kk >> 1][kk & 1], w2q[tt][kk], aD[tt]);
-    // dW2[own hid][out] += Hᵀ·dZ2 ; db2[out tile RHO] += ones·dZ2 (independent of B1: fills the pipe)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) dW2[tt][u] = mfma32(hR[tt][q], bd[u][q], dW2[tt][u]);
-#if !V6_DB2_16
-        if (u == RHO) db2 = mfma32(ones, bd[u][q], db2);
-#endif
-      }
-#if V6_DB2_16
-#pragma unroll
-    for (int m = 0; m < 2; ++m) db2[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bdb[m], db2[m], 0, 0, 0);
-#endif
-    if (FUSED_PROBE & 2) {
-      float a[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = (float)(lane + j) * 1e-3f + (float)k * 1e-6f;
-#pragma unroll
-      for (int it = 0; it < FUSED_PROBE_VALU / 8; ++it)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          a[j] = (it & 7) == 7 ? __builtin_amdgcn_exp2f(a[j]) : __builtin_fmaf(a[j], 0.999f, 0.25f);
-      asm volatile("" ::"v"(a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7]));
-    }
-    st.mark(7);
-    // dZ1 = dH * (H > 0), then dW1ᵀ[own hid][feat] += dZ1ᵀ·X
-    bf16x8 dz1[2][2];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) dz1[tt][q] = mask_by(hR[tt][q], aD[tt], q);
-    st.mark(8);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) dW1T[tt][u] = mfma32(dz1[tt][q], bx[u][q], dW1T[tt][u]);
-    st.mark(9);
-  };
-#endif
   if (V6_WIN & 2) {  // tiles parity, parity + 2, ... cycle through slots parity + 0/2/4/6: base + 0/16/32/48K
     const uint32_t SB0 = v6_slot(unit, parity);
     for (int k = parity; k < K; k += 4 * V6_NBP) {
@@ -797,7 +680,6 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
   } else {
     constexpr int RHO = ROLE - 2;
     v6_acc_t dW2, dW1T;
-#if V6_B16
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -805,36 +687,18 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
         dW2[t][u] = f32x4v{};
         dW1T[t][u] = f32x4v{};
       }
-#else
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        dW2[t][u] = f32x16{};
-        dW1T[t][u] = f32x16{};
-      }
-#endif
     v6_db2_t db2;
-#if V6_DB2_16 || V6_B16
     db2[0] = f32x4v{};
     db2[1] = f32x4v{};
-#else
-    db2 = f32x16{};
-#endif
     v6_backward<RHO>(smem, B, unit, sub, lane, dW2, dW1T, db2, ok, st);
     const int part = FUSED_SHARED ? sub : unit;
     dump();
     __syncthreads();
-#if V6_DB2_16 || V6_B16
     if (lane < 16) {  // 16x16 accumulator column lane = output 32 RHO + 16 m + lane (every row holds the sum)
       DB2S[part * 64 + 32 * RHO + lane] = db2[0][0];
       DB2S[part * 64 + 32 * RHO + 16 + lane] = db2[1][0];
     }
-#else
-    if (h == 0) DB2S[part * 64 + 32 * RHO + r] = db2[0];  // accumulator column r = output 32 RHO + r
-#endif
     if (lane == 0) LOSSS[wave] = ok ? 0.f : __builtin_nanf("");
-#if V6_B16
     // 16x16 tile (t, u), lane (j, g'): rows 16 (t & 1) + 4 g' .. + 3 of 32x32 tile (t >> 1, u >> 1), column
     // 16 (u & 1) + j -- the 32x32 layout's group 2 (t & 1) + (g' >> 1) of lane (16 (u & 1) + j, g' & 1)
 #pragma unroll
@@ -849,21 +713,6 @@ EM_DEVICE void v6_body(char* smem, const uint64_t* __restrict__ masks, const int
                                     v6_red_slot(T, 2 * (t & 1) + (gq >> 1), 16 * (u & 1) + (lane & 15), gq & 1) * 4) =
               f32x4{acc[0], acc[1], acc[2], acc[3]};
         }
-#else
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int which = 0; which < 2; ++which) {
-          const f32x16& acc = which ? dW1T[tt][u] : dW2[tt][u];
-          const int T = 8 * which + 2 * (2 * RHO + tt) + u;
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<f32x4*>(RED + part * 16384 + v6_red_slot(T, g, r, h) * 4) =
-                f32x4{acc[4 * g + 0], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
-        }
-#endif
     __syncthreads();
   }
 }

@@ -82,7 +82,7 @@ def swz_v4g(row, col):  # the kernel's v4_img<true> (H, D2 images)
 
 
 def v6_b16_patterns(swz=True):
-    """The 16x16x32 backward wave's per-tile reads (mlp_fused.hip V6_B16): lane group g = lane >> 4 holds
+    """The 16x16x32 backward wave's per-tile reads (mlp_fused.hip v6_backward): lane group g = lane >> 4 holds
     k = samples 16 (g >> 1) + 4 (g & 1) + 0..3 (+ 8) in the transposing reads, B1's dZ2 rows 8 s + 16 (i >> 3)
     + (i & 7) for i = lane & 15, and W2Q granule 4 kk + g of hidden row 64 rho + 16 t + i."""
     D2, HB, XB = 8192, 4096, 12288  # slot-relative (tile_img bases; any 128-B-aligned base models the same)
