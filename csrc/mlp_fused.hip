@@ -140,22 +140,9 @@ EM_DEVICE void lds_signal(char* smem, uint32_t flag_off, int value) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __hip_atomic_store(reinterpret_cast<int*>(smem + flag_off), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// The ring counters of K7 v6 without the release fence's s_waitcnt lgkmcnt(0): every access on both sides of
-// the hand-off is LDS, and the LDS performs one wave's instructions in issue order, so a counter write
-// issued after the slot's writes (FULL) or after the slot's reads (DONE) is performed after them and any
-// wave that then reads the counter sees a slot whose accesses are done.  The compiler barrier keeps the
-// program order.  (The reads' data may still be in flight to the reader's registers: its own lgkmcnt waits
-// before use cover that.)  Measured 82.6 vs 82.2 µs for the fenced form (profiles/r6/ab_v6_lds_order.jsonl;
-// the compiler then places the backward waves' DONE among their MFMAs anyway), so 0 -- fenced -- stays.
-#ifndef V6_LDS_ORDER
-#define V6_LDS_ORDER 0
-#endif
-EM_DEVICE void lds_signal_ordered(char* smem, uint32_t flag_off, int value) {
-  if (!V6_LDS_ORDER) return lds_signal(smem, flag_off, value);
-  asm volatile("" ::: "memory");  // (no sched_barrier: pinning DONE ahead of the MFMAs keeps all 41 read
-                                  // results live at once -- 356 B of scratch)
-  __hip_atomic_store(reinterpret_cast<int*>(smem + flag_off), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+// (Round 6 measured the ring counters without the release fence's s_waitcnt lgkmcnt(0) -- LDS performs one
+// wave's instructions in issue order -- at 82.6 vs 82.2 µs for the fenced form, profiles/r6/ab_v6_lds_order.jsonl;
+// the compiler places the backward waves' DONE among their MFMAs either way.  The fenced lds_signal stays.)
 
 // Diagnostic phase timers (build with --define FUSED_STAMPS=1; tools/fused_phases.py reads them):
 // s_memtime deltas summed per phase per wave, written into spare slab floats.  They force an
@@ -517,7 +504,7 @@ EM_DEVICE void v6_forward(char* smem, const uint64_t* __restrict__ masks, const 
         *reinterpret_cast<u32x2*>(smem + tile_img<true>(SB + V6_SD2, r, 32 * u + 16 * q + 8 + 4 * h)) =
             u32x2{fq[2], fq[3]};
       }
-    lds_signal_ordered(smem, FL + slot * 4, k + 1);  // FULL
+    lds_signal(smem, FL + slot * 4, k + 1);  // FULL
     st.mark(4);
   };
   if (V6_WIN & 1) {  // tiles f, f + 4, ... alternate slots f and f + 4: the second is the first + 32K
@@ -575,7 +562,7 @@ EM_DEVICE void v6_backward(char* smem, int B, int unit, int parity, int lane, v6
     for (int u = 0; u < 4; ++u) bd[u] = tile_tr16_frag<true>(smem, D2, 16 * u, lane);
 #pragma unroll
     for (int u = 0; u < 4; ++u) bx[u] = tile_tr16_frag<false>(smem, SB + V6_SX, 16 * u, lane);
-    lds_signal_ordered(smem, MYDONE + slot * 4, k + 1);  // DONE (fenced form: waits for every read above)
+    lds_signal(smem, MYDONE + slot * 4, k + 1);  // DONE (fenced form: waits for every read above)
     st.mark(6);
 
     // B1: dH[sample σ][own hidden] = dZ2·W2ᵀ, two sample tiles x four hidden tiles
