@@ -483,7 +483,7 @@ def _train_mlp(cfg: RunConfig, info: D.DistInfo, log) -> dict:
         from torch.profiler import ProfilerActivity, profile
 
         acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if dev.type == "cuda" else [])
-        prof = profile(activities=acts)
+        prof = profile(activities=acts, acc_events=True)  # one cycle: keep its events (and no torch warning)
         prof.__enter__()
     t0 = time.time()
     done = 0
